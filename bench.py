@@ -1,0 +1,322 @@
+#!/usr/bin/env python3
+"""Benchmark of the virtual-LiDAR pose search (BASELINE.json metric, configs[1]).
+
+A step = one pass of the hot path over one batch: the candidate poses of this rank (256 per
+GPU: BASELINE configs[1] at N=1, 4096 over 8 GPUs = configs[3]) each cast the dense
+1024 x 256 azimuth x elevation fan against the 1M-point excavation terrain with the
+reference's march rule (virtual_lidar.cpp:765-797), plus ONE collective: all-reduce(MIN)
+of the per-pose blocked-ray counts (RCCL over xGMI when N > 1), then the argmin.
+
+value = ray-hit tests/s: sample queries the reference would execute (samples up to and
+including the first hit, else all), summed over all ranks, / max-over-ranks wall time.
+Inputs (terrain index, direction tables, poses) are resident in HBM before timing starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fan|filter|cells]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "ray-hit tests/sec + candidate poses/sec (whole node), 1M-pt terrain"
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8 TB/s spec
+
+
+def _dist_init(n_gpus: int):
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return torch, (dist if world > 1 else None), world, rank, local
+
+
+def _poses_for(ctx, grid_bbox, zx, total: int):
+    """generateCandidatePositions with num_candidates grown until >= total survive."""
+    from pointcloud_processor_amd import _abi
+
+    nc = max(total, 100)
+    while True:
+        p = _abi.default_vl_params(num_candidates=nc)
+        poses = ctx.generate_candidates(grid_bbox, p, zx)
+        if poses.shape[0] >= total:
+            return poses[:total], nc
+        nc = int(nc * 1.3) + 16
+
+
+def _grid_bbox(area, res=0.1):
+    import numpy as np
+
+    p = area[:, :3].astype(np.float64)
+    return np.array([p[:, 0].min() - res, p[:, 0].max() + res, p[:, 1].min() - res,
+                     p[:, 1].max() + res, p[:, 2].min() - res, p[:, 2].max() + res])
+
+
+def _traffic_from_profiles(workload_key: str):
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(workload_key)
+    except Exception:
+        return None
+
+
+def cpu_baseline_fan(terrain, poses, fan, budget_s: float):
+    """The oracle (CPU restatement, single thread = the reference's executor) on a bounded
+    sample: the first k poses of this workload, whole fans, until ~budget_s elapsed."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle
+
+    pyoracle.set_threads(1)
+    T = pyoracle.Cloud(terrain)
+    units = 0
+    k = 0
+    t0 = time.perf_counter()
+    while k < len(poses) and time.perf_counter() - t0 < budget_s:
+        _, u, _ = pyoracle.raycast_fan(T, poses[k:k + 1], fan.n_az, fan.n_el, fan.el_min,
+                                       fan.el_max, fan.max_distance, want_first_hit=False)
+        units += int(u.sum())
+        k += 1
+    dt = time.perf_counter() - t0
+    return {"value": units / dt, "unit": "ray-hit tests/s", "cores": 1, "kind": "port",
+            "sample": f"{k} of {len(poses)} poses x full {fan.n_az}x{fan.n_el} fan, "
+                      f"{units} sample queries in {dt:.1f} s (oracle/pcp_oracle.c, 1 thread)"}
+
+
+def run_fan(args, torch, dist, world, rank, local):
+    import numpy as np
+
+    from pointcloud_processor_amd import _abi, synth
+
+    ctx = _abi.Context(local)
+    scene = synth.terrain_scene()
+    ctx.set_terrain(scene.terrain, point_step=32)
+    bbox = _grid_bbox(scene.area)
+    P_total = args.poses_per_gpu * world
+    poses_all, nc = _poses_for(ctx, bbox, scene.zx120_pose5, P_total)
+    lo, hi = rank * args.poses_per_gpu, (rank + 1) * args.poses_per_gpu
+    poses = np.ascontiguousarray(poses_all[lo:hi])
+    fan = _abi.fan_params(n_az=args.n_az, n_el=args.n_el)
+    on_gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
+
+    def step():
+        blocked, units, _, _ = ctx.raycast_fan(poses, fan)
+        key = torch.full((P_total,), torch.iinfo(torch.int64).max, dtype=torch.int64)
+        key[lo:hi] = torch.from_numpy(blocked.astype(np.int64))
+        key = key.to(dev)
+        if dist is not None:
+            dist.all_reduce(key, op=dist.ReduceOp.MIN)   # the single collective
+        k = key.cpu().numpy()
+        best = int(np.argmin(k))                          # ties -> lowest pose index
+        return int(units.sum()), best, k
+
+    def barrier_sync():
+        if dist is not None:
+            dist.barrier()
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.profile(True)
+    ctx.profile_reset()
+    barrier_sync()
+    t0 = time.perf_counter()
+    units_local = 0
+    best = -1
+    for _ in range(args.steps):
+        u, best, keys = step()
+        units_local += u
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    ctx.profile(False)
+    k_ms, k_n = ctx.profile_get("raycast_fan")
+    # max-over-ranks time, sum-over-ranks units
+    t = torch.tensor([dt], dtype=torch.float64)
+    u = torch.tensor([units_local], dtype=torch.float64)
+    if dist is not None:
+        t = t.to(dev); u = u.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+    dt_max, units_all = float(t.item()), float(u.item())
+    # diagnostic (untimed): algorithmic bytes of one launch
+    st = ctx.raycast_fan_stats(poses, fan)
+    units_per_launch = units_local / max(args.steps, 1)
+    alg_bytes = 64.0 * units_per_launch + 12.0 * st["point_tests"]
+    avg_kernel_s = (k_ms / max(k_n, 1)) * 1e-3
+    achieved = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else None
+    out = {
+        "metric": METRIC,
+        "value": units_all / dt_max,
+        "unit": "ray-hit tests/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt_max / max(args.steps, 1) * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64 march / f32 point test",
+        "data": "synthetic (seeded T1M L-pit terrain, reference candidate lattice)",
+        "config": {"workload": "C2: 1M-pt L-shape excavation terrain, 1024x256 ray fan, "
+                               f"{args.poses_per_gpu} candidate poses per GPU",
+                   "terrain_points": int(scene.terrain.shape[0]),
+                   "poses_total": P_total, "fan": [args.n_az, args.n_el],
+                   "num_candidates_lattice": nc, "parallelism": f"pose-shard x{world}"},
+        "poses_per_s": P_total * args.steps / dt_max,
+        "best_pose": best,
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": _traffic_from_profiles("fan"),
+            "kernel": "k_raycast_fan", "avg_kernel_ms": avg_kernel_s * 1e3,
+            "alg_bytes_per_launch": alg_bytes,
+            "model": "64 B/sample query + 12 B/point test (SURVEY 8d)",
+            "diag": st,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_fan(scene.terrain, poses, fan, args.cpu_seconds)
+    ctx.close()
+    return out
+
+
+def run_filter(args, torch, dist, world, rank, local):
+    """C3: crop + voxel(0.05) + transform on a 10M-pt dual-LiDAR frame, inputs in HBM."""
+    import math
+
+    import numpy as np
+
+    from pointcloud_processor_amd import _abi, synth
+
+    ctx = _abi.Context(local)
+    n_each = args.filter_points // 2
+    clouds = [synth.lidar_cloud(n_each, sensor_height=2.0, seed=1 + 2 * rank),
+              synth.lidar_cloud(n_each, sensor_height=3.5, seed=2 + 2 * rank)]
+    dptr = []
+    views = []
+    for c in clouds:
+        p = ctx.dev_alloc(c.nbytes)
+        ctx.h2d(p, c)
+        dptr.append(p)
+        views.append(_abi.CloudView(p, c.shape[0], 16, 0, 4, 8))
+    box = [0.0, 15.0, -10.0, 10.0, -1.5, 10.0]
+    yaw = math.radians(30.0)
+    tfs = [((8.0, -3.0, 0.0), (0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2))),
+           ((0.55, 0.4, 3.5), (0.0, math.sin(0.4363 / 2), 0.0, math.cos(0.4363 / 2)))]
+    cap = sum(c.shape[0] for c in clouds)
+    out_d = ctx.dev_alloc(cap * 32)
+
+    def step():
+        return ctx.filter_merge_device(views, [box, box], 0.05, tfs, [(255, 0, 0), (0, 0, 255)],
+                                       out_d, cap)
+
+    for _ in range(args.warmup):
+        n_out, per = step()
+    ctx.profile(True)
+    ctx.profile_reset()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n_out, per = step()
+    dt = time.perf_counter() - t0
+    ctx.profile(False)
+    n_in = sum(c.shape[0] for c in clouds)
+    kern = {k: ctx.profile_get(k) for k in ("crop", "voxel", "transform")}
+    k_total_ms = sum(v[0] for v in kern.values()) / max(args.steps, 1)
+    alg = 12.0 * n_in + 16.0 * n_out
+    res = {
+        "metric": "crop+voxel+transform points/s (C3)", "value": n_in * args.steps / dt,
+        "unit": "input points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / max(args.steps, 1) * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic 2 x LiDAR-like clouds, point_step 16",
+        "config": {"workload": f"C3: crop+voxel(0.05)+transform, {n_in} pts", "n_out": n_out,
+                   "per_cloud": [int(x) for x in per]},
+        "roofline": {"bound": "hbm", "achieved": alg / (k_total_ms * 1e-3) / 1e9,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": alg / (k_total_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "traffic": _traffic_from_profiles("filter"),
+                     "kernel_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in kern.items()},
+                     "model": "12 B/input point + 16 B/output point (SURVEY 8d)"},
+    }
+    for p in dptr + [out_d]:
+        ctx.dev_free(p)
+    ctx.close()
+    return res
+
+
+def run_cells(args, torch, dist, world, rank, local):
+    """Reference-mode scoring (runOptimization) for the same poses: poses/s."""
+    import numpy as np
+
+    from pointcloud_processor_amd import _abi, synth
+
+    ctx = _abi.Context(local)
+    scene = synth.terrain_scene()
+    cells = synth.excavation_cells(scene.area)
+    ctx.set_terrain(scene.terrain, point_step=32)
+    ctx.set_aux_cloud(synth.aux_cloud(), point_step=32)
+    ctx.set_cells(cells.xyz, cells.normals)
+    P_total = args.poses_per_gpu * world
+    poses_all, nc = _poses_for(ctx, cells.grid_bbox, scene.zx120_pose5, P_total)
+    poses = np.ascontiguousarray(poses_all[rank * args.poses_per_gpu:(rank + 1) * args.poses_per_gpu])
+    params = _abi.default_vl_params()
+    flags = np.zeros(cells.xyz.shape[0], np.uint8)
+    for _ in range(args.warmup):
+        ctx.score_poses(poses, scene.zx120_pose5, params, flags)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tot, cov, rep = ctx.score_poses(poses, scene.zx120_pose5, params, flags)
+    dt = time.perf_counter() - t0
+    ctx.close()
+    return {"metric": "candidate poses/sec (reference cell scoring)",
+            "value": P_total * args.steps / dt, "unit": "poses/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic", "config": {"workload": f"{P_total} poses x {cells.xyz.shape[0]} cells"},
+            "best_pose": int(rep.best_idx)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", choices=["fan", "filter", "cells"], default="fan")
+    ap.add_argument("--poses-per-gpu", type=int, default=256)
+    ap.add_argument("--n-az", type=int, default=1024)
+    ap.add_argument("--n-el", type=int, default=256)
+    ap.add_argument("--filter-points", type=int, default=10_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    torch, dist, world, rank, local = _dist_init(args.gpus)
+    fn = {"fan": run_fan, "filter": run_filter, "cells": run_cells}[args.mode]
+    out = fn(args, torch, dist, world, rank, local)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,226 @@
+/*
+ * pcp_abi.h -- C ABI of libpcp: the MI355X-native hot path of
+ * YamaguchiAtsushi/pointcloud_processor (crop/voxel -> SE(3)+concat -> virtual-LiDAR
+ * ray-trace pose search), re-designed for gfx950.
+ *
+ * The reference has no plugin/operator/FFI API: its only stable interface is the ROS2
+ * surface.  Each entry point below replaces one algorithm member function
+ * of a reference node (cited file:line); a node shell keeps the topics/params/QoS and calls
+ * these with the PointCloud2 buffers it already holds.  See INTEGRATION.md.
+ *
+ * Conventions
+ *  - every function returns int status (PCP_OK = 0, < 0 on error) and never throws;
+ *    the message is available from pcp_last_error(ctx).
+ *  - a pcp_ctx owns one HIP device, one HIP stream and all device buffers.  It is NOT
+ *    thread-safe (the reference runs callbacks on a single-threaded executor).
+ *  - unless a `flags` argument says otherwise, pointers are HOST pointers owned by the
+ *    caller; calls are synchronous (results are in host memory on return).
+ *  - empty inputs are not errors: they return PCP_OK with zero outputs / best_idx = -1.
+ *  - PCP_E_CAPACITY: an output buffer was too small; the *n_out argument holds the size
+ *    that was needed and nothing else was written.
+ */
+#ifndef PCP_ABI_H
+#define PCP_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCP_ABI_VERSION 1
+
+enum pcp_status {
+    PCP_OK = 0,
+    PCP_E_INVALID = -1,   /* bad argument (null pointer, misaligned field, bad size) */
+    PCP_E_HIP = -2,       /* HIP runtime / device error */
+    PCP_E_CAPACITY = -3,  /* output capacity too small (*n_out = required) */
+    PCP_E_STATE = -4,     /* missing prerequisite (e.g. pcp_set_cells not called) */
+    PCP_E_NOMEM = -5      /* device or host allocation failed */
+};
+
+typedef struct pcp_ctx pcp_ctx;
+
+/* A PointCloud2-like array-of-structs buffer: `n` points of `point_step` bytes each with
+ * FLOAT32 x/y/z at byte offsets off_x/off_y/off_z (sensor_msgs::PointField).  Offsets and
+ * point_step must be multiples of 4.  This is exactly what pcl::fromROSMsg reads. */
+typedef struct pcp_cloud_view {
+    const void *data;
+    uint64_t n;
+    uint32_t point_step;
+    uint32_t off_x, off_y, off_z;
+} pcp_cloud_view;
+
+/* ---- context ----------------------------------------------------------------------- */
+int pcp_abi_version(void);
+int pcp_device_count(int *n);
+int pcp_create(int device, pcp_ctx **out);
+void pcp_destroy(pcp_ctx *ctx);
+const char *pcp_last_error(const pcp_ctx *ctx);
+int pcp_synchronize(pcp_ctx *ctx);
+
+/* device buffers owned by the caller (for inputs resident in HBM, e.g. benchmarks) */
+int pcp_dev_alloc(pcp_ctx *ctx, uint64_t bytes, void **dptr);
+int pcp_dev_free(pcp_ctx *ctx, void *dptr);
+int pcp_memcpy_h2d(pcp_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+int pcp_memcpy_d2h(pcp_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+
+/* ---- in-library kernel timing (HIP events on the ctx stream) ------------------------ */
+enum pcp_kernel_id {
+    PCP_K_RAYCAST_FAN = 0,   /* fan ray-march (BASELINE configs[1], the headline)   */
+    PCP_K_SCORE_CELLS,       /* mobile pose x cell ray-march + score                 */
+    PCP_K_ZX120_CELLS,       /* pose-invariant zx120 cell evaluation                 */
+    PCP_K_POSE_SUM,          /* ordered per-pose score sums                          */
+    PCP_K_CELL_FLAGS,        /* stale-flag resolve + colour statistics              */
+    PCP_K_CANDIDATES,        /* candidate lattice + ground height                    */
+    PCP_K_INDEX_BUILD,       /* all kernels of a spatial index build                 */
+    PCP_K_CROP,              /* crop-box stream compaction                           */
+    PCP_K_VOXEL,             /* voxel keying + sort + centroid                       */
+    PCP_K_TRANSFORM,         /* SE(3) + RGB + concat                                  */
+    PCP_K_COUNT
+};
+int pcp_profile_enable(pcp_ctx *ctx, int enable);
+int pcp_profile_reset(pcp_ctx *ctx);
+int pcp_profile_get(pcp_ctx *ctx, int kernel_id, double *total_ms, uint64_t *launches);
+const char *pcp_kernel_name(int kernel_id);
+
+/* ---- pointcloud_filter (SimplifiedScanMatcher) --------------------------------------- */
+/* cropFrontArea, pointcloud_filter.cpp:87-120 (predicate :111-113).  Order-preserving
+ * strict box  box[0] < x < box[1], box[2] < y < box[3], box[4] < z < box[5]  with the
+ * float coordinate compared to the double bound.  kept_idx (nullable): input indices of
+ * the kept points, ascending.  out_xyz16 (nullable): kept points as PointXYZ (16-B
+ * stride: x,y,z,1.0f). */
+int pcp_crop_box(pcp_ctx *ctx, const pcp_cloud_view *in, const double box[6],
+                 uint32_t *kept_idx, float *out_xyz16, uint64_t cap, uint64_t *n_kept);
+
+/* downsampleCloud -> pcl::VoxelGrid<PointXYZ>, pointcloud_filter.cpp:122-139.
+ * out_xyz16: centroids (PointXYZ, 16-B stride) in ascending voxel index.
+ * voxel_idx / voxel_count (nullable): PCL's linear voxel index and points per voxel.
+ * *passthrough = 1 when PCL's int32 index-overflow guard fires (output = input). */
+int pcp_voxel_grid(pcp_ctx *ctx, const pcp_cloud_view *in, float leaf, float *out_xyz16,
+                   uint32_t *voxel_idx, uint32_t *voxel_count, uint64_t cap, uint64_t *n_out,
+                   int32_t *passthrough);
+
+/* processCloudSimple, pointcloud_filter.cpp:64-85: crop then voxel (leaf <= 0: crop only)
+ * fused on the device.  Output PointXYZ 16-B stride (the toROSMsg layout). */
+int pcp_crop_voxel(pcp_ctx *ctx, const pcp_cloud_view *in, const double box[6], float leaf,
+                   float *out_xyz16, uint64_t cap, uint64_t *n_out, uint64_t *n_cropped);
+
+/* ---- pointcloud_merger (GnssGicpMatcher cloud part) ------------------------------------ */
+typedef struct pcp_rigid {
+    double t[3];   /* geometry_msgs Transform.translation */
+    double q[4];   /* rotation x, y, z, w */
+} pcp_rigid;
+
+/* processPointClouds + processRobotCloud, pointcloud_merger.cpp:308-394: for each cloud i
+ * in order, tf2::doTransform (float32 Eigen Translation3f*Quaternionf, :370) and tag colour
+ * rgb[3i..3i+2] (:376-387), concatenated (robot first, then zx120, :316-325).
+ * out_xyzrgb32: PointXYZRGB memory image, 32-B stride (x,y,z,1.0f,rgba,pad). */
+int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds,
+                         const pcp_rigid *tf, const uint8_t *rgb, void *out_xyzrgb32,
+                         uint64_t cap, uint64_t *n_out);
+
+/* Full device pipeline (BASELINE configs[2]): per cloud crop -> voxel(leaf) -> transform +
+ * colour, concatenated.  boxes: 6 doubles per cloud.  flags: PCP_MEM_DEVICE_IN (cloud data
+ * pointers are device pointers) / PCP_MEM_DEVICE_OUT (out is a device pointer).
+ * n_per_cloud (nullable, k entries): points each cloud contributed. */
+#define PCP_MEM_DEVICE_IN 1u
+#define PCP_MEM_DEVICE_OUT 2u
+int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const double *boxes,
+                     float leaf, const pcp_rigid *tf, const uint8_t *rgb, void *out_xyzrgb32,
+                     uint64_t cap, uint64_t *n_out, uint64_t *n_per_cloud, uint32_t flags);
+
+/* ---- virtual_lidar (SimplifiedDualLidarOptimizer) -------------------------------------- */
+typedef struct pcp_vl_params {      /* virtual_lidar.cpp:66-71 */
+    double grid_resolution;         /* 0.1  */
+    double sensor_height;           /* 1.1  */
+    double search_radius;           /* 3.0  */
+    double max_distance;            /* 15.0 */
+    int32_t num_candidates;         /* 100  */
+    int32_t vertical_layers;        /* 10   */
+} pcp_vl_params;
+
+/* GridCell flag bits (virtual_lidar.cpp:20-44) as kept by the caller between ticks */
+#define PCP_F_RANGE_Z 1u
+#define PCP_F_FOV_Z 2u
+#define PCP_F_VIS_Z 4u
+#define PCP_F_RANGE_M 8u
+#define PCP_F_FOV_M 16u
+#define PCP_F_VIS_M 32u
+
+typedef struct pcp_vl_report {
+    int64_t best_idx;            /* -1: no candidates */
+    double best_score;           /* -inf when no candidates (:464) */
+    double zx120_total_score;    /* evaluateZX120Only (:360-452) */
+    int32_t zx120_range_ok, zx120_fov_ok, zx120_visible_ok;
+    int32_t total_cells;
+    int32_t zx120_green, zx120_red, zx120_blue, zx120_yellow;
+    int32_t green, red, blue, yellow;   /* dual configuration (:480-519) */
+} pcp_vl_report;
+
+/* terrainCallback (:180-192): replaces KdTreeFLANN::setInputCloud(terrain).  n == 0 keeps
+ * the previous index for ray casts (the reference keeps the stale tree) while ground
+ * heights see the empty cloud (:601). */
+int pcp_set_terrain(pcp_ctx *ctx, const pcp_cloud_view *terrain);
+/* zx120PointsCallback (:194-207): index of /zx120/filtered_points for the relaxed check. */
+int pcp_set_aux_cloud(pcp_ctx *ctx, const pcp_cloud_view *aux);
+/* the valid cells of generateExcavationGrid3D (:236-287): centres (x,y,z double) and
+ * surface normals (float, computeCellSurfaceNormal :301-340), in grid order. */
+int pcp_set_cells(pcp_ctx *ctx, const double *xyz, const float *normals, uint64_t n);
+
+/* generateCandidatePositions + getGroundHeight (:550-625).  grid_bbox = {grid_min_x,
+ * grid_max_x, grid_min_y, grid_max_y, excavation_min_z, excavation_max_z} after the
+ * margin (:251-254).  zx120_pose5 = {x,y,z,pitch,yaw} from getZX120Position (:342-358).
+ * poses5 out: x,y,z,pitch,yaw per candidate, in the reference's lattice order. */
+int pcp_generate_candidates(pcp_ctx *ctx, const double grid_bbox[6], const pcp_vl_params *p,
+                            const double zx120_pose5[5], double *poses5, uint64_t cap,
+                            uint64_t *n_out);
+
+/* runOptimization's scoring (:460-519): evaluateZX120Only, evaluatePosition per candidate
+ * (:627-654), strict-'>' argmax (:471-474) and the colour statistics from the stale
+ * GridCell flags (:487-501).  cell_flags: in/out, one byte per cell (PCP_F_*), the state
+ * the caller's GridCells hold.  total_score/covered (nullable): per candidate. */
+int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx120_pose5[5],
+                    const pcp_vl_params *p, uint8_t *cell_flags, double *total_score,
+                    int32_t *covered, pcp_vl_report *rep);
+
+/* Dense ray fan (BASELINE configs[1]): per pose, n_az x n_el rays, ray (i, j) with local
+ * direction (cos e_j cos a_i, cos e_j sin a_i, sin e_j), a_i = 2*pi*i/n_az,
+ * e_j = el_min + (el_max-el_min)*(j+0.5)/n_el, rotated by the pose yaw, marched with
+ * checkVisibilityWithRaycasting's rule (:765-797) to end = max_distance - 0.08.
+ * blocked[p]: rays that hit terrain (occlusion score); units[p] (nullable): sample
+ * queries the reference would execute; first_hit (nullable, [p][j][i] int16): sample
+ * index of the first blocked sample or -1 (depth = pcp_step_table[k]);
+ * best_idx (nullable): argmin blocked, ties -> lowest index. */
+typedef struct pcp_fan_params {
+    int32_t n_az, n_el;
+    double el_min, el_max;     /* radians */
+    double max_distance;
+} pcp_fan_params;
+int pcp_raycast_fan(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
+                    uint32_t *blocked, uint64_t *units, int16_t *first_hit, int64_t *best_idx);
+
+/* Diagnostic build of the same march (not for timing): stats[0] = samples visited after the
+ * exact clip, stats[1] = samples whose 2x2x2 stencil is occupied (directory reads),
+ * stats[2] = point tests.  Used to state the roofline's algorithmic bytes. */
+int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                          const pcp_fan_params *fan, uint64_t stats[3]);
+
+/* The march's sample distances: s_0 = 0.5, s_{k+1} = s_k + 0.3 (repeated double addition,
+ * :765-796) while s_k < end.  Returns the count in *n (writes min(cap, n) values). */
+int pcp_step_table(double end, double *steps, uint64_t cap, uint64_t *n);
+
+/* diagnostics of the terrain index (cell edge, dims, points) */
+typedef struct pcp_index_info {
+    uint64_t n_points;
+    double cell;
+    int32_t nx, ny, nz;
+    double bmin[3], bmax[3];
+} pcp_index_info;
+int pcp_terrain_info(pcp_ctx *ctx, pcp_index_info *info);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PCP_ABI_H */

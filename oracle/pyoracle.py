@@ -1,0 +1,200 @@
+"""ctypes binding of oracle/liboracle.so -- the CPU restatement of the reference hot path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker / timed CPU baseline.  Never a product path.
+Parity unpinned (see pcp_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "liboracle.so"
+
+
+class VlParams(C.Structure):
+    _fields_ = [("grid_resolution", C.c_double), ("sensor_height", C.c_double),
+                ("search_radius", C.c_double), ("max_distance", C.c_double),
+                ("num_candidates", C.c_int32), ("vertical_layers", C.c_int32)]
+
+
+class VlReport(C.Structure):
+    _fields_ = [("best_idx", C.c_int64), ("best_score", C.c_double),
+                ("zx120_total_score", C.c_double),
+                ("zx120_range_ok", C.c_int32), ("zx120_fov_ok", C.c_int32),
+                ("zx120_visible_ok", C.c_int32), ("total_cells", C.c_int32),
+                ("zx120_green", C.c_int32), ("zx120_red", C.c_int32),
+                ("zx120_blue", C.c_int32), ("zx120_yellow", C.c_int32),
+                ("green", C.c_int32), ("red", C.c_int32), ("blue", C.c_int32),
+                ("yellow", C.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_P = C.c_void_p
+_SIGS = [
+    ("orc_set_threads", None, [C.c_int]),
+    ("orc_get_threads", C.c_int, []),
+    ("orc_crop_box", C.c_int64, [_P, C.c_int64, C.c_int64, _P, _P]),
+    ("orc_voxel_grid", C.c_int64, [_P, C.c_int64, C.c_int64, C.c_float, _P, _P, _P,
+                                   C.POINTER(C.c_int)]),
+    ("orc_transform_rgb", None, [_P, C.c_int64, C.c_int64, _P, _P, C.c_uint8, C.c_uint8,
+                                 C.c_uint8, _P]),
+    ("orc_cloud_build", _P, [_P, C.c_int64, C.c_int64]),
+    ("orc_cloud_free", None, [_P]),
+    ("orc_cloud_any_within", C.c_int, [_P, C.c_float, C.c_float, C.c_float, C.c_double]),
+    ("orc_ground_height", C.c_double, [_P, C.c_double, C.c_double]),
+    ("orc_generate_candidates", C.c_int64, [_P, C.c_int, _P, C.POINTER(VlParams), _P, _P,
+                                            C.c_int64]),
+    ("orc_score_poses", None, [_P, _P, C.c_int64, _P, _P, C.c_int64, _P, C.c_int64, _P,
+                               C.POINTER(VlParams), _P, _P, _P, C.POINTER(VlReport)]),
+    ("orc_raycast_fan", None, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_double, C.c_double,
+                               C.c_double, _P, _P, _P]),
+    ("orc_fan_tables", None, [C.c_int32, C.c_int32, C.c_double, C.c_double, _P, _P, _P, _P]),
+]
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        l = C.CDLL(str(LIB))
+        for name, res, args in _SIGS:
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _f32(a):
+    a = np.ascontiguousarray(a, np.float32)
+    if a.ndim != 2 or a.shape[1] < 3:
+        raise ValueError("expected (N, k>=3) float32")
+    return a
+
+
+def set_threads(n: int):
+    lib().orc_set_threads(int(n))
+
+
+def crop_box(pts, box):
+    a = _f32(pts)
+    kept = np.empty(max(a.shape[0], 1), np.uint32)
+    box = np.ascontiguousarray(box, np.float64)
+    m = lib().orc_crop_box(_p(a), a.shape[0], a.shape[1], _p(box), _p(kept))
+    return kept[:m].copy()
+
+
+def voxel_grid(pts, leaf):
+    a = _f32(pts)
+    n = max(a.shape[0], 1)
+    out = np.empty((n, 3), np.float32)
+    idx = np.empty(n, np.uint32)
+    cnt = np.empty(n, np.uint32)
+    pt = C.c_int()
+    k = lib().orc_voxel_grid(_p(a), a.shape[0], a.shape[1], C.c_float(leaf), _p(out), _p(idx),
+                             _p(cnt), C.byref(pt))
+    return out[:k].copy(), idx[:k].copy(), cnt[:k].copy(), bool(pt.value)
+
+
+def transform_rgb(pts, t, q, rgb):
+    a = _f32(pts)
+    out = np.empty((max(a.shape[0], 1), 8), np.float32)
+    t = np.ascontiguousarray(t, np.float64)
+    q = np.ascontiguousarray(q, np.float64)
+    lib().orc_transform_rgb(_p(a), a.shape[0], a.shape[1], _p(t), _p(q), int(rgb[0]),
+                            int(rgb[1]), int(rgb[2]), _p(out))
+    return out[: a.shape[0]].copy()
+
+
+class Cloud:
+    """Exact radius-search structure over a point array (replaces KdTreeFLANN)."""
+
+    def __init__(self, pts):
+        a = _f32(pts)
+        self.n = a.shape[0]
+        self.h = lib().orc_cloud_build(_p(a), a.shape[0], a.shape[1])
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().orc_cloud_free(self.h)
+        except Exception:
+            pass
+
+    def any_within(self, q, radius):
+        return bool(lib().orc_cloud_any_within(self.h, C.c_float(q[0]), C.c_float(q[1]),
+                                               C.c_float(q[2]), radius))
+
+    def ground_height(self, x, y):
+        return lib().orc_ground_height(self.h, x, y)
+
+
+def vl_params(**kw):
+    p = VlParams(0.1, 1.1, 3.0, 15.0, 100, 10)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def generate_candidates(terrain: Cloud | None, grid_bbox, params, zx120_pose5, terrain_empty=False):
+    bb = np.ascontiguousarray(grid_bbox, np.float64)
+    zx = np.ascontiguousarray(zx120_pose5, np.float64)
+    gs = int(np.ceil(np.sqrt(float(params.num_candidates))))
+    cap = max(gs * gs, 1)
+    out = np.empty((cap, 5), np.float64)
+    n = lib().orc_generate_candidates(terrain.h if terrain else None, int(terrain_empty), _p(bb),
+                                      C.byref(params), _p(zx), _p(out), cap)
+    return out[:n].copy()
+
+
+def score_poses(terrain: Cloud | None, aux: Cloud | None, cells_xyz, cells_nrm, poses5,
+                zx120_pose5, params, cell_flags):
+    cx = np.ascontiguousarray(cells_xyz, np.float64).reshape(-1, 3)
+    cn = np.ascontiguousarray(cells_nrm, np.float32).reshape(-1, 3)
+    poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+    zx = np.ascontiguousarray(zx120_pose5, np.float64)
+    P = poses.shape[0]
+    tot = np.empty(max(P, 1), np.float64)
+    cov = np.empty(max(P, 1), np.int32)
+    rep = VlReport()
+    assert cell_flags.dtype == np.uint8
+    lib().orc_score_poses(terrain.h if terrain else None, aux.h if aux else None,
+                          aux.n if aux else 0, _p(cx), _p(cn), cx.shape[0], _p(poses), P, _p(zx),
+                          C.byref(params), _p(cell_flags), _p(tot), _p(cov), C.byref(rep))
+    return tot[:P].copy(), cov[:P].copy(), rep
+
+
+def raycast_fan(terrain: Cloud, poses5, n_az, n_el, el_min, el_max, max_distance,
+                want_first_hit=True):
+    poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+    P = poses.shape[0]
+    fh = np.empty((P, n_el, n_az), np.int16) if want_first_hit else None
+    blocked = np.zeros(max(P, 1), np.uint32)
+    units = np.zeros(max(P, 1), np.uint64)
+    lib().orc_raycast_fan(terrain.h, _p(poses), P, n_az, n_el, el_min, el_max, max_distance,
+                          _p(fh), _p(blocked), _p(units))
+    return blocked[:P].copy(), units[:P].copy(), fh
+
+
+def fan_tables(n_az, n_el, el_min, el_max):
+    ca = np.empty(n_az); sa = np.empty(n_az); ce = np.empty(n_el); se = np.empty(n_el)
+    lib().orc_fan_tables(n_az, n_el, el_min, el_max, _p(ca), _p(sa), _p(ce), _p(se))
+    return ca, sa, ce, se

@@ -1,0 +1,417 @@
+"""ctypes binding of libpcp's C ABI (include/pcp_abi.h).
+
+This is plumbing for tests, the benchmark and Python callers: every compute call goes to
+the HIP library.  There is no CPU fallback: if libpcp.so is missing or no GPU is present,
+the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "_lib" / "libpcp.so"
+
+PCP_OK = 0
+PCP_E_INVALID = -1
+PCP_E_HIP = -2
+PCP_E_CAPACITY = -3
+PCP_E_STATE = -4
+PCP_E_NOMEM = -5
+
+PCP_MEM_DEVICE_IN = 1
+PCP_MEM_DEVICE_OUT = 2
+
+F_RANGE_Z, F_FOV_Z, F_VIS_Z, F_RANGE_M, F_FOV_M, F_VIS_M = 1, 2, 4, 8, 16, 32
+
+KERNELS = ["raycast_fan", "score_cells", "zx120_cells", "pose_sum", "cell_flags",
+           "candidates", "index_build", "crop", "voxel", "transform"]
+
+
+class PcpError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"pcp error {code}: {msg}")
+        self.code = code
+
+
+class CloudView(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("n", C.c_uint64), ("point_step", C.c_uint32),
+                ("off_x", C.c_uint32), ("off_y", C.c_uint32), ("off_z", C.c_uint32)]
+
+
+class Rigid(C.Structure):
+    _fields_ = [("t", C.c_double * 3), ("q", C.c_double * 4)]
+
+
+class VlParams(C.Structure):
+    _fields_ = [("grid_resolution", C.c_double), ("sensor_height", C.c_double),
+                ("search_radius", C.c_double), ("max_distance", C.c_double),
+                ("num_candidates", C.c_int32), ("vertical_layers", C.c_int32)]
+
+
+class VlReport(C.Structure):
+    _fields_ = [("best_idx", C.c_int64), ("best_score", C.c_double),
+                ("zx120_total_score", C.c_double),
+                ("zx120_range_ok", C.c_int32), ("zx120_fov_ok", C.c_int32),
+                ("zx120_visible_ok", C.c_int32), ("total_cells", C.c_int32),
+                ("zx120_green", C.c_int32), ("zx120_red", C.c_int32),
+                ("zx120_blue", C.c_int32), ("zx120_yellow", C.c_int32),
+                ("green", C.c_int32), ("red", C.c_int32), ("blue", C.c_int32),
+                ("yellow", C.c_int32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class FanParams(C.Structure):
+    _fields_ = [("n_az", C.c_int32), ("n_el", C.c_int32), ("el_min", C.c_double),
+                ("el_max", C.c_double), ("max_distance", C.c_double)]
+
+
+class IndexInfo(C.Structure):
+    _fields_ = [("n_points", C.c_uint64), ("cell", C.c_double), ("nx", C.c_int32),
+                ("ny", C.c_int32), ("nz", C.c_int32), ("bmin", C.c_double * 3),
+                ("bmax", C.c_double * 3)]
+
+
+# (name, restype, argtypes) for every entry point of include/pcp_abi.h
+_P = C.c_void_p
+_SIGS = [
+    ("pcp_abi_version", C.c_int, []),
+    ("pcp_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("pcp_create", C.c_int, [C.c_int, C.POINTER(_P)]),
+    ("pcp_destroy", None, [_P]),
+    ("pcp_last_error", C.c_char_p, [_P]),
+    ("pcp_synchronize", C.c_int, [_P]),
+    ("pcp_dev_alloc", C.c_int, [_P, C.c_uint64, C.POINTER(_P)]),
+    ("pcp_dev_free", C.c_int, [_P, _P]),
+    ("pcp_memcpy_h2d", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("pcp_memcpy_d2h", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("pcp_profile_enable", C.c_int, [_P, C.c_int]),
+    ("pcp_profile_reset", C.c_int, [_P]),
+    ("pcp_profile_get", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    ("pcp_kernel_name", C.c_char_p, [C.c_int]),
+    ("pcp_crop_box", C.c_int, [_P, C.POINTER(CloudView), _P, _P, _P, C.c_uint64,
+                               C.POINTER(C.c_uint64)]),
+    ("pcp_voxel_grid", C.c_int, [_P, C.POINTER(CloudView), C.c_float, _P, _P, _P, C.c_uint64,
+                                 C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]),
+    ("pcp_crop_voxel", C.c_int, [_P, C.POINTER(CloudView), _P, C.c_float, _P, C.c_uint64,
+                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("pcp_transform_concat", C.c_int, [_P, C.c_int, C.POINTER(CloudView), C.POINTER(Rigid), _P,
+                                       _P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("pcp_filter_merge", C.c_int, [_P, C.c_int, C.POINTER(CloudView), _P, C.c_float,
+                                   C.POINTER(Rigid), _P, _P, C.c_uint64, C.POINTER(C.c_uint64),
+                                   _P, C.c_uint32]),
+    ("pcp_set_terrain", C.c_int, [_P, C.POINTER(CloudView)]),
+    ("pcp_set_aux_cloud", C.c_int, [_P, C.POINTER(CloudView)]),
+    ("pcp_set_cells", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("pcp_generate_candidates", C.c_int, [_P, _P, C.POINTER(VlParams), _P, _P, C.c_uint64,
+                                          C.POINTER(C.c_uint64)]),
+    ("pcp_score_poses", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams), _P, _P, _P,
+                                  C.POINTER(VlReport)]),
+    ("pcp_raycast_fan", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P, _P, _P,
+                                  C.POINTER(C.c_int64)]),
+    ("pcp_raycast_fan_stats", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P]),
+    ("pcp_step_table", C.c_int, [C.c_double, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("pcp_terrain_info", C.c_int, [_P, C.POINTER(IndexInfo)]),
+]
+ABI_SYMBOLS = [s[0] for s in _SIGS]
+
+_lib = None
+
+
+def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
+    """Load libpcp.so (raises OSError when it has not been built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise OSError(f"libpcp.so not found at {p}: run __graft_entry__.build() "
+                      f"(make -C pointcloud_processor_amd/csrc)")
+    lib = C.CDLL(str(p))
+    for name, res, args in _SIGS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def cloud_view(arr: np.ndarray, point_step: int | None = None, offs=(0, 4, 8)) -> CloudView:
+    """CloudView over a C-contiguous array whose rows are point records.
+
+    float32 (N, k>=3) arrays are read as k*4-byte records with x, y, z first; structured or
+    uint8 (N, point_step) arrays must pass point_step and offsets explicitly."""
+    if not arr.flags.c_contiguous:
+        raise ValueError("cloud array must be C-contiguous")
+    n = arr.shape[0] if arr.ndim >= 1 else 0
+    if point_step is None:
+        if arr.dtype != np.float32 or arr.ndim != 2 or arr.shape[1] < 3:
+            raise ValueError("pass point_step for non (N,k) float32 clouds")
+        point_step = arr.shape[1] * 4
+    return CloudView(arr.ctypes.data if n else None, n, point_step, *offs)
+
+
+class Context:
+    """One libpcp context: one HIP device + stream + resident buffers (not thread-safe)."""
+
+    def __init__(self, device: int = 0, lib_path=None):
+        self.lib = load_library(lib_path)
+        h = C.c_void_p()
+        rc = self.lib.pcp_create(device, C.byref(h))
+        if rc != PCP_OK:
+            raise PcpError(rc, f"pcp_create(device={device}) failed (is a gfx950 GPU visible?)")
+        self.h = h
+        self.device = device
+        self._keep = []
+
+    # -- plumbing ----------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pcp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != PCP_OK:
+            msg = self.lib.pcp_last_error(self.h)
+            raise PcpError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def synchronize(self):
+        self._check(self.lib.pcp_synchronize(self.h), "pcp_synchronize")
+
+    def profile(self, enable: bool = True):
+        self._check(self.lib.pcp_profile_enable(self.h, int(enable)), "pcp_profile_enable")
+
+    def profile_reset(self):
+        self._check(self.lib.pcp_profile_reset(self.h), "pcp_profile_reset")
+
+    def profile_get(self, kernel: str | int):
+        kid = KERNELS.index(kernel) if isinstance(kernel, str) else kernel
+        ms, n = C.c_double(), C.c_uint64()
+        self._check(self.lib.pcp_profile_get(self.h, kid, C.byref(ms), C.byref(n)),
+                    "pcp_profile_get")
+        return ms.value, n.value
+
+    def dev_alloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        self._check(self.lib.pcp_dev_alloc(self.h, nbytes, C.byref(p)), "pcp_dev_alloc")
+        return p.value
+
+    def dev_free(self, p: int):
+        self._check(self.lib.pcp_dev_free(self.h, p), "pcp_dev_free")
+
+    def h2d(self, dst: int, src: np.ndarray):
+        self._check(self.lib.pcp_memcpy_h2d(self.h, dst, _ptr(src), src.nbytes), "h2d")
+
+    def d2h(self, dst: np.ndarray, src: int):
+        self._check(self.lib.pcp_memcpy_d2h(self.h, _ptr(dst), src, dst.nbytes), "d2h")
+
+    # -- pointcloud_filter ------------------------------------------------------------------------
+    def crop_box(self, cloud: np.ndarray, box, point_step=None, offs=(0, 4, 8)):
+        """cropFrontArea: returns (kept_idx uint32, xyz float32 (m,4))."""
+        v = cloud_view(cloud, point_step, offs)
+        n = v.n
+        kept = np.empty(max(n, 1), np.uint32)
+        xyz = np.empty((max(n, 1), 4), np.float32)
+        box = np.ascontiguousarray(box, np.float64)
+        m = C.c_uint64()
+        self._check(self.lib.pcp_crop_box(self.h, C.byref(v), _ptr(box), _ptr(kept), _ptr(xyz),
+                                          n, C.byref(m)), "pcp_crop_box")
+        return kept[: m.value].copy(), xyz[: m.value].copy()
+
+    def voxel_grid(self, cloud: np.ndarray, leaf: float, point_step=None, offs=(0, 4, 8)):
+        """pcl::VoxelGrid: returns (xyz (k,4), voxel_idx, voxel_count, passthrough)."""
+        v = cloud_view(cloud, point_step, offs)
+        n = max(v.n, 1)
+        out = np.empty((n, 4), np.float32)
+        idx = np.empty(n, np.uint32)
+        cnt = np.empty(n, np.uint32)
+        k = C.c_uint64()
+        pt = C.c_int32()
+        self._check(self.lib.pcp_voxel_grid(self.h, C.byref(v), C.c_float(leaf), _ptr(out),
+                                            _ptr(idx), _ptr(cnt), n, C.byref(k), C.byref(pt)),
+                    "pcp_voxel_grid")
+        k = k.value
+        return out[:k].copy(), idx[:k].copy(), cnt[:k].copy(), bool(pt.value)
+
+    def crop_voxel(self, cloud: np.ndarray, box, leaf: float, point_step=None, offs=(0, 4, 8)):
+        """processCloudSimple: crop then voxel -> (xyz (k,4), n_cropped)."""
+        v = cloud_view(cloud, point_step, offs)
+        n = max(v.n, 1)
+        out = np.empty((n, 4), np.float32)
+        box = np.ascontiguousarray(box, np.float64)
+        k, nc = C.c_uint64(), C.c_uint64()
+        self._check(self.lib.pcp_crop_voxel(self.h, C.byref(v), _ptr(box), C.c_float(leaf),
+                                            _ptr(out), n, C.byref(k), C.byref(nc)),
+                    "pcp_crop_voxel")
+        return out[: k.value].copy(), nc.value
+
+    # -- pointcloud_merger ------------------------------------------------------------------------
+    @staticmethod
+    def _rigids(tfs):
+        arr = (Rigid * max(len(tfs), 1))()
+        for i, (t, q) in enumerate(tfs):
+            arr[i].t[:] = [float(x) for x in t]
+            arr[i].q[:] = [float(x) for x in q]
+        return arr
+
+    def transform_concat(self, clouds, tfs, rgbs):
+        """processPointClouds/processRobotCloud: -> (N, 8) float32 PointXYZRGB memory image."""
+        k = len(clouds)
+        views = (CloudView * max(k, 1))(*[cloud_view(c) for c in clouds])
+        total = sum(c.shape[0] for c in clouds)
+        out = np.empty((max(total, 1), 8), np.float32)
+        rgb = np.ascontiguousarray(np.asarray(rgbs, np.uint8).reshape(-1))
+        n = C.c_uint64()
+        self._check(self.lib.pcp_transform_concat(self.h, k, views, self._rigids(tfs), _ptr(rgb),
+                                                  _ptr(out), total, C.byref(n)),
+                    "pcp_transform_concat")
+        return out[: n.value].copy()
+
+    def filter_merge(self, clouds, boxes, leaf, tfs, rgbs):
+        k = len(clouds)
+        views = (CloudView * max(k, 1))(*[cloud_view(c) for c in clouds])
+        total = sum(c.shape[0] for c in clouds)
+        out = np.empty((max(total, 1), 8), np.float32)
+        rgb = np.ascontiguousarray(np.asarray(rgbs, np.uint8).reshape(-1))
+        bx = np.ascontiguousarray(np.asarray(boxes, np.float64).reshape(-1))
+        n = C.c_uint64()
+        per = np.zeros(max(k, 1), np.uint64)
+        self._check(self.lib.pcp_filter_merge(self.h, k, views, _ptr(bx), C.c_float(leaf),
+                                              self._rigids(tfs), _ptr(rgb), _ptr(out), total,
+                                              C.byref(n), _ptr(per), 0), "pcp_filter_merge")
+        return out[: n.value].copy(), per[:k].copy()
+
+    def filter_merge_device(self, views, boxes, leaf, tfs, rgbs, out_dev: int, cap: int):
+        """Device-resident pipeline (benchmark): views hold device pointers."""
+        k = len(views)
+        varr = (CloudView * max(k, 1))(*views)
+        rgb = np.ascontiguousarray(np.asarray(rgbs, np.uint8).reshape(-1))
+        bx = np.ascontiguousarray(np.asarray(boxes, np.float64).reshape(-1))
+        n = C.c_uint64()
+        per = np.zeros(max(k, 1), np.uint64)
+        self._keep = [rgb, bx]
+        self._check(self.lib.pcp_filter_merge(self.h, k, varr, _ptr(bx), C.c_float(leaf),
+                                              self._rigids(tfs), _ptr(rgb), out_dev, cap,
+                                              C.byref(n), _ptr(per),
+                                              PCP_MEM_DEVICE_IN | PCP_MEM_DEVICE_OUT),
+                    "pcp_filter_merge")
+        return n.value, per[:k].copy()
+
+    # -- virtual_lidar ------------------------------------------------------------------------
+    def set_terrain(self, cloud: np.ndarray, point_step=None, offs=(0, 4, 8)):
+        v = cloud_view(cloud, point_step, offs)
+        self._check(self.lib.pcp_set_terrain(self.h, C.byref(v)), "pcp_set_terrain")
+
+    def set_aux_cloud(self, cloud: np.ndarray, point_step=None, offs=(0, 4, 8)):
+        v = cloud_view(cloud, point_step, offs)
+        self._check(self.lib.pcp_set_aux_cloud(self.h, C.byref(v)), "pcp_set_aux_cloud")
+
+    def set_cells(self, xyz: np.ndarray, normals: np.ndarray):
+        xyz = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
+        nrm = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+        assert xyz.shape == nrm.shape
+        self._check(self.lib.pcp_set_cells(self.h, _ptr(xyz), _ptr(nrm), xyz.shape[0]),
+                    "pcp_set_cells")
+        self.n_cells = xyz.shape[0]
+
+    def terrain_info(self) -> dict:
+        info = IndexInfo()
+        self._check(self.lib.pcp_terrain_info(self.h, C.byref(info)), "pcp_terrain_info")
+        return {"n_points": info.n_points, "cell": info.cell,
+                "dims": (info.nx, info.ny, info.nz),
+                "bmin": tuple(info.bmin), "bmax": tuple(info.bmax)}
+
+    def generate_candidates(self, grid_bbox, params: VlParams, zx120_pose5, cap=None):
+        bb = np.ascontiguousarray(grid_bbox, np.float64)
+        zx = np.ascontiguousarray(zx120_pose5, np.float64)
+        gs = int(np.ceil(np.sqrt(float(params.num_candidates))))
+        cap = cap or max(gs * gs, 1)
+        out = np.empty((cap, 5), np.float64)
+        n = C.c_uint64()
+        self._check(self.lib.pcp_generate_candidates(self.h, _ptr(bb), C.byref(params), _ptr(zx),
+                                                     _ptr(out), cap, C.byref(n)),
+                    "pcp_generate_candidates")
+        return out[: n.value].copy()
+
+    def score_poses(self, poses5: np.ndarray, zx120_pose5, params: VlParams,
+                    cell_flags: np.ndarray):
+        """runOptimization scoring; cell_flags (uint8, n_cells) is updated in place."""
+        poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+        P = poses.shape[0]
+        zx = np.ascontiguousarray(zx120_pose5, np.float64)
+        assert cell_flags.dtype == np.uint8 and cell_flags.flags.c_contiguous
+        tot = np.empty(max(P, 1), np.float64)
+        cov = np.empty(max(P, 1), np.int32)
+        rep = VlReport()
+        self._check(self.lib.pcp_score_poses(self.h, _ptr(poses), P, _ptr(zx), C.byref(params),
+                                             _ptr(cell_flags), _ptr(tot), _ptr(cov),
+                                             C.byref(rep)), "pcp_score_poses")
+        return tot[:P].copy(), cov[:P].copy(), rep
+
+    def raycast_fan(self, poses5: np.ndarray, fan: FanParams, want_first_hit=False):
+        poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+        P = poses.shape[0]
+        blocked = np.zeros(max(P, 1), np.uint32)
+        units = np.zeros(max(P, 1), np.uint64)
+        fh = np.empty((P, fan.n_el, fan.n_az), np.int16) if want_first_hit else None
+        best = C.c_int64()
+        self._check(self.lib.pcp_raycast_fan(self.h, _ptr(poses), P, C.byref(fan), _ptr(blocked),
+                                             _ptr(units), _ptr(fh), C.byref(best)),
+                    "pcp_raycast_fan")
+        return blocked[:P].copy(), units[:P].copy(), fh, best.value
+
+
+def _fan_stats(self, poses5, fan):
+    poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+    st = np.zeros(3, np.uint64)
+    self._check(self.lib.pcp_raycast_fan_stats(self.h, _ptr(poses), poses.shape[0], C.byref(fan),
+                                               _ptr(st)), "pcp_raycast_fan_stats")
+    return {"samples_visited": int(st[0]), "occupied_stencils": int(st[1]),
+            "point_tests": int(st[2])}
+
+
+Context.raycast_fan_stats = _fan_stats
+
+
+def step_table(end: float) -> np.ndarray:
+    lib = load_library()
+    n = C.c_uint64()
+    lib.pcp_step_table(end, None, 0, C.byref(n))
+    out = np.empty(max(n.value, 1), np.float64)
+    lib.pcp_step_table(end, _ptr(out), n.value, C.byref(n))
+    return out[: n.value]
+
+
+def default_vl_params(**kw) -> VlParams:
+    """virtual_lidar.cpp:66-71 defaults."""
+    p = VlParams(0.1, 1.1, 3.0, 15.0, 100, 10)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def fan_params(n_az=1024, n_el=256, el_min_deg=-85.0, el_max_deg=85.0, max_distance=15.0):
+    return FanParams(n_az, n_el, el_min_deg * np.pi / 180.0, el_max_deg * np.pi / 180.0,
+                     max_distance)

@@ -1,0 +1,352 @@
+// pcp_context.hip -- context, errors, profiling, device helpers, prefix scan.
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+#include <new>
+
+#include "pcp_internal.hpp"
+
+namespace pcp {
+
+int set_err(pcp_ctx *ctx, int code, const char *fmt, ...) {
+    if (ctx) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        ctx->err = buf;
+    }
+    return code;
+}
+
+int hip_fail(pcp_ctx *ctx, hipError_t e, const char *what, const char *file, int line) {
+    const int code = (e == hipErrorOutOfMemory) ? PCP_E_NOMEM : PCP_E_HIP;
+    return set_err(ctx, code, "HIP error %d (%s) in %s at %s:%d", (int)e, hipGetErrorString(e),
+                   what, file, line);
+}
+
+int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what) {
+    if (!v) return set_err(ctx, PCP_E_INVALID, "%s: null cloud view", what);
+    if (v->n == 0) return PCP_OK;
+    if (!v->data) return set_err(ctx, PCP_E_INVALID, "%s: null data with n=%llu", what,
+                                 (unsigned long long)v->n);
+    if (v->point_step < 12 || (v->point_step & 3) || (v->off_x & 3) || (v->off_y & 3) ||
+        (v->off_z & 3) || v->off_x + 4 > v->point_step || v->off_y + 4 > v->point_step ||
+        v->off_z + 4 > v->point_step)
+        return set_err(ctx, PCP_E_INVALID,
+                       "%s: unsupported layout point_step=%u offsets=(%u,%u,%u) (FLOAT32 "
+                       "fields, 4-byte aligned)",
+                       what, v->point_step, v->off_x, v->off_y, v->off_z);
+    if (v->n > 0xFFFFFFF0ull) return set_err(ctx, PCP_E_INVALID, "%s: too many points", what);
+    return PCP_OK;
+}
+
+void fan_tables(int32_t n_az, int32_t n_el, double el_min, double el_max, double *ca, double *sa,
+                double *ce, double *se) {
+    // identical expression order to oracle/pcp_oracle.c:orc_fan_tables (glibc libm)
+    for (int32_t i = 0; i < n_az; ++i) {
+        const double a = 2.0 * kPi * (double)i / (double)n_az;
+        ca[i] = std::cos(a);
+        sa[i] = std::sin(a);
+    }
+    for (int32_t j = 0; j < n_el; ++j) {
+        const double e = el_min + (el_max - el_min) * ((double)j + 0.5) / (double)n_el;
+        ce[j] = std::cos(e);
+        se[j] = std::sin(e);
+    }
+}
+
+std::vector<double> step_table(double end) {
+    // virtual_lidar.cpp:765-796: step = 0.5; while (step < end) { ...; step += 0.3; }
+    std::vector<double> s;
+    double step = 0.5;   // repeated addition, not 0.5 + 0.3 k
+    while (step < end) {
+        s.push_back(step);
+        step = step + kRayStep;
+        if (s.size() > (1u << 24)) break;
+    }
+    return s;
+}
+
+// ---- profiling -------------------------------------------------------------------------
+static hipEvent_t take_event(pcp_ctx *ctx) {
+    if (!ctx->event_pool.empty()) {
+        hipEvent_t e = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+ProfScope::ProfScope(pcp_ctx *c, int k) : ctx(c), kid(k) {
+    if (!ctx->prof) return;
+    a = take_event(ctx);
+    b = take_event(ctx);
+    if (a) (void)hipEventRecord(a, ctx->stream);
+}
+
+ProfScope::~ProfScope() {
+    if (!ctx->prof || !a || !b) return;
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->pending.push_back({kid, a, b});
+}
+
+void prof_resolve(pcp_ctx *ctx) {
+    for (auto &pe : ctx->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+            ctx->slots[pe.kid].total_ms += ms;
+            ctx->slots[pe.kid].launches += 1;
+        }
+        ctx->event_pool.push_back(pe.a);
+        ctx->event_pool.push_back(pe.b);
+    }
+    ctx->pending.clear();
+}
+
+// ---- exclusive scan (uint32) ----------------------------------------------------------------
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanThreads * kScanItems;   // 2048
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// block-wide exclusive scan of one value per thread; returns exclusive prefix, *total
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds4, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) lds4[wid] = incl;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+        const uint32_t s = lds4[w];
+        if (w < wid) off += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + incl - v;
+}
+
+__global__ void __launch_bounds__(kScanThreads)
+k_scan_tile_sums(const uint32_t *__restrict__ in, uint64_t n, uint32_t *__restrict__ sums) {
+    __shared__ uint32_t lds4[4];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t k = base + (uint64_t)i * kScanThreads + threadIdx.x;
+        if (k < n) s += in[k];
+    }
+    uint32_t tot;
+    (void)block_excl_scan(s, lds4, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// scans each tile locally (thread owns kScanItems consecutive items), adds tile offset
+__global__ void __launch_bounds__(kScanThreads)
+k_scan_tiles(const uint32_t *__restrict__ in, uint64_t n, const uint32_t *__restrict__ offs,
+             uint32_t *__restrict__ out) {
+    __shared__ uint32_t lds4[4];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t k = base + i;
+        v[i] = (k < n) ? in[k] : 0u;
+        s += v[i];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan(s, lds4, &tot) + (offs ? offs[blockIdx.x] : 0u);
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t k = base + i;
+        if (k < n) out[k] = run;
+        run += v[i];
+    }
+    // out[n] written by the last tile's last thread
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = run;
+}
+
+size_t scan_tmp_bytes(uint64_t n) {
+    size_t bytes = 0;
+    while (n > (uint64_t)kScanTile) {
+        const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+        bytes += (tiles + 1) * 2 * sizeof(uint32_t) + 256;
+        n = tiles;
+    }
+    return bytes + 256;
+}
+
+int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp) {
+    if (n == 0) {
+        PCP_HIP(ctx, hipMemsetAsync(out, 0, sizeof(uint32_t), ctx->stream));
+        return PCP_OK;
+    }
+    const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+    if (tiles == 1) {
+        hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, ctx->stream, in, n,
+                           (const uint32_t *)nullptr, out);
+        PCP_CHECK_LAUNCH(ctx);
+        return PCP_OK;
+    }
+    uint32_t *sums = static_cast<uint32_t *>(tmp);
+    uint32_t *sums_scan = sums + tiles + 1;
+    void *next = reinterpret_cast<char *>(tmp) + (tiles + 1) * 2 * sizeof(uint32_t) + 256;
+    hipLaunchKernelGGL(k_scan_tile_sums, dim3((unsigned)tiles), dim3(kScanThreads), 0, ctx->stream,
+                       in, n, sums);
+    PCP_CHECK_LAUNCH(ctx);
+    int rc = exclusive_scan_u32(ctx, sums, sums_scan, tiles, next);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(kScanThreads), 0, ctx->stream, in,
+                       n, (const uint32_t *)sums_scan, out);
+    PCP_CHECK_LAUNCH(ctx);
+    return PCP_OK;
+}
+
+}  // namespace pcp
+
+using namespace pcp;
+
+// ======================================================================================
+// C ABI: context
+// ======================================================================================
+extern "C" {
+
+int pcp_abi_version(void) { return PCP_ABI_VERSION; }
+
+int pcp_device_count(int *n) {
+    if (!n) return PCP_E_INVALID;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return PCP_OK;
+}
+
+int pcp_create(int device, pcp_ctx **out) {
+    if (!out) return PCP_E_INVALID;
+    *out = nullptr;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess || c <= 0) return PCP_E_HIP;
+    if (device < 0 || device >= c) return PCP_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return PCP_E_HIP;
+    pcp_ctx *ctx = new (std::nothrow) pcp_ctx();
+    if (!ctx) return PCP_E_NOMEM;
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return PCP_E_HIP;
+    }
+    *out = ctx;
+    return PCP_OK;
+}
+
+void pcp_destroy(pcp_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    prof_resolve(ctx);
+    for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    ctx->terrain.release();
+    ctx->aux.release();
+    DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage,  &ctx->fan_tab, &ctx->poses_d,
+                      &ctx->steps_d,   &ctx->out_a,     &ctx->out_b,  &ctx->out_c,   &ctx->out_d,
+                      &ctx->stats_d,   &ctx->f_in,      &ctx->f_xyz,  &ctx->f_idx,   &ctx->f_keys[0],
+                      &ctx->f_keys[1], &ctx->f_vals[0], &ctx->f_vals[1], &ctx->f_hist, &ctx->f_out,
+                      &ctx->f_misc};
+    for (DevBuf *b : bufs) b->release();
+    for (auto &b : ctx->scratch) b.release();
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *pcp_last_error(const pcp_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pcp_synchronize(pcp_ctx *ctx) {
+    if (!ctx) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    prof_resolve(ctx);
+    return PCP_OK;
+}
+
+int pcp_dev_alloc(pcp_ctx *ctx, uint64_t bytes, void **dptr) {
+    if (!ctx || !dptr) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    PCP_HIP(ctx, hipMalloc(dptr, bytes ? bytes : 16));
+    return PCP_OK;
+}
+
+int pcp_dev_free(pcp_ctx *ctx, void *dptr) {
+    if (!ctx) return PCP_E_INVALID;
+    if (dptr) PCP_HIP(ctx, hipFree(dptr));
+    return PCP_OK;
+}
+
+int pcp_memcpy_h2d(pcp_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
+    if (!ctx || (bytes && (!dst || !src))) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return PCP_OK;
+}
+
+int pcp_memcpy_d2h(pcp_ctx *ctx, void *dst, const void *src, uint64_t bytes) {
+    if (!ctx || (bytes && (!dst || !src))) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return PCP_OK;
+}
+
+int pcp_profile_enable(pcp_ctx *ctx, int enable) {
+    if (!ctx) return PCP_E_INVALID;
+    ctx->prof = enable != 0;
+    return PCP_OK;
+}
+
+int pcp_profile_reset(pcp_ctx *ctx) {
+    if (!ctx) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    prof_resolve(ctx);
+    for (auto &s : ctx->slots) s = ProfSlot{};
+    return PCP_OK;
+}
+
+int pcp_profile_get(pcp_ctx *ctx, int kid, double *total_ms, uint64_t *launches) {
+    if (!ctx || kid < 0 || kid >= PCP_K_COUNT) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    prof_resolve(ctx);
+    if (total_ms) *total_ms = ctx->slots[kid].total_ms;
+    if (launches) *launches = ctx->slots[kid].launches;
+    return PCP_OK;
+}
+
+const char *pcp_kernel_name(int kid) {
+    static const char *names[PCP_K_COUNT] = {"raycast_fan", "score_cells", "zx120_cells",
+                                             "pose_sum",    "cell_flags",  "candidates",
+                                             "index_build", "crop",        "voxel",
+                                             "transform"};
+    if (kid < 0 || kid >= PCP_K_COUNT) return "unknown";
+    return names[kid];
+}
+
+int pcp_step_table(double end, double *steps, uint64_t cap, uint64_t *n) {
+    if (!n || (cap && !steps)) return PCP_E_INVALID;
+    std::vector<double> s = step_table(end);
+    *n = s.size();
+    for (uint64_t i = 0; i < s.size() && i < cap; ++i) steps[i] = s[i];
+    return PCP_OK;
+}
+
+}  // extern "C"

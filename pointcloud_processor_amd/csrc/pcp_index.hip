@@ -1,0 +1,332 @@
+// pcp_index.hip -- uniform-grid spatial index build (replaces KdTreeFLANN::setInputCloud,
+// virtual_lidar.cpp:172,187,201).  Layout in HBM (see DESIGN.md "Terrain index"):
+//   pts   : float4[n]   x, y, z, bitcast(original point index), sorted by cell
+//   start : u32[ncell+1] prefix offsets (cell c holds pts[start[c] .. start[c+1]) )
+//   occ2  : u32[(ncell+31)/32] dilated occupancy (bit c = any point in cells c + {0,1}^3)
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "pcp_internal.hpp"
+
+namespace pcp {
+
+constexpr uint64_t kMaxCells = 1ull << 25;
+constexpr int kThreads = 256;
+
+GridView GridIndex::view() const {
+    GridView v{};
+    v.pts = pts.as<const float4>();
+    v.start = start.as<const uint32_t>();
+    v.occ2 = occ2.as<const uint32_t>();
+    v.c = c;
+    v.inv_c = c > 0 ? 1.0 / c : 0.0;
+    v.ox = bmin[0] - c;   // one padding cell below the points
+    v.oy = bmin[1] - c;
+    v.oz = bmin[2] - c;
+    const double rm = r_q + kQueryMargin;
+    // the clip box also absorbs the float rounding of a sample position near the points
+    double amax = 0.0;
+    for (int a = 0; a < 3; ++a) amax = fmax(amax, fmax(fabs(bmin[a]), fabs(bmax[a])));
+    const double rb = rm + 1e-6 * amax;
+    v.lo_x = v.ox + rm;
+    v.lo_y = v.oy + rm;
+    v.lo_z = v.oz + rm;
+    v.nx = nx;
+    v.ny = ny;
+    v.nz = nz;
+    v.n_pts = (uint32_t)n_pts;
+    v.bx0 = bmin[0] - rb;
+    v.bx1 = bmax[0] + rb;
+    v.by0 = bmin[1] - rb;
+    v.by1 = bmax[1] + rb;
+    v.bz0 = bmin[2] - rb;
+    v.bz1 = bmax[2] + rb;
+    return v;
+}
+
+__device__ __forceinline__ float ld_f32(const unsigned char *base, uint32_t off) {
+    return *reinterpret_cast<const float *>(base + off);
+}
+
+// extract x,y,z (4-byte aligned FLOAT32 fields) to float4 + per-block bbox of finite pts
+__global__ void __launch_bounds__(kThreads)
+k_extract(const unsigned char *__restrict__ raw, uint64_t n, uint32_t step, uint32_t ox,
+          uint32_t oy, uint32_t oz, float4 *__restrict__ xyz, float *__restrict__ part,
+          uint32_t *__restrict__ part_n) {
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    uint32_t cnt = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kThreads) {
+        const unsigned char *p = raw + i * step;
+        const float x = ld_f32(p, ox), y = ld_f32(p, oy), z = ld_f32(p, oz);
+        const bool fin = isfinite(x) && isfinite(y) && isfinite(z);
+        xyz[i] = make_float4(x, y, z, __uint_as_float(fin ? (uint32_t)i : 0xFFFFFFFFu));
+        if (fin) {
+            ++cnt;
+            mn[0] = fminf(mn[0], x); mx[0] = fmaxf(mx[0], x);
+            mn[1] = fminf(mn[1], y); mx[1] = fmaxf(mx[1], y);
+            mn[2] = fminf(mn[2], z); mx[2] = fmaxf(mx[2], z);
+        }
+    }
+    // wave reduce then block reduce through LDS
+    __shared__ float s[6][kThreads / 64];
+    __shared__ uint32_t sc[kThreads / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+        }
+        cnt += __shfl_xor(cnt, o, 64);
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) {
+        for (int a = 0; a < 3; ++a) { s[a][w] = mn[a]; s[3 + a][w] = mx[a]; }
+        sc[w] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int ww = 1; ww < kThreads / 64; ++ww) {
+            for (int a = 0; a < 3; ++a) {
+                s[a][0] = fminf(s[a][0], s[a][ww]);
+                s[3 + a][0] = fmaxf(s[3 + a][0], s[3 + a][ww]);
+            }
+            sc[0] += sc[ww];
+        }
+        for (int a = 0; a < 6; ++a) part[blockIdx.x * 6 + a] = s[a][0];
+        part_n[blockIdx.x] = sc[0];
+    }
+}
+
+__global__ void k_bbox_final(const float *__restrict__ part, const uint32_t *__restrict__ part_n,
+                             int nb, float *__restrict__ out, uint32_t *__restrict__ out_n) {
+    if (threadIdx.x != 0) return;
+    float r[6] = {FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
+    uint32_t c = 0;
+    for (int b = 0; b < nb; ++b) {
+        for (int a = 0; a < 3; ++a) {
+            r[a] = fminf(r[a], part[b * 6 + a]);
+            r[3 + a] = fmaxf(r[3 + a], part[b * 6 + 3 + a]);
+        }
+        c += part_n[b];
+    }
+    for (int a = 0; a < 6; ++a) out[a] = r[a];
+    *out_n = c;
+}
+
+struct CellMap {
+    double ox, oy, oz, inv_c;
+    int32_t nx, ny, nz;
+};
+
+__device__ __forceinline__ uint32_t cell_of(const CellMap &m, float x, float y, float z) {
+    int ix = (int)floor(((double)x - m.ox) * m.inv_c);
+    int iy = (int)floor(((double)y - m.oy) * m.inv_c);
+    int iz = (int)floor(((double)z - m.oz) * m.inv_c);
+    // points lie in [1, n-2] by construction; clamp defensively
+    ix = min(max(ix, 0), m.nx - 1);
+    iy = min(max(iy, 0), m.ny - 1);
+    iz = min(max(iz, 0), m.nz - 1);
+    return (uint32_t)ix + (uint32_t)m.nx * ((uint32_t)iy + (uint32_t)m.ny * (uint32_t)iz);
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_cell_count(const float4 *__restrict__ xyz, uint64_t n, CellMap m, uint32_t *__restrict__ cid,
+             uint32_t *__restrict__ count) {
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = xyz[i];
+    if (__float_as_uint(p.w) == 0xFFFFFFFFu) {
+        cid[i] = 0xFFFFFFFFu;
+        return;
+    }
+    const uint32_t c = cell_of(m, p.x, p.y, p.z);
+    cid[i] = c;
+    atomicAdd(&count[c], 1u);
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_cell_scatter(const float4 *__restrict__ xyz, uint64_t n, const uint32_t *__restrict__ cid,
+               uint32_t *__restrict__ cursor, float4 *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = cid[i];
+    if (c == 0xFFFFFFFFu) return;
+    const uint32_t pos = atomicAdd(&cursor[c], 1u);
+    out[pos] = xyz[i];
+}
+
+// dilated occupancy: bit for lower corner (ix,iy,iz) = any point in the 2x2x2 block
+__global__ void __launch_bounds__(kThreads)
+k_occ2(const uint32_t *__restrict__ start, CellMap m, uint64_t ncell, uint32_t *__restrict__ occ2) {
+    const uint64_t w = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    const uint64_t nw = (ncell + 31) / 32;
+    if (w >= nw) return;
+    uint32_t bits = 0;
+    const uint64_t sxy = (uint64_t)m.nx * m.ny;
+    for (int b = 0; b < 32; ++b) {
+        const uint64_t c = w * 32 + b;
+        if (c >= ncell) break;
+        const int ix = (int)(c % m.nx);
+        const int iy = (int)((c / m.nx) % m.ny);
+        const int iz = (int)(c / sxy);
+        bool any = false;
+        for (int dz = 0; dz < 2 && !any; ++dz)
+            for (int dy = 0; dy < 2 && !any; ++dy) {
+                const int y = iy + dy, z = iz + dz;
+                if (y >= m.ny || z >= m.nz) continue;
+                const uint64_t row = (uint64_t)m.nx * ((uint64_t)y + (uint64_t)m.ny * z);
+                const int x1 = min(ix + 2, m.nx);
+                if (start[row + x1] > start[row + ix]) any = true;
+            }
+        if (any) bits |= 1u << b;
+    }
+    occ2[w] = bits;
+}
+
+int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q) {
+    const uint64_t n = v.n;
+    hipStream_t st = ctx->stream;
+    ProfScope prof(ctx, PCP_K_INDEX_BUILD);
+    // 1. stage the raw AoS bytes (the PointCloud2 data blob)
+    const uint64_t raw_bytes = n * (uint64_t)v.point_step;
+    PCP_HIP(ctx, ctx->stage.ensure(raw_bytes));
+    PCP_HIP(ctx, hipMemcpyAsync(ctx->stage.p, v.data, raw_bytes, hipMemcpyHostToDevice, st));
+    // 2. extract + bbox
+    const int nb = (int)std::min<uint64_t>((n + kThreads - 1) / kThreads, 1024);
+    PCP_HIP(ctx, ctx->scratch[0].ensure(n * sizeof(float4)));
+    PCP_HIP(ctx, ctx->scratch[1].ensure((size_t)nb * 6 * sizeof(float) + 64 + nb * 4));
+    PCP_HIP(ctx, ctx->stats_d.ensure(64));
+    float *part = ctx->scratch[1].as<float>();
+    uint32_t *part_n = reinterpret_cast<uint32_t *>(part + nb * 6);
+    hipLaunchKernelGGL(k_extract, dim3(nb), dim3(kThreads), 0, st, ctx->stage.as<unsigned char>(),
+                       n, v.point_step, v.off_x, v.off_y, v.off_z, ctx->scratch[0].as<float4>(),
+                       part, part_n);
+    PCP_CHECK_LAUNCH(ctx);
+    float *bb_d = ctx->stats_d.as<float>();
+    hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, st, part, part_n, nb, bb_d,
+                       reinterpret_cast<uint32_t *>(bb_d + 8));
+    PCP_CHECK_LAUNCH(ctx);
+    float bb_h[10];
+    PCP_HIP(ctx, hipMemcpyAsync(bb_h, bb_d, sizeof(bb_h), hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    uint32_t nfin;
+    memcpy(&nfin, &bb_h[8], 4);
+    g.present = true;
+    g.r_q = r_q;
+    g.n_pts = nfin;
+    if (nfin == 0) {   // a tree over zero valid points: never returns neighbours
+        g.c = 1.0;
+        g.nx = g.ny = g.nz = 1;
+        for (int a = 0; a < 3; ++a) g.bmin[a] = g.bmax[a] = 0.0;
+        PCP_HIP(ctx, g.pts.ensure(16));
+        PCP_HIP(ctx, g.start.ensure(16));
+        PCP_HIP(ctx, g.occ2.ensure(16));
+        PCP_HIP(ctx, hipMemsetAsync(g.start.p, 0, 16, st));
+        PCP_HIP(ctx, hipMemsetAsync(g.occ2.p, 0, 16, st));
+        return PCP_OK;
+    }
+    for (int a = 0; a < 3; ++a) {
+        g.bmin[a] = bb_h[a];
+        g.bmax[a] = bb_h[3 + a];
+    }
+    // 3. grid geometry: edge c > 2 (r_q + margin) so a query box spans <= 2 cells per axis
+    double c = 2.0 * (r_q + kCellMargin);
+    uint64_t ncell = 0;
+    for (;;) {
+        int64_t d[3];
+        for (int a = 0; a < 3; ++a)
+            d[a] = (int64_t)std::floor((g.bmax[a] - (g.bmin[a] - c)) / c) + 2;
+        ncell = (uint64_t)d[0] * (uint64_t)d[1] * (uint64_t)d[2];
+        if (ncell <= kMaxCells && d[0] < (1 << 30) && d[1] < (1 << 30) && d[2] < (1 << 30)) {
+            g.nx = (int32_t)d[0];
+            g.ny = (int32_t)d[1];
+            g.nz = (int32_t)d[2];
+            break;
+        }
+        c *= 1.25;
+    }
+    g.c = c;
+    const GridView gv = g.view();
+    CellMap m{gv.ox, gv.oy, gv.oz, gv.inv_c, g.nx, g.ny, g.nz};
+    // 4. count per cell
+    PCP_HIP(ctx, ctx->scratch[2].ensure(n * sizeof(uint32_t)));
+    PCP_HIP(ctx, ctx->scratch[3].ensure((ncell + 1) * sizeof(uint32_t)));
+    PCP_HIP(ctx, hipMemsetAsync(ctx->scratch[3].p, 0, (ncell + 1) * sizeof(uint32_t), st));
+    const unsigned gridn = (unsigned)((n + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(k_cell_count, dim3(gridn), dim3(kThreads), 0, st,
+                       ctx->scratch[0].as<const float4>(), n, m, ctx->scratch[2].as<uint32_t>(),
+                       ctx->scratch[3].as<uint32_t>());
+    PCP_CHECK_LAUNCH(ctx);
+    // 5. prefix -> start
+    PCP_HIP(ctx, g.start.ensure((ncell + 1) * sizeof(uint32_t)));
+    PCP_HIP(ctx, ctx->scratch[4].ensure(scan_tmp_bytes(ncell) + (ncell + 1) * sizeof(uint32_t)));
+    int rc = exclusive_scan_u32(ctx, ctx->scratch[3].as<const uint32_t>(), g.start.as<uint32_t>(),
+                                ncell, ctx->scratch[4].p);
+    if (rc) return rc;
+    // 6. scatter (cursor = copy of start)
+    PCP_HIP(ctx, hipMemcpyAsync(ctx->scratch[3].p, g.start.p, ncell * sizeof(uint32_t),
+                                hipMemcpyDeviceToDevice, st));
+    PCP_HIP(ctx, g.pts.ensure((size_t)nfin * sizeof(float4)));
+    hipLaunchKernelGGL(k_cell_scatter, dim3(gridn), dim3(kThreads), 0, st,
+                       ctx->scratch[0].as<const float4>(), n, ctx->scratch[2].as<const uint32_t>(),
+                       ctx->scratch[3].as<uint32_t>(), g.pts.as<float4>());
+    PCP_CHECK_LAUNCH(ctx);
+    // 7. dilated occupancy
+    const uint64_t nw = (ncell + 31) / 32;
+    PCP_HIP(ctx, g.occ2.ensure(nw * sizeof(uint32_t)));
+    hipLaunchKernelGGL(k_occ2, dim3((unsigned)((nw + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                       st, g.start.as<const uint32_t>(), m, ncell, g.occ2.as<uint32_t>());
+    PCP_CHECK_LAUNCH(ctx);
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    return PCP_OK;
+}
+
+}  // namespace pcp
+
+using namespace pcp;
+
+extern "C" {
+
+int pcp_set_terrain(pcp_ctx *ctx, const pcp_cloud_view *terrain) {
+    if (!ctx) return PCP_E_INVALID;
+    int rc = check_view(ctx, terrain, "pcp_set_terrain");
+    if (rc) return rc;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    ctx->terrain_cloud_n = terrain->n;
+    if (terrain->n == 0) return PCP_OK;   // terrainCallback: no rebuild on an empty cloud
+    rc = build_index(ctx, ctx->terrain, *terrain, kRayRadius);
+    prof_resolve(ctx);
+    return rc;
+}
+
+int pcp_set_aux_cloud(pcp_ctx *ctx, const pcp_cloud_view *aux) {
+    if (!ctx) return PCP_E_INVALID;
+    int rc = check_view(ctx, aux, "pcp_set_aux_cloud");
+    if (rc) return rc;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    ctx->aux_cloud_n = aux->n;
+    if (aux->n == 0) return PCP_OK;
+    rc = build_index(ctx, ctx->aux, *aux, kRelaxedRadius);
+    prof_resolve(ctx);
+    return rc;
+}
+
+int pcp_terrain_info(pcp_ctx *ctx, pcp_index_info *info) {
+    if (!ctx || !info) return PCP_E_INVALID;
+    const GridIndex &g = ctx->terrain;
+    info->n_points = g.n_pts;
+    info->cell = g.c;
+    info->nx = g.nx;
+    info->ny = g.ny;
+    info->nz = g.nz;
+    for (int a = 0; a < 3; ++a) {
+        info->bmin[a] = g.bmin[a];
+        info->bmax[a] = g.bmax[a];
+    }
+    return PCP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,173 @@
+// pcp_internal.hpp -- shared host/device declarations of libpcp (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "pcp_abi.h"
+
+namespace pcp {
+
+// ---------------------------------------------------------------------------------------
+// reference constants (virtual_lidar.cpp:100-114)
+// ---------------------------------------------------------------------------------------
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kMinDistance = 0.5;
+constexpr double kRayStep = 0.3;
+constexpr double kVisRadius = 0.08;
+constexpr double kRayRadius = kVisRadius * 0.7;     // radiusSearch radius at :782
+constexpr double kRelaxedRadius = kVisRadius * 3.0; // :743
+constexpr double kMinElevation = -85.0 * kPi / 180.0;
+constexpr double kMaxElevation = 85.0 * kPi / 180.0;
+constexpr double kCellMargin = 4e-3;   // conservative margin of the stencil
+constexpr double kQueryMargin = 1e-3;
+
+// ---------------------------------------------------------------------------------------
+// device buffer (grow-only)
+// ---------------------------------------------------------------------------------------
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes < 256 ? 256 : bytes;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+// ---------------------------------------------------------------------------------------
+// Uniform-grid spatial index (replaces pcl::KdTreeFLANN).  Points sorted by cell, cell
+// start offsets (prefix sum, ncell+1 entries), and a dilated occupancy bitmask: bit of
+// cell c = any point in the 2x2x2 block whose lower corner is c.  Cells are padded by one
+// on every side so that a stencil whose lower corner falls outside [0, n-2] is provably
+// empty.  See DESIGN.md "Terrain index".
+// ---------------------------------------------------------------------------------------
+struct GridView {               // POD passed to kernels by value
+    const float4 *pts;          // x, y, z, bitcast(original index)
+    const uint32_t *start;      // ncell + 1
+    const uint32_t *occ2;       // dilated occupancy bits, (ncell + 31) / 32 words
+    double ox, oy, oz;          // origin (lower corner of cell 0)
+    double inv_c, c;
+    double lo_x, lo_y, lo_z;    // origin + r_q + margin (stencil lower corner offset)
+    int32_t nx, ny, nz;
+    uint32_t n_pts;
+    // tight bbox of the points, inflated by r_q + margin: samples outside are empty
+    double bx0, bx1, by0, by1, bz0, bz1;
+};
+
+struct GridIndex {
+    bool present = false;        // a tree exists (KdTreeFLANN::Ptr non-null)
+    uint64_t n_pts = 0;
+    double r_q = 0.0;            // stencil radius the cell edge was sized for
+    double c = 0.0;
+    int32_t nx = 0, ny = 0, nz = 0;
+    double bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
+    DevBuf pts, start, occ2;
+    GridView view() const;
+    void release() {
+        pts.release();
+        start.release();
+        occ2.release();
+        present = false;
+        n_pts = 0;
+    }
+};
+
+// ---------------------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------------------
+struct ProfSlot {
+    double total_ms = 0.0;
+    uint64_t launches = 0;
+};
+
+struct PendingEvent {
+    int kid;
+    hipEvent_t a, b;
+};
+
+}  // namespace pcp
+
+struct pcp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // virtual_lidar state
+    pcp::GridIndex terrain;      // raycast index (r_q = 0.056)
+    uint64_t terrain_cloud_n = 0;  // current terrain cloud size (stale-tree semantics)
+    pcp::GridIndex aux;          // zx120 cloud index (r_q = 0.24)
+    uint64_t aux_cloud_n = 0;
+    uint64_t n_cells = 0;
+    pcp::DevBuf cells_xyz, cells_nrm;
+    // scratch
+    pcp::DevBuf stage, scratch[8];
+    pcp::DevBuf fan_tab, poses_d, steps_d, out_a, out_b, out_c, out_d, stats_d;
+    int32_t fan_naz = -1, fan_nel = -1;      // cached fan direction tables
+    double fan_elmin = 0.0, fan_elmax = 0.0;
+    double steps_end = -1e300;               // cached step table
+    int steps_K = 0;
+    // filter/merge scratch
+    pcp::DevBuf f_in, f_xyz, f_idx, f_keys[2], f_vals[2], f_hist, f_out, f_misc;
+    // profiling
+    bool prof = false;
+    pcp::ProfSlot slots[PCP_K_COUNT];
+    std::vector<pcp::PendingEvent> pending;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace pcp {
+
+// error helpers --------------------------------------------------------------------------
+int set_err(pcp_ctx *ctx, int code, const char *fmt, ...);
+int hip_fail(pcp_ctx *ctx, hipError_t e, const char *what, const char *file, int line);
+
+#define PCP_HIP(ctx, expr)                                                       \
+    do {                                                                         \
+        hipError_t _e = (expr);                                                  \
+        if (_e != hipSuccess) return ::pcp::hip_fail((ctx), _e, #expr, __FILE__, __LINE__); \
+    } while (0)
+
+#define PCP_CHECK_LAUNCH(ctx) PCP_HIP(ctx, hipGetLastError())
+
+// profiling: bracket launches on ctx->stream
+struct ProfScope {
+    pcp_ctx *ctx;
+    int kid;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(pcp_ctx *c, int k);
+    ~ProfScope();
+};
+void prof_resolve(pcp_ctx *ctx);   // after a stream sync
+
+// index ----------------------------------------------------------------------------------
+int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q);
+
+// scan: exclusive prefix sum of n uint32 values into out (n + 1 entries, out[n] = total).
+// tmp must hold scan_tmp_bytes(n).
+size_t scan_tmp_bytes(uint64_t n);
+int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp);
+
+// validate a cloud view
+int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what);
+
+// fan tables (shared definition with the oracle's orc_fan_tables)
+void fan_tables(int32_t n_az, int32_t n_el, double el_min, double el_max, double *ca,
+                double *sa, double *ce, double *se);
+std::vector<double> step_table(double end);
+
+}  // namespace pcp

@@ -1,0 +1,807 @@
+// pcp_vlidar.hip -- virtual_lidar.cpp hot path on gfx950: candidate generation, per
+// (pose, cell) visibility scoring, and the dense ray-fan occlusion march.
+//
+// Numerics: compiled with -ffp-contract=off (no FMA) so every double/float operation
+// rounds exactly as the reference's SSE2 build.  The radius predicate restates FLANN's
+// L2_Simple<float> (x, y, z accumulated in order, strict '<' against float(r*r)).
+#pragma clang fp contract(off)
+
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "pcp_internal.hpp"
+
+namespace pcp {
+
+constexpr int kT = 256;
+
+// ---------------------------------------------------------------------------------------
+// FLANN L2_Simple<float>: result += diff*diff over x, y, z; returned iff result < r2
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool flann_within(float qx, float qy, float qz, const float4 &p,
+                                             float r2) {
+    const float d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
+    float acc = 0.0f;
+    acc = acc + d0 * d0;
+    acc = acc + d1 * d1;
+    acc = acc + d2 * d2;
+    return acc < r2;
+}
+
+// KdTreeFLANN::radiusSearch(q, r) > 0 for r <= the index's stencil radius.  2x2x2 cell
+// stencil anchored at the cell of (q - r - margin); cells along x are contiguous in the
+// sorted point array, so the stencil is 4 ranges.  STATS counts occupied stencils and point
+// tests (diagnostic build of the roofline's algorithmic bytes; never in timed runs).
+template <bool STATS>
+__device__ __forceinline__ bool stencil_any_t(const GridView &g, float qx, float qy, float qz,
+                                              float r2, uint32_t *cnt) {
+    const double fx = ((double)qx - g.lo_x) * g.inv_c;
+    const double fy = ((double)qy - g.lo_y) * g.inv_c;
+    const double fz = ((double)qz - g.lo_z) * g.inv_c;
+    if (!(fx >= 0.0 && fx < (double)(g.nx - 1) && fy >= 0.0 && fy < (double)(g.ny - 1) &&
+          fz >= 0.0 && fz < (double)(g.nz - 1)))
+        return false;   // stencil touches only padding / outside cells: provably empty
+    const uint32_t nx = (uint32_t)g.nx, nxy = nx * (uint32_t)g.ny;
+    const uint32_t lin = (uint32_t)fx + nx * (uint32_t)fy + nxy * (uint32_t)fz;
+    if (!((__ldg(&g.occ2[lin >> 5]) >> (lin & 31)) & 1u)) return false;
+    if (STATS) cnt[1] += 1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t row = lin + (r & 1) * nx + (r >> 1) * nxy;
+        const uint32_t s = g.start[row], e = g.start[row + 2];
+        for (uint32_t k = s; k < e; ++k) {
+            if (STATS) cnt[2] += 1;
+            if (flann_within(qx, qy, qz, g.pts[k], r2)) return true;
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ bool stencil_any(const GridView &g, float qx, float qy, float qz,
+                                            float r2) {
+    return stencil_any_t<false>(g, qx, qy, qz, r2, nullptr);
+}
+
+// sample index range [klo, khi] whose positions can lie in the index's clip box
+__device__ __forceinline__ void clip_k(const GridView &g, double px, double py, double pz,
+                                       double dx, double dy, double dz, int K, int &klo,
+                                       int &khi) {
+    double t0 = 0.0, t1 = 1e300;
+    const double p[3] = {px, py, pz}, d[3] = {dx, dy, dz};
+    const double lo[3] = {g.bx0, g.by0, g.bz0}, hi[3] = {g.bx1, g.by1, g.bz1};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (d[a] == 0.0) {
+            if (p[a] < lo[a] || p[a] > hi[a]) t1 = -1.0;
+        } else {
+            const double ta = (lo[a] - p[a]) / d[a], tb = (hi[a] - p[a]) / d[a];
+            t0 = fmax(t0, fmin(ta, tb));
+            t1 = fmin(t1, fmax(ta, tb));
+        }
+    }
+    if (!(t0 <= t1)) {
+        klo = 0;
+        khi = -1;
+        return;
+    }
+    // s_k = 0.5 + 0.3 k up to ~1e-13; widen by one sample each side
+    const double kl = ceil((t0 - 0.5) / kRayStep) - 1.0;
+    const double kh = floor((t1 - 0.5) / kRayStep) + 1.0;
+    klo = (int)fmin(fmax(kl, 0.0), (double)K);
+    khi = (int)fmin(fmax(kh, -1.0), (double)(K - 1));
+}
+
+// checkVisibilityWithRaycasting's march (virtual_lidar.cpp:765-797) from pos along unit dir.
+// Visits samples k (s_k from the repeated-addition table) with s_k < end; returns the first
+// blocked k or -1.  Samples outside the clip box have no point within r (skipped exactly).
+template <bool STATS>
+__device__ __forceinline__ int march_t(const GridView &g, double px, double py, double pz,
+                                       double dx, double dy, double dz,
+                                       const double *__restrict__ steps, int K, double end,
+                                       float r2, uint32_t *cnt) {
+    int klo, khi;
+    clip_k(g, px, py, pz, dx, dy, dz, K, klo, khi);
+    for (int k = klo; k <= khi; ++k) {
+        const double s = steps[k];
+        if (!(s < end)) break;
+        if (STATS) cnt[0] += 1;
+        const float qx = (float)(px + dx * s);
+        const float qy = (float)(py + dy * s);
+        const float qz = (float)(pz + dz * s);
+        if (stencil_any_t<STATS>(g, qx, qy, qz, r2, cnt)) return k;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ int march(const GridView &g, double px, double py, double pz, double dx,
+                                     double dy, double dz, const double *__restrict__ steps, int K,
+                                     double end, float r2) {
+    return march_t<false>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, nullptr);
+}
+
+// ---------------------------------------------------------------------------------------
+// cell scoring (evaluateCellScore, virtual_lidar.cpp:656-714)
+// ---------------------------------------------------------------------------------------
+struct VisEnv {
+    GridView terrain;
+    GridView aux;
+    int terrain_present;   // terrain_kdtree_ non-null
+    int aux_present;       // zx120 tree non-null and cloud non-empty
+    double max_distance;
+    const double *steps;
+    int K;
+    float r2_ray, r2_relaxed;
+};
+
+// result bits: 1 = in_range, 2 = in_fov (valid if in_range), 4 = visible (valid if both)
+__device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double py, double pz,
+                                            double pitch, double cx, double cy, double cz,
+                                            float nx, float ny, float nz, bool is_zx120,
+                                            uint32_t &bits) {
+    const double dx = cx - px, dy = cy - py, dz = cz - pz;
+    const double L = sqrt(dx * dx + dy * dy + dz * dz);
+    bits = 0;
+    const bool in_range = (L >= kMinDistance && L <= E.max_distance);
+    if (!in_range) return 0.0;
+    bits |= 1u;
+    const double elevation = atan2(dz, sqrt(dx * dx + dy * dy));
+    const double elevation_diff = elevation - pitch;
+    const double fov_local = 180.0 * kPi / 180.0;
+    if (!(fabs(elevation_diff) <= fov_local / 2.0)) return 0.0;
+    bits |= 2u;
+    bool visible;
+    const double ndx = dx / L, ndy = dy / L, ndz = dz / L;
+    const double end = L - kVisRadius;
+    if (is_zx120 && E.aux_present &&
+        stencil_any(E.aux, (float)cx, (float)cy, (float)cz, E.r2_relaxed)) {
+        visible = true;   // checkVisibilityWithPointCloudRelaxed (:745-747)
+    } else if (!E.terrain_present) {
+        visible = true;   // (:721, :727, :750)
+    } else {
+        visible = march(E.terrain, px, py, pz, ndx, ndy, ndz, E.steps, E.K, end, E.r2_ray) < 0;
+    }
+    if (!visible) return 0.0;
+    bits |= 4u;
+    const double dot = ndx * (double)nx + ndy * (double)ny + ndz * (double)nz;
+    const double theta = acos(fmax(0.0, fmin(1.0, fabs(dot))));
+    const double score = 1.0 * sin(kPi / 2 - theta) + 1.0 * (1.0 / L);
+    return fmax(0.0, score);
+}
+
+__global__ void __launch_bounds__(kT)
+k_zx120_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict__ cn, int C,
+              double zx, double zy, double zz, double zpitch, double *__restrict__ score_z,
+              uint8_t *__restrict__ zbits) {
+    const int c = blockIdx.x * kT + threadIdx.x;
+    if (c >= C) return;
+    uint32_t bits;
+    const double s = eval_cell(E, zx, zy, zz, zpitch, cxyz[3 * c], cxyz[3 * c + 1], cxyz[3 * c + 2],
+                               cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], true, bits);
+    score_z[c] = s;
+    zbits[c] = (uint8_t)bits;
+}
+
+// one thread per (cell c, pose p); comb/mbits laid out [p][c] (coalesced writes)
+__global__ void __launch_bounds__(kT)
+k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict__ cn, int C,
+              const double *__restrict__ poses5, const double *__restrict__ score_z,
+              double *__restrict__ comb, uint8_t *__restrict__ mbits) {
+    const int c = blockIdx.x * kT + threadIdx.x;
+    const int p = blockIdx.y;
+    if (c >= C) return;
+    const double *P = poses5 + 5 * (size_t)p;
+    uint32_t bits;
+    const double sm = eval_cell(E, P[0], P[1], P[2], P[3], cxyz[3 * c], cxyz[3 * c + 1],
+                                cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], false, bits);
+    const double sz = score_z[c];
+    comb[(size_t)p * C + c] = (sz < sm) ? sm : sz;   // std::max(score_zx120, score_mobile)
+    mbits[(size_t)p * C + c] = (uint8_t)bits;
+}
+
+// ordered sequential sum per row (evaluatePosition :634-645): one wave per row, every lane
+// carries the same running sum so the addition order is exactly the cell order.
+__global__ void __launch_bounds__(kT)
+k_row_sum(const double *__restrict__ rows, int C, int R, double *__restrict__ total,
+          int32_t *__restrict__ covered) {
+    const int r = blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= R) return;
+    const double *row = rows + (size_t)r * C;
+    double acc = 0.0;
+    int32_t cov = 0;
+    for (int base = 0; base < C; base += 64) {
+        const double v = (base + lane < C) ? row[base + lane] : 0.0;
+        const int m = min(64, C - base);
+        for (int j = 0; j < m; ++j) {
+            const double x = __shfl(v, j, 64);
+            if (x > 0) {
+                acc += x;
+                ++cov;
+            }
+        }
+    }
+    if (lane == 0) {
+        total[r] = acc;
+        covered[r] = cov;
+    }
+}
+
+// stats slots
+enum {
+    S_TOTAL = 0, S_ZR, S_ZF, S_ZV, S_ZG, S_ZRED, S_ZB, S_ZY, S_G, S_RED, S_B, S_Y, S_N
+};
+
+// stale-flag resolution (virtual_lidar.cpp:487-501 read flags written by the LAST
+// evaluation that reached each assignment, :662-687) + colour statistics
+__global__ void __launch_bounds__(kT)
+k_cell_flags(const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbits, int C, int P,
+             uint8_t *__restrict__ flags, int32_t *__restrict__ stats) {
+    const int c = blockIdx.x * kT + threadIdx.x;
+    if (c >= C) return;
+    uint32_t f = flags[c];
+    const uint32_t z = zbits[c];
+    f = (z & 1u) ? (f | PCP_F_RANGE_Z) : (f & ~PCP_F_RANGE_Z);
+    if (z & 1u) f = (z & 2u) ? (f | PCP_F_FOV_Z) : (f & ~PCP_F_FOV_Z);
+    if ((z & 3u) == 3u) f = (z & 4u) ? (f | PCP_F_VIS_Z) : (f & ~PCP_F_VIS_Z);
+    // evaluateZX120Only statistics use the zx120 flags right after its evaluation (:377-397)
+    const bool zr = f & PCP_F_RANGE_Z, zf = f & PCP_F_FOV_Z, zv = f & PCP_F_VIS_Z;
+    if (P > 0) {
+        const uint32_t last = mbits[(size_t)(P - 1) * C + c];
+        f = (last & 1u) ? (f | PCP_F_RANGE_M) : (f & ~PCP_F_RANGE_M);
+        for (int p = P - 1; p >= 0; --p) {
+            const uint32_t b = mbits[(size_t)p * C + c];
+            if (b & 1u) {
+                f = (b & 2u) ? (f | PCP_F_FOV_M) : (f & ~PCP_F_FOV_M);
+                break;
+            }
+        }
+        for (int p = P - 1; p >= 0; --p) {
+            const uint32_t b = mbits[(size_t)p * C + c];
+            if ((b & 3u) == 3u) {
+                f = (b & 4u) ? (f | PCP_F_VIS_M) : (f & ~PCP_F_VIS_M);
+                break;
+            }
+        }
+    }
+    flags[c] = (uint8_t)f;
+    atomicAdd(&stats[S_TOTAL], 1);
+    if (zr) atomicAdd(&stats[S_ZR], 1);
+    if (zf) atomicAdd(&stats[S_ZF], 1);
+    if (zv) atomicAdd(&stats[S_ZV], 1);
+    if (!zr) atomicAdd(&stats[S_ZB], 1);
+    else if (!zf) atomicAdd(&stats[S_ZY], 1);
+    else if (!zv) atomicAdd(&stats[S_ZRED], 1);
+    else atomicAdd(&stats[S_ZG], 1);
+    const bool mr = f & PCP_F_RANGE_M, mf = f & PCP_F_FOV_M, mv = f & PCP_F_VIS_M;
+    const bool zr2 = f & PCP_F_RANGE_Z, zf2 = f & PCP_F_FOV_Z, zv2 = f & PCP_F_VIS_Z;
+    if (!zr2 && !mr) atomicAdd(&stats[S_B], 1);
+    else if (!zf2 && !mf) atomicAdd(&stats[S_Y], 1);
+    else if (!zv2 && !mv) atomicAdd(&stats[S_RED], 1);
+    else atomicAdd(&stats[S_G], 1);
+}
+
+// ---------------------------------------------------------------------------------------
+// candidates (generateCandidatePositions :550-598, getGroundHeight :600-625)
+// ---------------------------------------------------------------------------------------
+struct CandArgs {
+    GridView g;
+    int ground_enabled;    // terrain cloud non-empty (:601)
+    int gs;
+    double exminx, exminy, xs, ys;
+    double gminx, gmaxx, gminy, gmaxy;
+    double cx, cy, cz;
+    double zxx, zxy;
+    double sensor_height;
+    double *lat;           // gs*gs x 6: valid, x, y, z, pitch, yaw
+};
+
+__global__ void __launch_bounds__(kT) k_candidates(CandArgs a) {
+    const int l = blockIdx.x;
+    const int i = l / a.gs, j = l - i * a.gs;
+    const double x = a.exminx + i * a.xs;
+    const double y = a.exminy + j * a.ys;
+    double *out = a.lat + 6 * (size_t)l;
+    const double ddx = x - a.zxx, ddy = y - a.zxy;
+    if (sqrt(ddx * ddx + ddy * ddy) < 0.5 ||
+        (x >= a.gminx && x <= a.gmaxx && y >= a.gminy && y <= a.gmaxy)) {
+        if (threadIdx.x == 0) out[0] = 0.0;
+        return;
+    }
+    // getGroundHeight: radiusSearch((float)x,(float)y,0; r=2) then 2-D distance < 1.0
+    double mz = -DBL_MAX;
+    if (a.ground_enabled && a.g.n_pts > 0) {
+        const GridView &g = a.g;
+        const float qx = (float)x, qy = (float)y, qz = 0.0f;
+        const float r2 = (float)(2.0 * 2.0);
+        const double m = kQueryMargin;
+        auto rng = [&](double lo, double hi, double o, int n, int &i0, int &i1) {
+            i0 = (int)fmax(floor((lo - o) * g.inv_c), 0.0);
+            i1 = (int)fmin(floor((hi - o) * g.inv_c), (double)(n - 1));
+        };
+        int x0, x1, y0, y1, z0, z1;
+        rng(x - 1.0 - m, x + 1.0 + m, g.ox, g.nx, x0, x1);
+        rng(y - 1.0 - m, y + 1.0 + m, g.oy, g.ny, y0, y1);
+        rng(-2.0 - m, 2.0 + m, g.oz, g.nz, z0, z1);
+        if (x0 <= x1 && y0 <= y1 && z0 <= z1) {
+            const int ny_r = y1 - y0 + 1, rows = ny_r * (z1 - z0 + 1);
+            for (int r = threadIdx.x; r < rows; r += kT) {
+                const int iy = y0 + r % ny_r, iz = z0 + r / ny_r;
+                const size_t row = (size_t)g.nx * ((size_t)iy + (size_t)g.ny * iz);
+                const uint32_t s = g.start[row + x0], e = g.start[row + x1 + 1];
+                for (uint32_t k = s; k < e; ++k) {
+                    const float4 p = g.pts[k];
+                    if (!flann_within(qx, qy, qz, p, r2)) continue;
+                    const double dx = (double)p.x - x, dy = (double)p.y - y;
+                    if (sqrt(dx * dx + dy * dy) < 1.0) mz = fmax(mz, (double)p.z);
+                }
+            }
+        }
+    }
+    // block max
+    __shared__ double red[kT / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mz = fmax(mz, __shfl_xor(mz, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mz;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int w = 1; w < kT / 64; ++w) mz = fmax(mz, red[w]);
+    const double ground = (mz != -DBL_MAX) ? mz : 0.0;
+    const double z = ground + a.sensor_height;
+    const double dx = a.cx - x, dy = a.cy - y, dz = a.cz - z;
+    const double hd = sqrt(dx * dx + dy * dy);
+    if (hd < 0.1) {
+        out[0] = 0.0;
+        return;
+    }
+    const double elev = atan2(-dz, hd);
+    if (elev >= kMinElevation && elev <= kMaxElevation) {
+        out[0] = 1.0;
+        out[1] = x;
+        out[2] = y;
+        out[3] = z;
+        out[4] = -kPi / 2 + elev;
+        out[5] = atan2(dy, dx);
+    } else {
+        out[0] = 0.0;
+    }
+}
+
+// order-preserving compaction of the lattice (single block)
+__global__ void __launch_bounds__(1024)
+k_cand_compact(const double *__restrict__ lat, int L, double *__restrict__ out, uint32_t *n_out) {
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t base_s;
+    if (threadIdx.x == 0) base_s = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int chunk = 0; chunk < L; chunk += 1024) {
+        const int l = chunk + threadIdx.x;
+        const bool v = l < L && lat[6 * (size_t)l] != 0.0;
+        const uint64_t bal = __ballot(v);
+        const uint32_t pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = __popcll(bal);
+        __syncthreads();
+        uint32_t off = base_s;
+        uint32_t tot = 0;
+        for (int k = 0; k < 16; ++k) {
+            if (k < w) off += wsum[k];
+            tot += wsum[k];
+        }
+        if (v) {
+            const uint32_t d = off + pre;
+            for (int q = 0; q < 5; ++q) out[5 * (size_t)d + q] = lat[6 * (size_t)l + 1 + q];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) base_s += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *n_out = base_s;
+}
+
+// ---------------------------------------------------------------------------------------
+// dense ray fan (BASELINE configs[1])
+// ---------------------------------------------------------------------------------------
+struct FanArgs {
+    GridView g;
+    const double *ca, *sa, *ce, *se;
+    const double *pose;    // P x 8: x, y, z, pitch, yaw, cos(yaw), sin(yaw), pad
+    const double *steps;
+    int K;
+    int n_az;
+    uint32_t rays;
+    float r2;
+    int present;
+    int16_t *first_hit;
+    uint32_t *blocked;
+    unsigned long long *units;
+    unsigned long long *stats;   // STATS build only: samples visited, occupied stencils, point tests
+};
+
+// one lane = one ray; 64 consecutive azimuths of one elevation ring per wave (coherent
+// termination on near-flat terrain); blockIdx.y = pose.
+template <bool STATS> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
+    const uint32_t p = blockIdx.y;
+    const uint32_t ray = blockIdx.x * kT + threadIdx.x;
+    const bool active = ray < a.rays;
+    int hit = -1;
+    uint32_t cnt[3] = {0, 0, 0};
+    if (active && a.present) {
+        const uint32_t j = ray / (uint32_t)a.n_az, i = ray - j * (uint32_t)a.n_az;
+        const double *P = a.pose + 8 * (size_t)p;
+        const double cej = a.ce[j];
+        const double lx = cej * a.ca[i], ly = cej * a.sa[i], lz = a.se[j];
+        const double cy = P[5], sy = P[6];
+        const double dx = cy * lx - sy * ly;
+        const double dy = sy * lx + cy * ly;
+        const double dz = lz;
+        hit = march_t<STATS>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K, 1e300, a.r2, cnt);
+    }
+    if (active && a.first_hit) a.first_hit[(size_t)p * a.rays + ray] = (int16_t)hit;
+    const uint64_t bal = __ballot(active && hit >= 0);
+    uint32_t u = active ? (hit >= 0 ? (uint32_t)hit + 1u : (uint32_t)a.K) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o, 64);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&a.blocked[p], (uint32_t)__popcll(bal));
+        atomicAdd(&a.units[p], (unsigned long long)u);
+    }
+    if (STATS) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            unsigned long long v = cnt[q];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if ((threadIdx.x & 63) == 0) atomicAdd(&a.stats[q], v);
+        }
+    }
+}
+
+static VisEnv make_env(pcp_ctx *ctx, const pcp_vl_params *p, const double *steps_d, int K) {
+    VisEnv E{};
+    E.terrain_present = ctx->terrain.present ? 1 : 0;
+    if (E.terrain_present) E.terrain = ctx->terrain.view();
+    E.aux_present = (ctx->aux.present && ctx->aux_cloud_n > 0) ? 1 : 0;
+    if (E.aux_present) E.aux = ctx->aux.view();
+    E.max_distance = p->max_distance;
+    E.steps = steps_d;
+    E.K = K;
+    E.r2_ray = (float)(kRayRadius * kRayRadius);
+    E.r2_relaxed = (float)(kRelaxedRadius * kRelaxedRadius);
+    return E;
+}
+
+}  // namespace pcp
+
+using namespace pcp;
+
+extern "C" {
+
+int pcp_set_cells(pcp_ctx *ctx, const double *xyz, const float *normals, uint64_t n) {
+    if (!ctx) return PCP_E_INVALID;
+    if (n && (!xyz || !normals)) return set_err(ctx, PCP_E_INVALID, "pcp_set_cells: null input");
+    if (n > (1u << 30)) return set_err(ctx, PCP_E_INVALID, "pcp_set_cells: too many cells");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    PCP_HIP(ctx, ctx->cells_xyz.ensure(n * 3 * sizeof(double) + 16));
+    PCP_HIP(ctx, ctx->cells_nrm.ensure(n * 3 * sizeof(float) + 16));
+    if (n) {
+        PCP_HIP(ctx, hipMemcpyAsync(ctx->cells_xyz.p, xyz, n * 3 * sizeof(double),
+                                    hipMemcpyHostToDevice, ctx->stream));
+        PCP_HIP(ctx, hipMemcpyAsync(ctx->cells_nrm.p, normals, n * 3 * sizeof(float),
+                                    hipMemcpyHostToDevice, ctx->stream));
+    }
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->n_cells = n;
+    return PCP_OK;
+}
+
+int pcp_generate_candidates(pcp_ctx *ctx, const double bb[6], const pcp_vl_params *p,
+                            const double zx[5], double *poses5, uint64_t cap, uint64_t *n_out) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!bb || !p || !zx || !n_out || (cap && !poses5))
+        return set_err(ctx, PCP_E_INVALID, "pcp_generate_candidates: null argument");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    *n_out = 0;
+    const int gs = (int)std::ceil(std::sqrt((double)p->num_candidates));
+    if (gs <= 0) return PCP_OK;
+    if ((int64_t)gs * gs > (1 << 24))
+        return set_err(ctx, PCP_E_INVALID, "pcp_generate_candidates: num_candidates too large");
+    CandArgs a{};
+    a.ground_enabled = (ctx->terrain_cloud_n > 0 && ctx->terrain.present) ? 1 : 0;
+    if (a.ground_enabled) a.g = ctx->terrain.view();
+    a.gs = gs;
+    const double exminx = bb[0] - p->search_radius, exmaxx = bb[1] + p->search_radius;
+    const double exminy = bb[2] - p->search_radius, exmaxy = bb[3] + p->search_radius;
+    a.exminx = exminx;
+    a.exminy = exminy;
+    a.xs = (exmaxx - exminx) / (gs - 1);
+    a.ys = (exmaxy - exminy) / (gs - 1);
+    a.gminx = bb[0];
+    a.gmaxx = bb[1];
+    a.gminy = bb[2];
+    a.gmaxy = bb[3];
+    a.cx = (bb[0] + bb[1]) / 2.0;
+    a.cy = (bb[2] + bb[3]) / 2.0;
+    a.cz = (bb[4] + bb[5]) / 2.0;
+    a.zxx = zx[0];
+    a.zxy = zx[1];
+    a.sensor_height = p->sensor_height;
+    const int L = gs * gs;
+    PCP_HIP(ctx, ctx->out_a.ensure((size_t)L * 6 * sizeof(double)));
+    PCP_HIP(ctx, ctx->out_b.ensure((size_t)L * 5 * sizeof(double) + 64));
+    a.lat = ctx->out_a.as<double>();
+    uint32_t *n_d = reinterpret_cast<uint32_t *>(ctx->out_b.as<char>() + (size_t)L * 5 * sizeof(double));
+    {
+        ProfScope ps(ctx, PCP_K_CANDIDATES);
+        hipLaunchKernelGGL(k_candidates, dim3(L), dim3(kT), 0, ctx->stream, a);
+        PCP_CHECK_LAUNCH(ctx);
+        hipLaunchKernelGGL(k_cand_compact, dim3(1), dim3(1024), 0, ctx->stream,
+                           ctx->out_a.as<const double>(), L, ctx->out_b.as<double>(), n_d);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    uint32_t nh = 0;
+    PCP_HIP(ctx, hipMemcpyAsync(&nh, n_d, 4, hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *n_out = nh;
+    if (nh > cap) {
+        prof_resolve(ctx);
+        return set_err(ctx, PCP_E_CAPACITY, "pcp_generate_candidates: need %u poses, cap %llu", nh,
+                       (unsigned long long)cap);
+    }
+    if (nh)
+        PCP_HIP(ctx, hipMemcpyAsync(poses5, ctx->out_b.p, (size_t)nh * 5 * sizeof(double),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    prof_resolve(ctx);
+    return PCP_OK;
+}
+
+static int ensure_steps(pcp_ctx *ctx, double end, int *K) {
+    if (ctx->steps_end == end) {
+        *K = ctx->steps_K;
+        return PCP_OK;
+    }
+    std::vector<double> s = step_table(end);
+    PCP_HIP(ctx, ctx->steps_d.ensure((s.size() + 1) * sizeof(double)));
+    if (!s.empty()) {
+        PCP_HIP(ctx, hipMemcpyAsync(ctx->steps_d.p, s.data(), s.size() * sizeof(double),
+                                    hipMemcpyHostToDevice, ctx->stream));
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    ctx->steps_end = end;
+    ctx->steps_K = (int)s.size();
+    *K = ctx->steps_K;
+    return PCP_OK;
+}
+
+int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
+                    const pcp_vl_params *p, uint8_t *cell_flags, double *total_score,
+                    int32_t *covered, pcp_vl_report *rep) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!zx || !p || !rep || (n && !poses5) || (ctx->n_cells && !cell_flags))
+        return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: null argument");
+    if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: at most 65535 poses per call");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const int C = (int)ctx->n_cells, P = (int)n;
+    int K = 0;
+    int rc = ensure_steps(ctx, p->max_distance - kVisRadius, &K);
+    if (rc) return rc;
+    VisEnv E = make_env(ctx, p, ctx->steps_d.as<const double>(), K);
+    // buffers
+    const size_t pc = (size_t)P * (size_t)C;
+    PCP_HIP(ctx, ctx->poses_d.ensure((size_t)P * 5 * sizeof(double) + 16));
+    PCP_HIP(ctx, ctx->out_a.ensure(pc * sizeof(double) + (size_t)C * sizeof(double) + 64));
+    PCP_HIP(ctx, ctx->out_b.ensure(pc + (size_t)C * 2 + 64));
+    PCP_HIP(ctx, ctx->out_c.ensure((size_t)(P + 1) * (sizeof(double) + sizeof(int32_t)) + 64));
+    PCP_HIP(ctx, ctx->stats_d.ensure(64 * sizeof(int32_t)));
+    double *comb = ctx->out_a.as<double>();
+    double *score_z = comb + pc;
+    uint8_t *mbits = ctx->out_b.as<uint8_t>();
+    uint8_t *zbits = mbits + pc;
+    uint8_t *flags_d = zbits + C;
+    double *tot_d = ctx->out_c.as<double>();
+    int32_t *cov_d = reinterpret_cast<int32_t *>(tot_d + (P + 1));
+    int32_t *stats = ctx->stats_d.as<int32_t>();
+    if (P) PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, poses5, (size_t)P * 5 * sizeof(double),
+                                       hipMemcpyHostToDevice, st));
+    if (C) PCP_HIP(ctx, hipMemcpyAsync(flags_d, cell_flags, C, hipMemcpyHostToDevice, st));
+    PCP_HIP(ctx, hipMemsetAsync(stats, 0, 64 * sizeof(int32_t), st));
+    const unsigned cb = (unsigned)((C + kT - 1) / kT);
+    if (C) {
+        {
+            ProfScope ps(ctx, PCP_K_ZX120_CELLS);
+            hipLaunchKernelGGL(k_zx120_cells, dim3(cb), dim3(kT), 0, st, E,
+                               ctx->cells_xyz.as<const double>(), ctx->cells_nrm.as<const float>(),
+                               C, zx[0], zx[1], zx[2], zx[3], score_z, zbits);
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        if (P) {
+            ProfScope ps(ctx, PCP_K_SCORE_CELLS);
+            hipLaunchKernelGGL(k_score_cells, dim3(cb, P), dim3(kT), 0, st, E,
+                               ctx->cells_xyz.as<const double>(), ctx->cells_nrm.as<const float>(),
+                               C, ctx->poses_d.as<const double>(), (const double *)score_z, comb,
+                               mbits);
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        {
+            ProfScope ps(ctx, PCP_K_POSE_SUM);
+            if (P)
+                hipLaunchKernelGGL(k_row_sum, dim3((P + 3) / 4), dim3(kT), 0, st,
+                                   (const double *)comb, C, P, tot_d, cov_d);
+            hipLaunchKernelGGL(k_row_sum, dim3(1), dim3(kT), 0, st, (const double *)score_z, C, 1,
+                               tot_d + P, cov_d + P);
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        {
+            ProfScope ps(ctx, PCP_K_CELL_FLAGS);
+            hipLaunchKernelGGL(k_cell_flags, dim3(cb), dim3(kT), 0, st, (const uint8_t *)zbits,
+                               (const uint8_t *)mbits, C, P, flags_d, stats);
+            PCP_CHECK_LAUNCH(ctx);
+        }
+    } else {
+        PCP_HIP(ctx, hipMemsetAsync(tot_d, 0, (size_t)(P + 1) * sizeof(double), st));
+        PCP_HIP(ctx, hipMemsetAsync(cov_d, 0, (size_t)(P + 1) * sizeof(int32_t), st));
+    }
+    std::vector<double> tot_h(P + 1);
+    std::vector<int32_t> cov_h(P + 1);
+    int32_t st_h[S_N];
+    PCP_HIP(ctx, hipMemcpyAsync(tot_h.data(), tot_d, (size_t)(P + 1) * sizeof(double),
+                                hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipMemcpyAsync(cov_h.data(), cov_d, (size_t)(P + 1) * sizeof(int32_t),
+                                hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipMemcpyAsync(st_h, stats, sizeof(st_h), hipMemcpyDeviceToHost, st));
+    if (C) PCP_HIP(ctx, hipMemcpyAsync(cell_flags, flags_d, C, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    prof_resolve(ctx);
+    // runOptimization candidate loop (:464-475): strict '>' keeps the first maximum
+    double best = -INFINITY;
+    int64_t best_idx = -1;
+    for (int k = 0; k < P; ++k) {
+        if (total_score) total_score[k] = tot_h[k];
+        if (covered) covered[k] = cov_h[k];
+        if (tot_h[k] > best) {
+            best = tot_h[k];
+            best_idx = k;
+        }
+    }
+    std::memset(rep, 0, sizeof(*rep));
+    rep->best_idx = best_idx;
+    rep->best_score = best;
+    rep->zx120_total_score = tot_h[P];
+    rep->total_cells = st_h[S_TOTAL];
+    rep->zx120_range_ok = st_h[S_ZR];
+    rep->zx120_fov_ok = st_h[S_ZF];
+    rep->zx120_visible_ok = st_h[S_ZV];
+    rep->zx120_green = st_h[S_ZG];
+    rep->zx120_red = st_h[S_ZRED];
+    rep->zx120_blue = st_h[S_ZB];
+    rep->zx120_yellow = st_h[S_ZY];
+    rep->green = st_h[S_G];
+    rep->red = st_h[S_RED];
+    rep->blue = st_h[S_B];
+    rep->yellow = st_h[S_Y];
+    return PCP_OK;
+}
+
+static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                            const pcp_fan_params *fan, uint32_t *blocked, uint64_t *units,
+                            int16_t *first_hit, int64_t *best_idx, uint64_t *stats) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!fan || (n && (!poses5 || !blocked)))
+        return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: null argument");
+    if (fan->n_az <= 0 || fan->n_el <= 0 || (int64_t)fan->n_az * fan->n_el > (1ll << 30))
+        return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: bad fan size %d x %d", fan->n_az,
+                       fan->n_el);
+    if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: at most 65535 poses per call");
+    if (best_idx) *best_idx = -1;
+    if (n == 0) return PCP_OK;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const int P = (int)n;
+    const uint32_t rays = (uint32_t)fan->n_az * (uint32_t)fan->n_el;
+    // direction tables (host libm, identical to the oracle), cached per fan shape
+    const size_t tab_doubles = 2 * (size_t)fan->n_az + 2 * (size_t)fan->n_el;
+    if (ctx->fan_naz != fan->n_az || ctx->fan_nel != fan->n_el || ctx->fan_elmin != fan->el_min ||
+        ctx->fan_elmax != fan->el_max) {
+        std::vector<double> t(tab_doubles);
+        fan_tables(fan->n_az, fan->n_el, fan->el_min, fan->el_max, t.data(), t.data() + fan->n_az,
+                   t.data() + 2 * fan->n_az, t.data() + 2 * fan->n_az + fan->n_el);
+        PCP_HIP(ctx, ctx->fan_tab.ensure(tab_doubles * sizeof(double)));
+        PCP_HIP(ctx, hipMemcpyAsync(ctx->fan_tab.p, t.data(), tab_doubles * sizeof(double),
+                                    hipMemcpyHostToDevice, st));
+        PCP_HIP(ctx, hipStreamSynchronize(st));
+        ctx->fan_naz = fan->n_az;
+        ctx->fan_nel = fan->n_el;
+        ctx->fan_elmin = fan->el_min;
+        ctx->fan_elmax = fan->el_max;
+    }
+    int K = 0;
+    int rc = ensure_steps(ctx, fan->max_distance - kVisRadius, &K);
+    if (rc) return rc;
+    std::vector<double> pose8((size_t)P * 8);
+    for (int k = 0; k < P; ++k) {
+        const double *s = poses5 + 5 * (size_t)k;
+        double *d = pose8.data() + 8 * (size_t)k;
+        for (int q = 0; q < 5; ++q) d[q] = s[q];
+        d[5] = std::cos(s[4]);
+        d[6] = std::sin(s[4]);
+        d[7] = 0.0;
+    }
+    PCP_HIP(ctx, ctx->poses_d.ensure(pose8.size() * sizeof(double)));
+    PCP_HIP(ctx, ctx->out_c.ensure((size_t)P * (sizeof(uint32_t) + sizeof(uint64_t)) + 64));
+    PCP_HIP(ctx, ctx->stats_d.ensure(64 * sizeof(uint64_t)));
+    PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pose8.data(), pose8.size() * sizeof(double),
+                                hipMemcpyHostToDevice, st));
+    unsigned long long *units_d = ctx->out_c.as<unsigned long long>();
+    uint32_t *blocked_d = reinterpret_cast<uint32_t *>(units_d + P);
+    PCP_HIP(ctx, hipMemsetAsync(ctx->out_c.p, 0, (size_t)P * (sizeof(uint32_t) + sizeof(uint64_t)), st));
+    int16_t *fh_d = nullptr;
+    if (first_hit) {
+        PCP_HIP(ctx, ctx->out_d.ensure((size_t)P * rays * sizeof(int16_t)));
+        fh_d = ctx->out_d.as<int16_t>();
+    }
+    FanArgs a{};
+    a.present = ctx->terrain.present ? 1 : 0;
+    if (a.present) a.g = ctx->terrain.view();
+    const double *tab = ctx->fan_tab.as<const double>();
+    a.ca = tab;
+    a.sa = tab + fan->n_az;
+    a.ce = tab + 2 * fan->n_az;
+    a.se = tab + 2 * fan->n_az + fan->n_el;
+    a.pose = ctx->poses_d.as<const double>();
+    a.steps = ctx->steps_d.as<const double>();
+    a.K = K;
+    a.n_az = fan->n_az;
+    a.rays = rays;
+    a.r2 = (float)(kRayRadius * kRayRadius);
+    a.first_hit = fh_d;
+    a.blocked = blocked_d;
+    a.units = units_d;
+    a.stats = ctx->stats_d.as<unsigned long long>();
+    if (stats) {
+        PCP_HIP(ctx, hipMemsetAsync(a.stats, 0, 4 * sizeof(uint64_t), st));
+        hipLaunchKernelGGL(k_raycast_fan<true>, dim3((rays + kT - 1) / kT, P), dim3(kT), 0, st, a);
+        PCP_CHECK_LAUNCH(ctx);
+        PCP_HIP(ctx, hipMemcpyAsync(stats, a.stats, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    } else {
+        ProfScope ps(ctx, PCP_K_RAYCAST_FAN);
+        hipLaunchKernelGGL(k_raycast_fan<false>, dim3((rays + kT - 1) / kT, P), dim3(kT), 0, st, a);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    std::vector<uint64_t> u_h(P);
+    PCP_HIP(ctx, hipMemcpyAsync(blocked, blocked_d, (size_t)P * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipMemcpyAsync(u_h.data(), units_d, (size_t)P * sizeof(uint64_t),
+                                hipMemcpyDeviceToHost, st));
+    if (first_hit)
+        PCP_HIP(ctx, hipMemcpyAsync(first_hit, fh_d, (size_t)P * rays * sizeof(int16_t),
+                                    hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    prof_resolve(ctx);
+    if (units)
+        for (int k = 0; k < P; ++k) units[k] = u_h[k];
+    if (best_idx) {
+        int64_t b = 0;
+        for (int k = 1; k < P; ++k)
+            if (blocked[k] < blocked[b]) b = k;
+        *best_idx = b;
+    }
+    return PCP_OK;
+}
+
+int pcp_raycast_fan(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
+                    uint32_t *blocked, uint64_t *units, int16_t *first_hit, int64_t *best_idx) {
+    return raycast_fan_impl(ctx, poses5, n, fan, blocked, units, first_hit, best_idx, nullptr);
+}
+
+int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                          const pcp_fan_params *fan, uint64_t stats[3]) {
+    if (!ctx || !stats) return PCP_E_INVALID;
+    std::vector<uint32_t> blocked(n ? n : 1);
+    stats[0] = stats[1] = stats[2] = 0;
+    return raycast_fan_impl(ctx, poses5, n, fan, blocked.data(), nullptr, nullptr, nullptr, stats);
+}
+
+}  // extern "C"

@@ -1,0 +1,308 @@
+"""CPU tests of the checker itself: the oracle (oracle/pcp_oracle.c) against independent
+numpy/scipy restatements and against the committed golden fixtures (tests/golden/).
+
+Parity with the reference is unpinned (the reference cannot be built and ships no golden
+data); these tests pin the restatement's semantics: strict float-vs-double
+crop compares, PCL VoxelGrid keying in float, the FLANN float radius predicate, Eigen's
+float transform order, the repeated-addition march and the runOptimization loop.
+"""
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+GOLD = Path(__file__).resolve().parent / "golden"
+F32 = np.float32
+
+
+# ------------------------------------------------------------------------------ golden pins
+def test_golden_crop(oracle):
+    d = np.load(GOLD / "crop.npz")
+    np.testing.assert_array_equal(oracle.crop_box(d["cloud"], d["box"]), d["kept"])
+
+
+def test_golden_voxel(oracle):
+    d = np.load(GOLD / "voxel.npz")
+    for s in "ab":
+        xyz, idx, cnt, pt = oracle.voxel_grid(d[f"cloud_{s}"], float(d[f"leaf_{s}"]))
+        np.testing.assert_array_equal(idx, d[f"idx_{s}"])
+        np.testing.assert_array_equal(cnt, d[f"cnt_{s}"])
+        np.testing.assert_array_equal(xyz, d[f"xyz_{s}"])
+
+
+def test_golden_transform(oracle):
+    d = np.load(GOLD / "transform.npz")
+    out = oracle.transform_rgb(d["cloud"], d["t"], d["q"], d["rgb"])
+    np.testing.assert_array_equal(out.view(np.uint32), d["out"].view(np.uint32))
+
+
+def test_golden_fan(oracle):
+    d = np.load(GOLD / "fan.npz")
+    T = oracle.Cloud(d["terrain"])
+    b, u, fh = oracle.raycast_fan(T, d["poses"], int(d["n_az"]), int(d["n_el"]),
+                                  float(d["el_min"]), float(d["el_max"]),
+                                  float(d["max_distance"]))
+    np.testing.assert_array_equal(fh, d["first_hit"])
+    np.testing.assert_array_equal(b, d["blocked"])
+    np.testing.assert_array_equal(u, d["units"])
+
+
+def test_golden_score(oracle):
+    d = np.load(GOLD / "score.npz")
+    T, A = oracle.Cloud(d["terrain"]), oracle.Cloud(d["aux"])
+    cand = oracle.generate_candidates(T, d["grid_bbox"],
+                                      oracle.vl_params(num_candidates=int(d["num_candidates"])),
+                                      d["zx"])
+    np.testing.assert_array_equal(cand, d["candidates"])
+    flags = np.zeros(d["cells"].shape[0], np.uint8)
+    tot, cov, rep = oracle.score_poses(T, A, d["cells"], d["normals"], cand, d["zx"],
+                                       oracle.vl_params(max_distance=float(d["max_distance"])),
+                                       flags)
+    np.testing.assert_array_equal(flags, d["flags"])
+    np.testing.assert_array_equal(tot, d["total"])
+    np.testing.assert_array_equal(cov, d["covered"])
+    r = [rep.best_idx, rep.total_cells, rep.green, rep.red, rep.blue, rep.yellow,
+         rep.zx120_green, rep.zx120_red, rep.zx120_blue, rep.zx120_yellow]
+    np.testing.assert_array_equal(r, d["report"])
+
+
+# ------------------------------------------------------------------------------ independent checks
+def test_crop_vs_numpy(oracle):
+    rng = np.random.default_rng(0)
+    a = rng.uniform(-5, 20, (20000, 4)).astype(F32)
+    a[::97, 1] = np.nan
+    box = np.array([0.0, 15.0, -10.0, 10.0, -1.5, 10.0])
+    x, y, z = (a[:, i].astype(np.float64) for i in range(3))
+    m = (x > box[0]) & (x < box[1]) & (y > box[2]) & (y < box[3]) & (z > box[4]) & (z < box[5])
+    np.testing.assert_array_equal(oracle.crop_box(a, box), np.nonzero(m)[0])
+    # a bound that is not a float: the double compare matters (10.000000001 vs float 10.0)
+    b2 = box.copy()
+    b2[3] = 10.0 + 1e-9
+    a[:50, 1] = F32(10.0)
+    a[:50, 0] = F32(1.0)
+    a[:50, 2] = F32(0.0)
+    assert set(range(50)) <= set(oracle.crop_box(a, b2).tolist())
+    assert not set(range(50)) & set(oracle.crop_box(a, box).tolist())
+
+
+def _pcl_voxel_numpy(p, leaf):
+    """Independent numpy restatement of VoxelGrid::applyFilter (float32 keying)."""
+    leaf = F32(leaf)
+    inv = F32(1.0) / leaf
+    mn, mx = p.min(0), p.max(0)
+    dxyz = ((mx - mn) * inv).astype(np.int64) + 1
+    if int(np.prod(dxyz)) > 2**31 - 1:
+        return None
+    min_b = np.floor(mn * inv).astype(np.int64)
+    max_b = np.floor(mx * inv).astype(np.int64)
+    div = max_b - min_b + 1
+    ijk = (np.floor(p * inv) - min_b.astype(F32)).astype(np.int64)
+    idx = ijk[:, 0] + ijk[:, 1] * div[0] + ijk[:, 2] * div[0] * div[1]
+    order = np.argsort(idx, kind="stable")
+    keys, starts, counts = np.unique(idx[order], return_index=True, return_counts=True)
+    cent = np.empty((keys.size, 3), F32)
+    for k, (s, c) in enumerate(zip(starts, counts)):
+        acc = np.zeros(3, F32)
+        for j in order[s:s + c]:
+            acc = acc + p[j]
+        cent[k] = acc / F32(c)
+    return keys.astype(np.uint32), counts.astype(np.uint32), cent
+
+
+@pytest.mark.parametrize("leaf", [0.2, 0.05, 0.37])
+def test_voxel_vs_numpy(oracle, leaf):
+    rng = np.random.default_rng(1)
+    p = rng.uniform(-2, 3, (3000, 3)).astype(F32)
+    p = np.concatenate([p, p[:500] + F32(0.001)])
+    keys, counts, cent = _pcl_voxel_numpy(p, leaf)
+    xyz, idx, cnt, pt = oracle.voxel_grid(p, leaf)
+    assert not pt
+    np.testing.assert_array_equal(idx, keys)
+    np.testing.assert_array_equal(cnt, counts)
+    np.testing.assert_array_equal(xyz, cent)
+
+
+def test_voxel_overflow_guard(oracle):
+    p = np.array([[0, 0, 0], [2000, 2000, 2000], [1, 1, 1]], F32)
+    assert _pcl_voxel_numpy(p, 0.001) is None
+    xyz, idx, cnt, pt = oracle.voxel_grid(p, 0.001)
+    assert pt
+    np.testing.assert_array_equal(xyz, p)
+
+
+def _flann_any(pts, q, radius):
+    """Brute-force FLANN L2_Simple<float> predicate: ((0+dx^2)+dy^2)+dz^2 < float(r*r)."""
+    q = q.astype(F32)
+    d = q[None, :] - pts[:, :3]
+    acc = F32(0) + d[:, 0] * d[:, 0]
+    acc = acc + d[:, 1] * d[:, 1]
+    acc = acc + d[:, 2] * d[:, 2]
+    return bool(np.any(acc < F32(radius * radius)))
+
+
+def test_radius_predicate_vs_bruteforce(oracle, small_scene):
+    pts = small_scene.terrain[:, :3]
+    C = oracle.Cloud(small_scene.terrain)
+    rng = np.random.default_rng(2)
+    base = pts[rng.integers(0, pts.shape[0], 400)]
+    q = base + rng.normal(0, 0.04, base.shape).astype(F32)
+    r = 0.08 * 0.7
+    for i in range(q.shape[0]):
+        assert C.any_within(q[i], r) == _flann_any(pts, q[i], r)
+    # boundary: a point exactly at float(r) distance along x is NOT within (strict <)
+    one = np.array([[0.0, 0.0, 0.0, 0, 0, 0, 0, 0]], F32)
+    C1 = oracle.Cloud(one)
+    qq = np.array([F32(math.sqrt(F32(r * r))), 0, 0], F32)
+    assert C1.any_within(qq, r) == _flann_any(one, qq, r)
+
+
+def test_transform_vs_numpy(oracle):
+    rng = np.random.default_rng(3)
+    p = rng.uniform(-20, 20, (1000, 4)).astype(F32)
+    yaw = 0.7
+    t = np.array([1.5, -2.25, 0.3])
+    q = np.array([0.1, -0.05, math.sin(yaw / 2), math.cos(yaw / 2)])
+    qx, qy, qz, qw = (F32(v) for v in q)
+    tx, ty, tz = F32(2) * qx, F32(2) * qy, F32(2) * qz
+    m = np.array([[F32(1) - (ty * qy + tz * qz), ty * qx - tz * qw, tz * qx + ty * qw],
+                  [ty * qx + tz * qw, F32(1) - (tx * qx + tz * qz), tz * qy - tx * qw],
+                  [tz * qx - ty * qw, tz * qy + tx * qw, F32(1) - (tx * qx + ty * qy)]], F32)
+    T = t.astype(F32)
+    exp = np.empty((p.shape[0], 3), F32)
+    for r in range(3):
+        exp[:, r] = ((m[r, 0] * p[:, 0] + m[r, 1] * p[:, 1]) + m[r, 2] * p[:, 2]) + T[r]
+    out = oracle.transform_rgb(p, t, q, (0, 0, 255))
+    np.testing.assert_array_equal(out[:, :3], exp)
+    assert np.all(out[:, 4].view(np.uint32) == np.uint32(0xFF0000FF))
+
+
+def _march_numpy(pts, pos, d, end, r):
+    s, k = 0.5, 0
+    while s < end:
+        q = np.array([pos[0] + d[0] * s, pos[1] + d[1] * s, pos[2] + d[2] * s]).astype(F32)
+        if _flann_any(pts, q, r):
+            return k
+        s += 0.3
+        k += 1
+    return -1
+
+
+def test_fan_vs_bruteforce(oracle):
+    d = np.load(GOLD / "fan.npz")
+    terr, poses = d["terrain"], d["poses"]
+    n_az, n_el = int(d["n_az"]), int(d["n_el"])
+    ca, sa, ce, se = oracle.fan_tables(n_az, n_el, float(d["el_min"]), float(d["el_max"]))
+    fh = d["first_hit"]
+    rng = np.random.default_rng(4)
+    r = 0.08 * 0.7
+    for _ in range(40):
+        p, j, i = rng.integers(0, poses.shape[0]), rng.integers(0, n_el), rng.integers(0, n_az)
+        lx, ly, lz = ce[j] * ca[i], ce[j] * sa[i], se[j]
+        cyw, syw = math.cos(poses[p, 4]), math.sin(poses[p, 4])
+        dvec = (cyw * lx - syw * ly, syw * lx + cyw * ly, lz)
+        assert _march_numpy(terr[:, :3], poses[p], dvec, 15.0 - 0.08, r) == fh[p, j, i]
+
+
+def _eval_cell_py(terr, aux, pose, c, n, is_zx, maxd, flags):
+    """Pure-Python evaluateCellScore (virtual_lidar.cpp:656-752) with brute-force searches."""
+    dx, dy, dz = c[0] - pose[0], c[1] - pose[1], c[2] - pose[2]
+    L = math.sqrt(dx * dx + dy * dy + dz * dz)
+    fr, ff, fv = (1, 2, 4) if is_zx else (8, 16, 32)
+    in_range = 0.5 <= L <= maxd
+    flags = (flags | fr) if in_range else (flags & ~fr)
+    if not in_range:
+        return 0.0, flags
+    elev = math.atan2(dz, math.sqrt(dx * dx + dy * dy))
+    in_fov = abs(elev - pose[3]) <= (180.0 * math.pi / 180.0) / 2.0
+    flags = (flags | ff) if in_fov else (flags & ~ff)
+    if not in_fov:
+        return 0.0, flags
+    vis = None
+    if is_zx and aux is not None and _flann_any(aux, np.array(c, F32), 0.08 * 3.0):
+        vis = True
+    if vis is None:
+        vis = _march_numpy(terr, pose, (dx / L, dy / L, dz / L), L - 0.08, 0.08 * 0.7) < 0
+    flags = (flags | fv) if vis else (flags & ~fv)
+    if not vis:
+        return 0.0, flags
+    dot = (dx / L) * float(n[0]) + (dy / L) * float(n[1]) + (dz / L) * float(n[2])
+    theta = math.acos(max(0.0, min(1.0, abs(dot))))
+    return max(0.0, math.sin(math.pi / 2 - theta) + 1.0 / L), flags
+
+
+def test_score_vs_python_loop(oracle):
+    d = np.load(GOLD / "score.npz")
+    terr, aux = d["terrain"][:, :3], d["aux"][:, :3]
+    cells, nrm, zx = d["cells"], d["normals"], d["zx"]
+    cand = d["candidates"][:4]
+    maxd = float(d["max_distance"])
+    flags = np.zeros(cells.shape[0], np.int64)
+    totals = []
+    for c in range(cells.shape[0]):
+        _, flags[c] = _eval_cell_py(terr, aux, zx, cells[c], nrm[c], True, maxd, flags[c])
+    for p in cand:
+        tot = 0.0
+        for c in range(cells.shape[0]):
+            sz, flags[c] = _eval_cell_py(terr, aux, zx, cells[c], nrm[c], True, maxd, flags[c])
+            sm, flags[c] = _eval_cell_py(terr, aux, p, cells[c], nrm[c], False, maxd, flags[c])
+            comb = max(sz, sm)
+            if comb > 0:
+                tot += comb
+        totals.append(tot)
+    T, A = oracle.Cloud(d["terrain"]), oracle.Cloud(d["aux"])
+    of = np.zeros(cells.shape[0], np.uint8)
+    ot, oc, rep = oracle.score_poses(T, A, cells, nrm, cand, zx,
+                                     oracle.vl_params(max_distance=maxd), of)
+    np.testing.assert_array_equal(of, flags.astype(np.uint8))
+    np.testing.assert_array_equal(ot, np.array(totals))
+
+
+def test_candidates_vs_python(oracle, small_scene):
+    """generateCandidatePositions + getGroundHeight with a brute-force radius search."""
+    terr = small_scene.terrain
+    pts = terr[:, :3]
+    T = oracle.Cloud(terr)
+    bb = np.array([3.2, 6.4, -1.3, 1.3, -1.1, 0.05])
+    zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])
+    p = oracle.vl_params(num_candidates=49)
+    got = oracle.generate_candidates(T, bb, p, zx)
+    exp = []
+    gs = 7
+    exminx, exmaxx, exminy, exmaxy = bb[0] - 3.0, bb[1] + 3.0, bb[2] - 3.0, bb[3] + 3.0
+    cx, cy, cz = (bb[0] + bb[1]) / 2, (bb[2] + bb[3]) / 2, (bb[4] + bb[5]) / 2
+    xs, ys = (exmaxx - exminx) / (gs - 1), (exmaxy - exminy) / (gs - 1)
+    for i in range(gs):
+        for j in range(gs):
+            x, y = exminx + i * xs, exminy + j * ys
+            if math.sqrt((x - zx[0]) ** 2 + (y - zx[1]) ** 2) < 0.5:
+                continue
+            if bb[0] <= x <= bb[1] and bb[2] <= y <= bb[3]:
+                continue
+            q = np.array([x, y, 0.0], F32)
+            dd = q[None, :] - pts
+            acc = F32(0) + dd[:, 0] * dd[:, 0]
+            acc = acc + dd[:, 1] * dd[:, 1]
+            acc = acc + dd[:, 2] * dd[:, 2]
+            sel = pts[acc < F32(4.0)].astype(np.float64)
+            d2 = np.sqrt((sel[:, 0] - x) ** 2 + (sel[:, 1] - y) ** 2)
+            zz = sel[d2 < 1.0, 2]
+            ground = float(zz.max()) if zz.size else 0.0
+            z = ground + 1.1
+            dx, dy, dz = cx - x, cy - y, cz - z
+            hd = math.sqrt(dx * dx + dy * dy)
+            if hd < 0.1:
+                continue
+            el = math.atan2(-dz, hd)
+            if -85.0 * math.pi / 180.0 <= el <= 85.0 * math.pi / 180.0:
+                exp.append([x, y, z, -math.pi / 2 + el, math.atan2(dy, dx)])
+    np.testing.assert_array_equal(got, np.array(exp))
+
+
+def test_step_table_repeated_addition():
+    s, out = 0.5, []
+    while s < 14.92:
+        out.append(s)
+        s += 0.3
+    assert len(out) == 49
+    assert out[10] != 0.5 + 0.3 * 10     # repeated addition differs from the closed form

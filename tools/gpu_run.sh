@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, a short bench, a rocprofv3 kernel-trace summary.
+# Each GPU step has its own time limit; a crash/timeout (exit >= 124 or signal) ends the
+# script immediately; plain test failures (exit 1) do not stop the later measurements.
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+WHAT=${1:-all}
+if [ "$WHAT" = all ] || [ "$WHAT" = test ]; then
+  step pytest_gpu 900 python -m pytest tests -q -m gpu -rf
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
+  step bench 600 python bench.py --steps 10 --warmup 3
+fi
+if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
+  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline
+fi
+echo "=== done"
