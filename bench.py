@@ -108,9 +108,11 @@ def run_fan(args, torch, dist, world, rank, local):
     scene = synth.terrain_scene()
     ctx.set_terrain(scene.terrain, point_step=32)
     bbox = _grid_bbox(scene.area)
+    from pointcloud_processor_amd import dist as pd
+
     P_total = args.poses_per_gpu * world
     poses_all, nc = _poses_for(ctx, bbox, scene.zx120_pose5, P_total)
-    lo, hi = rank * args.poses_per_gpu, (rank + 1) * args.poses_per_gpu
+    lo, hi = pd.shard(P_total, world, rank)
     poses = np.ascontiguousarray(poses_all[lo:hi])
     fan = _abi.fan_params(n_az=args.n_az, n_el=args.n_el)
     on_gpu = torch.cuda.is_available()
@@ -118,14 +120,8 @@ def run_fan(args, torch, dist, world, rank, local):
 
     def step():
         blocked, units, _, _ = ctx.raycast_fan(poses, fan)
-        key = torch.full((P_total,), torch.iinfo(torch.int64).max, dtype=torch.int64)
-        key[lo:hi] = torch.from_numpy(blocked.astype(np.int64))
-        key = key.to(dev)
-        if dist is not None:
-            dist.all_reduce(key, op=dist.ReduceOp.MIN)   # the single collective
-        k = key.cpu().numpy()
-        best = int(np.argmin(k))                          # ties -> lowest pose index
-        return int(units.sum()), best, k
+        keys, best = pd.reduce_fan(blocked, lo, hi, P_total, dist, dev)   # the one collective
+        return int(units.sum()), best, keys
 
     def barrier_sync():
         if dist is not None:

@@ -207,6 +207,12 @@ int pcp_raycast_fan(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fa
 int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
                           const pcp_fan_params *fan, uint64_t stats[3]);
 
+/* Diagnostic build with s_memtime stamps (shader clock) per wave: stamps[(p*W + w)*4 + i],
+ * W = ceil(n_az*n_el/64), i = 0 start, 1 after direction setup, 2 after the march, 3 end.
+ * For locating where wave lifetime goes; never used for timing. */
+int pcp_raycast_fan_stamps(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                           const pcp_fan_params *fan, uint64_t *stamps);
+
 /* The march's sample distances: s_0 = 0.5, s_{k+1} = s_k + 0.3 (repeated double addition,
  * :765-796) while s_k < end.  Returns the count in *n (writes min(cap, n) values). */
 int pcp_step_table(double end, double *steps, uint64_t cap, uint64_t *n);

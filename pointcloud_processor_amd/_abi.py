@@ -115,6 +115,7 @@ _SIGS = [
     ("pcp_raycast_fan", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P, _P, _P,
                                   C.POINTER(C.c_int64)]),
     ("pcp_raycast_fan_stats", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P]),
+    ("pcp_raycast_fan_stamps", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P]),
     ("pcp_step_table", C.c_int, [C.c_double, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pcp_terrain_info", C.c_int, [_P, C.POINTER(IndexInfo)]),
 ]
@@ -393,6 +394,20 @@ def _fan_stats(self, poses5, fan):
 
 
 Context.raycast_fan_stats = _fan_stats
+
+
+def _fan_stamps(self, poses5, fan):
+    """Per-wave shader-clock stamps (diagnostic build): (P, waves, 4) uint64."""
+    poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+    waves = (fan.n_az * fan.n_el + 63) // 64
+    st = np.zeros((poses.shape[0], waves, 4), np.uint64)
+    self._check(self.lib.pcp_raycast_fan_stamps(self.h, _ptr(poses), poses.shape[0],
+                                                C.byref(fan), _ptr(st)),
+                "pcp_raycast_fan_stamps")
+    return st
+
+
+Context.raycast_fan_stamps = _fan_stamps
 
 
 def step_table(end: float) -> np.ndarray:

@@ -30,33 +30,65 @@ __device__ __forceinline__ bool flann_within(float qx, float qy, float qz, const
     return acc < r2;
 }
 
-// KdTreeFLANN::radiusSearch(q, r) > 0 for r <= the index's stencil radius.  2x2x2 cell
-// stencil anchored at the cell of (q - r - margin); cells along x are contiguous in the
-// sorted point array, so the stencil is 4 ranges.  STATS counts occupied stencils and point
-// tests (diagnostic build of the roofline's algorithmic bytes; never in timed runs).
-template <bool STATS>
-__device__ __forceinline__ bool stencil_any_t(const GridView &g, float qx, float qy, float qz,
-                                              float r2, uint32_t *cnt) {
+// Lower-corner cell of the 2x2x2 stencil of a query (q - r - margin).  False when the corner
+// falls outside [0, n-2]^3: then the stencil holds only padding / outside cells and no point
+// can be within r (exact skip, see DESIGN.md "Terrain index").
+__device__ __forceinline__ bool stencil_cell(const GridView &g, float qx, float qy, float qz,
+                                             uint32_t &lin) {
     const double fx = ((double)qx - g.lo_x) * g.inv_c;
     const double fy = ((double)qy - g.lo_y) * g.inv_c;
     const double fz = ((double)qz - g.lo_z) * g.inv_c;
     if (!(fx >= 0.0 && fx < (double)(g.nx - 1) && fy >= 0.0 && fy < (double)(g.ny - 1) &&
           fz >= 0.0 && fz < (double)(g.nz - 1)))
-        return false;   // stencil touches only padding / outside cells: provably empty
+        return false;
     const uint32_t nx = (uint32_t)g.nx, nxy = nx * (uint32_t)g.ny;
-    const uint32_t lin = (uint32_t)fx + nx * (uint32_t)fy + nxy * (uint32_t)fz;
-    if (!((__ldg(&g.occ2[lin >> 5]) >> (lin & 31)) & 1u)) return false;
-    if (STATS) cnt[1] += 1;
+    lin = (uint32_t)fx + nx * (uint32_t)fy + nxy * (uint32_t)fz;
+    return true;
+}
+
+// Exact point tests of an occupied stencil.  Cells along x are contiguous in the sorted point
+// array, so the stencil is 4 ranges; the 8 directory entries are loaded together and each
+// range is tested 4 points per step (indices clamped to the range: duplicates are harmless
+// for an any-hit query) to keep several gathers in flight per lane.
+template <bool STATS>
+__device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, float qx, float qy,
+                                             float qz, float r2, uint32_t *cnt) {
+    const uint32_t nx = (uint32_t)g.nx, nxy = nx * (uint32_t)g.ny;
+    uint32_t s[4], e[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const uint32_t row = lin + (r & 1) * nx + (r >> 1) * nxy;
-        const uint32_t s = g.start[row], e = g.start[row + 2];
-        for (uint32_t k = s; k < e; ++k) {
-            if (STATS) cnt[2] += 1;
-            if (flann_within(qx, qy, qz, g.pts[k], r2)) return true;
+        s[r] = g.start[row];
+        e[r] = g.start[row + 2];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t last = e[r] - 1;
+        for (uint32_t k = s[r]; k < e[r]; k += 4) {
+            const float4 p0 = g.pts[k];
+            const float4 p1 = g.pts[min(k + 1, last)];
+            const float4 p2 = g.pts[min(k + 2, last)];
+            const float4 p3 = g.pts[min(k + 3, last)];
+            if (STATS) cnt[2] += min(4u, e[r] - k);
+            const int h = (int)flann_within(qx, qy, qz, p0, r2) |
+                          (int)flann_within(qx, qy, qz, p1, r2) |
+                          (int)flann_within(qx, qy, qz, p2, r2) |
+                          (int)flann_within(qx, qy, qz, p3, r2);
+            if (h) return true;
         }
     }
     return false;
+}
+
+// KdTreeFLANN::radiusSearch(q, r) > 0 for r <= the index's stencil radius.
+template <bool STATS>
+__device__ __forceinline__ bool stencil_any_t(const GridView &g, float qx, float qy, float qz,
+                                              float r2, uint32_t *cnt) {
+    uint32_t lin;
+    if (!stencil_cell(g, qx, qy, qz, lin)) return false;
+    if (!((g.occ2[lin >> 5] >> (lin & 31)) & 1u)) return false;
+    if (STATS) cnt[1] += 1;
+    return scan_stencil<STATS>(g, lin, qx, qy, qz, r2, cnt);
 }
 
 __device__ __forceinline__ bool stencil_any(const GridView &g, float qx, float qy, float qz,
@@ -76,7 +108,8 @@ __device__ __forceinline__ void clip_k(const GridView &g, double px, double py, 
         if (d[a] == 0.0) {
             if (p[a] < lo[a] || p[a] > hi[a]) t1 = -1.0;
         } else {
-            const double ta = (lo[a] - p[a]) / d[a], tb = (hi[a] - p[a]) / d[a];
+            const double inv = 1.0 / d[a];
+            const double ta = (lo[a] - p[a]) * inv, tb = (hi[a] - p[a]) * inv;
             t0 = fmax(t0, fmin(ta, tb));
             t1 = fmin(t1, fmax(ta, tb));
         }
@@ -86,7 +119,7 @@ __device__ __forceinline__ void clip_k(const GridView &g, double px, double py, 
         khi = -1;
         return;
     }
-    // s_k = 0.5 + 0.3 k up to ~1e-13; widen by one sample each side
+    // s_k = 0.5 + 0.3 k up to ~1e-13 and t0/t1 are within a few ulps: widen by one sample
     const double kl = ceil((t0 - 0.5) / kRayStep) - 1.0;
     const double kh = floor((t1 - 0.5) / kRayStep) + 1.0;
     klo = (int)fmin(fmax(kl, 0.0), (double)K);
@@ -94,8 +127,10 @@ __device__ __forceinline__ void clip_k(const GridView &g, double px, double py, 
 }
 
 // checkVisibilityWithRaycasting's march (virtual_lidar.cpp:765-797) from pos along unit dir.
-// Visits samples k (s_k from the repeated-addition table) with s_k < end; returns the first
-// blocked k or -1.  Samples outside the clip box have no point within r (skipped exactly).
+// Visits samples k with s_k < end; returns the first blocked k or -1.  Samples outside the
+// clip box have no point within r (skipped exactly).  s_k comes from ONE table read at klo and
+// then the same repeated addition that built the table (identical doubles).  Samples are
+// processed 4 at a time: the 4 occupancy words are loaded together, then tested in order.
 template <bool STATS>
 __device__ __forceinline__ int march_t(const GridView &g, double px, double py, double pz,
                                        double dx, double dy, double dz,
@@ -103,14 +138,32 @@ __device__ __forceinline__ int march_t(const GridView &g, double px, double py, 
                                        float r2, uint32_t *cnt) {
     int klo, khi;
     clip_k(g, px, py, pz, dx, dy, dz, K, klo, khi);
-    for (int k = klo; k <= khi; ++k) {
-        const double s = steps[k];
-        if (!(s < end)) break;
-        if (STATS) cnt[0] += 1;
-        const float qx = (float)(px + dx * s);
-        const float qy = (float)(py + dy * s);
-        const float qz = (float)(pz + dz * s);
-        if (stencil_any_t<STATS>(g, qx, qy, qz, r2, cnt)) return k;
+    if (klo > khi) return -1;
+    double s = steps[klo];
+    for (int k0 = klo; k0 <= khi; k0 += 4) {
+        float qx[4], qy[4], qz[4];
+        uint32_t lin[4], word[4];
+        bool vis[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            vis[i] = (k0 + i <= khi) && (s < end);
+            qx[i] = (float)(px + dx * s);
+            qy[i] = (float)(py + dy * s);
+            qz[i] = (float)(pz + dz * s);
+            lin[i] = 0;
+            const bool in = vis[i] && stencil_cell(g, qx[i], qy[i], qz[i], lin[i]);
+            word[i] = in ? g.occ2[lin[i] >> 5] : 0u;
+            s = s + kRayStep;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (STATS && vis[i]) cnt[0] += 1;
+            if ((word[i] >> (lin[i] & 31)) & 1u) {
+                if (STATS) cnt[1] += 1;
+                if (scan_stencil<STATS>(g, lin[i], qx[i], qy[i], qz[i], r2, cnt)) return k0 + i;
+            }
+        }
+        if (!vis[3]) break;
     }
     return -1;
 }
@@ -410,25 +463,37 @@ struct FanArgs {
     const double *steps;
     int K;
     int n_az;
+    int uniform_el;        // every wave lies in one elevation ring
     uint32_t rays;
+    uint32_t waves;        // waves per pose = ceil(rays / 64)
     float r2;
     int present;
     int16_t *first_hit;
-    uint32_t *blocked;
-    unsigned long long *units;
-    unsigned long long *stats;   // STATS build only: samples visited, occupied stencils, point tests
+    uint32_t *wave_blocked;        // [P][waves] per-wave partials (no atomics)
+    uint32_t *wave_units;
+    unsigned long long *stats;     // MODE 1: samples visited, occupied stencils, point tests
+                                   // MODE 2: per-wave s_memtime stamps [P*waves][4]
 };
 
+enum { FAN_PLAIN = 0, FAN_STATS = 1, FAN_STAMPS = 2 };
+
 // one lane = one ray; 64 consecutive azimuths of one elevation ring per wave (coherent
-// termination on near-flat terrain); blockIdx.y = pose.
-template <bool STATS> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
+// termination on near-flat terrain); blockIdx.y = pose.  Each wave writes its blocked-ray
+// count and its sample-query count to its own slot: the per-pose sums are formed by
+// k_fan_reduce in a fixed order (deterministic, no same-address atomics).
+template <int MODE> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
     const uint32_t p = blockIdx.y;
     const uint32_t ray = blockIdx.x * kT + threadIdx.x;
     const bool active = ray < a.rays;
+    const uint32_t wslot = (uint32_t)p * a.waves + (ray >> 6);
+    unsigned long long t0 = 0, t1 = 0, t2 = 0;
+    if (MODE == FAN_STAMPS) t0 = __builtin_amdgcn_s_memtime();
     int hit = -1;
     uint32_t cnt[3] = {0, 0, 0};
     if (active && a.present) {
-        const uint32_t j = ray / (uint32_t)a.n_az, i = ray - j * (uint32_t)a.n_az;
+        uint32_t j = ray / (uint32_t)a.n_az;
+        if (a.uniform_el) j = __builtin_amdgcn_readfirstlane(j);   // n_az % 64 == 0
+        const uint32_t i = ray - j * (uint32_t)a.n_az;
         const double *P = a.pose + 8 * (size_t)p;
         const double cej = a.ce[j];
         const double lx = cej * a.ca[i], ly = cej * a.sa[i], lz = a.se[j];
@@ -436,18 +501,27 @@ template <bool STATS> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArg
         const double dx = cy * lx - sy * ly;
         const double dy = sy * lx + cy * ly;
         const double dz = lz;
-        hit = march_t<STATS>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K, 1e300, a.r2, cnt);
+        if (MODE == FAN_STAMPS) {
+            asm volatile("" ::"v"(dx), "v"(dy));
+            t1 = __builtin_amdgcn_s_memtime();
+        }
+        hit = march_t<MODE == FAN_STATS>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K, 1e300,
+                                         a.r2, cnt);
+    }
+    if (MODE == FAN_STAMPS) {
+        asm volatile("" ::"v"(hit));
+        t2 = __builtin_amdgcn_s_memtime();
     }
     if (active && a.first_hit) a.first_hit[(size_t)p * a.rays + ray] = (int16_t)hit;
     const uint64_t bal = __ballot(active && hit >= 0);
     uint32_t u = active ? (hit >= 0 ? (uint32_t)hit + 1u : (uint32_t)a.K) : 0u;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o, 64);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&a.blocked[p], (uint32_t)__popcll(bal));
-        atomicAdd(&a.units[p], (unsigned long long)u);
+    if ((threadIdx.x & 63) == 0 && (ray >> 6) < a.waves) {
+        a.wave_blocked[wslot] = (uint32_t)__popcll(bal);
+        a.wave_units[wslot] = u;
     }
-    if (STATS) {
+    if (MODE == FAN_STATS) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             unsigned long long v = cnt[q];
@@ -455,6 +529,43 @@ template <bool STATS> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArg
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
             if ((threadIdx.x & 63) == 0) atomicAdd(&a.stats[q], v);
         }
+    }
+    if (MODE == FAN_STAMPS && (threadIdx.x & 63) == 0 && (ray >> 6) < a.waves) {
+        const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+        unsigned long long *o = a.stats + 4 * (size_t)wslot;
+        o[0] = t0;
+        o[1] = t1;
+        o[2] = t2;
+        o[3] = t3;
+    }
+}
+
+// per-pose sums of the per-wave partials, fixed order
+__global__ void __launch_bounds__(kT)
+k_fan_reduce(const uint32_t *__restrict__ wb, const uint32_t *__restrict__ wu, uint32_t waves,
+             uint32_t *__restrict__ blocked, unsigned long long *__restrict__ units) {
+    const uint32_t p = blockIdx.x;
+    uint32_t b = 0;
+    unsigned long long u = 0;
+    for (uint32_t w = threadIdx.x; w < waves; w += kT) {
+        b += wb[(size_t)p * waves + w];
+        u += wu[(size_t)p * waves + w];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        b += __shfl_xor(b, o, 64);
+        u += __shfl_xor(u, o, 64);
+    }
+    __shared__ uint32_t sb[kT / 64];
+    __shared__ unsigned long long su[kT / 64];
+    if ((threadIdx.x & 63) == 0) {
+        sb[threadIdx.x >> 6] = b;
+        su[threadIdx.x >> 6] = u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        blocked[p] = sb[0] + sb[1] + sb[2] + sb[3];
+        units[p] = su[0] + su[1] + su[2] + su[3];
     }
 }
 
@@ -687,7 +798,8 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
 
 static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
                             const pcp_fan_params *fan, uint32_t *blocked, uint64_t *units,
-                            int16_t *first_hit, int64_t *best_idx, uint64_t *stats) {
+                            int16_t *first_hit, int64_t *best_idx, uint64_t *stats,
+                            uint64_t *stamps) {
     if (!ctx) return PCP_E_INVALID;
     if (!fan || (n && (!poses5 || !blocked)))
         return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: null argument");
@@ -730,13 +842,15 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
         d[7] = 0.0;
     }
     PCP_HIP(ctx, ctx->poses_d.ensure(pose8.size() * sizeof(double)));
+    const uint32_t waves = (rays + 63) / 64;
     PCP_HIP(ctx, ctx->out_c.ensure((size_t)P * (sizeof(uint32_t) + sizeof(uint64_t)) + 64));
-    PCP_HIP(ctx, ctx->stats_d.ensure(64 * sizeof(uint64_t)));
+    PCP_HIP(ctx, ctx->out_b.ensure((size_t)P * waves * 2 * sizeof(uint32_t) + 64));
+    const size_t stats_bytes = stamps ? (size_t)P * waves * 4 * sizeof(uint64_t) : 64 * sizeof(uint64_t);
+    PCP_HIP(ctx, ctx->stats_d.ensure(stats_bytes));
     PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pose8.data(), pose8.size() * sizeof(double),
                                 hipMemcpyHostToDevice, st));
     unsigned long long *units_d = ctx->out_c.as<unsigned long long>();
     uint32_t *blocked_d = reinterpret_cast<uint32_t *>(units_d + P);
-    PCP_HIP(ctx, hipMemsetAsync(ctx->out_c.p, 0, (size_t)P * (sizeof(uint32_t) + sizeof(uint64_t)), st));
     int16_t *fh_d = nullptr;
     if (first_hit) {
         PCP_HIP(ctx, ctx->out_d.ensure((size_t)P * rays * sizeof(int16_t)));
@@ -754,22 +868,32 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     a.steps = ctx->steps_d.as<const double>();
     a.K = K;
     a.n_az = fan->n_az;
+    a.uniform_el = (fan->n_az % 64 == 0) ? 1 : 0;
     a.rays = rays;
+    a.waves = waves;
     a.r2 = (float)(kRayRadius * kRayRadius);
     a.first_hit = fh_d;
-    a.blocked = blocked_d;
-    a.units = units_d;
+    a.wave_blocked = ctx->out_b.as<uint32_t>();
+    a.wave_units = a.wave_blocked + (size_t)P * waves;
     a.stats = ctx->stats_d.as<unsigned long long>();
+    const dim3 grid((rays + kT - 1) / kT, P);
     if (stats) {
         PCP_HIP(ctx, hipMemsetAsync(a.stats, 0, 4 * sizeof(uint64_t), st));
-        hipLaunchKernelGGL(k_raycast_fan<true>, dim3((rays + kT - 1) / kT, P), dim3(kT), 0, st, a);
+        hipLaunchKernelGGL(k_raycast_fan<FAN_STATS>, grid, dim3(kT), 0, st, a);
         PCP_CHECK_LAUNCH(ctx);
         PCP_HIP(ctx, hipMemcpyAsync(stats, a.stats, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    } else if (stamps) {
+        hipLaunchKernelGGL(k_raycast_fan<FAN_STAMPS>, grid, dim3(kT), 0, st, a);
+        PCP_CHECK_LAUNCH(ctx);
+        PCP_HIP(ctx, hipMemcpyAsync(stamps, a.stats, stats_bytes, hipMemcpyDeviceToHost, st));
     } else {
         ProfScope ps(ctx, PCP_K_RAYCAST_FAN);
-        hipLaunchKernelGGL(k_raycast_fan<false>, dim3((rays + kT - 1) / kT, P), dim3(kT), 0, st, a);
+        hipLaunchKernelGGL(k_raycast_fan<FAN_PLAIN>, grid, dim3(kT), 0, st, a);
         PCP_CHECK_LAUNCH(ctx);
     }
+    hipLaunchKernelGGL(k_fan_reduce, dim3(P), dim3(kT), 0, st, (const uint32_t *)a.wave_blocked,
+                       (const uint32_t *)a.wave_units, waves, blocked_d, units_d);
+    PCP_CHECK_LAUNCH(ctx);
     std::vector<uint64_t> u_h(P);
     PCP_HIP(ctx, hipMemcpyAsync(blocked, blocked_d, (size_t)P * sizeof(uint32_t),
                                 hipMemcpyDeviceToHost, st));
@@ -793,7 +917,8 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
 
 int pcp_raycast_fan(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
                     uint32_t *blocked, uint64_t *units, int16_t *first_hit, int64_t *best_idx) {
-    return raycast_fan_impl(ctx, poses5, n, fan, blocked, units, first_hit, best_idx, nullptr);
+    return raycast_fan_impl(ctx, poses5, n, fan, blocked, units, first_hit, best_idx, nullptr,
+                            nullptr);
 }
 
 int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
@@ -801,7 +926,16 @@ int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
     if (!ctx || !stats) return PCP_E_INVALID;
     std::vector<uint32_t> blocked(n ? n : 1);
     stats[0] = stats[1] = stats[2] = 0;
-    return raycast_fan_impl(ctx, poses5, n, fan, blocked.data(), nullptr, nullptr, nullptr, stats);
+    return raycast_fan_impl(ctx, poses5, n, fan, blocked.data(), nullptr, nullptr, nullptr, stats,
+                            nullptr);
+}
+
+int pcp_raycast_fan_stamps(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                           const pcp_fan_params *fan, uint64_t *stamps) {
+    if (!ctx || !stamps) return PCP_E_INVALID;
+    std::vector<uint32_t> blocked(n ? n : 1);
+    return raycast_fan_impl(ctx, poses5, n, fan, blocked.data(), nullptr, nullptr, nullptr,
+                            nullptr, stamps);
 }
 
 }  // extern "C"

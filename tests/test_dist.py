@@ -1,0 +1,113 @@
+"""Multi-process (world_size 2, gloo on CPU) coverage of the pose-sharded search: each rank
+scores its contiguous shard and ONE all-reduce yields the same best pose and score vector as a
+single process over all poses.  The per-rank scorer stands in for the GPU
+kernel: the oracle (CPU restatement) of the fan march / cell scoring on the golden mini scene.
+"""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLD = ROOT / "tests" / "golden"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_q):
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import pyoracle
+
+        from pointcloud_processor_amd import dist as pd
+
+        d = np.load(GOLD / "fan.npz")
+        T = pyoracle.Cloud(d["terrain"])
+        poses = np.concatenate([d["poses"], d["poses"][:, :] + [0.3, -0.2, 0.0, 0.0, 0.5]])
+        P = poses.shape[0]
+        lo, hi = pd.shard(P, world, rank)
+        b, _, _ = pyoracle.raycast_fan(T, poses[lo:hi], int(d["n_az"]), int(d["n_el"]),
+                                       float(d["el_min"]), float(d["el_max"]),
+                                       float(d["max_distance"]), want_first_hit=False)
+        keys, best = pd.reduce_fan(b, lo, hi, P, dist, "cpu")
+        s = np.load(GOLD / "score.npz")
+        Ts, A = pyoracle.Cloud(s["terrain"]), pyoracle.Cloud(s["aux"])
+        cand = s["candidates"]
+        lo2, hi2 = pd.shard(cand.shape[0], world, rank)
+        flags = np.zeros(s["cells"].shape[0], np.uint8)
+        tot, _, _ = pyoracle.score_poses(Ts, A, s["cells"], s["normals"], cand[lo2:hi2], s["zx"],
+                                         pyoracle.vl_params(max_distance=float(s["max_distance"])),
+                                         flags)
+        vec, bidx, bscore = pd.reduce_scores(tot, lo2, hi2, cand.shape[0], dist, "cpu")
+        out_q.put((rank, keys, best, vec, bidx, bscore))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_partition():
+    from pointcloud_processor_amd import dist as pd
+
+    for total in (0, 1, 7, 256, 4096, 4097):
+        for world in (1, 2, 3, 8):
+            parts = [pd.shard(total, world, r) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+            sizes = [h - l for l, h in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_reduce_single_process_semantics():
+    from pointcloud_processor_amd import dist as pd
+
+    keys, best = pd.reduce_fan(np.array([5, 3, 3, 9]), 0, 4, 4)
+    assert best == 1                                  # ties -> lowest index
+    vec, bidx, bs = pd.reduce_scores(np.array([1.0, 4.0, 4.0, 2.0]), 0, 4, 4)
+    assert bidx == 1 and bs == 4.0                    # strict '>' keeps the first maximum
+    vec, bidx, bs = pd.reduce_scores(np.zeros(0), 0, 0, 0)
+    assert bidx == -1 and bs == -np.inf
+
+
+def test_two_rank_gloo_matches_single_process():
+    import pyoracle
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference over all poses
+    d = np.load(GOLD / "fan.npz")
+    T = pyoracle.Cloud(d["terrain"])
+    poses = np.concatenate([d["poses"], d["poses"][:, :] + [0.3, -0.2, 0.0, 0.0, 0.5]])
+    b, _, _ = pyoracle.raycast_fan(T, poses, int(d["n_az"]), int(d["n_el"]), float(d["el_min"]),
+                                   float(d["el_max"]), float(d["max_distance"]),
+                                   want_first_hit=False)
+    s = np.load(GOLD / "score.npz")
+    for rank, keys, best, vec, bidx, bscore in res:
+        np.testing.assert_array_equal(keys, b.astype(np.int64))
+        assert best == int(np.argmin(b))
+        np.testing.assert_array_equal(vec, s["total"])     # golden: one process, all poses
+        assert bidx == int(s["report"][0])
+        assert bscore == float(s["best_score"])

@@ -27,4 +27,18 @@ fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline
 fi
+if [ "$WHAT" = modes ]; then
+  step bench_filter 300 python bench.py --mode filter --steps 10 --warmup 2
+  step bench_cells 300 python bench.py --mode cells --steps 5 --warmup 1
+fi
+if [ "$WHAT" = pmc ] || [ "$WHAT" = modes ]; then
+  # counters in their own passes (no trace domains besides kernel dispatch)
+  i=0
+  for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
+             "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+             "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    step pmc$i 300 rocprofv3 --pmc $set -d gpurun_out/pmc$i -o pmc --output-format csv -- python3 bench.py ${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}
+  done
+fi
 echo "=== done"
