@@ -78,6 +78,7 @@ enum pcp_kernel_id {
     PCP_K_CROP,              /* crop-box stream compaction                           */
     PCP_K_VOXEL,             /* voxel keying + sort + centroid                       */
     PCP_K_TRANSFORM,         /* SE(3) + RGB + concat                                  */
+    PCP_K_FILTER_MERGE,      /* whole crop->voxel->transform pipeline (graph replay)   */
     PCP_K_COUNT
 };
 int pcp_profile_enable(pcp_ctx *ctx, int enable);

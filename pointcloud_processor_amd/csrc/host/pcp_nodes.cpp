@@ -1,0 +1,251 @@
+// pcp_nodes.cpp -- host-side node cores over libpcp's C ABI (see pcp_nodes.hpp).
+#include "pcp_nodes.hpp"
+
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <stdexcept>
+
+namespace pcp {
+
+// ---- PointCloud2 helpers -------------------------------------------------------------------
+static PointCloud2 make_cloud(const void *rec, size_t n, uint32_t step,
+                              std::vector<PointField> fields, const std::string &frame) {
+    PointCloud2 m;
+    m.frame_id = frame;
+    m.height = 1;
+    m.width = (uint32_t)n;
+    m.fields = std::move(fields);
+    m.point_step = step;
+    m.row_step = step * m.width;
+    m.data.resize(n * step);
+    if (n) std::memcpy(m.data.data(), rec, n * step);
+    m.is_dense = true;
+    return m;
+}
+
+PointCloud2 make_xyz_cloud(const float *xyz16, size_t n, const std::string &frame) {
+    return make_cloud(xyz16, n, 16, {{"x", 0}, {"y", 4}, {"z", 8}}, frame);
+}
+
+PointCloud2 make_xyzrgb_cloud(const void *rec32, size_t n, const std::string &frame) {
+    return make_cloud(rec32, n, 32, {{"x", 0}, {"y", 4}, {"z", 8}, {"rgb", 16}}, frame);
+}
+
+bool cloud_view(const PointCloud2 &m, pcp_cloud_view &v, std::string *why) {
+    int ox = -1, oy = -1, oz = -1;
+    for (const auto &f : m.fields) {
+        if (f.datatype != PointField::FLOAT32) continue;
+        if (f.name == "x") ox = (int)f.offset;
+        else if (f.name == "y") oy = (int)f.offset;
+        else if (f.name == "z") oz = (int)f.offset;
+    }
+    if (ox < 0 || oy < 0 || oz < 0) {
+        if (why) *why = "cloud has no FLOAT32 x/y/z fields";
+        return false;
+    }
+    if (m.is_bigendian || (m.size() && m.row_step != m.width * m.point_step) ||
+        m.data.size() < m.size() * m.point_step) {
+        if (why) *why = "unsupported PointCloud2 layout (big endian or padded rows)";
+        return false;
+    }
+    v.data = m.data.empty() ? nullptr : m.data.data();
+    v.n = m.size();
+    v.point_step = m.point_step;
+    v.off_x = (uint32_t)ox;
+    v.off_y = (uint32_t)oy;
+    v.off_z = (uint32_t)oz;
+    return true;
+}
+
+Device::Device(int device) {
+    const int rc = pcp_create(device, &ctx_);
+    if (rc != PCP_OK) throw std::runtime_error("pcp_create failed (no gfx950 device?)");
+}
+
+Device::~Device() { pcp_destroy(ctx_); }
+
+// ---- pointcloud_filter -----------------------------------------------------------------------
+PointCloud2 SimplifiedScanMatcher::processCloudSimple(const PointCloud2 &in,
+                                                      const std::string &vehicle_type) {
+    // cropFrontArea parameter selection (:93-101)
+    double front, side, height;
+    if (vehicle_type == "robot") {
+        front = p_.robot_front_range;
+        side = p_.robot_side_range;
+        height = p_.robot_height_range;
+    } else {
+        front = p_.backhoe_front_range;
+        side = p_.backhoe_side_range;
+        height = p_.backhoe_height_range;
+    }
+    const double box[6] = {0.0, front, -side, side, -1.5, height};   // :111-113
+    pcp_cloud_view v{};
+    PointCloud2 out = make_xyz_cloud(nullptr, 0, in.frame_id);
+    out.stamp = in.stamp;   // output_msg->header = input_msg->header (:79)
+    if (!cloud_view(in, v, &err_)) return out;
+    std::vector<float> buf(4 * (v.n ? v.n : 1));
+    uint64_t n_out = 0, n_crop = 0;
+    if (pcp_crop_voxel(dev_.ctx(), &v, box, (float)p_.voxel_leaf_size, buf.data(), v.n, &n_out,
+                       &n_crop) != PCP_OK) {
+        err_ = dev_.error();
+        return out;
+    }
+    last_cropped_ = n_crop;
+    out = make_xyz_cloud(buf.data(), n_out, in.frame_id);
+    out.stamp = in.stamp;
+    return out;
+}
+
+// ---- pointcloud_merger -----------------------------------------------------------------------
+GnssGicpMatcher::Output GnssGicpMatcher::processPointClouds(bool origin_set,
+                                                           const Transform *robot_tf,
+                                                           const Transform *zx120_tf) {
+    Output o;
+    o.merged = make_xyzrgb_cloud(nullptr, 0, "map");
+    o.robot_colored = o.merged;
+    o.backhoe_colored = o.merged;
+    if (!origin_set) return o;   // :309
+    pcp_cloud_view v[2];
+    pcp_rigid tf[2];
+    uint8_t rgb[6];
+    int k = 0, which[2];
+    struct Src { const PointCloud2 *m; const Transform *t; uint8_t r, g, b; };
+    const Src src[2] = {{have_robot_ ? &robot_ : nullptr, robot_tf, 255, 0, 0},       // red
+                        {have_backhoe_ ? &backhoe_ : nullptr, zx120_tf, 0, 0, 255}};  // blue
+    for (int i = 0; i < 2; ++i) {
+        if (!src[i].m || !src[i].t) continue;   // no message yet / TF lookup failed: skip
+        if (!cloud_view(*src[i].m, v[k], &err_)) continue;
+        std::memcpy(tf[k].t, src[i].t->t, sizeof(tf[k].t));
+        std::memcpy(tf[k].q, src[i].t->q, sizeof(tf[k].q));
+        rgb[3 * k] = src[i].r;
+        rgb[3 * k + 1] = src[i].g;
+        rgb[3 * k + 2] = src[i].b;
+        which[k++] = i;
+    }
+    uint64_t total = 0;
+    for (int i = 0; i < k; ++i) total += v[i].n;
+    std::vector<uint8_t> buf(32 * (total ? total : 1));
+    uint64_t n = 0;
+    if (k && pcp_transform_concat(dev_.ctx(), k, v, tf, rgb, buf.data(), total, &n) != PCP_OK) {
+        err_ = dev_.error();
+        return o;
+    }
+    o.merged = make_xyzrgb_cloud(buf.data(), n, "map");
+    uint64_t base = 0;
+    for (int i = 0; i < k; ++i) {
+        PointCloud2 part = make_xyzrgb_cloud(buf.data() + 32 * base, v[i].n, "map");
+        (which[i] == 0 ? o.robot_colored : o.backhoe_colored) = std::move(part);
+        base += v[i].n;
+    }
+    return o;
+}
+
+// ---- virtual_lidar ---------------------------------------------------------------------------
+void SimplifiedDualLidarOptimizer::terrainCallback(const PointCloud2 &msg) {
+    terrain_cloud_ = true;
+    pcp_cloud_view v{};
+    if (!cloud_view(msg, v, &err_)) return;
+    // empty cloud: the old tree stays (:184-191), ground heights see the empty cloud
+    if (pcp_set_terrain(dev_.ctx(), &v) != PCP_OK) err_ = dev_.error();
+}
+
+void SimplifiedDualLidarOptimizer::zx120PointsCallback(const PointCloud2 &msg) {
+    pcp_cloud_view v{};
+    if (!cloud_view(msg, v, &err_)) return;
+    if (pcp_set_aux_cloud(dev_.ctx(), &v) != PCP_OK) err_ = dev_.error();
+}
+
+void SimplifiedDualLidarOptimizer::setExcavationGrid(const std::vector<double> &xyz,
+                                                     const std::vector<float> &normals,
+                                                     const double grid_bbox[6]) {
+    n_cells_ = xyz.size() / 3;
+    flags_.assign(n_cells_, 0);   // fresh GridCells (:259, ctor :34-43)
+    std::memcpy(bbox_, grid_bbox, sizeof(bbox_));
+    if (pcp_set_cells(dev_.ctx(), xyz.data(), normals.data(), n_cells_) != PCP_OK) {
+        err_ = dev_.error();
+        n_cells_ = 0;
+    }
+}
+
+static void appendf(std::string &s, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+static void appendf(std::string &s, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    s += buf;
+    s += '\n';
+}
+
+SimplifiedDualLidarOptimizer::Result SimplifiedDualLidarOptimizer::runOptimization(
+    const Transform *zx120_base) {
+    Result r;
+    // :455 -- no grid, no terrain message, or getZX120Position failed
+    if (n_cells_ == 0 || !terrain_cloud_ || !zx120_base) return r;
+    // getZX120Position (:342-358)
+    r.zx120.x = zx120_base->t[0] + 0.4;
+    r.zx120.y = zx120_base->t[1] + 0.5;
+    r.zx120.z = zx120_base->t[2] + 3.5;
+    r.zx120.pitch = -M_PI / 6;
+    r.zx120.yaw = 0.0;
+    const double zx[5] = {r.zx120.x, r.zx120.y, r.zx120.z, r.zx120.pitch, r.zx120.yaw};
+    const pcp_vl_params p{p_.grid_resolution, p_.sensor_height, p_.search_radius, p_.max_distance,
+                          p_.num_candidates, p_.vertical_layers};
+    const int gs = (int)std::ceil(std::sqrt((double)p_.num_candidates));
+    std::vector<double> poses(5 * (size_t)std::max(1, gs * gs));
+    uint64_t n = 0;
+    if (pcp_generate_candidates(dev_.ctx(), bbox_, &p, zx, poses.data(), poses.size() / 5, &n) !=
+        PCP_OK) {
+        err_ = dev_.error();
+        return r;
+    }
+    std::vector<double> totals(n ? n : 1);
+    if (pcp_score_poses(dev_.ctx(), poses.data(), n, zx, &p, flags_.data(), totals.data(), nullptr,
+                        &r.report) != PCP_OK) {
+        err_ = dev_.error();
+        return r;
+    }
+    r.ran = true;
+    r.candidates.resize(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        LidarPosition &c = r.candidates[i];
+        c.x = poses[5 * i];
+        c.y = poses[5 * i + 1];
+        c.z = poses[5 * i + 2];
+        c.pitch = poses[5 * i + 3];
+        c.yaw = poses[5 * i + 4];
+        c.total_score = totals[i];
+    }
+    r.best_score = r.report.best_score;
+    if (r.report.best_idx >= 0) r.best = r.candidates[r.report.best_idx];   // else default (:465)
+    // the two RCLCPP_INFO tables
+    const pcp_vl_report &q = r.report;
+    const int tc = q.total_cells;
+    auto pct = [tc](int v) { return tc > 0 ? (double)v / tc * 100.0 : 0.0; };
+    appendf(r.log, "ZX120 Position: (%.2f, %.2f, %.2f)", r.zx120.x, r.zx120.y, r.zx120.z);
+    appendf(r.log, "Total Score (ZX120 only): %.2f", q.zx120_total_score);
+    appendf(r.log, "  Cells in range: %d (%.1f%%)", q.zx120_range_ok, pct(q.zx120_range_ok));
+    appendf(r.log, "  Cells in FOV: %d (%.1f%%)", q.zx120_fov_ok, pct(q.zx120_fov_ok));
+    appendf(r.log, "  Cells visible: %d (%.1f%%)", q.zx120_visible_ok, pct(q.zx120_visible_ok));
+    appendf(r.log, "  Green (Observable): %d cells (%.1f%%)", q.zx120_green, pct(q.zx120_green));
+    appendf(r.log, "  Red (Occluded): %d cells (%.1f%%)", q.zx120_red, pct(q.zx120_red));
+    appendf(r.log, "  Blue (Out of range): %d cells (%.1f%%)", q.zx120_blue, pct(q.zx120_blue));
+    appendf(r.log, "  Yellow (Out of FOV): %d cells (%.1f%%)", q.zx120_yellow, pct(q.zx120_yellow));
+    appendf(r.log, "Best Mobile LiDAR Position: (%.2f, %.2f, %.2f)", r.best.x, r.best.y, r.best.z);
+    appendf(r.log, "Total Score: %.2f", r.best_score);
+    appendf(r.log, "  Total cells: %d", tc);
+    appendf(r.log, "  Green (Observable): %d cells (%.1f%%)", q.green, pct(q.green));
+    appendf(r.log, "  Red (Occluded): %d cells (%.1f%%)", q.red, pct(q.red));
+    appendf(r.log, "  Blue (Out of range): %d cells (%.1f%%)", q.blue, pct(q.blue));
+    appendf(r.log, "  Yellow (Out of FOV): %d cells (%.1f%%)", q.yellow, pct(q.yellow));
+    const double rg = q.green > 0 ? (double)q.red / q.green
+                                  : (q.red > 0 ? std::numeric_limits<double>::infinity() : 0.0);
+    appendf(r.log, "  Red/Green Ratio: %.3f", rg);
+    const int unobs = q.red + q.blue + q.yellow;
+    appendf(r.log, "  Total Unobservable: %d cells (%.1f%%)", unobs, pct(unobs));
+    return r;
+}
+
+}  // namespace pcp

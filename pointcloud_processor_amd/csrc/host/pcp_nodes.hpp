@@ -1,0 +1,153 @@
+// pcp_nodes.hpp -- C++ host side above the C ABI: the algorithm part of the reference's three
+// ROS2 nodes, with the reference's class and method names, parameter names/defaults and
+// log-and-skip error behaviour.  No ROS dependency: an rclcpp shell owns one of these per node
+// and forwards its callbacks.  Every compute call goes to libpcp (HIP).
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pcp_abi.h"
+
+namespace pcp {
+
+// ---- sensor_msgs::msg::PointCloud2 (the fields the nodes read/write) -------------------------
+struct PointField {
+    enum : uint8_t { INT8 = 1, UINT8, INT16, UINT16, INT32, UINT32, FLOAT32, FLOAT64 };
+    std::string name;
+    uint32_t offset = 0;
+    uint8_t datatype = FLOAT32;
+    uint32_t count = 1;
+};
+
+struct PointCloud2 {
+    std::string frame_id;
+    double stamp = 0.0;
+    uint32_t height = 1, width = 0;
+    std::vector<PointField> fields;
+    bool is_bigendian = false;
+    uint32_t point_step = 0, row_step = 0;
+    std::vector<uint8_t> data;
+    bool is_dense = true;
+    size_t size() const { return (size_t)width * height; }
+    bool empty() const { return size() == 0; }
+};
+
+// pcl::toROSMsg layouts
+PointCloud2 make_xyz_cloud(const float *xyz16, size_t n, const std::string &frame);  // PointXYZ
+PointCloud2 make_xyzrgb_cloud(const void *rec32, size_t n, const std::string &frame);
+// the pcl::fromROSMsg field lookup: FLOAT32 x/y/z by name
+bool cloud_view(const PointCloud2 &m, pcp_cloud_view &v, std::string *why = nullptr);
+
+struct Transform {   // geometry_msgs::msg::Transform
+    double t[3] = {0, 0, 0};
+    double q[4] = {0, 0, 0, 1};   // x, y, z, w
+};
+
+// one HIP device context shared by the node cores of a process
+class Device {
+   public:
+    explicit Device(int device = 0);
+    ~Device();
+    Device(const Device &) = delete;
+    Device &operator=(const Device &) = delete;
+    pcp_ctx *ctx() const { return ctx_; }
+    const char *error() const { return pcp_last_error(ctx_); }
+
+   private:
+    pcp_ctx *ctx_ = nullptr;
+};
+
+// ---- pointcloud_filter.cpp (SimplifiedScanMatcher) -----------------------------------------
+class SimplifiedScanMatcher {
+   public:
+    struct Params {   // pointcloud_filter.cpp:30-39
+        double robot_front_range = 15.0, robot_side_range = 10.0, robot_height_range = 10.0;
+        double backhoe_front_range = 15.0, backhoe_side_range = 10.0, backhoe_height_range = 10.0;
+        double voxel_leaf_size = 0.2;
+    };
+    explicit SimplifiedScanMatcher(Device &dev, Params p = {}) : dev_(dev), p_(p) {}
+    Params &params() { return p_; }
+    // callbacks (:52-62): the returned message is what the node publishes
+    PointCloud2 robotCloudCallback(const PointCloud2 &msg) { return processCloudSimple(msg, "robot"); }
+    PointCloud2 backhoeCloudCallback(const PointCloud2 &msg) { return processCloudSimple(msg, "backhoe"); }
+    // fromROSMsg -> cropFrontArea -> downsampleCloud -> toROSMsg, header kept (:64-85)
+    PointCloud2 processCloudSimple(const PointCloud2 &in, const std::string &vehicle_type);
+    size_t lastCroppedSize() const { return last_cropped_; }
+    const std::string &lastError() const { return err_; }
+
+   private:
+    Device &dev_;
+    Params p_;
+    size_t last_cropped_ = 0;
+    std::string err_;
+};
+
+// ---- pointcloud_merger.cpp (GnssGicpMatcher, cloud part) ------------------------------------
+class GnssGicpMatcher {
+   public:
+    explicit GnssGicpMatcher(Device &dev) : dev_(dev) {}
+    void robotCloudCallback(const PointCloud2 &msg) { robot_ = msg; have_robot_ = true; }      // :176-178
+    void backhoeCloudCallback(const PointCloud2 &msg) { backhoe_ = msg; have_backhoe_ = true; } // :180-182
+    struct Output {
+        PointCloud2 merged, robot_colored, backhoe_colored;   // /matched_point_cloud, ...
+    };
+    // processPointClouds (:308-352).  The caller did the TF lookups map <- */velodyne_link
+    // (:362-366); nullptr = the lookup threw, and that robot is skipped (:389-393).
+    Output processPointClouds(bool origin_set, const Transform *robot_tf, const Transform *zx120_tf);
+    const std::string &lastError() const { return err_; }
+
+   private:
+    Device &dev_;
+    PointCloud2 robot_, backhoe_;
+    bool have_robot_ = false, have_backhoe_ = false;
+    std::string err_;
+};
+
+// ---- virtual_lidar.cpp (SimplifiedDualLidarOptimizer) --------------------------------------
+class SimplifiedDualLidarOptimizer {
+   public:
+    struct Params {   // virtual_lidar.cpp:66-71
+        double grid_resolution = 0.1, sensor_height = 1.1, search_radius = 3.0,
+               max_distance = 15.0;
+        int num_candidates = 100, vertical_layers = 10;
+    };
+    struct LidarPosition {   // :46-51
+        double x = 0, y = 0, z = 10, pitch = -M_PI / 2, yaw = 0, total_score = 0;
+    };
+    struct Result {
+        bool ran = false;                  // false: early return of :455
+        LidarPosition best;                // /optimal_mobile_lidar_position
+        double best_score = -INFINITY;
+        LidarPosition zx120;
+        std::vector<LidarPosition> candidates;   // with total_score (publishCandidatePositions)
+        pcp_vl_report report{};
+        std::string log;                   // the RCLCPP_INFO tables (:419-451, :522-543)
+    };
+    explicit SimplifiedDualLidarOptimizer(Device &dev, Params p = {}) : dev_(dev), p_(p) {}
+    Params &params() { return p_; }
+    void terrainCallback(const PointCloud2 &msg);       // :180-192
+    void zx120PointsCallback(const PointCloud2 &msg);   // :194-207
+    // the valid cells of generateExcavationGrid3D (:236-287) with computeCellSurfaceNormal;
+    // grid_bbox = grid_min_x, grid_max_x, grid_min_y, grid_max_y, excavation_min_z/max_z
+    void setExcavationGrid(const std::vector<double> &xyz, const std::vector<float> &normals,
+                           const double grid_bbox[6]);
+    // runOptimization (:454-548); zx120_base = TF map -> zx120/base_link, nullptr = missing
+    Result runOptimization(const Transform *zx120_base);
+    const std::vector<uint8_t> &cellFlags() const { return flags_; }
+    const std::string &lastError() const { return err_; }
+
+   private:
+    Device &dev_;
+    Params p_;
+    bool terrain_cloud_ = false;   // terrain_cloud_ non-null (a message arrived)
+    size_t n_cells_ = 0;
+    double bbox_[6] = {0, 0, 0, 0, 0, 0};
+    std::vector<uint8_t> flags_;   // GridCell flag state across ticks
+    std::string err_;
+};
+
+}  // namespace pcp

@@ -1,6 +1,7 @@
 // pcp_context.hip -- context, errors, profiling, device helpers, prefix scan.
 #include <cmath>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -81,16 +82,16 @@ static hipEvent_t take_event(pcp_ctx *ctx) {
     return e;
 }
 
-ProfScope::ProfScope(pcp_ctx *c, int k) : ctx(c), kid(k) {
-    if (!ctx->prof) return;
+ProfScope::ProfScope(pcp_ctx *c, int k, hipStream_t s) : ctx(c), kid(k), st(s ? s : c->stream) {
+    if (!ctx->prof || kid < 0 || ctx->capturing) return;
     a = take_event(ctx);
     b = take_event(ctx);
-    if (a) (void)hipEventRecord(a, ctx->stream);
+    if (a) (void)hipEventRecord(a, st);
 }
 
 ProfScope::~ProfScope() {
-    if (!ctx->prof || !a || !b) return;
-    (void)hipEventRecord(b, ctx->stream);
+    if (!a || !b) return;
+    (void)hipEventRecord(b, st);
     ctx->pending.push_back({kid, a, b});
 }
 
@@ -246,6 +247,8 @@ int pcp_create(int device, pcp_ctx **out) {
     pcp_ctx *ctx = new (std::nothrow) pcp_ctx();
     if (!ctx) return PCP_E_NOMEM;
     ctx->device = device;
+    if (const char *fb = std::getenv("PCP_FAN_BATCH")) ctx->fan_batch = std::atoi(fb);
+    if (const char *ng = std::getenv("PCP_NO_GRAPHS")) ctx->use_graphs = std::atoi(ng) == 0;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return PCP_E_HIP;
@@ -262,13 +265,18 @@ void pcp_destroy(pcp_ctx *ctx) {
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     ctx->terrain.release();
     ctx->aux.release();
-    DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage,  &ctx->fan_tab, &ctx->poses_d,
-                      &ctx->steps_d,   &ctx->out_a,     &ctx->out_b,  &ctx->out_c,   &ctx->out_d,
-                      &ctx->stats_d,   &ctx->f_in,      &ctx->f_xyz,  &ctx->f_idx,   &ctx->f_keys[0],
-                      &ctx->f_keys[1], &ctx->f_vals[0], &ctx->f_vals[1], &ctx->f_hist, &ctx->f_out,
+    DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage, &ctx->fan_tab,
+                      &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,
+                      &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->f_in,
                       &ctx->f_misc};
     for (DevBuf *b : bufs) b->release();
     for (auto &b : ctx->scratch) b.release();
+    for (auto &b : ctx->fbuf) b.release();
+    for (hipStream_t s2 : ctx->side) (void)hipStreamDestroy(s2);
+    for (hipEvent_t e : ctx->side_ev) (void)hipEventDestroy(e);
+    if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
+    if (ctx->fm_exec) (void)hipGraphExecDestroy(ctx->fm_exec);
+    if (ctx->fm_graph) (void)hipGraphDestroy(ctx->fm_graph);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -336,7 +344,7 @@ const char *pcp_kernel_name(int kid) {
     static const char *names[PCP_K_COUNT] = {"raycast_fan", "score_cells", "zx120_cells",
                                              "pose_sum",    "cell_flags",  "candidates",
                                              "index_build", "crop",        "voxel",
-                                             "transform"};
+                                             "transform",   "filter_merge"};
     if (kid < 0 || kid >= PCP_K_COUNT) return "unknown";
     return names[kid];
 }

@@ -77,12 +77,22 @@ __global__ void __launch_bounds__(kFT) k_crop_count(CloudIn c, Box b, uint32_t *
 
 // ---- crop pass 2: stable write + bbox partials of the kept points -------------------------
 __global__ void __launch_bounds__(kFT)
-k_crop_write(CloudIn c, Box b, const uint32_t *__restrict__ offs, uint32_t *__restrict__ kept_idx,
-             float4 *__restrict__ out, float *__restrict__ part) {
+k_crop_write(CloudIn c, Box b, const uint32_t *__restrict__ counts, uint32_t *__restrict__ m_out,
+             uint32_t *__restrict__ kept_idx, float4 *__restrict__ out, float *__restrict__ part) {
     const uint64_t base = (uint64_t)blockIdx.x * kCropTile;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     __shared__ uint32_t wcnt[kFT / 64];
-    uint32_t run = offs[blockIdx.x];
+    // this tile's output offset = sum of the kept counts of all earlier tiles (each block sums
+    // them itself: no separate scan launch; nb is at most a few thousand)
+    uint32_t pre_t = 0;
+    for (uint32_t t = threadIdx.x; t < blockIdx.x; t += kFT) pre_t += counts[t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pre_t += __shfl_xor(pre_t, o, 64);
+    if (lane == 0) wcnt[wid] = pre_t;
+    __syncthreads();
+    uint32_t run = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    __syncthreads();
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *m_out = run + counts[blockIdx.x];
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (int it = 0; it < kCropItems; ++it) {
         const uint64_t i = base + (uint64_t)it * kFT + threadIdx.x;
@@ -139,8 +149,9 @@ k_crop_write(CloudIn c, Box b, const uint32_t *__restrict__ offs, uint32_t *__re
 
 // ---- voxel parameters (VoxelGrid::applyFilter, computed in float exactly) -------------------
 struct VoxParams {
-    uint32_t m;          // points into the voxel stage
+    uint32_t m;          // points after the crop
     int32_t overflow;    // PCL int32 guard fired -> passthrough
+    int32_t do_voxel;    // leaf > 0
     float inv;
     int32_t min_b[3];
     int32_t div_b[3];
@@ -148,20 +159,46 @@ struct VoxParams {
     uint64_t nvox;       // div product (key upper bound)
 };
 
-__global__ void k_vox_params(const float *__restrict__ part, int nb, const uint32_t *__restrict__ m_d,
-                             float leaf, VoxParams *__restrict__ vp) {
-    if (threadIdx.x != 0) return;
+// block-reduced voxel parameters (VoxelGrid::applyFilter arithmetic in float, exactly)
+__global__ void __launch_bounds__(kFT)
+k_vox_params(const float *__restrict__ part, int nb, const uint32_t *__restrict__ m_d, float leaf,
+             VoxParams *__restrict__ vp) {
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-    for (int b = 0; b < nb; ++b)
+    for (int b = threadIdx.x; b < nb; b += kFT)
         for (int a = 0; a < 3; ++a) {
             mn[a] = fminf(mn[a], part[b * 6 + a]);
             mx[a] = fmaxf(mx[a], part[b * 6 + 3 + a]);
         }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
+            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
+        }
+    __shared__ float s[6][kFT / 64];
+    if ((threadIdx.x & 63) == 0)
+        for (int a = 0; a < 3; ++a) {
+            s[a][threadIdx.x >> 6] = mn[a];
+            s[3 + a][threadIdx.x >> 6] = mx[a];
+        }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int w = 1; w < kFT / 64; ++w)
+        for (int a = 0; a < 3; ++a) {
+            s[a][0] = fminf(s[a][0], s[a][w]);
+            s[3 + a][0] = fmaxf(s[3 + a][0], s[3 + a][w]);
+        }
+    for (int a = 0; a < 3; ++a) {
+        mn[a] = s[a][0];
+        mx[a] = s[3 + a][0];
+    }
     VoxParams p{};
     p.m = *m_d;
-    const float inv = 1.0f / leaf;
+    p.do_voxel = leaf > 0.0f ? 1 : 0;
+    const float inv = p.do_voxel ? 1.0f / leaf : 0.0f;
     p.inv = inv;
-    if (p.m == 0) {
+    if (p.m == 0 || !p.do_voxel) {
         *vp = p;
         return;
     }
@@ -181,53 +218,94 @@ __global__ void k_vox_params(const float *__restrict__ part, int nb, const uint3
     *vp = p;
 }
 
+// points that go through the sort: all cropped points when voxelising without overflow
+__device__ __forceinline__ uint32_t sort_count(const VoxParams &vp) {
+    return (vp.do_voxel && !vp.overflow) ? vp.m : 0u;
+}
+
 __global__ void __launch_bounds__(kFT)
 k_vox_keys(const float4 *__restrict__ xyz, const VoxParams *__restrict__ vpp,
            uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     const VoxParams vp = *vpp;
-    const uint32_t i = blockIdx.x * kFT + threadIdx.x;
-    if (i >= vp.m) return;
-    const float4 p = xyz[i];
-    const int ijk0 = (int)(floorf(p.x * vp.inv) - (float)vp.min_b[0]);
-    const int ijk1 = (int)(floorf(p.y * vp.inv) - (float)vp.min_b[1]);
-    const int ijk2 = (int)(floorf(p.z * vp.inv) - (float)vp.min_b[2]);
-    keys[i] = (uint32_t)ijk0 + (uint32_t)ijk1 * vp.mul1 + (uint32_t)ijk2 * vp.mul2;
-    vals[i] = i;
+    const uint32_t m = sort_count(vp);
+    for (uint32_t i = blockIdx.x * kFT + threadIdx.x; i < m; i += gridDim.x * kFT) {
+        const float4 p = xyz[i];
+        const int ijk0 = (int)(floorf(p.x * vp.inv) - (float)vp.min_b[0]);
+        const int ijk1 = (int)(floorf(p.y * vp.inv) - (float)vp.min_b[1]);
+        const int ijk2 = (int)(floorf(p.z * vp.inv) - (float)vp.min_b[2]);
+        keys[i] = (uint32_t)ijk0 + (uint32_t)ijk1 * vp.mul1 + (uint32_t)ijk2 * vp.mul2;
+        vals[i] = i;
+    }
 }
 
-// ---- LSD radix sort (stable), 8-bit digit -------------------------------------------------
+// ---- LSD radix sort (stable), 8-bit digits; tile count from the host-known upper bound -------
 __global__ void __launch_bounds__(kFT)
-k_radix_hist(const uint32_t *__restrict__ keys, uint32_t m, int shift, uint32_t nblk,
-             uint32_t *__restrict__ hist) {
+k_radix_hist(const uint32_t *__restrict__ keys, const VoxParams *__restrict__ vpp, int shift,
+             uint32_t nblk, uint32_t *__restrict__ hist) {
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
+    const uint32_t m = sort_count(*vpp);
     const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    if (base < m) {
 #pragma unroll 4
-    for (int it = 0; it < kSortItems; ++it) {
-        const uint64_t i = base + (uint64_t)it * kFT + threadIdx.x;
-        if (i < m) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+        for (int it = 0; it < kSortItems; ++it) {
+            const uint64_t i = base + (uint64_t)it * kFT + threadIdx.x;
+            if (i < m) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+        }
     }
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * nblk + blockIdx.x] = h[threadIdx.x];
+    hist[(uint64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+// digit offsets of every (tile, digit): base[d] (exclusive over digits of the totals) + sum of
+// earlier tiles' counts of d.  One block, thread = digit, tiles read coalesced (block-major).
+__global__ void __launch_bounds__(kFT)
+k_digit_offsets(const uint32_t *__restrict__ hist, const VoxParams *__restrict__ vpp,
+                uint32_t *__restrict__ offs) {
+    const uint32_t m = sort_count(*vpp);
+    const uint32_t nact = (m + kSortTile - 1) / kSortTile;
+    const uint32_t d = threadIdx.x;
+    uint32_t tot = 0;
+    for (uint32_t t = 0; t < nact; ++t) tot += hist[(size_t)t * 256 + d];
+    __shared__ uint32_t lds4[kFT / 64];
+    // exclusive scan of the 256 digit totals
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) lds4[wid] = incl;
+    __syncthreads();
+    uint32_t run = incl - tot;
+    for (int w = 0; w < wid; ++w) run += lds4[w];
+    for (uint32_t t = 0; t < nact; ++t) {
+        offs[(size_t)t * 256 + d] = run;
+        run += hist[(size_t)t * 256 + d];
+    }
 }
 
 __global__ void __launch_bounds__(kFT)
-k_radix_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin, uint32_t m,
-                int shift, uint32_t nblk, const uint32_t *__restrict__ offs,
-                uint32_t *__restrict__ kout, uint32_t *__restrict__ vout) {
+k_radix_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                const VoxParams *__restrict__ vpp, int shift, uint32_t nblk,
+                const uint32_t *__restrict__ offs, uint32_t *__restrict__ kout,
+                uint32_t *__restrict__ vout) {
+    const uint32_t m = sort_count(*vpp);
+    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    if (base >= m) return;   // uniform per block
     __shared__ uint32_t run[256];
     __shared__ uint32_t wc[kFT / 64][256];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    run[threadIdx.x] = offs[(uint64_t)threadIdx.x * nblk + blockIdx.x];
-    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    run[threadIdx.x] = offs[(uint64_t)blockIdx.x * 256 + threadIdx.x];
     for (int it = 0; it < kSortItems; ++it) {
         const uint64_t i = base + (uint64_t)it * kFT + threadIdx.x;
         const bool act = i < m;
         const uint32_t k = act ? kin[i] : 0u;
         const uint32_t v = act ? vin[i] : 0u;
         const uint32_t d = (k >> shift) & 255u;
-        // lanes of this wave with the same digit (match_any by 8 ballots)
+        // lanes of this wave with the same digit (match-any from 8 ballots)
         uint64_t same = __ballot(act);
 #pragma unroll
         for (int bit = 0; bit < 8; ++bit) {
@@ -237,39 +315,89 @@ k_radix_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ v
         for (int w = 0; w < kFT / 64; ++w) wc[w][threadIdx.x] = 0;
         __syncthreads();
         const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-        const bool leader = act && rank == 0;
-        if (leader) wc[wid][d] = (uint32_t)__popcll(same);
+        if (act && rank == 0) wc[wid][d] = (uint32_t)__popcll(same);
         __syncthreads();
         if (act) {
             uint32_t pre = run[d];
             for (int w = 0; w < wid; ++w) pre += wc[w][d];
-            const uint32_t pos = pre + rank;
-            kout[pos] = k;
-            vout[pos] = v;
+            kout[pre + rank] = k;
+            vout[pre + rank] = v;
         }
         __syncthreads();
-        {
-            const uint32_t dd = threadIdx.x;   // 256 threads = 256 digits
-            run[dd] += wc[0][dd] + wc[1][dd] + wc[2][dd] + wc[3][dd];
-        }
+        run[threadIdx.x] += wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] +
+                            wc[3][threadIdx.x];
         __syncthreads();
     }
 }
 
-// ---- segments + centroids -------------------------------------------------------------------
-__global__ void __launch_bounds__(kFT)
-k_seg_heads(const uint32_t *__restrict__ keys, uint32_t m, uint32_t *__restrict__ head) {
-    const uint32_t i = blockIdx.x * kFT + threadIdx.x;
-    if (i >= m) return;
-    head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+// ---- segments + centroids (sizes on the device) ----------------------------------------------
+// a sorted position starts a voxel iff its key differs from the previous one
+__device__ __forceinline__ bool seg_head(const uint32_t *keys, uint32_t i, uint32_t m) {
+    return i < m && (i == 0 || keys[i] != keys[i - 1]);
 }
 
 __global__ void __launch_bounds__(kFT)
-k_seg_start(const uint32_t *__restrict__ head, const uint32_t *__restrict__ sid, uint32_t m,
-            uint32_t *__restrict__ seg_start) {
-    const uint32_t i = blockIdx.x * kFT + threadIdx.x;
-    if (i < m && head[i]) seg_start[sid[i]] = i;
-    if (i == 0) seg_start[sid[m]] = m;
+k_seg_count(const uint32_t *__restrict__ keys, const VoxParams *__restrict__ vpp,
+            uint32_t *__restrict__ tcount) {
+    const uint32_t m = sort_count(*vpp);
+    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    uint32_t c = 0;
+    if (base < m)
+        for (int it = 0; it < kSortItems; ++it)
+            c += seg_head(keys, (uint32_t)(base + (uint64_t)it * kFT + threadIdx.x), m) ? 1u : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    __shared__ uint32_t w[kFT / 64];
+    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tcount[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
+}
+
+// seg_start[s] = sorted position of voxel s (ascending key), seg_start[nseg] = m, *nseg_out
+__global__ void __launch_bounds__(kFT)
+k_seg_emit(const uint32_t *__restrict__ keys, const VoxParams *__restrict__ vpp,
+           const uint32_t *__restrict__ tcount, uint32_t *__restrict__ seg_start,
+           uint32_t *__restrict__ nseg_out) {
+    const uint32_t m = sort_count(*vpp);
+    const uint32_t nact = (m + kSortTile - 1) / kSortTile;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ uint32_t wcnt[kFT / 64];
+    if (blockIdx.x >= nact) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {   // m == 0
+            *nseg_out = 0;
+            seg_start[0] = 0;
+        }
+        return;
+    }
+    uint32_t pre_t = 0;
+    for (uint32_t t = threadIdx.x; t < blockIdx.x; t += kFT) pre_t += tcount[t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pre_t += __shfl_xor(pre_t, o, 64);
+    if (lane == 0) wcnt[wid] = pre_t;
+    __syncthreads();
+    uint32_t run = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kSortTile;
+    for (int it = 0; it < kSortItems; ++it) {
+        const uint32_t i = (uint32_t)(base + (uint64_t)it * kFT + threadIdx.x);
+        const bool h = seg_head(keys, i, m);
+        const uint64_t bal = __ballot(h);
+        if (lane == 0) wcnt[wid] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kFT / 64; ++w) {
+            pre += (w < wid) ? wcnt[w] : 0u;
+            tot += wcnt[w];
+        }
+        if (h) seg_start[run + pre + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = i;
+        run += tot;
+        __syncthreads();
+    }
+    if (blockIdx.x == nact - 1 && threadIdx.x == 0) {
+        *nseg_out = run;
+        seg_start[run] = m;
+    }
 }
 
 // CentroidPoint<PointXYZ>: float sums in (stable) input order, then / (float)n
@@ -278,20 +406,32 @@ k_centroid(const float4 *__restrict__ xyz, const uint32_t *__restrict__ keys,
            const uint32_t *__restrict__ vals, const uint32_t *__restrict__ seg_start,
            const uint32_t *__restrict__ nseg_p, float4 *__restrict__ out,
            uint32_t *__restrict__ out_idx, uint32_t *__restrict__ out_cnt) {
-    const uint32_t s = blockIdx.x * kFT + threadIdx.x;
-    if (s >= *nseg_p) return;
-    const uint32_t a = seg_start[s], e = seg_start[s + 1];
-    float sx = 0.f, sy = 0.f, sz = 0.f;
-    for (uint32_t l = a; l < e; ++l) {
-        const float4 p = xyz[vals[l]];
-        sx = sx + p.x;
-        sy = sy + p.y;
-        sz = sz + p.z;
+    const uint32_t nseg = *nseg_p;
+    for (uint32_t s = blockIdx.x * kFT + threadIdx.x; s < nseg; s += gridDim.x * kFT) {
+        const uint32_t a = seg_start[s], e = seg_start[s + 1];
+        float sx = 0.f, sy = 0.f, sz = 0.f;
+        for (uint32_t l = a; l < e; ++l) {
+            const float4 p = xyz[vals[l]];
+            sx = sx + p.x;
+            sy = sy + p.y;
+            sz = sz + p.z;
+        }
+        const float cnt = (float)(e - a);
+        out[s] = make_float4(sx / cnt, sy / cnt, sz / cnt, 1.0f);
+        out_idx[s] = keys[a];
+        out_cnt[s] = e - a;
     }
-    const float cnt = (float)(e - a);
-    out[s] = make_float4(sx / cnt, sy / cnt, sz / cnt, 1.0f);
-    if (out_idx) out_idx[s] = keys[a];
-    if (out_cnt) out_cnt[s] = e - a;
+}
+
+// per-cloud result size: voxel count, or the cropped count (crop only / PCL passthrough)
+__global__ void k_finish(const VoxParams *__restrict__ vpp, const uint32_t *__restrict__ nseg_p,
+                         uint32_t *__restrict__ counts, uint32_t *__restrict__ info, int slot) {
+    if (threadIdx.x != 0) return;
+    const VoxParams vp = *vpp;
+    const bool vox = vp.do_voxel && !vp.overflow;
+    counts[slot] = vox ? *nseg_p : vp.m;
+    info[2 * slot] = vp.m;          // points after the crop
+    info[2 * slot + 1] = vp.overflow;
 }
 
 // ---- SE(3) + colour (tf2::doTransform + processRobotCloud loop) ------------------------------
@@ -324,6 +464,7 @@ static Rigid make_rigid(const pcp_rigid &t, const uint8_t rgb[3]) {
     return r;
 }
 
+// Affine3f * Vector3f as the homogeneous 4x4 packet product: ((m0 x + m1 y) + m2 z) + t
 __device__ __forceinline__ void xform_store(const Rigid &r, float x, float y, float z, float4 *o) {
     const float X = ((r.m00 * x + r.m01 * y) + r.m02 * z) + r.tx;
     const float Y = ((r.m10 * x + r.m11 * y) + r.m12 * z) + r.ty;
@@ -332,18 +473,23 @@ __device__ __forceinline__ void xform_store(const Rigid &r, float x, float y, fl
     o[1] = make_float4(__uint_as_float(r.rgba), 0.f, 0.f, 0.f);
 }
 
-// from a float4 xyz stream (voxel/crop output); count from device (or host if cnt_d null)
+// transform + colour of cloud `slot`'s result into the concatenated output (robot first)
 __global__ void __launch_bounds__(kFT)
-k_xform_f4(const float4 *__restrict__ in, const uint32_t *__restrict__ cnt_d, uint32_t cnt_h,
+k_emit_rgb(const float4 *__restrict__ cropped, const float4 *__restrict__ voxels,
+           const VoxParams *__restrict__ vpp, const uint32_t *__restrict__ counts, int slot,
            Rigid r, float4 *__restrict__ out) {
-    const uint32_t n = cnt_d ? *cnt_d : cnt_h;
-    const uint32_t i = blockIdx.x * kFT + threadIdx.x;
-    if (i >= n) return;
-    const float4 p = in[i];
-    xform_store(r, p.x, p.y, p.z, out + 2 * (size_t)i);
+    const VoxParams vp = *vpp;
+    const float4 *src = (vp.do_voxel && !vp.overflow) ? voxels : cropped;
+    uint32_t base = 0;
+    for (int j = 0; j < slot; ++j) base += counts[j];
+    const uint32_t n = counts[slot];
+    for (uint32_t i = blockIdx.x * kFT + threadIdx.x; i < n; i += gridDim.x * kFT) {
+        const float4 p = src[i];
+        xform_store(r, p.x, p.y, p.z, out + 2 * ((size_t)base + i));
+    }
 }
 
-// from a raw PointCloud2 blob
+// from a raw PointCloud2 blob (pcp_transform_concat)
 __global__ void __launch_bounds__(kFT) k_xform_raw(CloudIn c, Rigid r, float4 *__restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * kFT + threadIdx.x;
     if (i >= c.n) return;
@@ -353,8 +499,163 @@ __global__ void __launch_bounds__(kFT) k_xform_raw(CloudIn c, Rigid r, float4 *_
 }
 
 // =========================================================================================
-// host orchestration
+// host orchestration: every stage enqueued on ctx->stream with sizes kept on the device, so a
+// whole crop -> voxel -> transform pipeline runs without host round trips (and can be captured
+// into a hipGraph, see pcp_filter_merge).
 // =========================================================================================
+constexpr int kMaxClouds = 64;
+
+// device views of one cloud's scratch (ctx->fbuf[slot]) plus the shared per-slot results
+struct Scratch {
+    CloudBufs *B = nullptr;
+    uint64_t ncap = 0;        // points the buffers hold
+    uint32_t nb = 0;          // crop tiles
+    uint32_t nt = 0;          // sort tiles
+    uint32_t *counts = nullptr, *mcrop = nullptr;  // crop tile counts, cropped count
+    float *part = nullptr;                         // crop bbox partials
+    uint32_t *rhist = nullptr, *rhoff = nullptr;   // radix [tile][digit]
+    uint32_t *tcount = nullptr, *nseg = nullptr;   // voxel-head counts per sort tile, voxels
+    VoxParams *vp = nullptr;  // [kMaxClouds]
+    uint32_t *res = nullptr;  // [kMaxClouds] result counts, [2*kMaxClouds] info
+    float4 *xyz() const { return B->xyz.as<float4>(); }
+    float4 *out4() const { return B->out.as<float4>(); }
+    uint32_t *seg_start() const { return reinterpret_cast<uint32_t *>(out4() + ncap + 1); }
+    uint32_t *vidx() const { return seg_start() + ncap + 2; }
+    uint32_t *vcnt() const { return vidx() + ncap + 1; }
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// (callers holding Scratch objects of several slots must size ctx->fbuf beforehand)
+static int ensure_scratch(pcp_ctx *ctx, int slot, uint64_t ncap, bool want_idx, Scratch &S) {
+    if ((int)ctx->fbuf.size() <= slot) ctx->fbuf.resize(slot + 1);
+    CloudBufs &B = ctx->fbuf[slot];
+    S.B = &B;
+    ncap = ncap ? ncap : 1;
+    S.ncap = ncap;
+    S.nb = (uint32_t)((ncap + kCropTile - 1) / kCropTile);
+    S.nt = (uint32_t)((ncap + kSortTile - 1) / kSortTile);
+    PCP_HIP(ctx, B.xyz.ensure((ncap + 1) * sizeof(float4)));
+    if (want_idx) PCP_HIP(ctx, B.idx.ensure((ncap + 1) * sizeof(uint32_t)));
+    for (int q = 0; q < 2; ++q) {
+        PCP_HIP(ctx, B.keys[q].ensure((ncap + 16) * sizeof(uint32_t)));
+        PCP_HIP(ctx, B.vals[q].ensure((ncap + 16) * sizeof(uint32_t)));
+    }
+    const size_t cb = align256((S.nb + 1) * 4), pb = align256((size_t)S.nb * 24);
+    const size_t hb = align256((size_t)S.nt * 256 * 4), tb = align256((S.nt + 1) * 4);
+    PCP_HIP(ctx, B.hist.ensure(cb + 256 + pb + 2 * hb + tb + 256));
+    char *h = B.hist.as<char>();
+    S.counts = reinterpret_cast<uint32_t *>(h);
+    S.mcrop = reinterpret_cast<uint32_t *>(h + cb);
+    S.part = reinterpret_cast<float *>(h + cb + 256);
+    S.rhist = reinterpret_cast<uint32_t *>(h + cb + 256 + pb);
+    S.rhoff = reinterpret_cast<uint32_t *>(h + cb + 256 + pb + hb);
+    S.tcount = reinterpret_cast<uint32_t *>(h + cb + 256 + pb + 2 * hb);
+    S.nseg = S.tcount + S.nt;
+    // voxel results: out4 (ncap+1) | seg_start (ncap+2) | idx (ncap+1) | cnt (ncap+1)
+    PCP_HIP(ctx, B.out.ensure((ncap + 1) * sizeof(float4) + (3 * ncap + 8) * 4 + 256));
+    PCP_HIP(ctx, ctx->f_misc.ensure(align256(kMaxClouds * sizeof(VoxParams)) + 3 * kMaxClouds * 4));
+    S.vp = reinterpret_cast<VoxParams *>(ctx->f_misc.as<char>());
+    S.res = reinterpret_cast<uint32_t *>(ctx->f_misc.as<char>() + align256(kMaxClouds * sizeof(VoxParams)));
+    return PCP_OK;
+}
+
+// radix passes needed for the voxel keys: from the crop box when it is finite (keys are below
+// prod((hi-lo)/leaf + 3)), else all 32 bits
+static int radix_passes(const Box &b, float leaf) {
+    const double lo[3] = {b.x0, b.y0, b.z0}, hi[3] = {b.x1, b.y1, b.z1};
+    double nv = 1.0;
+    for (int a = 0; a < 3; ++a) {
+        if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) return 4;
+        nv *= std::floor((hi[a] - lo[a]) / (double)leaf) + 3.0;
+    }
+    int bits = 0;
+    while (bits < 32 && std::ldexp(1.0, bits) < nv) ++bits;
+    return std::max(1, (bits + 7) / 8);
+}
+
+// enqueue crop [-> voxel] for one cloud into slot `slot` on stream `st` (results stay on the
+// device: S.res[slot] = result count)
+static int enqueue_cloud(pcp_ctx *ctx, Scratch &S, const CloudIn &c, const Box &b, float leaf,
+                         bool want_idx, int slot, hipStream_t st) {
+    const uint32_t nb = (uint32_t)((c.n + kCropTile - 1) / kCropTile);
+    {
+        ProfScope ps(ctx, PCP_K_CROP, st);
+        if (nb) {
+            hipLaunchKernelGGL(k_crop_count, dim3(nb), dim3(kFT), 0, st, c, b, S.counts);
+            PCP_CHECK_LAUNCH(ctx);
+            hipLaunchKernelGGL(k_crop_write, dim3(nb), dim3(kFT), 0, st, c, b,
+                               (const uint32_t *)S.counts, S.mcrop,
+                               want_idx ? S.B->idx.as<uint32_t>() : nullptr, S.xyz(), S.part);
+            PCP_CHECK_LAUNCH(ctx);
+        } else {
+            PCP_HIP(ctx, hipMemsetAsync(S.mcrop, 0, 4, st));
+        }
+    }
+    VoxParams *vp = S.vp + slot;
+    ProfScope ps(ctx, PCP_K_VOXEL, st);
+    hipLaunchKernelGGL(k_vox_params, dim3(1), dim3(kFT), 0, st, (const float *)S.part, (int)nb,
+                       (const uint32_t *)S.mcrop, leaf, vp);
+    PCP_CHECK_LAUNCH(ctx);
+    const uint32_t *nseg = S.mcrop;
+    if (leaf > 0.0f && c.n > 0) {
+        const uint32_t ncap = (uint32_t)c.n;
+        const unsigned gk = std::min<unsigned>((ncap + kFT - 1) / kFT, 2048);
+        CloudBufs &B = *S.B;
+        hipLaunchKernelGGL(k_vox_keys, dim3(gk), dim3(kFT), 0, st, (const float4 *)S.xyz(),
+                           (const VoxParams *)vp, B.keys[0].as<uint32_t>(), B.vals[0].as<uint32_t>());
+        PCP_CHECK_LAUNCH(ctx);
+        const uint32_t nblk = (ncap + kSortTile - 1) / kSortTile;
+        const int passes = radix_passes(b, leaf);
+        int cur = 0;
+        for (int pass = 0; pass < passes; ++pass) {
+            const int shift = 8 * pass;
+            hipLaunchKernelGGL(k_radix_hist, dim3(nblk), dim3(kFT), 0, st,
+                               B.keys[cur].as<const uint32_t>(), (const VoxParams *)vp, shift, nblk,
+                               S.rhist);
+            PCP_CHECK_LAUNCH(ctx);
+            hipLaunchKernelGGL(k_digit_offsets, dim3(1), dim3(kFT), 0, st,
+                               (const uint32_t *)S.rhist, (const VoxParams *)vp, S.rhoff);
+            PCP_CHECK_LAUNCH(ctx);
+            hipLaunchKernelGGL(k_radix_scatter, dim3(nblk), dim3(kFT), 0, st,
+                               B.keys[cur].as<const uint32_t>(), B.vals[cur].as<const uint32_t>(),
+                               (const VoxParams *)vp, shift, nblk, (const uint32_t *)S.rhoff,
+                               B.keys[cur ^ 1].as<uint32_t>(), B.vals[cur ^ 1].as<uint32_t>());
+            PCP_CHECK_LAUNCH(ctx);
+            cur ^= 1;
+        }
+        const uint32_t *keys = B.keys[cur].as<const uint32_t>();
+        const uint32_t *vals = B.vals[cur].as<const uint32_t>();
+        hipLaunchKernelGGL(k_seg_count, dim3(nblk), dim3(kFT), 0, st, keys, (const VoxParams *)vp,
+                           S.tcount);
+        PCP_CHECK_LAUNCH(ctx);
+        hipLaunchKernelGGL(k_seg_emit, dim3(nblk), dim3(kFT), 0, st, keys, (const VoxParams *)vp,
+                           (const uint32_t *)S.tcount, S.seg_start(), S.nseg);
+        PCP_CHECK_LAUNCH(ctx);
+        hipLaunchKernelGGL(k_centroid, dim3(gk), dim3(kFT), 0, st, (const float4 *)S.xyz(), keys,
+                           vals, (const uint32_t *)S.seg_start(), (const uint32_t *)S.nseg,
+                           S.out4(), S.vidx(), S.vcnt());
+        PCP_CHECK_LAUNCH(ctx);
+        nseg = S.nseg;
+    }
+    hipLaunchKernelGGL(k_finish, dim3(1), dim3(64), 0, st, (const VoxParams *)vp, nseg, S.res,
+                       S.res + kMaxClouds, slot);
+    PCP_CHECK_LAUNCH(ctx);
+    return PCP_OK;
+}
+
+static int enqueue_emit(pcp_ctx *ctx, Scratch &S, uint64_t ncap, int slot, const Rigid &r,
+                        float4 *out) {
+    if (ncap == 0) return PCP_OK;
+    ProfScope ps(ctx, PCP_K_TRANSFORM);
+    const unsigned g = (unsigned)std::min<uint64_t>((ncap + kFT - 1) / kFT, 4096);
+    hipLaunchKernelGGL(k_emit_rgb, dim3(g), dim3(kFT), 0, ctx->stream, (const float4 *)S.xyz(),
+                       (const float4 *)S.out4(), (const VoxParams *)(S.vp + slot),
+                       (const uint32_t *)S.res, slot, r, out);
+    PCP_CHECK_LAUNCH(ctx);
+    return PCP_OK;
+}
+
 static int stage_cloud(pcp_ctx *ctx, const pcp_cloud_view &v, bool device_in, DevBuf &buf,
                        CloudIn &c) {
     c.n = v.n;
@@ -362,10 +663,8 @@ static int stage_cloud(pcp_ctx *ctx, const pcp_cloud_view &v, bool device_in, De
     c.ox = v.off_x;
     c.oy = v.off_y;
     c.oz = v.off_z;
-    if (v.n == 0) {
-        c.raw = nullptr;
-        return PCP_OK;
-    }
+    c.raw = nullptr;
+    if (v.n == 0) return PCP_OK;
     if (device_in) {
         c.raw = static_cast<const unsigned char *>(v.data);
         return PCP_OK;
@@ -377,153 +676,19 @@ static int stage_cloud(pcp_ctx *ctx, const pcp_cloud_view &v, bool device_in, De
     return PCP_OK;
 }
 
-// crop into ctx->f_xyz (float4) [+ kept idx into ctx->f_idx]; device count at *m_d; bbox
-// partials in part (nb*6).  Returns nb through *nb_out.
-static int run_crop(pcp_ctx *ctx, const CloudIn &c, const Box &b, bool want_idx, uint32_t **m_d,
-                    float **part, int *nb_out) {
-    hipStream_t st = ctx->stream;
-    const uint64_t nb = (c.n + kCropTile - 1) / kCropTile;
-    const uint64_t nbx = nb ? nb : 1;
-    PCP_HIP(ctx, ctx->f_xyz.ensure((c.n + 1) * sizeof(float4)));
-    if (want_idx) PCP_HIP(ctx, ctx->f_idx.ensure((c.n + 1) * sizeof(uint32_t)));
-    const size_t cnt_bytes = (nbx + 1) * sizeof(uint32_t);
-    const size_t offs_bytes = (nbx + 1) * sizeof(uint32_t);
-    const size_t part_bytes = nbx * 6 * sizeof(float);
-    const size_t tmp_bytes = scan_tmp_bytes(nbx);
-    PCP_HIP(ctx, ctx->f_hist.ensure(cnt_bytes + offs_bytes + part_bytes + tmp_bytes + 1024));
-    char *h = ctx->f_hist.as<char>();
-    uint32_t *counts = reinterpret_cast<uint32_t *>(h);
-    uint32_t *offs = reinterpret_cast<uint32_t *>(h + cnt_bytes);
-    float *pp = reinterpret_cast<float *>(h + cnt_bytes + offs_bytes);
-    void *tmp = h + cnt_bytes + offs_bytes + part_bytes + 256;
-    if (nb == 0) {
-        PCP_HIP(ctx, hipMemsetAsync(offs, 0, sizeof(uint32_t), st));
-        float init[6] = {FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
-        PCP_HIP(ctx, hipMemcpyAsync(pp, init, sizeof(init), hipMemcpyHostToDevice, st));
-        PCP_HIP(ctx, hipStreamSynchronize(st));
-        *m_d = offs;
-        *part = pp;
-        *nb_out = 1;
-        return PCP_OK;
-    }
-    {
-        ProfScope ps(ctx, PCP_K_CROP);
-        hipLaunchKernelGGL(k_crop_count, dim3((unsigned)nb), dim3(kFT), 0, st, c, b, counts);
-        PCP_CHECK_LAUNCH(ctx);
-        int rc = exclusive_scan_u32(ctx, counts, offs, nb, tmp);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_crop_write, dim3((unsigned)nb), dim3(kFT), 0, st, c, b,
-                           (const uint32_t *)offs, want_idx ? ctx->f_idx.as<uint32_t>() : nullptr,
-                           ctx->f_xyz.as<float4>(), pp);
-        PCP_CHECK_LAUNCH(ctx);
-    }
-    *m_d = offs + nb;   // exclusive scan total
-    *part = pp;
-    *nb_out = (int)nb;
-    return PCP_OK;
-}
+struct ResultInfo {
+    uint32_t n;          // result points
+    uint32_t m;          // points after the crop
+    uint32_t overflow;
+};
 
-// voxel stage on ctx->f_xyz[0..m): result float4 in *res (device), count in host *n_out and
-// device *nres_d; idx/count device arrays (nullable outputs).  Sets *passthrough.
-// NOTE: m_d and part live in ctx->f_hist, which this function re-uses: they are dead after
-// k_vox_params; the cropped count is returned in *m_out.
-static int run_voxel(pcp_ctx *ctx, const uint32_t *m_d, const float *part, int nb, float leaf,
-                     const float4 **res, uint32_t **nres_d, uint32_t **idx_d, uint32_t **cnt_d,
-                     uint64_t *n_out, int32_t *passthrough, uint32_t *m_out) {
-    hipStream_t st = ctx->stream;
-    PCP_HIP(ctx, ctx->f_misc.ensure(4096));
-    VoxParams *vp_d = reinterpret_cast<VoxParams *>(ctx->f_misc.as<char>());
-    uint32_t *nseg_d = reinterpret_cast<uint32_t *>(ctx->f_misc.as<char>() + 512);
-    ProfScope ps(ctx, PCP_K_VOXEL);
-    hipLaunchKernelGGL(k_vox_params, dim3(1), dim3(64), 0, st, part, nb, m_d, leaf, vp_d);
-    PCP_CHECK_LAUNCH(ctx);
-    VoxParams vp;
-    PCP_HIP(ctx, hipMemcpyAsync(&vp, vp_d, sizeof(vp), hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipStreamSynchronize(st));
-    const uint32_t m = vp.m;
-    *m_out = m;
-    *passthrough = 0;
-    *idx_d = nullptr;
-    *cnt_d = nullptr;
-    if (m == 0) {
-        *res = ctx->f_xyz.as<const float4>();
-        PCP_HIP(ctx, hipMemsetAsync(nseg_d, 0, 4, st));
-        *nres_d = nseg_d;
-        *n_out = 0;
-        return PCP_OK;
-    }
-    if (vp.overflow) {   // PCL: "Leaf size is too small ... Integer indices would overflow."
-        *passthrough = 1;
-        *res = ctx->f_xyz.as<const float4>();
-        *nres_d = nullptr;
-        *n_out = m;
-        return PCP_OK;
-    }
-    const size_t mb = ((size_t)m + 16) * sizeof(uint32_t);
-    for (int q = 0; q < 2; ++q) {
-        PCP_HIP(ctx, ctx->f_keys[q].ensure(mb));
-        PCP_HIP(ctx, ctx->f_vals[q].ensure(mb));
-    }
-    const unsigned gm = (m + kFT - 1) / kFT;
-    hipLaunchKernelGGL(k_vox_keys, dim3(gm), dim3(kFT), 0, st, ctx->f_xyz.as<const float4>(),
-                       (const VoxParams *)vp_d, ctx->f_keys[0].as<uint32_t>(),
-                       ctx->f_vals[0].as<uint32_t>());
-    PCP_CHECK_LAUNCH(ctx);
-    int bits = 0;
-    while (bits < 32 && (vp.nvox - 1) >> bits) ++bits;
-    const int passes = (bits + 7) / 8;
-    const uint32_t nblk = (m + kSortTile - 1) / kSortTile;
-    const uint64_t hn = 256ull * nblk;
-    PCP_HIP(ctx, ctx->f_hist.ensure(2 * (hn + 1) * sizeof(uint32_t) + scan_tmp_bytes(hn) + 1024));
-    uint32_t *hist = ctx->f_hist.as<uint32_t>();
-    uint32_t *hoff = hist + hn + 1;
-    void *tmp = hoff + hn + 1;
-    int cur = 0;
-    for (int pass = 0; pass < passes; ++pass) {
-        const int shift = 8 * pass;
-        hipLaunchKernelGGL(k_radix_hist, dim3(nblk), dim3(kFT), 0, st,
-                           ctx->f_keys[cur].as<const uint32_t>(), m, shift, nblk, hist);
-        PCP_CHECK_LAUNCH(ctx);
-        int rc = exclusive_scan_u32(ctx, hist, hoff, hn, tmp);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_radix_scatter, dim3(nblk), dim3(kFT), 0, st,
-                           ctx->f_keys[cur].as<const uint32_t>(), ctx->f_vals[cur].as<const uint32_t>(),
-                           m, shift, nblk, (const uint32_t *)hoff, ctx->f_keys[cur ^ 1].as<uint32_t>(),
-                           ctx->f_vals[cur ^ 1].as<uint32_t>());
-        PCP_CHECK_LAUNCH(ctx);
-        cur ^= 1;
-    }
-    // segments: heads -> scan -> starts -> centroids
-    const uint32_t *keys = ctx->f_keys[cur].as<const uint32_t>();
-    const uint32_t *vals = ctx->f_vals[cur].as<const uint32_t>();
-    uint32_t *head = ctx->f_keys[cur ^ 1].as<uint32_t>();
-    uint32_t *sid = ctx->f_vals[cur ^ 1].as<uint32_t>();   // m + 1 entries
-    hipLaunchKernelGGL(k_seg_heads, dim3(gm), dim3(kFT), 0, st, keys, m, head);
-    PCP_CHECK_LAUNCH(ctx);
-    PCP_HIP(ctx, ctx->f_hist.ensure(scan_tmp_bytes(m) + 1024));
-    int rc = exclusive_scan_u32(ctx, head, sid, m, ctx->f_hist.p);
-    if (rc) return rc;
-    // seg_start (m + 1), result float4 (m), idx (m), count (m)
-    PCP_HIP(ctx, ctx->f_out.ensure(((size_t)m + 1) * (sizeof(uint32_t) * 3 + sizeof(float4)) + 256));
-    float4 *out4 = ctx->f_out.as<float4>();
-    uint32_t *seg_start = reinterpret_cast<uint32_t *>(out4 + m + 1);
-    uint32_t *oidx = seg_start + m + 1;
-    uint32_t *ocnt = oidx + m + 1;
-    hipLaunchKernelGGL(k_seg_start, dim3(gm), dim3(kFT), 0, st, (const uint32_t *)head,
-                       (const uint32_t *)sid, m, seg_start);
-    PCP_CHECK_LAUNCH(ctx);
-    hipLaunchKernelGGL(k_centroid, dim3(gm), dim3(kFT), 0, st, ctx->f_xyz.as<const float4>(), keys,
-                       vals, (const uint32_t *)seg_start, (const uint32_t *)(sid + m), out4, oidx,
-                       ocnt);
-    PCP_CHECK_LAUNCH(ctx);
-    uint32_t nseg = 0;
-    PCP_HIP(ctx, hipMemcpyAsync(&nseg, sid + m, 4, hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipStreamSynchronize(st));
-    *res = out4;
-    *nres_d = sid + m;
-    *idx_d = oidx;
-    *cnt_d = ocnt;
-    *n_out = nseg;
+static int read_result(pcp_ctx *ctx, const Scratch &S, int slot, ResultInfo &ri) {
+    uint32_t buf[3 * kMaxClouds];
+    PCP_HIP(ctx, hipMemcpyAsync(buf, S.res, sizeof(buf), hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ri.n = buf[slot];
+    ri.m = buf[kMaxClouds + 2 * slot];
+    ri.overflow = buf[kMaxClouds + 2 * slot + 1];
     return PCP_OK;
 }
 
@@ -542,30 +707,26 @@ int pcp_crop_box(pcp_ctx *ctx, const pcp_cloud_view *in, const double box[6], ui
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     *n_kept = 0;
     if (in->n == 0) return PCP_OK;
+    Scratch S;
+    if ((rc = ensure_scratch(ctx, 0, in->n, kept_idx != nullptr, S))) return rc;
     CloudIn c;
-    rc = stage_cloud(ctx, *in, false, ctx->f_in, c);
-    if (rc) return rc;
-    Box b{box[0], box[1], box[2], box[3], box[4], box[5]};
-    uint32_t *m_d;
-    float *part;
-    int nb;
-    rc = run_crop(ctx, c, b, kept_idx != nullptr, &m_d, &part, &nb);
-    if (rc) return rc;
-    uint32_t m = 0;
-    PCP_HIP(ctx, hipMemcpyAsync(&m, m_d, 4, hipMemcpyDeviceToHost, ctx->stream));
-    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    *n_kept = m;
-    if ((kept_idx || out_xyz16) && m > cap) {
+    if ((rc = stage_cloud(ctx, *in, false, ctx->f_in, c))) return rc;
+    const Box b{box[0], box[1], box[2], box[3], box[4], box[5]};
+    if ((rc = enqueue_cloud(ctx, S, c, b, 0.0f, kept_idx != nullptr, 0, ctx->stream))) return rc;
+    ResultInfo ri;
+    if ((rc = read_result(ctx, S, 0, ri))) return rc;
+    *n_kept = ri.m;
+    if ((kept_idx || out_xyz16) && ri.m > cap) {
         prof_resolve(ctx);
-        return set_err(ctx, PCP_E_CAPACITY, "pcp_crop_box: need %u, cap %llu", m,
+        return set_err(ctx, PCP_E_CAPACITY, "pcp_crop_box: need %u, cap %llu", ri.m,
                        (unsigned long long)cap);
     }
-    if (kept_idx && m)
-        PCP_HIP(ctx, hipMemcpyAsync(kept_idx, ctx->f_idx.p, (size_t)m * 4, hipMemcpyDeviceToHost,
+    if (kept_idx && ri.m)
+        PCP_HIP(ctx, hipMemcpyAsync(kept_idx, S.B->idx.p, (size_t)ri.m * 4, hipMemcpyDeviceToHost,
                                     ctx->stream));
-    if (out_xyz16 && m)
-        PCP_HIP(ctx, hipMemcpyAsync(out_xyz16, ctx->f_xyz.p, (size_t)m * 16, hipMemcpyDeviceToHost,
-                                    ctx->stream));
+    if (out_xyz16 && ri.m)
+        PCP_HIP(ctx, hipMemcpyAsync(out_xyz16, S.xyz(), (size_t)ri.m * 16,
+                                    hipMemcpyDeviceToHost, ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     prof_resolve(ctx);
     return PCP_OK;
@@ -575,44 +736,33 @@ static int crop_voxel_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b,
                            float *out_xyz16, uint32_t *voxel_idx, uint32_t *voxel_count,
                            uint64_t cap, uint64_t *n_out, uint64_t *n_cropped,
                            int32_t *passthrough) {
+    Scratch S;
+    int rc = ensure_scratch(ctx, 0, in->n, false, S);
+    if (rc) return rc;
     CloudIn c;
-    int rc = stage_cloud(ctx, *in, false, ctx->f_in, c);
-    if (rc) return rc;
-    uint32_t *m_d;
-    float *part;
-    int nb;
-    rc = run_crop(ctx, c, b, false, &m_d, &part, &nb);
-    if (rc) return rc;
-    const float4 *res;
-    uint32_t *nres_d, *idx_d = nullptr, *cnt_d = nullptr;
-    uint64_t n = 0;
-    int32_t pt = 0;
-    if (leaf > 0.0f) {
-        uint32_t m = 0;
-        rc = run_voxel(ctx, m_d, part, nb, leaf, &res, &nres_d, &idx_d, &cnt_d, &n, &pt, &m);
-        if (rc) return rc;
-        if (n_cropped) *n_cropped = m;
-    } else {
-        uint32_t m = 0;
-        PCP_HIP(ctx, hipMemcpyAsync(&m, m_d, 4, hipMemcpyDeviceToHost, ctx->stream));
-        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        res = ctx->f_xyz.as<const float4>();
-        n = m;
-        if (n_cropped) *n_cropped = m;
-    }
-    if (passthrough) *passthrough = pt;
-    *n_out = n;
-    if (n > cap) {
+    if ((rc = stage_cloud(ctx, *in, false, ctx->f_in, c))) return rc;
+    if ((rc = enqueue_cloud(ctx, S, c, b, leaf, false, 0, ctx->stream))) return rc;
+    ResultInfo ri;
+    if ((rc = read_result(ctx, S, 0, ri))) return rc;
+    const bool vox = leaf > 0.0f && !ri.overflow;
+    if (passthrough) *passthrough = (leaf > 0.0f && ri.overflow) ? 1 : 0;
+    if (n_cropped) *n_cropped = ri.m;
+    *n_out = ri.n;
+    if (ri.n > cap) {
         prof_resolve(ctx);
-        return set_err(ctx, PCP_E_CAPACITY, "voxel output needs %llu points, cap %llu",
-                       (unsigned long long)n, (unsigned long long)cap);
+        return set_err(ctx, PCP_E_CAPACITY, "voxel output needs %u points, cap %llu", ri.n,
+                       (unsigned long long)cap);
     }
-    if (n) {
-        PCP_HIP(ctx, hipMemcpyAsync(out_xyz16, res, n * 16, hipMemcpyDeviceToHost, ctx->stream));
-        if (voxel_idx && idx_d)
-            PCP_HIP(ctx, hipMemcpyAsync(voxel_idx, idx_d, n * 4, hipMemcpyDeviceToHost, ctx->stream));
-        if (voxel_count && cnt_d)
-            PCP_HIP(ctx, hipMemcpyAsync(voxel_count, cnt_d, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (ri.n) {
+        const void *src = vox ? (const void *)S.out4() : (const void *)S.xyz();
+        PCP_HIP(ctx, hipMemcpyAsync(out_xyz16, src, (size_t)ri.n * 16, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+        if (vox && voxel_idx)
+            PCP_HIP(ctx, hipMemcpyAsync(voxel_idx, S.vidx(), (size_t)ri.n * 4,
+                                        hipMemcpyDeviceToHost, ctx->stream));
+        if (vox && voxel_count)
+            PCP_HIP(ctx, hipMemcpyAsync(voxel_count, S.vcnt(), (size_t)ri.n * 4,
+                                        hipMemcpyDeviceToHost, ctx->stream));
     }
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     prof_resolve(ctx);
@@ -686,8 +836,7 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, cons
                                ctx->stream, c, r, o + 2 * base);
             PCP_CHECK_LAUNCH(ctx);
         }
-        // f_in is reused by the next cloud: finish this one first
-        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));   // f_in is reused by the next cloud
         base += c.n;
     }
     PCP_HIP(ctx, hipMemcpyAsync(out, o, total * 32, hipMemcpyDeviceToHost, ctx->stream));
@@ -696,21 +845,41 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, cons
     return PCP_OK;
 }
 
+// key of a captured filter_merge graph: everything baked into its nodes
+static std::vector<uint8_t> fm_key(int k, const pcp_cloud_view *clouds, const double *boxes,
+                                   float leaf, const pcp_rigid *tf, const uint8_t *rgb,
+                                   const void *out, uint64_t cap) {
+    std::vector<uint8_t> key;
+    auto put = [&key](const void *p, size_t n) {
+        const uint8_t *b = static_cast<const uint8_t *>(p);
+        key.insert(key.end(), b, b + n);
+    };
+    put(&k, sizeof(k));
+    put(clouds, sizeof(pcp_cloud_view) * k);
+    put(boxes, sizeof(double) * 6 * k);
+    put(&leaf, sizeof(leaf));
+    put(tf, sizeof(pcp_rigid) * k);
+    put(rgb, 3 * (size_t)k);
+    put(&out, sizeof(out));
+    put(&cap, sizeof(cap));
+    return key;
+}
+
 int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const double *boxes,
                      float leaf, const pcp_rigid *tf, const uint8_t *rgb, void *out, uint64_t cap,
                      uint64_t *n_out, uint64_t *n_per_cloud, uint32_t flags) {
     if (!ctx) return PCP_E_INVALID;
-    if (k < 0 || (k && (!clouds || !boxes || !tf || !rgb)) || !n_out)
+    if (k < 0 || k > kMaxClouds || (k && (!clouds || !boxes || !tf || !rgb)) || !n_out)
         return set_err(ctx, PCP_E_INVALID, "pcp_filter_merge: bad argument");
+    uint64_t upper = 0;
     for (int i = 0; i < k; ++i) {
         int rc = check_view(ctx, &clouds[i], "pcp_filter_merge");
         if (rc) return rc;
+        upper += clouds[i].n;
     }
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     const bool dev_in = flags & PCP_MEM_DEVICE_IN, dev_out = flags & PCP_MEM_DEVICE_OUT;
-    // worst case output = sum of inputs; results land in a device buffer, then out
-    uint64_t upper = 0;
-    for (int i = 0; i < k; ++i) upper += clouds[i].n;
+    if (dev_out && !out && upper) return set_err(ctx, PCP_E_INVALID, "pcp_filter_merge: null output");
     float4 *obuf;
     if (dev_out) {
         obuf = static_cast<float4 *>(out);
@@ -718,64 +887,128 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
         PCP_HIP(ctx, ctx->out_d.ensure(upper * 32 + 32));
         obuf = ctx->out_d.as<float4>();
     }
-    uint64_t base = 0;
+    // staging (host input): one region per cloud, so no buffer is reused while in flight
+    std::vector<size_t> soff(k + 1, 0);
+    for (int i = 0; i < k; ++i)
+        soff[i + 1] = soff[i] + (dev_in ? 0 : align256(clouds[i].n * clouds[i].point_step));
+    if (!dev_in) PCP_HIP(ctx, ctx->f_in.ensure(soff[k] + 256));
+    // per-cloud scratch and one side stream per cloud (clouds run as concurrent branches).
+    // Size fbuf once: Scratch keeps CloudBufs pointers, a later resize would invalidate them.
+    if ((int)ctx->fbuf.size() < k) ctx->fbuf.resize(k);
+    std::vector<Scratch> S(k);
     for (int i = 0; i < k; ++i) {
-        uint64_t n = 0;
-        if (clouds[i].n) {
-            CloudIn c;
-            int rc = stage_cloud(ctx, clouds[i], dev_in, ctx->f_in, c);
-            if (rc) return rc;
+        int rc = ensure_scratch(ctx, i, clouds[i].n, false, S[i]);
+        if (rc) return rc;
+    }
+    while ((int)ctx->side.size() < k) {
+        hipStream_t s2 = nullptr;
+        PCP_HIP(ctx, hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        ctx->side.push_back(s2);
+        hipEvent_t e = nullptr;
+        PCP_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->side_ev.push_back(e);
+    }
+    if (!ctx->fork_ev) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
+    // fork: every cloud's crop/voxel chain on its own stream; join; then the emits (they need
+    // every earlier cloud's count for their output offset)
+    auto enqueue_all = [&]() -> int {
+        PCP_HIP(ctx, hipEventRecord(ctx->fork_ev, ctx->stream));
+        for (int i = 0; i < k; ++i) {
+            hipStream_t si = ctx->side[i];
+            PCP_HIP(ctx, hipStreamWaitEvent(si, ctx->fork_ev, 0));
+            CloudIn c{};
+            c.n = clouds[i].n;
+            c.step = clouds[i].point_step;
+            c.ox = clouds[i].off_x;
+            c.oy = clouds[i].off_y;
+            c.oz = clouds[i].off_z;
+            c.raw = static_cast<const unsigned char *>(clouds[i].data);
+            if (!dev_in && c.n) {
+                unsigned char *dst = ctx->f_in.as<unsigned char>() + soff[i];
+                PCP_HIP(ctx, hipMemcpyAsync(dst, clouds[i].data, c.n * (uint64_t)c.step,
+                                            hipMemcpyHostToDevice, si));
+                c.raw = dst;
+            }
             const double *bx = boxes + 6 * i;
             const Box b{bx[0], bx[1], bx[2], bx[3], bx[4], bx[5]};
-            uint32_t *m_d;
-            float *part;
-            int nb;
-            rc = run_crop(ctx, c, b, false, &m_d, &part, &nb);
+            int r = enqueue_cloud(ctx, S[i], c, b, leaf, false, i, si);
+            if (r) return r;
+            PCP_HIP(ctx, hipEventRecord(ctx->side_ev[i], si));
+        }
+        for (int i = 0; i < k; ++i) PCP_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[i], 0));
+        if (dev_out && upper > cap) return PCP_OK;   // sizes checked on the host afterwards
+        for (int i = 0; i < k; ++i) {
+            int r = enqueue_emit(ctx, S[i], clouds[i].n, i, make_rigid(tf[i], rgb + 3 * i), obuf);
+            if (r) return r;
+        }
+        return PCP_OK;
+    };
+    int rc = PCP_OK;
+    const bool graphable = dev_in && dev_out && upper <= cap && ctx->use_graphs;
+    if (graphable) {
+        std::vector<uint8_t> key = fm_key(k, clouds, boxes, leaf, tf, rgb, out, cap);
+        std::vector<const void *> sp;
+        for (int i = 0; i < k; ++i) {
+            const CloudBufs &B = ctx->fbuf[i];
+            const void *v[] = {B.xyz.p, B.keys[0].p, B.keys[1].p, B.vals[0].p, B.vals[1].p,
+                               B.hist.p, B.out.p};
+            sp.insert(sp.end(), v, v + 7);
+        }
+        sp.push_back(ctx->f_misc.p);
+        key.insert(key.end(), reinterpret_cast<const uint8_t *>(sp.data()),
+                   reinterpret_cast<const uint8_t *>(sp.data() + sp.size()));
+        if (!ctx->fm_exec || key != ctx->fm_key) {
+            if (ctx->fm_exec) (void)hipGraphExecDestroy(ctx->fm_exec);
+            if (ctx->fm_graph) (void)hipGraphDestroy(ctx->fm_graph);
+            ctx->fm_exec = nullptr;
+            ctx->fm_graph = nullptr;
+            ctx->fm_key.clear();
+            PCP_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+            ctx->capturing = true;
+            rc = enqueue_all();
+            ctx->capturing = false;
+            hipGraph_t g = nullptr;
+            const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+            if (rc) {
+                if (g) (void)hipGraphDestroy(g);
+                return rc;
+            }
+            if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamEndCapture", __FILE__, __LINE__);
+            ctx->fm_graph = g;
+            PCP_HIP(ctx, hipGraphInstantiate(&ctx->fm_exec, g, nullptr, nullptr, 0));
+            ctx->fm_key = key;
+        }
+        ProfScope ps(ctx, PCP_K_FILTER_MERGE);
+        PCP_HIP(ctx, hipGraphLaunch(ctx->fm_exec, ctx->stream));
+    } else {
+        ProfScope ps(ctx, PCP_K_FILTER_MERGE);
+        rc = enqueue_all();
+        if (rc) return rc;
+    }
+    uint32_t res[3 * kMaxClouds];
+    PCP_HIP(ctx, hipMemcpyAsync(res, ctx->f_misc.as<char>() + align256(kMaxClouds * sizeof(VoxParams)),
+                                sizeof(res), hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t total = 0;
+    for (int i = 0; i < k; ++i) {
+        if (n_per_cloud) n_per_cloud[i] = clouds[i].n ? res[i] : 0;
+        total += clouds[i].n ? res[i] : 0;
+    }
+    *n_out = total;
+    if (total > cap) {
+        prof_resolve(ctx);
+        return set_err(ctx, PCP_E_CAPACITY, "pcp_filter_merge: need %llu, cap %llu",
+                       (unsigned long long)total, (unsigned long long)cap);
+    }
+    if (dev_out && upper > cap && total) {   // emits were deferred until the size was known
+        for (int i = 0; i < k; ++i) {
+            rc = enqueue_emit(ctx, S[i], clouds[i].n, i, make_rigid(tf[i], rgb + 3 * i), obuf);
             if (rc) return rc;
-            const float4 *res = ctx->f_xyz.as<const float4>();
-            uint32_t *nres_d = m_d;
-            if (leaf > 0.0f) {
-                uint32_t *idx_d, *cnt_d, m = 0;
-                int32_t pt;
-                rc = run_voxel(ctx, m_d, part, nb, leaf, &res, &nres_d, &idx_d, &cnt_d, &n, &pt, &m);
-                if (rc) return rc;
-            } else {
-                uint32_t m = 0;
-                PCP_HIP(ctx, hipMemcpyAsync(&m, m_d, 4, hipMemcpyDeviceToHost, ctx->stream));
-                PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-                n = m;
-            }
-            if (dev_out && base + n > cap) {
-                *n_out = base + n;
-                prof_resolve(ctx);
-                return set_err(ctx, PCP_E_CAPACITY, "pcp_filter_merge: output capacity %llu",
-                               (unsigned long long)cap);
-            }
-            if (n) {
-                const Rigid r = make_rigid(tf[i], rgb + 3 * i);
-                ProfScope ps(ctx, PCP_K_TRANSFORM);
-                hipLaunchKernelGGL(k_xform_f4, dim3((unsigned)((n + kFT - 1) / kFT)), dim3(kFT), 0,
-                                   ctx->stream, res, (const uint32_t *)nullptr, (uint32_t)n, r,
-                                   obuf + 2 * base);
-                PCP_CHECK_LAUNCH(ctx);
-            }
-            // scratch (f_xyz, f_out) is reused by the next cloud
-            PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
         }
-        if (n_per_cloud) n_per_cloud[i] = n;
-        base += n;
     }
-    *n_out = base;
-    if (!dev_out) {
-        if (base > cap) {
-            prof_resolve(ctx);
-            return set_err(ctx, PCP_E_CAPACITY, "pcp_filter_merge: need %llu, cap %llu",
-                           (unsigned long long)base, (unsigned long long)cap);
-        }
-        if (base)
-            PCP_HIP(ctx, hipMemcpyAsync(out, obuf, base * 32, hipMemcpyDeviceToHost, ctx->stream));
-        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    }
+    if (!dev_out && total)
+        PCP_HIP(ctx, hipMemcpyAsync(out, obuf, total * 32, hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     prof_resolve(ctx);
     return PCP_OK;
 }

@@ -158,6 +158,24 @@ k_cell_scatter(const float4 *__restrict__ xyz, uint64_t n, const uint32_t *__res
     out[pos] = xyz[i];
 }
 
+// points of each cell in descending z: lets a query stop scanning a cell at the first point
+// that is more than r below it (exact early exit, see scan_stencil)
+__global__ void __launch_bounds__(kThreads)
+k_cell_sort_z(const uint32_t *__restrict__ start, uint64_t ncell, float4 *__restrict__ pts) {
+    const uint64_t c = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (c >= ncell) return;
+    const uint32_t s = start[c], e = start[c + 1];
+    for (uint32_t i = s + 1; i < e; ++i) {   // insertion sort (cells hold few points)
+        const float4 v = pts[i];
+        uint32_t j = i;
+        while (j > s && pts[j - 1].z < v.z) {
+            pts[j] = pts[j - 1];
+            --j;
+        }
+        pts[j] = v;
+    }
+}
+
 // dilated occupancy: bit for lower corner (ix,iy,iz) = any point in the 2x2x2 block
 __global__ void __launch_bounds__(kThreads)
 k_occ2(const uint32_t *__restrict__ start, CellMap m, uint64_t ncell, uint32_t *__restrict__ occ2) {
@@ -274,7 +292,12 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q)
                        ctx->scratch[0].as<const float4>(), n, ctx->scratch[2].as<const uint32_t>(),
                        ctx->scratch[3].as<uint32_t>(), g.pts.as<float4>());
     PCP_CHECK_LAUNCH(ctx);
-    // 7. dilated occupancy
+    // 7. descending z inside each cell
+    hipLaunchKernelGGL(k_cell_sort_z, dim3((unsigned)((ncell + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, st, g.start.as<const uint32_t>(), ncell,
+                       g.pts.as<float4>());
+    PCP_CHECK_LAUNCH(ctx);
+    // 8. dilated occupancy
     const uint64_t nw = (ncell + 31) / 32;
     PCP_HIP(ctx, g.occ2.ensure(nw * sizeof(uint32_t)));
     hipLaunchKernelGGL(k_occ2, dim3((unsigned)((nw + kThreads - 1) / kThreads)), dim3(kThreads), 0,

@@ -96,6 +96,20 @@ struct ProfSlot {
     uint64_t launches = 0;
 };
 
+struct CloudBufs {                 // one cloud's filter-pipeline scratch
+    DevBuf xyz, idx, keys[2], vals[2], hist, out;
+    void release() {
+        xyz.release();
+        idx.release();
+        for (int q = 0; q < 2; ++q) {
+            keys[q].release();
+            vals[q].release();
+        }
+        hist.release();
+        out.release();
+    }
+};
+
 struct PendingEvent {
     int kid;
     hipEvent_t a, b;
@@ -121,8 +135,19 @@ struct pcp_ctx {
     double fan_elmin = 0.0, fan_elmax = 0.0;
     double steps_end = -1e300;               // cached step table
     int steps_K = 0;
+    int fan_batch = 1;                       // tuning knob (PCP_FAN_BATCH), A/B only
     // filter/merge scratch
-    pcp::DevBuf f_in, f_xyz, f_idx, f_keys[2], f_vals[2], f_hist, f_out, f_misc;
+    pcp::DevBuf f_in, f_misc;
+    std::vector<pcp::CloudBufs> fbuf;        // per-cloud scratch of the filter pipeline
+    std::vector<hipStream_t> side;           // per-cloud branch streams
+    std::vector<hipEvent_t> side_ev;
+    hipEvent_t fork_ev = nullptr;
+    // captured filter_merge pipeline (device-resident inputs), replayed while its key matches
+    hipGraph_t fm_graph = nullptr;
+    hipGraphExec_t fm_exec = nullptr;
+    std::vector<uint8_t> fm_key;
+    bool capturing = false;
+    bool use_graphs = true;
     // profiling
     bool prof = false;
     pcp::ProfSlot slots[PCP_K_COUNT];
@@ -148,8 +173,9 @@ int hip_fail(pcp_ctx *ctx, hipError_t e, const char *what, const char *file, int
 struct ProfScope {
     pcp_ctx *ctx;
     int kid;
+    hipStream_t st;
     hipEvent_t a = nullptr, b = nullptr;
-    ProfScope(pcp_ctx *c, int k);
+    ProfScope(pcp_ctx *c, int k, hipStream_t s = nullptr);
     ~ProfScope();
 };
 void prof_resolve(pcp_ctx *ctx);   // after a stream sync

@@ -46,35 +46,57 @@ __device__ __forceinline__ bool stencil_cell(const GridView &g, float qx, float 
     return true;
 }
 
-// Exact point tests of an occupied stencil.  Cells along x are contiguous in the sorted point
-// array, so the stencil is 4 ranges; the 8 directory entries are loaded together and each
-// range is tested 4 points per step (indices clamped to the range: duplicates are harmless
-// for an any-hit query) to keep several gathers in flight per lane.
+// Exact point tests of an occupied stencil: 2 x 2 rows (y, z) x 2 cells (x) = 8 runs.  Points
+// of a cell are sorted by descending z, so a run ends at the first point with dz = qz - pz >= 0
+// and fl(dz*dz) >= r2: FLANN's accumulator ((0 + dx^2) + dy^2) + dz^2 is >= fl(dz^2) (adding
+// non-negative floats never decreases), and every later point of the run has a larger dz, so
+// none of them can be within r (exact).
+// Latency shape: round 1 = the 12 directory entries; round 2 = the first point of all 8 runs
+// (independent loads; most runs end here); only runs that continue are walked, 2 points/step.
 template <bool STATS>
 __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, float qx, float qy,
                                              float qz, float r2, uint32_t *cnt) {
     const uint32_t nx = (uint32_t)g.nx, nxy = nx * (uint32_t)g.ny;
-    uint32_t s[4], e[4];
+    uint32_t b[4][3];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const uint32_t row = lin + (r & 1) * nx + (r >> 1) * nxy;
-        s[r] = g.start[row];
-        e[r] = g.start[row + 2];
+        b[r][0] = g.start[row];
+        b[r][1] = g.start[row + 1];
+        b[r][2] = g.start[row + 2];
     }
+    const uint32_t last = g.n_pts - 1;
+    float4 f[8];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint32_t last = e[r] - 1;
-        for (uint32_t k = s[r]; k < e[r]; k += 4) {
+    for (int i = 0; i < 8; ++i) f[i] = g.pts[min(b[i >> 1][i & 1], last)];
+    uint32_t live = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t k = b[i >> 1][i & 1], e = b[i >> 1][(i & 1) + 1];
+        if (k < e) {
+            if (STATS) cnt[2] += 1;
+            if (flann_within(qx, qy, qz, f[i], r2)) return true;
+            const float dz = qz - f[i].z;
+            if (!(dz >= 0.0f && dz * dz >= r2) && k + 1 < e) live |= 1u << i;
+        }
+    }
+    if (!live) return false;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (!(live & (1u << i))) continue;
+        const uint32_t e = b[i >> 1][(i & 1) + 1];
+        for (uint32_t k = b[i >> 1][i & 1] + 1; k < e; k += 2) {
             const float4 p0 = g.pts[k];
-            const float4 p1 = g.pts[min(k + 1, last)];
-            const float4 p2 = g.pts[min(k + 2, last)];
-            const float4 p3 = g.pts[min(k + 3, last)];
-            if (STATS) cnt[2] += min(4u, e[r] - k);
-            const int h = (int)flann_within(qx, qy, qz, p0, r2) |
-                          (int)flann_within(qx, qy, qz, p1, r2) |
-                          (int)flann_within(qx, qy, qz, p2, r2) |
-                          (int)flann_within(qx, qy, qz, p3, r2);
-            if (h) return true;
+            const float4 p1 = g.pts[min(k + 1, e - 1)];
+            if (STATS) cnt[2] += 1;
+            if (flann_within(qx, qy, qz, p0, r2)) return true;
+            float dz = qz - p0.z;
+            if (dz >= 0.0f && dz * dz >= r2) break;
+            if (k + 1 >= e) break;
+            if (STATS) cnt[2] += 1;
+            if (flann_within(qx, qy, qz, p1, r2)) return true;
+            dz = qz - p1.z;
+            if (dz >= 0.0f && dz * dz >= r2) break;
         }
     }
     return false;
@@ -131,7 +153,7 @@ __device__ __forceinline__ void clip_k(const GridView &g, double px, double py, 
 // clip box have no point within r (skipped exactly).  s_k comes from ONE table read at klo and
 // then the same repeated addition that built the table (identical doubles).  Samples are
 // processed 4 at a time: the 4 occupancy words are loaded together, then tested in order.
-template <bool STATS>
+template <bool STATS, int B = 1>
 __device__ __forceinline__ int march_t(const GridView &g, double px, double py, double pz,
                                        double dx, double dy, double dz,
                                        const double *__restrict__ steps, int K, double end,
@@ -140,12 +162,12 @@ __device__ __forceinline__ int march_t(const GridView &g, double px, double py, 
     clip_k(g, px, py, pz, dx, dy, dz, K, klo, khi);
     if (klo > khi) return -1;
     double s = steps[klo];
-    for (int k0 = klo; k0 <= khi; k0 += 4) {
-        float qx[4], qy[4], qz[4];
-        uint32_t lin[4], word[4];
-        bool vis[4];
+    for (int k0 = klo; k0 <= khi; k0 += B) {
+        float qx[B], qy[B], qz[B];
+        uint32_t lin[B], word[B];
+        bool vis[B];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < B; ++i) {
             vis[i] = (k0 + i <= khi) && (s < end);
             qx[i] = (float)(px + dx * s);
             qy[i] = (float)(py + dy * s);
@@ -156,14 +178,14 @@ __device__ __forceinline__ int march_t(const GridView &g, double px, double py, 
             s = s + kRayStep;
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < B; ++i) {
             if (STATS && vis[i]) cnt[0] += 1;
             if ((word[i] >> (lin[i] & 31)) & 1u) {
                 if (STATS) cnt[1] += 1;
                 if (scan_stencil<STATS>(g, lin[i], qx[i], qy[i], qz[i], r2, cnt)) return k0 + i;
             }
         }
-        if (!vis[3]) break;
+        if (!vis[B - 1]) break;
     }
     return -1;
 }
@@ -481,7 +503,7 @@ enum { FAN_PLAIN = 0, FAN_STATS = 1, FAN_STAMPS = 2 };
 // termination on near-flat terrain); blockIdx.y = pose.  Each wave writes its blocked-ray
 // count and its sample-query count to its own slot: the per-pose sums are formed by
 // k_fan_reduce in a fixed order (deterministic, no same-address atomics).
-template <int MODE> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
+template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
     const uint32_t p = blockIdx.y;
     const uint32_t ray = blockIdx.x * kT + threadIdx.x;
     const bool active = ray < a.rays;
@@ -505,8 +527,8 @@ template <int MODE> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs 
             asm volatile("" ::"v"(dx), "v"(dy));
             t1 = __builtin_amdgcn_s_memtime();
         }
-        hit = march_t<MODE == FAN_STATS>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K, 1e300,
-                                         a.r2, cnt);
+        hit = march_t<MODE == FAN_STATS, B>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K,
+                                            1e300, a.r2, cnt);
     }
     if (MODE == FAN_STAMPS) {
         asm volatile("" ::"v"(hit));
@@ -879,16 +901,21 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     const dim3 grid((rays + kT - 1) / kT, P);
     if (stats) {
         PCP_HIP(ctx, hipMemsetAsync(a.stats, 0, 4 * sizeof(uint64_t), st));
-        hipLaunchKernelGGL(k_raycast_fan<FAN_STATS>, grid, dim3(kT), 0, st, a);
+        hipLaunchKernelGGL((k_raycast_fan<FAN_STATS, 1>), grid, dim3(kT), 0, st, a);
         PCP_CHECK_LAUNCH(ctx);
         PCP_HIP(ctx, hipMemcpyAsync(stats, a.stats, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     } else if (stamps) {
-        hipLaunchKernelGGL(k_raycast_fan<FAN_STAMPS>, grid, dim3(kT), 0, st, a);
+        hipLaunchKernelGGL((k_raycast_fan<FAN_STAMPS, 1>), grid, dim3(kT), 0, st, a);
         PCP_CHECK_LAUNCH(ctx);
         PCP_HIP(ctx, hipMemcpyAsync(stamps, a.stats, stats_bytes, hipMemcpyDeviceToHost, st));
     } else {
         ProfScope ps(ctx, PCP_K_RAYCAST_FAN);
-        hipLaunchKernelGGL(k_raycast_fan<FAN_PLAIN>, grid, dim3(kT), 0, st, a);
+        // samples per occupancy round: 1 by default (fewest VGPRs); PCP_FAN_BATCH (2/4) for A/B
+        switch (ctx->fan_batch) {
+        case 2: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 2>), grid, dim3(kT), 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 4>), grid, dim3(kT), 0, st, a); break;
+        default: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 1>), grid, dim3(kT), 0, st, a); break;
+        }
         PCP_CHECK_LAUNCH(ctx);
     }
     hipLaunchKernelGGL(k_fan_reduce, dim3(P), dim3(kT), 0, st, (const uint32_t *)a.wave_blocked,

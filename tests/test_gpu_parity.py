@@ -134,6 +134,45 @@ def test_filter_merge_pipeline(gpu, oracle):
     np.testing.assert_array_equal(out[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
 
 
+def test_filter_merge_device_graph_replay(gpu, oracle):
+    """Device-resident inputs: the pipeline is captured into a hipGraph and replayed; every
+    replay must equal the eager host-path result and the oracle."""
+    a = synth.lidar_cloud(250_000, seed=5)
+    b = synth.lidar_cloud(150_000, seed=6, sensor_height=3.5)
+    tfs = _tfs()
+    rgbs = [(255, 0, 0), (0, 0, 255)]
+    ref, per_ref = gpu.filter_merge([a, b], [BOX, BOX], 0.05, tfs, rgbs)
+    dp = [gpu.dev_alloc(c.nbytes) for c in (a, b)]
+    for p, c in zip(dp, (a, b)):
+        gpu.h2d(p, c)
+    views = [_abi.CloudView(p, c.shape[0], 16, 0, 4, 8) for p, c in zip(dp, (a, b))]
+    cap = a.shape[0] + b.shape[0]
+    out_d = gpu.dev_alloc(cap * 32)
+    try:
+        for _ in range(3):   # capture, then replays
+            n, per = gpu.filter_merge_device(views, [BOX, BOX], 0.05, tfs, rgbs, out_d, cap)
+            assert n == ref.shape[0] and list(per) == list(per_ref)
+            got = np.empty((n, 8), np.float32)
+            gpu.d2h(got, out_d)
+            np.testing.assert_array_equal(got[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
+        # a different box invalidates the captured graph
+        box2 = BOX.copy()
+        box2[1] = 8.0
+        n2, _ = gpu.filter_merge_device(views, [box2, box2], 0.05, tfs, rgbs, out_d, cap)
+        ref2, _ = gpu.filter_merge([a, b], [box2, box2], 0.05, tfs, rgbs)
+        assert n2 == ref2.shape[0] and n2 < n
+    finally:
+        for p in dp + [out_d]:
+            gpu.dev_free(p)
+    parts = []
+    for c, tf, rgb in zip([a, b], tfs, rgbs):
+        k = oracle.crop_box(c, BOX)
+        v, _, _, _ = oracle.voxel_grid(c[k], 0.05)
+        parts.append(oracle.transform_rgb(v, *tf, rgb))
+    np.testing.assert_array_equal(ref[:, :5].view(np.uint32),
+                                  np.concatenate(parts)[:, :5].view(np.uint32))
+
+
 # ---------------------------------------------------------------------------------- virtual_lidar
 @pytest.fixture(scope="module")
 def loaded(gpu, oracle, scene, cells, aux):
