@@ -67,12 +67,14 @@ def _grid_bbox(area, res=0.1):
 
 
 def _traffic_from_profiles(workload_key: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py), or
+    None when no measurement for this workload is committed."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
         return None
     try:
-        d = json.loads(f.read_text())
-        return d.get(workload_key)
+        d = json.loads(f.read_text()).get(workload_key)
+        return None if d is None else float(d["bytes_per_launch"])
     except Exception:
         return None
 

@@ -1,6 +1,7 @@
 // pcp_nodes.cpp -- host-side node cores over libpcp's C ABI (see pcp_nodes.hpp).
 #include "pcp_nodes.hpp"
 
+#include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <limits>

@@ -69,7 +69,8 @@ class SimplifiedScanMatcher {
         double backhoe_front_range = 15.0, backhoe_side_range = 10.0, backhoe_height_range = 10.0;
         double voxel_leaf_size = 0.2;
     };
-    explicit SimplifiedScanMatcher(Device &dev, Params p = {}) : dev_(dev), p_(p) {}
+    explicit SimplifiedScanMatcher(Device &dev) : dev_(dev) {}
+    SimplifiedScanMatcher(Device &dev, const Params &p) : dev_(dev), p_(p) {}
     Params &params() { return p_; }
     // callbacks (:52-62): the returned message is what the node publishes
     PointCloud2 robotCloudCallback(const PointCloud2 &msg) { return processCloudSimple(msg, "robot"); }
@@ -127,7 +128,8 @@ class SimplifiedDualLidarOptimizer {
         pcp_vl_report report{};
         std::string log;                   // the RCLCPP_INFO tables (:419-451, :522-543)
     };
-    explicit SimplifiedDualLidarOptimizer(Device &dev, Params p = {}) : dev_(dev), p_(p) {}
+    explicit SimplifiedDualLidarOptimizer(Device &dev) : dev_(dev) {}
+    SimplifiedDualLidarOptimizer(Device &dev, const Params &p) : dev_(dev), p_(p) {}
     Params &params() { return p_; }
     void terrainCallback(const PointCloud2 &msg);       // :180-192
     void zx120PointsCallback(const PointCloud2 &msg);   // :194-207

@@ -1,0 +1,253 @@
+// pcp_nodes_cli.cpp -- drives the C++ node cores (pcp_nodes.hpp) from files, for the parity
+// tests, and runs the streaming replay benchmark (BASELINE configs[4] on one GPU).
+//
+//   pcp_nodes_cli filter  IN.f32 N STEP LEAF FRONT SIDE HEIGHT OUT.f32
+//   pcp_nodes_cli merge   ROBOT.f32 RN ZX.f32 ZN TR(7) TZ(7) OUT.f32        (t xyz, q xyzw)
+//   pcp_nodes_cli vlidar  TERRAIN.f32 TN AUX.f32 AN CELLS.f64 NORMALS.f32 CN BBOX(6) ZXT(3) NUMC
+//                         MAXD OUT_TOTALS.f64 OUT_FLAGS.u8 OUT_REPORT.txt [TICKS]
+//   pcp_nodes_cli replay  TERRAIN.f32 TN CELLS.f64 NORMALS.f32 CN BBOX(6) FRAMES POINTS
+//
+// Tuples are comma-separated doubles.  .f32 clouds are PointXYZRGB-like records of STEP bytes
+// (terrain/aux: 32 B, x/y/z at 0/4/8).
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "pcp_nodes.hpp"
+
+using namespace pcp;
+
+static std::vector<uint8_t> read_file(const char *path) {
+    std::vector<uint8_t> b;
+    FILE *f = std::fopen(path, "rb");
+    if (!f) {
+        std::fprintf(stderr, "cannot open %s\n", path);
+        std::exit(2);
+    }
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    b.resize((size_t)n);
+    if (n && std::fread(b.data(), 1, (size_t)n, f) != (size_t)n) std::exit(2);
+    std::fclose(f);
+    return b;
+}
+
+static void write_file(const char *path, const void *p, size_t n) {
+    FILE *f = std::fopen(path, "wb");
+    if (!f || (n && std::fwrite(p, 1, n, f) != n)) {
+        std::fprintf(stderr, "cannot write %s\n", path);
+        std::exit(2);
+    }
+    std::fclose(f);
+}
+
+static std::vector<double> tuple(const char *s) {
+    std::vector<double> v;
+    std::stringstream ss(s);
+    std::string tok;
+    while (std::getline(ss, tok, ',')) v.push_back(std::strtod(tok.c_str(), nullptr));
+    return v;
+}
+
+static PointCloud2 cloud_from(const std::vector<uint8_t> &raw, size_t n, uint32_t step,
+                              const std::string &frame) {
+    PointCloud2 m;
+    m.frame_id = frame;
+    m.width = (uint32_t)n;
+    m.point_step = step;
+    m.row_step = step * (uint32_t)n;
+    m.fields = {{"x", 0}, {"y", 4}, {"z", 8}};
+    m.data.assign(raw.begin(), raw.begin() + std::min(raw.size(), n * step));
+    return m;
+}
+
+static Transform tf_from(const std::vector<double> &v) {
+    Transform t;
+    for (int i = 0; i < 3; ++i) t.t[i] = v[i];
+    for (int i = 0; i < 4; ++i) t.q[i] = v[3 + i];
+    return t;
+}
+
+static int cmd_filter(Device &dev, char **a) {
+    const auto raw = read_file(a[0]);
+    const size_t n = std::strtoull(a[1], nullptr, 10);
+    SimplifiedScanMatcher::Params p;
+    p.voxel_leaf_size = std::strtod(a[3], nullptr);
+    p.robot_front_range = std::strtod(a[4], nullptr);
+    p.robot_side_range = std::strtod(a[5], nullptr);
+    p.robot_height_range = std::strtod(a[6], nullptr);
+    SimplifiedScanMatcher node(dev, p);
+    PointCloud2 in = cloud_from(raw, n, (uint32_t)std::strtoul(a[2], nullptr, 10), "velodyne_link");
+    in.stamp = 12.5;
+    PointCloud2 out = node.robotCloudCallback(in);
+    if (!node.lastError().empty()) {
+        std::fprintf(stderr, "filter: %s\n", node.lastError().c_str());
+        return 1;
+    }
+    if (out.frame_id != in.frame_id || out.stamp != in.stamp || out.point_step != 16) return 3;
+    write_file(a[7], out.data.data(), out.data.size());
+    std::printf("{\"n_out\": %zu, \"n_cropped\": %zu}\n", out.size(), node.lastCroppedSize());
+    return 0;
+}
+
+static int cmd_merge(Device &dev, char **a) {
+    const auto r = read_file(a[0]), z = read_file(a[2]);
+    const size_t rn = std::strtoull(a[1], nullptr, 10), zn = std::strtoull(a[3], nullptr, 10);
+    GnssGicpMatcher node(dev);
+    node.robotCloudCallback(make_xyz_cloud(reinterpret_cast<const float *>(r.data()), rn, "four_wheel_robot/velodyne_link"));
+    node.backhoeCloudCallback(make_xyz_cloud(reinterpret_cast<const float *>(z.data()), zn, "zx120/velodyne_link"));
+    const Transform tr = tf_from(tuple(a[4])), tz = tf_from(tuple(a[5]));
+    auto o = node.processPointClouds(true, &tr, &tz);
+    if (!node.lastError().empty()) {
+        std::fprintf(stderr, "merge: %s\n", node.lastError().c_str());
+        return 1;
+    }
+    if (o.merged.size() != o.robot_colored.size() + o.backhoe_colored.size()) return 3;
+    auto none = node.processPointClouds(false, &tr, &tz);   // origin not set: nothing (:309)
+    if (!none.merged.empty()) return 4;
+    auto only_robot = node.processPointClouds(true, &tr, nullptr);   // zx120 TF failed
+    if (only_robot.merged.size() != o.robot_colored.size()) return 5;
+    write_file(a[6], o.merged.data.data(), o.merged.data.size());
+    std::printf("{\"n_out\": %zu, \"robot\": %zu, \"backhoe\": %zu}\n", o.merged.size(),
+                o.robot_colored.size(), o.backhoe_colored.size());
+    return 0;
+}
+
+static int cmd_vlidar(Device &dev, char **a, int argc) {
+    const auto t = read_file(a[0]), ax = read_file(a[2]), c = read_file(a[4]),
+               nr = read_file(a[5]);
+    const size_t tn = std::strtoull(a[1], nullptr, 10), an = std::strtoull(a[3], nullptr, 10),
+                 cn = std::strtoull(a[6], nullptr, 10);
+    const auto bbox = tuple(a[7]), zxt = tuple(a[8]);
+    SimplifiedDualLidarOptimizer::Params p;
+    p.num_candidates = std::atoi(a[9]);
+    p.max_distance = std::strtod(a[10], nullptr);
+    SimplifiedDualLidarOptimizer node(dev, p);
+    Transform zx;
+    zx.t[0] = zxt[0];
+    zx.t[1] = zxt[1];
+    zx.t[2] = zxt[2];
+    // before any data: the early return of :455
+    if (node.runOptimization(&zx).ran) return 3;
+    node.terrainCallback(cloud_from(t, tn, 32, "map"));
+    node.zx120PointsCallback(cloud_from(ax, an, 32, "velodyne_link"));
+    std::vector<double> xyz(cn * 3);
+    std::vector<float> nrm(cn * 3);
+    std::memcpy(xyz.data(), c.data(), xyz.size() * 8);
+    std::memcpy(nrm.data(), nr.data(), nrm.size() * 4);
+    node.setExcavationGrid(xyz, nrm, bbox.data());
+    if (node.runOptimization(nullptr).ran) return 4;   // TF missing
+    const int ticks = argc > 14 ? std::atoi(a[14]) : 1;
+    SimplifiedDualLidarOptimizer::Result r;
+    for (int i = 0; i < ticks; ++i) r = node.runOptimization(&zx);   // flags carry over
+    if (!r.ran) {
+        std::fprintf(stderr, "vlidar: %s\n", node.lastError().c_str());
+        return 1;
+    }
+    std::vector<double> tot(r.candidates.size());
+    for (size_t i = 0; i < tot.size(); ++i) tot[i] = r.candidates[i].total_score;
+    write_file(a[11], tot.data(), tot.size() * 8);
+    write_file(a[12], node.cellFlags().data(), node.cellFlags().size());
+    write_file(a[13], r.log.data(), r.log.size());
+    std::printf("{\"n_candidates\": %zu, \"best_idx\": %lld, \"best\": [%.17g, %.17g, %.17g]}\n",
+                r.candidates.size(), (long long)r.report.best_idx, r.best.x, r.best.y, r.best.z);
+    return 0;
+}
+
+// HDL-64-like scan (64 rings, -24.9..+2 deg) of n points against a ground plane
+static std::vector<float> synth_scan(size_t n, double h, std::mt19937_64 &rng) {
+    std::uniform_real_distribution<double> ua(-M_PI, M_PI), ur(1.0, 40.0);
+    std::uniform_int_distribution<int> ring(0, 63);
+    std::vector<float> p(4 * n);
+    for (size_t i = 0; i < n; ++i) {
+        const double el = (-24.9 + 26.9 * ring(rng) / 63.0) * M_PI / 180.0, az = ua(rng);
+        double r = ur(rng);
+        if (el < 0) r = std::min(r, h / std::sin(-el));
+        p[4 * i] = (float)(r * std::cos(el) * std::cos(az));
+        p[4 * i + 1] = (float)(r * std::cos(el) * std::sin(az));
+        p[4 * i + 2] = (float)(r * std::sin(el));
+        p[4 * i + 3] = 0.f;
+    }
+    return p;
+}
+
+static int cmd_replay(Device &dev, char **a) {
+    const auto t = read_file(a[0]), c = read_file(a[2]), nr = read_file(a[3]);
+    const size_t tn = std::strtoull(a[1], nullptr, 10), cn = std::strtoull(a[4], nullptr, 10);
+    const auto bbox = tuple(a[5]);
+    const int frames = std::atoi(a[6]);
+    const size_t npts = std::strtoull(a[7], nullptr, 10);
+    SimplifiedScanMatcher filt(dev);
+    GnssGicpMatcher merger(dev);
+    SimplifiedDualLidarOptimizer vl(dev);
+    vl.terrainCallback(cloud_from(t, tn, 32, "map"));
+    std::vector<double> xyz(cn * 3);
+    std::vector<float> nrm(cn * 3);
+    std::memcpy(xyz.data(), c.data(), xyz.size() * 8);
+    std::memcpy(nrm.data(), nr.data(), nrm.size() * 4);
+    vl.setExcavationGrid(xyz, nrm, bbox.data());
+    std::mt19937_64 rng(20260227);
+    const Transform robot_tf{{8.0, -3.0, 2.0}, {0.0, 0.0, 0.2588190451025208, 0.9659258262890683}};
+    const Transform zx_tf{{0.55, 0.4, 3.5}, {0.0, 0.21633, 0.0, 0.97632}};
+    const Transform zx_base{{0.0, 0.0, 0.0}, {0, 0, 0, 1}};
+    std::vector<double> lat;
+    size_t merged_n = 0, best = 0;
+    for (int f = 0; f < frames + 2; ++f) {
+        auto rs = synth_scan(npts, 2.0, rng), zs = synth_scan(npts, 3.5, rng);
+        PointCloud2 rm = make_xyz_cloud(rs.data(), npts, "four_wheel_robot/velodyne_link");
+        PointCloud2 zm = make_xyz_cloud(zs.data(), npts, "zx120/velodyne_link");
+        const auto t0 = std::chrono::steady_clock::now();
+        // pointcloud_filter: both sensors; pointcloud_merger: 10 Hz tick; virtual_lidar: zx120
+        // filtered cloud + the pose search
+        PointCloud2 rf = filt.robotCloudCallback(rm), zf = filt.backhoeCloudCallback(zm);
+        merger.robotCloudCallback(rf);
+        merger.backhoeCloudCallback(zf);
+        auto o = merger.processPointClouds(true, &robot_tf, &zx_tf);
+        vl.zx120PointsCallback(zf);
+        auto r = vl.runOptimization(&zx_base);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (!r.ran) {
+            std::fprintf(stderr, "replay: pose search did not run: %s\n", vl.lastError().c_str());
+            return 1;
+        }
+        merged_n = o.merged.size();
+        best = (size_t)r.report.best_idx;
+        if (f >= 2) lat.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+    }
+    std::sort(lat.begin(), lat.end());
+    auto q = [&lat](double p) { return lat[std::min(lat.size() - 1, (size_t)(p * lat.size()))]; };
+    std::printf("{\"frames\": %zu, \"points_per_scan\": %zu, \"p50_ms\": %.4f, \"p99_ms\": %.4f, "
+                "\"max_ms\": %.4f, \"merged_points\": %zu, \"best_idx\": %zu}\n",
+                lat.size(), npts, q(0.5), q(0.99), lat.back(), merged_n, best);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: pcp_nodes_cli filter|merge|vlidar|replay ...\n");
+        return 2;
+    }
+    const std::string cmd = argv[1];
+    const int need = cmd == "filter" ? 8 : cmd == "merge" ? 7 : cmd == "vlidar" ? 14 : cmd == "replay" ? 8 : -1;
+    if (need < 0 || argc - 2 < need) {
+        std::fprintf(stderr, "bad arguments for %s\n", cmd.c_str());
+        return 2;
+    }
+    try {
+        Device dev(0);
+        if (cmd == "filter") return cmd_filter(dev, argv + 2);
+        if (cmd == "merge") return cmd_merge(dev, argv + 2);
+        if (cmd == "vlidar") return cmd_vlidar(dev, argv + 2, argc - 2);
+        return cmd_replay(dev, argv + 2);
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "%s\n", e.what());
+        return 1;
+    }
+}

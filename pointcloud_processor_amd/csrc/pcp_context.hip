@@ -248,6 +248,10 @@ int pcp_create(int device, pcp_ctx **out) {
     if (!ctx) return PCP_E_NOMEM;
     ctx->device = device;
     if (const char *fb = std::getenv("PCP_FAN_BATCH")) ctx->fan_batch = std::atoi(fb);
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        cus > 0)
+        ctx->num_cus = cus;
     if (const char *ng = std::getenv("PCP_NO_GRAPHS")) ctx->use_graphs = std::atoi(ng) == 0;
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;

@@ -42,6 +42,10 @@ GridView GridIndex::view() const {
     v.by1 = bmax[1] + rb;
     v.bz0 = bmin[2] - rb;
     v.bz1 = bmax[2] + rb;
+    v.colmap = colmap_ok ? colmap.as<const uint16_t>() : nullptr;
+    v.ncx = ncx;
+    v.ncy = ncy;
+    v.col_shift = col_shift;
     return v;
 }
 
@@ -204,6 +208,28 @@ k_occ2(const uint32_t *__restrict__ start, CellMap m, uint64_t ncell, uint32_t *
     occ2[w] = bits;
 }
 
+// column z-range map over the dilated occupancy (one thread per column)
+__global__ void __launch_bounds__(kThreads)
+k_colmap(const uint32_t *__restrict__ occ2, CellMap m, int shift, int ncx, int ncy,
+         uint16_t *__restrict__ colmap) {
+    const int c = blockIdx.x * kThreads + threadIdx.x;
+    if (c >= ncx * ncy) return;
+    const int cx = c % ncx, cy = c / ncx;
+    int lo = 255, hi = 0;
+    const int x0 = cx << shift, y0 = cy << shift;
+    const int x1 = min(x0 + (1 << shift), m.nx), y1 = min(y0 + (1 << shift), m.ny);
+    for (int iz = 0; iz < m.nz; ++iz)
+        for (int iy = y0; iy < y1; ++iy)
+            for (int ix = x0; ix < x1; ++ix) {
+                const uint64_t lin = (uint64_t)ix + (uint64_t)m.nx * ((uint64_t)iy + (uint64_t)m.ny * iz);
+                if ((occ2[lin >> 5] >> (lin & 31)) & 1u) {
+                    lo = min(lo, iz);
+                    hi = max(hi, iz);
+                }
+            }
+    colmap[c] = (uint16_t)(lo | (hi << 8));
+}
+
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q) {
     const uint64_t n = v.n;
     hipStream_t st = ctx->stream;
@@ -244,6 +270,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q)
         PCP_HIP(ctx, g.occ2.ensure(16));
         PCP_HIP(ctx, hipMemsetAsync(g.start.p, 0, 16, st));
         PCP_HIP(ctx, hipMemsetAsync(g.occ2.p, 0, 16, st));
+        g.colmap_ok = false;
         return PCP_OK;
     }
     for (int a = 0; a < 3; ++a) {
@@ -303,6 +330,28 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q)
     hipLaunchKernelGGL(k_occ2, dim3((unsigned)((nw + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                        st, g.start.as<const uint32_t>(), m, ncell, g.occ2.as<uint32_t>());
     PCP_CHECK_LAUNCH(ctx);
+    // 9. column z-range map (fits the LDS budget of the persistent fan kernel: <= 32 KiB)
+    g.colmap_ok = false;
+    if (g.nz <= 255) {
+        for (int sh = 2; sh <= 6; ++sh) {
+            const int ncx = (g.nx + (1 << sh) - 1) >> sh, ncy = (g.ny + (1 << sh) - 1) >> sh;
+            if ((size_t)ncx * ncy * 2 <= 32768) {
+                g.ncx = ncx;
+                g.ncy = ncy;
+                g.col_shift = sh;
+                g.colmap_ok = true;
+                break;
+            }
+        }
+    }
+    if (g.colmap_ok) {
+        const int nc = g.ncx * g.ncy;
+        PCP_HIP(ctx, g.colmap.ensure((size_t)nc * 2 + 16));
+        hipLaunchKernelGGL(k_colmap, dim3((nc + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
+                           g.occ2.as<const uint32_t>(), m, g.col_shift, g.ncx, g.ncy,
+                           g.colmap.as<uint16_t>());
+        PCP_CHECK_LAUNCH(ctx);
+    }
     PCP_HIP(ctx, hipStreamSynchronize(st));
     return PCP_OK;
 }

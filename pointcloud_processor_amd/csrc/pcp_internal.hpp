@@ -68,6 +68,11 @@ struct GridView {               // POD passed to kernels by value
     uint32_t n_pts;
     // tight bbox of the points, inflated by r_q + margin: samples outside are empty
     double bx0, bx1, by0, by1, bz0, bz1;
+    // column z-range map: for each column of 2^col_shift x 2^col_shift stencil corners, the
+    // lowest (low byte) and highest (high byte) corner z-index whose occ2 bit is set; empty
+    // columns hold lo 255 / hi 0.  A corner outside its column's range is provably empty.
+    const uint16_t *colmap;     // null when disabled (nz > 255 or too large for LDS)
+    int32_t ncx, ncy, col_shift;
 };
 
 struct GridIndex {
@@ -77,12 +82,16 @@ struct GridIndex {
     double c = 0.0;
     int32_t nx = 0, ny = 0, nz = 0;
     double bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
-    DevBuf pts, start, occ2;
+    DevBuf pts, start, occ2, colmap;
+    int32_t ncx = 0, ncy = 0, col_shift = 0;
+    bool colmap_ok = false;
     GridView view() const;
     void release() {
         pts.release();
         start.release();
         occ2.release();
+        colmap.release();
+        colmap_ok = false;
         present = false;
         n_pts = 0;
     }
@@ -135,6 +144,7 @@ struct pcp_ctx {
     double fan_elmin = 0.0, fan_elmax = 0.0;
     double steps_end = -1e300;               // cached step table
     int steps_K = 0;
+    int num_cus = 256;                       // multiprocessors of the device
     int fan_batch = 1;                       // tuning knob (PCP_FAN_BATCH), A/B only
     // filter/merge scratch
     pcp::DevBuf f_in, f_misc;

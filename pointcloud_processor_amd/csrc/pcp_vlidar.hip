@@ -6,6 +6,7 @@
 // L2_Simple<float> (x, y, z accumulated in order, strict '<' against float(r*r)).
 #pragma clang fp contract(off)
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -33,16 +34,26 @@ __device__ __forceinline__ bool flann_within(float qx, float qy, float qz, const
 // Lower-corner cell of the 2x2x2 stencil of a query (q - r - margin).  False when the corner
 // falls outside [0, n-2]^3: then the stencil holds only padding / outside cells and no point
 // can be within r (exact skip, see DESIGN.md "Terrain index").
-__device__ __forceinline__ bool stencil_cell(const GridView &g, float qx, float qy, float qz,
-                                             uint32_t &lin) {
+__device__ __forceinline__ bool stencil_cell3(const GridView &g, float qx, float qy, float qz,
+                                              uint32_t &ix, uint32_t &iy, uint32_t &iz) {
     const double fx = ((double)qx - g.lo_x) * g.inv_c;
     const double fy = ((double)qy - g.lo_y) * g.inv_c;
     const double fz = ((double)qz - g.lo_z) * g.inv_c;
     if (!(fx >= 0.0 && fx < (double)(g.nx - 1) && fy >= 0.0 && fy < (double)(g.ny - 1) &&
           fz >= 0.0 && fz < (double)(g.nz - 1)))
         return false;
+    ix = (uint32_t)fx;
+    iy = (uint32_t)fy;
+    iz = (uint32_t)fz;
+    return true;
+}
+
+__device__ __forceinline__ bool stencil_cell(const GridView &g, float qx, float qy, float qz,
+                                             uint32_t &lin) {
+    uint32_t ix, iy, iz;
+    if (!stencil_cell3(g, qx, qy, qz, ix, iy, iz)) return false;
     const uint32_t nx = (uint32_t)g.nx, nxy = nx * (uint32_t)g.ny;
-    lin = (uint32_t)fx + nx * (uint32_t)fy + nxy * (uint32_t)fz;
+    lin = ix + nx * iy + nxy * iz;
     return true;
 }
 
@@ -153,11 +164,13 @@ __device__ __forceinline__ void clip_k(const GridView &g, double px, double py, 
 // clip box have no point within r (skipped exactly).  s_k comes from ONE table read at klo and
 // then the same repeated addition that built the table (identical doubles).  Samples are
 // processed 4 at a time: the 4 occupancy words are loaded together, then tested in order.
+// col (optional, LDS copy of g.colmap): a stencil corner outside its column's occupied z-range
+// is empty, decided from LDS without touching the occupancy bits in global memory.
 template <bool STATS, int B = 1>
 __device__ __forceinline__ int march_t(const GridView &g, double px, double py, double pz,
                                        double dx, double dy, double dz,
                                        const double *__restrict__ steps, int K, double end,
-                                       float r2, uint32_t *cnt) {
+                                       float r2, uint32_t *cnt, const uint16_t *col = nullptr) {
     int klo, khi;
     clip_k(g, px, py, pz, dx, dy, dz, K, klo, khi);
     if (klo > khi) return -1;
@@ -173,7 +186,13 @@ __device__ __forceinline__ int march_t(const GridView &g, double px, double py, 
             qy[i] = (float)(py + dy * s);
             qz[i] = (float)(pz + dz * s);
             lin[i] = 0;
-            const bool in = vis[i] && stencil_cell(g, qx[i], qy[i], qz[i], lin[i]);
+            uint32_t ix = 0, iy = 0, iz = 0;
+            bool in = vis[i] && stencil_cell3(g, qx[i], qy[i], qz[i], ix, iy, iz);
+            if (in && col) {
+                const uint32_t zr = col[(iy >> g.col_shift) * (uint32_t)g.ncx + (ix >> g.col_shift)];
+                in = iz >= (zr & 255u) && iz <= (zr >> 8);
+            }
+            lin[i] = ix + (uint32_t)g.nx * (iy + (uint32_t)g.ny * iz);
             word[i] = in ? g.occ2[lin[i] >> 5] : 0u;
             s = s + kRayStep;
         }
@@ -488,6 +507,8 @@ struct FanArgs {
     int uniform_el;        // every wave lies in one elevation ring
     uint32_t rays;
     uint32_t waves;        // waves per pose = ceil(rays / 64)
+    uint32_t items;        // P * ceil(rays / 256) work items of the persistent kernel
+    uint32_t *queue;       // persistent kernel's work-queue head
     float r2;
     int present;
     int16_t *first_hit;
@@ -503,9 +524,10 @@ enum { FAN_PLAIN = 0, FAN_STATS = 1, FAN_STAMPS = 2 };
 // termination on near-flat terrain); blockIdx.y = pose.  Each wave writes its blocked-ray
 // count and its sample-query count to its own slot: the per-pose sums are formed by
 // k_fan_reduce in a fixed order (deterministic, no same-address atomics).
-template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
-    const uint32_t p = blockIdx.y;
-    const uint32_t ray = blockIdx.x * kT + threadIdx.x;
+template <int MODE, int B>
+__device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t rblock,
+                                         const uint16_t *col) {
+    const uint32_t ray = rblock * kT + threadIdx.x;
     const bool active = ray < a.rays;
     const uint32_t wslot = (uint32_t)p * a.waves + (ray >> 6);
     unsigned long long t0 = 0, t1 = 0, t2 = 0;
@@ -528,7 +550,7 @@ template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan(F
             t1 = __builtin_amdgcn_s_memtime();
         }
         hit = march_t<MODE == FAN_STATS, B>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K,
-                                            1e300, a.r2, cnt);
+                                            1e300, a.r2, cnt, col);
     }
     if (MODE == FAN_STAMPS) {
         asm volatile("" ::"v"(hit));
@@ -559,6 +581,42 @@ template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan(F
         o[1] = t1;
         o[2] = t2;
         o[3] = t3;
+    }
+}
+
+// one block per (ray block, pose); no column map
+template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
+    fan_body<MODE, B>(a, blockIdx.y, blockIdx.x, nullptr);
+}
+
+// persistent: a CU-filling grid strides over the (pose, ray block) items; each block stages the
+// column z-range map in LDS once (dynamic LDS, 16-B aligned base per the LDS guideline)
+template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan_p(FanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t s_col[];
+    const uint16_t *col = nullptr;
+    if (a.g.colmap) {
+        const uint32_t n16 = ((uint32_t)(a.g.ncx * a.g.ncy) + 7) / 8;   // uint4 chunks
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.g.colmap);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_col);
+        for (uint32_t k = threadIdx.x; k < n16; k += kT) dst[k] = src[k];
+        __syncthreads();
+        col = s_col;
+    }
+    const uint32_t per_pose = (a.rays + kT - 1) / kT;
+    // dynamic work queue: chunks of 8 items from one head word (zeroed before every launch);
+    // every block exits once the head passes the item count, whatever the residency
+    __shared__ uint32_t s_chunk;
+    for (;;) {
+        if (threadIdx.x == 0) s_chunk = atomicAdd(a.queue, 8u);
+        __syncthreads();
+        const uint32_t c0 = s_chunk;
+        __syncthreads();
+        if (c0 >= a.items) break;
+        const uint32_t c1 = min(c0 + 8u, a.items);
+        for (uint32_t w = c0; w < c1; ++w) {
+            const uint32_t p = w / per_pose;
+            fan_body<MODE, B>(a, p, w - p * per_pose, col);
+        }
     }
 }
 
@@ -899,6 +957,18 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     a.wave_units = a.wave_blocked + (size_t)P * waves;
     a.stats = ctx->stats_d.as<unsigned long long>();
     const dim3 grid((rays + kT - 1) / kT, P);
+    const uint32_t per_pose = (rays + kT - 1) / kT;
+    a.items = per_pose * (uint32_t)P;
+    // persistent launch: 6 blocks per CU (the SGPR budget admits 6), column map in LDS
+    const size_t lds = a.g.colmap ? ((size_t)a.g.ncx * a.g.ncy * 2 + 15) / 16 * 16 : 0;
+    int occ_blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_blocks, k_raycast_fan_p<FAN_PLAIN, 1>, kT,
+                                                     lds) != hipSuccess || occ_blocks < 1)
+        occ_blocks = 4;
+    const unsigned pgrid = std::min<unsigned>(a.items, (unsigned)ctx->num_cus * (unsigned)occ_blocks);
+    PCP_HIP(ctx, ctx->out_a.ensure(256));
+    a.queue = ctx->out_a.as<uint32_t>();
+    PCP_HIP(ctx, hipMemsetAsync(a.queue, 0, 16, st));
     if (stats) {
         PCP_HIP(ctx, hipMemsetAsync(a.stats, 0, 4 * sizeof(uint64_t), st));
         hipLaunchKernelGGL((k_raycast_fan<FAN_STATS, 1>), grid, dim3(kT), 0, st, a);
@@ -910,10 +980,10 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
         PCP_HIP(ctx, hipMemcpyAsync(stamps, a.stats, stats_bytes, hipMemcpyDeviceToHost, st));
     } else {
         ProfScope ps(ctx, PCP_K_RAYCAST_FAN);
-        // samples per occupancy round: 1 by default (fewest VGPRs); PCP_FAN_BATCH (2/4) for A/B
+        // default: one block per (ray block, pose); PCP_FAN_BATCH selects A/B variants
         switch (ctx->fan_batch) {
-        case 2: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 2>), grid, dim3(kT), 0, st, a); break;
-        case 4: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 4>), grid, dim3(kT), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((k_raycast_fan_p<FAN_PLAIN, 1>), dim3(pgrid), dim3(kT), lds, st, a); break;
+        case 4: hipLaunchKernelGGL((k_raycast_fan_p<FAN_PLAIN, 2>), dim3(pgrid), dim3(kT), lds, st, a); break;
         default: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 1>), grid, dim3(kT), 0, st, a); break;
         }
         PCP_CHECK_LAUNCH(ctx);
