@@ -106,14 +106,13 @@ struct ProfSlot {
 };
 
 struct CloudBufs {                 // one cloud's filter-pipeline scratch
-    DevBuf xyz, idx, keys[2], vals[2], hist, out;
+    DevBuf xyz, idx, keys[2], sparse, sparse_idx, hist, out;
     void release() {
         xyz.release();
         idx.release();
-        for (int q = 0; q < 2; ++q) {
-            keys[q].release();
-            vals[q].release();
-        }
+        for (int q = 0; q < 2; ++q) keys[q].release();
+        sparse.release();
+        sparse_idx.release();
         hist.release();
         out.release();
     }
@@ -150,7 +149,7 @@ struct pcp_ctx {
     pcp::DevBuf f_in, f_misc;
     std::vector<pcp::CloudBufs> fbuf;        // per-cloud scratch of the filter pipeline
     std::vector<hipStream_t> side;           // per-cloud branch streams
-    std::vector<hipEvent_t> side_ev;
+    std::vector<hipEvent_t> side_ev, emit_ev;
     hipEvent_t fork_ev = nullptr;
     // captured filter_merge pipeline (device-resident inputs), replayed while its key matches
     hipGraph_t fm_graph = nullptr;

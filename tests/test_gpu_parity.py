@@ -70,6 +70,21 @@ def test_voxel_grid_exact(gpu, oracle, n, leaf):
     assert np.array_equal(out[:, :3], r_xyz)
 
 
+@pytest.mark.parametrize("n,span", [(200_000, 1.0), (100_000, 0.01)])
+def test_voxel_grid_dense_voxels(gpu, oracle, n, span):
+    """Thousands of points per voxel (span 1 m / leaf 0.2 = 125 voxels) and a single voxel
+    holding every point: segments crossing many sort tiles, long in-order centroid sums."""
+    rng = np.random.default_rng(n)
+    a = np.zeros((n, 4), np.float32)
+    a[:, :3] = rng.uniform(0.0, span, (n, 3))
+    out, idx, cnt, pt = gpu.voxel_grid(a, 0.2)
+    r_xyz, r_idx, r_cnt, _ = oracle.voxel_grid(a, 0.2)
+    assert not pt
+    np.testing.assert_array_equal(idx, r_idx)
+    np.testing.assert_array_equal(cnt, r_cnt)
+    np.testing.assert_array_equal(out[:, :3], r_xyz)
+
+
 def test_voxel_grid_nan_and_overflow(gpu, oracle):
     a = _cloud(20_000, 3, nan_frac=0.05)
     out, idx, cnt, pt = gpu.voxel_grid(a, 0.2)
