@@ -276,10 +276,6 @@ void pcp_destroy(pcp_ctx *ctx) {
     for (DevBuf *b : bufs) b->release();
     for (auto &b : ctx->scratch) b.release();
     for (auto &b : ctx->fbuf) b.release();
-    for (hipStream_t s2 : ctx->side) (void)hipStreamDestroy(s2);
-    for (hipEvent_t e : ctx->side_ev) (void)hipEventDestroy(e);
-    for (hipEvent_t e : ctx->emit_ev) (void)hipEventDestroy(e);
-    if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
     if (ctx->fm_exec) (void)hipGraphExecDestroy(ctx->fm_exec);
     if (ctx->fm_graph) (void)hipGraphDestroy(ctx->fm_graph);
     (void)hipStreamDestroy(ctx->stream);

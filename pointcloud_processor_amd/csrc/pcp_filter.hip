@@ -1,10 +1,14 @@
 // pcp_filter.hip -- pointcloud_filter.cpp (crop + VoxelGrid) and pointcloud_merger.cpp
 // (tf2::doTransform + colour + concat) on gfx950.
 //
-//  crop    : two-pass stable stream compaction (wave ballot + block scan, order kept)
-//  voxel   : PCL VoxelGrid<PointXYZ> keying in float exactly as applyFilter, stable LSD
-//            radix sort of (key, cropped index) with 8-bit digits, segment heads + scan,
-//            per-voxel float centroid summed in input order
+// Every kernel is batched over clouds: blockIdx.y = cloud, its job (input view, box, leaf,
+// scratch, transform) read from a device table, so a dual-LiDAR frame is one chain of ~12
+// launches in which every launch covers all clouds' tiles.
+//  crop    : one read of the input; stable compaction per 4096-point tile into a sparse buffer,
+//            gaps closed (and voxel keys computed) by a second, small kernel
+//  voxel   : PCL VoxelGrid<PointXYZ> keying in float exactly as applyFilter; stable LSD radix
+//            sort of (key, point) with 9-bit digits (LDS-staged, coalesced scatter); voxel
+//            heads + float centroids summed in input order
 //  merge   : Eigen float Affine3f * p = ((m0 x + m1 y) + m2 z) + t, PointXYZRGB records
 #pragma clang fp contract(off)
 
@@ -62,6 +66,29 @@ __device__ __forceinline__ void load_xyz(const CloudIn &c, uint64_t i, float &x,
         x = *reinterpret_cast<const float *>(p + c.ox);
         y = *reinterpret_cast<const float *>(p + c.oy);
         z = *reinterpret_cast<const float *>(p + c.oz);
+    }
+}
+
+// a crop tile's points: item j of thread t is base + j*kFT + t (coalesced); indices past the
+// end are clamped to the last point (the caller masks them)
+template <bool PXYZ16>
+__device__ __forceinline__ void load_tile(const CloudIn &c, uint64_t base, float (&x)[kCropItems],
+                                          float (&y)[kCropItems], float (&z)[kCropItems]) {
+    const uint64_t last = c.n - 1;
+#pragma unroll
+    for (int j = 0; j < kCropItems; ++j) {
+        const uint64_t i = min(base + (uint64_t)j * kFT + threadIdx.x, last);
+        if constexpr (PXYZ16) {
+            const float4 v = reinterpret_cast<const float4 *>(c.raw)[i];
+            x[j] = v.x;
+            y[j] = v.y;
+            z[j] = v.z;
+        } else {
+            const unsigned char *p = c.raw + i * c.step;
+            x[j] = *reinterpret_cast<const float *>(p + c.ox);
+            y[j] = *reinterpret_cast<const float *>(p + c.oy);
+            z[j] = *reinterpret_cast<const float *>(p + c.oz);
+        }
     }
 }
 
@@ -143,20 +170,117 @@ __device__ __forceinline__ uint32_t round_offsets(const uint64_t (&bal)[J], uint
     return tot;
 }
 
+// ---- voxel parameters (VoxelGrid::applyFilter, computed in float exactly) -------------------
+struct VoxParams {
+    uint32_t m;          // points after the crop
+    int32_t overflow;    // PCL int32 guard fired -> passthrough
+    int32_t do_voxel;    // leaf > 0
+    float inv;
+    int32_t min_b[3];
+    int32_t div_b[3];
+    uint32_t mul1, mul2;
+    uint64_t nvox;       // div product (key upper bound)
+};
+
+// points that go through the sort: all cropped points when voxelising without overflow
+__device__ __forceinline__ uint32_t sort_count(const VoxParams &vp) {
+    return (vp.do_voxel && !vp.overflow) ? vp.m : 0u;
+}
+__device__ __forceinline__ uint32_t sort_tiles(const VoxParams &vp) {
+    return (sort_count(vp) + kSortTile - 1) / kSortTile;
+}
+
+// ---- SE(3) + colour (tf2::doTransform + processRobotCloud loop) ------------------------------
+struct Rigid {
+    float m00, m01, m02, m10, m11, m12, m20, m21, m22, tx, ty, tz;
+    uint32_t rgba;
+};
+
+static Rigid make_rigid(const pcp_rigid &t, const uint8_t rgb[3]) {
+    // Eigen::Quaternionf(w,x,y,z).toRotationMatrix() in float
+    const float qx = (float)t.q[0], qy = (float)t.q[1], qz = (float)t.q[2], qw = (float)t.q[3];
+    const float tx = 2.0f * qx, ty = 2.0f * qy, tz = 2.0f * qz;
+    const float twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    const float txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    Rigid r;
+    r.m00 = 1.0f - (tyy + tzz);
+    r.m01 = txy - twz;
+    r.m02 = txz + twy;
+    r.m10 = txy + twz;
+    r.m11 = 1.0f - (txx + tzz);
+    r.m12 = tyz - twx;
+    r.m20 = txz - twy;
+    r.m21 = tyz + twx;
+    r.m22 = 1.0f - (txx + tyy);
+    r.tx = (float)t.t[0];
+    r.ty = (float)t.t[1];
+    r.tz = (float)t.t[2];
+    r.rgba = (uint32_t)rgb[2] | ((uint32_t)rgb[1] << 8) | ((uint32_t)rgb[0] << 16) | (255u << 24);
+    return r;
+}
+
+// Affine3f * Vector3f as the homogeneous 4x4 packet product: ((m0 x + m1 y) + m2 z) + t
+__device__ __forceinline__ void xform_store(const Rigid &r, float x, float y, float z, float4 *o) {
+    const float X = ((r.m00 * x + r.m01 * y) + r.m02 * z) + r.tx;
+    const float Y = ((r.m10 * x + r.m11 * y) + r.m12 * z) + r.ty;
+    const float Z = ((r.m20 * x + r.m21 * y) + r.m22 * z) + r.tz;
+    o[0] = make_float4(X, Y, Z, 1.0f);
+    o[1] = make_float4(__uint_as_float(r.rgba), 0.f, 0.f, 0.f);
+}
+
+// one cloud's job in a batched launch (blockIdx.y indexes the device table of these)
+struct CloudJob {
+    CloudIn in;           // input view (raw may be null when n == 0)
+    Box box;
+    float leaf;           // <= 0: crop only
+    int32_t passes;       // radix passes (0: no voxel stage)
+    uint32_t nb;          // crop tiles, ceil(n / kCropTile)
+    uint32_t ntp, ngp, nzero;
+    uint32_t *counts;     // [nb] kept points per crop tile
+    float *part;          // [nb][6] bbox partials
+    float4 *sparse;       // crop tiles, later the odd radix passes' payload
+    uint32_t *sparse_idx; // crop tiles' input indices (null unless kept indices wanted)
+    float4 *xyz;          // compact cropped points, the even passes' payload
+    uint32_t *kept_idx;   // compact kept indices (null unless wanted)
+    uint32_t *keys0, *keys1;
+    uint32_t *zero;       // digit totals [kMaxPasses][kBins] then group sums [kMaxPasses][ngp][kBins]
+    uint32_t *rhist;      // [kBins][ntp] tile digit counts (reused by every pass)
+    uint32_t *tcount, *fhead;
+    float4 *out4;         // voxel centroids
+    uint32_t *vidx, *vcnt;
+    VoxParams *vp;
+    Rigid rig;            // pcp_filter_merge's transform + colour of this cloud
+    int32_t slot;         // result slot (index of the cloud in the call)
+};
+
+// up to kBatch clouds per launch, passed BY VALUE: pointers loaded from kernel arguments are
+// known to be global (global_load, independent waits), which a table in memory would lose
+constexpr int kBatch = 8;
+struct JobBatch {
+    CloudJob j[kBatch];
+};
+
 // ---- crop: one read of the input; stable compaction of each tile into its own slot of a
 //      sparse buffer (kept count + bbox partial per tile); k_compact_keys closes the gaps ----
-__global__ void __launch_bounds__(kFT)
-k_crop_tile(CloudIn c, Box b, uint32_t *__restrict__ counts, float *__restrict__ part,
-            float4 *__restrict__ sparse, uint32_t *__restrict__ sparse_idx) {
+__global__ void __launch_bounds__(kFT) k_crop_tile(const JobBatch jobs) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    if (blockIdx.x >= J.nb) return;
+    const CloudIn c = J.in;
+    const Box b = J.box;
+    uint32_t *counts = J.counts;
+    float *part = J.part;
+    float4 *sparse = J.sparse;
+    uint32_t *sparse_idx = J.sparse_idx;
     const uint64_t base = (uint64_t)blockIdx.x * kCropTile;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     float x[kCropItems], y[kCropItems], z[kCropItems];
-#pragma unroll
-    for (int j = 0; j < kCropItems; ++j) {
-        const uint64_t i = base + (uint64_t)j * kFT + threadIdx.x;
-        x[j] = y[j] = z[j] = 0.f;
-        if (i < c.n) load_xyz(c, i, x[j], y[j], z[j]);
-    }
+    // one uniform layout branch, then unconditional loads (indices clamped to the last point,
+    // masked below): no control flow between the loads, all 16 in flight at once
+    if (c.step == 16 && c.ox == 0 && c.oy == 4 && c.oz == 8)
+        load_tile<true>(c, base, x, y, z);
+    else
+        load_tile<false>(c, base, x, y, z);
     uint64_t bal[kCropItems];
     uint32_t keep = 0;
 #pragma unroll
@@ -204,32 +328,18 @@ k_crop_tile(CloudIn c, Box b, uint32_t *__restrict__ counts, float *__restrict__
     }
 }
 
-// ---- voxel parameters (VoxelGrid::applyFilter, computed in float exactly) -------------------
-struct VoxParams {
-    uint32_t m;          // points after the crop
-    int32_t overflow;    // PCL int32 guard fired -> passthrough
-    int32_t do_voxel;    // leaf > 0
-    float inv;
-    int32_t min_b[3];
-    int32_t div_b[3];
-    uint32_t mul1, mul2;
-    uint64_t nvox;       // div product (key upper bound)
-};
-
-// points that go through the sort: all cropped points when voxelising without overflow
-__device__ __forceinline__ uint32_t sort_count(const VoxParams &vp) {
-    return (vp.do_voxel && !vp.overflow) ? vp.m : 0u;
-}
-__device__ __forceinline__ uint32_t sort_tiles(const VoxParams &vp) {
-    return (sort_count(vp) + kSortTile - 1) / kSortTile;
-}
-
 // cropped count + bbox -> parameters; the result count of a crop-only / passthrough cloud
 // (res[slot] = m; a voxelised cloud's count is written by k_seg_centroid)
 __global__ void __launch_bounds__(kFT)
-k_vox_params(const float *__restrict__ part, const uint32_t *__restrict__ counts, int nb,
-             float leaf, VoxParams *__restrict__ vp, uint32_t *__restrict__ res,
-             uint32_t *__restrict__ info, int slot) {
+k_vox_params(const JobBatch jobs, uint32_t *__restrict__ res,
+             uint32_t *__restrict__ info) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    const float *part = J.part;
+    const uint32_t *counts = J.counts;
+    const int nb = (int)J.nb;
+    const float leaf = J.leaf;
+    VoxParams *vp = J.vp;
+    const int slot = J.slot;
     __shared__ uint32_t lds4[kFT / 64];
     const uint32_t m = block_prefix_sum<kFT>(counts, (uint32_t)nb, lds4);
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -290,13 +400,18 @@ k_vox_params(const float *__restrict__ part, const uint32_t *__restrict__ counts
 }
 
 // ---- gaps closed: tile t's kept points go to [sum of earlier counts ...); voxel keys -------
-__global__ void __launch_bounds__(kFT)
-k_compact_keys(const float4 *__restrict__ sparse, const uint32_t *__restrict__ sparse_idx,
-               const uint32_t *__restrict__ counts, const VoxParams *__restrict__ vpp,
-               float4 *__restrict__ xyz, uint32_t *__restrict__ kept_idx,
-               uint32_t *__restrict__ keys, uint32_t *__restrict__ zero, uint32_t nzero) {
+__global__ void __launch_bounds__(kFT) k_compact_keys(const JobBatch jobs) {
+    const CloudJob &J = jobs.j[blockIdx.y];
     // digit totals + group sums of every radix pass (accumulated by k_radix_hist) start at 0
-    for (uint32_t q = blockIdx.x * kFT + threadIdx.x; q < nzero; q += gridDim.x * kFT) zero[q] = 0;
+    if (J.passes > 0)
+        for (uint32_t q = blockIdx.x * kFT + threadIdx.x; q < J.nzero; q += gridDim.x * kFT)
+            J.zero[q] = 0;
+    if (blockIdx.x >= J.nb) return;
+    const float4 *sparse = J.sparse;
+    const uint32_t *sparse_idx = J.sparse_idx, *counts = J.counts;
+    const VoxParams *vpp = J.vp;
+    float4 *xyz = J.xyz;
+    uint32_t *kept_idx = J.kept_idx, *keys = J.keys0;
     const uint32_t cnt = counts[blockIdx.x];
     if (cnt == 0) return;   // uniform per block
     __shared__ uint32_t lds4[kFT / 64];
@@ -322,10 +437,16 @@ k_compact_keys(const float4 *__restrict__ sparse, const uint32_t *__restrict__ s
 // hist[d * ntp + t] = count of digit d in tile t; totals[d] and the group sums
 // gsum[(t / kGroup) * kBins + d] accumulate the tiles' counts (one 256-B atomic row per wave),
 // so a tile's count of earlier items of digit d needs <= ngroups + 4 independent loads.
-__global__ void __launch_bounds__(kST)
-k_radix_hist(const uint32_t *__restrict__ keys, const VoxParams *__restrict__ vpp, int shift,
-             uint32_t ntp, uint32_t *__restrict__ hist, uint32_t *__restrict__ totals,
-             uint32_t *__restrict__ gsum) {
+__global__ void __launch_bounds__(kST) k_radix_hist(const JobBatch jobs, int pass) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    if (pass >= J.passes) return;
+    const uint32_t *keys = (pass & 1) ? J.keys1 : J.keys0;
+    const VoxParams *vpp = J.vp;
+    const int shift = kDigitBits * pass;
+    const uint32_t ntp = J.ntp;
+    uint32_t *hist = J.rhist;
+    uint32_t *totals = J.zero + pass * kBins;
+    uint32_t *gsum = J.zero + (size_t)kMaxPasses * kBins + (size_t)pass * J.ngp * kBins;
     const VoxParams vp = *vpp;
     const uint32_t m = sort_count(vp);
     const uint32_t nact = sort_tiles(vp);
@@ -363,11 +484,20 @@ k_radix_hist(const uint32_t *__restrict__ keys, const VoxParams *__restrict__ vp
 // in digit order and written out run by run (each digit's items are contiguous in the output),
 // so the global stores are coalesced instead of one cache line per item.
 __global__ void __launch_bounds__(kST)
-k_radix_scatter(const uint32_t *__restrict__ kin, const float4 *__restrict__ pin,
-                const VoxParams *__restrict__ vpp, int shift, uint32_t ntp,
-                const uint32_t *__restrict__ hist, const uint32_t *__restrict__ totals,
-                const uint32_t *__restrict__ gsum, uint32_t *__restrict__ kout,
-                float4 *__restrict__ pout) {
+k_radix_scatter(const JobBatch jobs, int pass) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    if (pass >= J.passes) return;
+    const bool odd = pass & 1;
+    const uint32_t *kin = odd ? J.keys1 : J.keys0;
+    uint32_t *kout = odd ? J.keys0 : J.keys1;
+    const float4 *pin = odd ? J.sparse : J.xyz;
+    float4 *pout = odd ? J.xyz : J.sparse;
+    const VoxParams *vpp = J.vp;
+    const int shift = kDigitBits * pass;
+    const uint32_t ntp = J.ntp;
+    const uint32_t *hist = J.rhist;
+    const uint32_t *totals = J.zero + pass * kBins;
+    const uint32_t *gsum = J.zero + (size_t)kMaxPasses * kBins + (size_t)pass * J.ngp * kBins;
     const VoxParams vp = *vpp;
     const uint32_t m = sort_count(vp);
     const uint32_t nact = sort_tiles(vp);
@@ -479,9 +609,12 @@ __device__ __forceinline__ bool seg_head(const uint32_t *keys, uint64_t i, uint3
 }
 
 // heads per sort tile and the tile's first head position (UINT32_MAX: none)
-__global__ void __launch_bounds__(kST)
-k_seg_count(const uint32_t *__restrict__ keys, const VoxParams *__restrict__ vpp,
-            uint32_t *__restrict__ tcount, uint32_t *__restrict__ fhead) {
+__global__ void __launch_bounds__(kST) k_seg_count(const JobBatch jobs) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    if (J.passes == 0) return;
+    const uint32_t *keys = (J.passes & 1) ? J.keys1 : J.keys0;
+    const VoxParams *vpp = J.vp;
+    uint32_t *tcount = J.tcount, *fhead = J.fhead;
     const VoxParams vp = *vpp;
     const uint32_t m = sort_count(vp);
     const uint32_t nact = sort_tiles(vp);
@@ -525,11 +658,16 @@ k_seg_count(const uint32_t *__restrict__ keys, const VoxParams *__restrict__ vpp
 // come from the tile's head list and the next tile holding a head.  The last tile writes the
 // voxel count (res[slot]).
 __global__ void __launch_bounds__(kST)
-k_seg_centroid(const uint32_t *__restrict__ keys, const float4 *__restrict__ pay,
-               const VoxParams *__restrict__ vpp, const uint32_t *__restrict__ tcount,
-               const uint32_t *__restrict__ fhead, float4 *__restrict__ out,
-               uint32_t *__restrict__ out_idx, uint32_t *__restrict__ out_cnt,
-               uint32_t *__restrict__ res, int slot) {
+k_seg_centroid(const JobBatch jobs, uint32_t *__restrict__ res) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    if (J.passes == 0) return;
+    const uint32_t *keys = (J.passes & 1) ? J.keys1 : J.keys0;
+    const float4 *pay = (J.passes & 1) ? J.sparse : J.xyz;
+    const VoxParams *vpp = J.vp;
+    const uint32_t *tcount = J.tcount, *fhead = J.fhead;
+    float4 *out = J.out4;
+    uint32_t *out_idx = J.vidx, *out_cnt = J.vcnt;
+    const int slot = J.slot;
     const VoxParams vp = *vpp;
     const uint32_t m = sort_count(vp);
     const uint32_t nact = sort_tiles(vp);
@@ -581,25 +719,42 @@ k_seg_centroid(const uint32_t *__restrict__ keys, const float4 *__restrict__ pay
     FLT_STAMP(1, t, 3);
     // run sums, point index outer / head inner: the sum of each voxel still runs in input order,
     // while the loads of one step (LDS, or global past the tile) are independent of each other
-    uint32_t a_[kSortItems], n_[kSortItems], nmax = 0;
+    uint32_t a_[kSortItems], n_[kSortItems];
 #pragma unroll
     for (int j = 0; j < kSortItems; ++j) {
         const bool h = (head >> j) & 1u;
         a_[j] = h ? hpos[loc[j]] : 0u;
         n_[j] = h ? hpos[loc[j] + 1] - a_[j] : 0u;
-        nmax = max(nmax, n_[j]);
     }
     float sx[kSortItems], sy[kSortItems], sz[kSortItems];
 #pragma unroll
     for (int j = 0; j < kSortItems; ++j) sx[j] = sy[j] = sz[j] = 0.f;
-    const uint64_t tend = base + kSortTile;
+    // the part of each run inside this tile comes from LDS; only the tile's last run can go on
+    // past the tile end (global loads, in order, after its in-tile part)
+    const uint32_t tend = (uint32_t)(base + kSortTile);
+    uint32_t nin[kSortItems], nmax_in = 0;
+#pragma unroll
+    for (int j = 0; j < kSortItems; ++j) {
+        nin[j] = min(n_[j], tend - a_[j]);
+        nmax_in = max(nmax_in, nin[j]);
+    }
     FLT_STAMP(1, t, 4);
-    for (uint32_t q = 0; q < nmax; ++q) {
+    for (uint32_t q = 0; q < nmax_in; ++q) {
 #pragma unroll
         for (int j = 0; j < kSortItems; ++j) {
-            if (q < n_[j]) {
-                const uint32_t l = a_[j] + q;
-                const float4 p = l < tend ? lp[l - base] : pay[l];
+            if (q < nin[j]) {
+                const float4 p = lp[a_[j] + q - (uint32_t)base];
+                sx[j] = sx[j] + p.x;
+                sy[j] = sy[j] + p.y;
+                sz[j] = sz[j] + p.z;
+            }
+        }
+    }
+    {
+#pragma unroll
+        for (int j = 0; j < kSortItems; ++j) {
+            for (uint32_t l = a_[j] + nin[j]; l < a_[j] + n_[j]; ++l) {
+                const float4 p = pay[l];
                 sx[j] = sx[j] + p.x;
                 sy[j] = sy[j] + p.y;
                 sz[j] = sz[j] + p.z;
@@ -621,52 +776,16 @@ k_seg_centroid(const uint32_t *__restrict__ keys, const float4 *__restrict__ pay
     }
 }
 
-// ---- SE(3) + colour (tf2::doTransform + processRobotCloud loop) ------------------------------
-struct Rigid {
-    float m00, m01, m02, m10, m11, m12, m20, m21, m22, tx, ty, tz;
-    uint32_t rgba;
-};
-
-static Rigid make_rigid(const pcp_rigid &t, const uint8_t rgb[3]) {
-    // Eigen::Quaternionf(w,x,y,z).toRotationMatrix() in float
-    const float qx = (float)t.q[0], qy = (float)t.q[1], qz = (float)t.q[2], qw = (float)t.q[3];
-    const float tx = 2.0f * qx, ty = 2.0f * qy, tz = 2.0f * qz;
-    const float twx = tx * qw, twy = ty * qw, twz = tz * qw;
-    const float txx = tx * qx, txy = ty * qx, txz = tz * qx;
-    const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
-    Rigid r;
-    r.m00 = 1.0f - (tyy + tzz);
-    r.m01 = txy - twz;
-    r.m02 = txz + twy;
-    r.m10 = txy + twz;
-    r.m11 = 1.0f - (txx + tzz);
-    r.m12 = tyz - twx;
-    r.m20 = txz - twy;
-    r.m21 = tyz + twx;
-    r.m22 = 1.0f - (txx + tyy);
-    r.tx = (float)t.t[0];
-    r.ty = (float)t.t[1];
-    r.tz = (float)t.t[2];
-    r.rgba = (uint32_t)rgb[2] | ((uint32_t)rgb[1] << 8) | ((uint32_t)rgb[0] << 16) | (255u << 24);
-    return r;
-}
-
-// Affine3f * Vector3f as the homogeneous 4x4 packet product: ((m0 x + m1 y) + m2 z) + t
-__device__ __forceinline__ void xform_store(const Rigid &r, float x, float y, float z, float4 *o) {
-    const float X = ((r.m00 * x + r.m01 * y) + r.m02 * z) + r.tx;
-    const float Y = ((r.m10 * x + r.m11 * y) + r.m12 * z) + r.ty;
-    const float Z = ((r.m20 * x + r.m21 * y) + r.m22 * z) + r.tz;
-    o[0] = make_float4(X, Y, Z, 1.0f);
-    o[1] = make_float4(__uint_as_float(r.rgba), 0.f, 0.f, 0.f);
-}
-
-// transform + colour of cloud `slot`'s result into the concatenated output (robot first)
+// transform + colour of every cloud's result into the concatenated output (cloud order: the
+// robot first), counts[] = result counts of the clouds
 __global__ void __launch_bounds__(kFT)
-k_emit_rgb(const float4 *__restrict__ cropped, const float4 *__restrict__ voxels,
-           const VoxParams *__restrict__ vpp, const uint32_t *__restrict__ counts, int slot,
-           Rigid r, float4 *__restrict__ out) {
-    const VoxParams vp = *vpp;
-    const float4 *src = (vp.do_voxel && !vp.overflow) ? voxels : cropped;
+k_emit_rgb(const JobBatch jobs, const uint32_t *__restrict__ counts,
+           float4 *__restrict__ out) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    const int slot = J.slot;
+    const VoxParams vp = *J.vp;
+    const float4 *src = (vp.do_voxel && !vp.overflow) ? J.out4 : J.xyz;
+    const Rigid r = J.rig;
     uint32_t base = 0;
     for (int j = 0; j < slot; ++j) base += counts[j];
     const uint32_t n = counts[slot];
@@ -686,78 +805,22 @@ __global__ void __launch_bounds__(kFT) k_xform_raw(CloudIn c, Rigid r, float4 *_
 }
 
 // =========================================================================================
-// host orchestration: every stage enqueued on ctx->stream with sizes kept on the device, so a
-// whole crop -> voxel -> transform pipeline runs without host round trips (and can be captured
-// into a hipGraph, see pcp_filter_merge).
+// host orchestration: one job per cloud in a device table; every stage is one batched launch
+// (grid.y = clouds) on ctx->stream with sizes kept on the device, so a whole crop -> voxel ->
+// transform frame runs without host round trips (and is captured into a hipGraph by
+// pcp_filter_merge when its inputs are device-resident).
 // =========================================================================================
 constexpr int kMaxClouds = 64;
 
-// device views of one cloud's scratch (ctx->fbuf[slot]) plus the shared per-slot results
-struct Scratch {
-    CloudBufs *B = nullptr;
-    uint64_t ncap = 0;        // points the buffers hold
-    uint32_t nb = 0;          // crop tiles
-    uint32_t nt = 0;          // sort tiles (upper bound)
-    uint32_t ntp = 0;         // radix histogram row stride (nt rounded up to 16)
-    uint32_t ngp = 0;         // prefix groups of kGroup sort tiles
-    uint32_t *counts = nullptr;                    // crop tile kept counts
-    float *part = nullptr;                         // crop bbox partials
-    uint32_t *totals = nullptr;                    // [kMaxPasses][kBins] digit totals, then
-                                                   // [kMaxPasses][ngp][kBins] group sums
-    uint32_t nzero = 0;                            // words of totals + group sums
-    uint32_t *rhist = nullptr;                     // [kBins][ntp] tile digit counts
-    uint32_t *tcount = nullptr;                    // voxel heads per sort tile
-    uint32_t *fhead = nullptr;                     // first head position per sort tile
-    VoxParams *vp = nullptr;  // [kMaxClouds]
-    uint32_t *res = nullptr;  // [kMaxClouds] result counts, [2*kMaxClouds] info
-    float4 *xyz() const { return B->xyz.as<float4>(); }        // compact cropped points
-    float4 *sparse() const { return B->sparse.as<float4>(); }  // crop tiles / sort ping-pong
-    float4 *out4() const { return B->out.as<float4>(); }
-    uint32_t *vidx() const { return reinterpret_cast<uint32_t *>(out4() + ncap + 1); }
-    uint32_t *vcnt() const { return vidx() + ncap + 1; }
-};
-
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// (callers holding Scratch objects of several slots must size ctx->fbuf beforehand)
-static int ensure_scratch(pcp_ctx *ctx, int slot, uint64_t ncap, bool want_idx, Scratch &S) {
-    if (ncap >= (1ull << 31))
-        return set_err(ctx, PCP_E_INVALID, "cloud of %llu points: at most 2^31-1 per call",
-                       (unsigned long long)ncap);
-    if ((int)ctx->fbuf.size() <= slot) ctx->fbuf.resize(slot + 1);
-    CloudBufs &B = ctx->fbuf[slot];
-    S.B = &B;
-    ncap = ncap ? ncap : 1;
-    S.ncap = ncap;
-    S.nb = (uint32_t)((ncap + kCropTile - 1) / kCropTile);
-    S.nt = (uint32_t)((ncap + kSortTile - 1) / kSortTile);
-    S.ntp = (S.nt + 15) & ~15u;
-    S.ngp = (S.nt + kGroup - 1) / kGroup;
-    // sparse crop tiles are whole tiles: nb * kCropTile points
-    PCP_HIP(ctx, B.xyz.ensure((ncap + 1) * sizeof(float4)));
-    PCP_HIP(ctx, B.sparse.ensure((size_t)S.nb * kCropTile * sizeof(float4)));
-    if (want_idx) {
-        PCP_HIP(ctx, B.idx.ensure((ncap + 1) * sizeof(uint32_t)));
-        PCP_HIP(ctx, B.sparse_idx.ensure((size_t)S.nb * kCropTile * sizeof(uint32_t)));
-    }
-    for (int q = 0; q < 2; ++q) PCP_HIP(ctx, B.keys[q].ensure((ncap + 16) * sizeof(uint32_t)));
-    const size_t cb = align256((size_t)(S.nb + 4) * 4), pb = align256((size_t)S.nb * 24);
-    S.nzero = (uint32_t)((size_t)kMaxPasses * kBins * (1 + S.ngp));
-    const size_t tb = align256((size_t)S.nzero * 4);
-    const size_t hb = align256((size_t)kBins * S.ntp * 4), sb = align256((size_t)(S.ntp + 4) * 4);
-    PCP_HIP(ctx, B.hist.ensure(cb + pb + tb + hb + 2 * sb));
-    char *h = B.hist.as<char>();
-    S.counts = reinterpret_cast<uint32_t *>(h);
-    S.part = reinterpret_cast<float *>(h + cb);
-    S.totals = reinterpret_cast<uint32_t *>(h + cb + pb);
-    S.rhist = reinterpret_cast<uint32_t *>(h + cb + pb + tb);
-    S.tcount = reinterpret_cast<uint32_t *>(h + cb + pb + tb + hb);
-    S.fhead = reinterpret_cast<uint32_t *>(h + cb + pb + tb + hb + sb);
-    // voxel results: out4 (ncap+1) | idx (ncap+1) | cnt (ncap+1)
-    PCP_HIP(ctx, B.out.ensure((ncap + 1) * sizeof(float4) + (2 * ncap + 8) * 4 + 256));
-    PCP_HIP(ctx, ctx->f_misc.ensure(align256(kMaxClouds * sizeof(VoxParams)) + 3 * kMaxClouds * 4));
-    S.vp = reinterpret_cast<VoxParams *>(ctx->f_misc.as<char>());
-    S.res = reinterpret_cast<uint32_t *>(ctx->f_misc.as<char>() + align256(kMaxClouds * sizeof(VoxParams)));
+// per-slot results shared by all clouds of a call: VoxParams[kMaxClouds], then
+// res[kMaxClouds] result counts and info[2*kMaxClouds] (cropped count, passthrough flag)
+static int ensure_misc(pcp_ctx *ctx, VoxParams *&vp, uint32_t *&res) {
+    const size_t vb = align256(kMaxClouds * sizeof(VoxParams));
+    PCP_HIP(ctx, ctx->f_misc.ensure(vb + 3 * kMaxClouds * 4));
+    vp = reinterpret_cast<VoxParams *>(ctx->f_misc.as<char>());
+    res = reinterpret_cast<uint32_t *>(ctx->f_misc.as<char>() + vb);
     return PCP_OK;
 }
 
@@ -779,83 +842,152 @@ static int radix_passes(const Box &b, float leaf) {
     return std::max(1, (bits + kDigitBits - 1) / kDigitBits);
 }
 
-// enqueue crop [-> voxel] for one cloud into slot `slot` on stream `st` (results stay on the
-// device: S.res[slot] = result count)
-static int enqueue_cloud(pcp_ctx *ctx, Scratch &S, const CloudIn &c, const Box &b, float leaf,
-                         bool want_idx, int slot, hipStream_t st) {
-    const uint32_t nb = (uint32_t)((c.n + kCropTile - 1) / kCropTile);
-    CloudBufs &B = *S.B;
-    VoxParams *vp = S.vp + slot;
+// scratch of cloud `slot` (ctx->fbuf[slot], grow-only) and its job; the caller sized ctx->fbuf
+static int make_job(pcp_ctx *ctx, int slot, const CloudIn &c, const Box &b, float leaf,
+                    bool want_idx, const Rigid &rig, VoxParams *vp_all, CloudJob &J) {
+    if (c.n >= (1ull << 31))
+        return set_err(ctx, PCP_E_INVALID, "cloud of %llu points: at most 2^31-1 per call",
+                       (unsigned long long)c.n);
+    CloudBufs &B = ctx->fbuf[slot];
+    const uint64_t ncap = c.n ? c.n : 1;
+    const uint32_t nb = (uint32_t)((ncap + kCropTile - 1) / kCropTile);
+    const uint32_t nt = (uint32_t)((ncap + kSortTile - 1) / kSortTile);
+    const uint32_t ntp = (nt + 15) & ~15u, ngp = (nt + kGroup - 1) / kGroup;
+    const uint32_t nzero = (uint32_t)((size_t)kMaxPasses * kBins * (1 + ngp));
+    PCP_HIP(ctx, B.xyz.ensure((ncap + 1) * sizeof(float4)));
+    PCP_HIP(ctx, B.sparse.ensure((size_t)nb * kCropTile * sizeof(float4)));   // whole tiles
+    if (want_idx) {
+        PCP_HIP(ctx, B.idx.ensure((ncap + 1) * sizeof(uint32_t)));
+        PCP_HIP(ctx, B.sparse_idx.ensure((size_t)nb * kCropTile * sizeof(uint32_t)));
+    }
+    for (int q = 0; q < 2; ++q) PCP_HIP(ctx, B.keys[q].ensure((ncap + 16) * sizeof(uint32_t)));
+    const size_t cb = align256((size_t)(nb + 4) * 4), pb = align256((size_t)nb * 24);
+    const size_t zb = align256((size_t)nzero * 4);
+    const size_t hb = align256((size_t)kBins * ntp * 4), sb = align256((size_t)(ntp + 4) * 4);
+    PCP_HIP(ctx, B.hist.ensure(cb + pb + zb + hb + 2 * sb));
+    // voxel results: out4 (ncap+1) | idx (ncap+1) | cnt (ncap+1)
+    PCP_HIP(ctx, B.out.ensure((ncap + 1) * sizeof(float4) + (2 * ncap + 8) * 4 + 256));
+    char *h = B.hist.as<char>();
+    J = CloudJob{};
+    J.in = c;
+    J.box = b;
+    J.leaf = leaf;
+    J.passes = (leaf > 0.0f && c.n > 0) ? radix_passes(b, leaf) : 0;
+    J.nb = c.n ? nb : 0;
+    J.ntp = ntp;
+    J.ngp = ngp;
+    J.nzero = nzero;
+    J.counts = reinterpret_cast<uint32_t *>(h);
+    J.part = reinterpret_cast<float *>(h + cb);
+    J.zero = reinterpret_cast<uint32_t *>(h + cb + pb);
+    J.rhist = reinterpret_cast<uint32_t *>(h + cb + pb + zb);
+    J.tcount = reinterpret_cast<uint32_t *>(h + cb + pb + zb + hb);
+    J.fhead = reinterpret_cast<uint32_t *>(h + cb + pb + zb + hb + sb);
+    J.sparse = B.sparse.as<float4>();
+    J.sparse_idx = want_idx ? B.sparse_idx.as<uint32_t>() : nullptr;
+    J.xyz = B.xyz.as<float4>();
+    J.kept_idx = want_idx ? B.idx.as<uint32_t>() : nullptr;
+    J.keys0 = B.keys[0].as<uint32_t>();
+    J.keys1 = B.keys[1].as<uint32_t>();
+    J.out4 = B.out.as<float4>();
+    J.vidx = reinterpret_cast<uint32_t *>(J.out4 + ncap + 1);
+    J.vcnt = J.vidx + ncap + 1;
+    J.vp = vp_all + slot;
+    J.rig = rig;
+    J.slot = slot;
+    return PCP_OK;
+}
+
+struct Batch {
+    JobBatch jb{};
+    int k = 0;
+    uint32_t max_nb = 0, max_nt = 0;
+    int max_passes = 0;
+    uint64_t max_n = 0;
+};
+
+// the clouds in launch batches of <= kBatch (one batch for any realistic frame)
+static std::vector<Batch> batches_of(const std::vector<CloudJob> &jobs) {
+    std::vector<Batch> out;
+    for (size_t b0 = 0; b0 < jobs.size(); b0 += kBatch) {
+        Batch bt;
+        bt.k = (int)std::min<size_t>(kBatch, jobs.size() - b0);
+        for (int i = 0; i < bt.k; ++i) {
+            const CloudJob &J = jobs[b0 + i];
+            bt.jb.j[i] = J;
+            bt.max_nb = std::max(bt.max_nb, J.nb);
+            bt.max_nt = std::max(bt.max_nt, (uint32_t)((J.in.n + kSortTile - 1) / kSortTile));
+            bt.max_passes = std::max(bt.max_passes, (int)J.passes);
+            bt.max_n = std::max<uint64_t>(bt.max_n, J.in.n);
+        }
+        out.push_back(bt);
+    }
+    return out;
+}
+
+// crop [-> voxel] of every cloud of one batch, on stream st
+static int enqueue_chain(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream_t st) {
+    const unsigned k = (unsigned)bt.k;
     {
         ProfScope ps(ctx, PCP_K_CROP, st);
-        if (nb) {
-            hipLaunchKernelGGL(k_crop_tile, dim3(nb), dim3(kFT), 0, st, c, b, S.counts, S.part,
-                               S.sparse(), want_idx ? B.sparse_idx.as<uint32_t>() : nullptr);
+        if (bt.max_nb) {
+            hipLaunchKernelGGL(k_crop_tile, dim3(bt.max_nb, k), dim3(kFT), 0, st, bt.jb);
             PCP_CHECK_LAUNCH(ctx);
         }
-        hipLaunchKernelGGL(k_vox_params, dim3(1), dim3(kFT), 0, st, (const float *)S.part,
-                           (const uint32_t *)S.counts, (int)nb, leaf, vp, S.res,
-                           S.res + kMaxClouds, slot);
+        hipLaunchKernelGGL(k_vox_params, dim3(1, k), dim3(kFT), 0, st, bt.jb, res,
+                           res + kMaxClouds);
         PCP_CHECK_LAUNCH(ctx);
-        if (nb) {
-            hipLaunchKernelGGL(k_compact_keys, dim3(nb), dim3(kFT), 0, st,
-                               (const float4 *)S.sparse(),
-                               want_idx ? B.sparse_idx.as<const uint32_t>() : nullptr,
-                               (const uint32_t *)S.counts, (const VoxParams *)vp, S.xyz(),
-                               want_idx ? B.idx.as<uint32_t>() : nullptr, B.keys[0].as<uint32_t>(),
-                               S.totals, S.nzero);
+        if (bt.max_nb) {
+            hipLaunchKernelGGL(k_compact_keys, dim3(bt.max_nb, k), dim3(kFT), 0, st, bt.jb);
             PCP_CHECK_LAUNCH(ctx);
         }
     }
-    if (!(leaf > 0.0f) || c.n == 0) return PCP_OK;
-    ProfScope ps(ctx, PCP_K_VOXEL, st);
-    const uint32_t nt = (uint32_t)((c.n + kSortTile - 1) / kSortTile);
-    const int passes = radix_passes(b, leaf);
-    const uint32_t ntg = std::min<uint32_t>(nt, (uint32_t)std::max(ctx->num_cus, 1));
-    // payload ping-pong: the compact points, then the (dead) sparse crop buffer
-    float4 *pay[2] = {S.xyz(), S.sparse()};
-    int cur = 0;
-    for (int pass = 0; pass < passes; ++pass) {
-        const int shift = kDigitBits * pass;
-        uint32_t *tot = S.totals + pass * kBins;
-        uint32_t *gs = S.totals + (size_t)kMaxPasses * kBins + (size_t)pass * S.ngp * kBins;
-        hipLaunchKernelGGL(k_radix_hist, dim3(ntg), dim3(kST), 0, st,
-                           B.keys[cur].as<const uint32_t>(), (const VoxParams *)vp, shift, S.ntp,
-                           S.rhist, tot, gs);
+    if (bt.max_passes > 0) {
+        ProfScope ps(ctx, PCP_K_VOXEL, st);
+        // sort-tile kernels: LDS admits one block per CU; the clouds share the CUs
+        const unsigned gx = std::max(1u, std::min<unsigned>(
+                                             bt.max_nt, (unsigned)std::max(ctx->num_cus, 1) / k));
+        for (int pass = 0; pass < bt.max_passes; ++pass) {
+            hipLaunchKernelGGL(k_radix_hist, dim3(gx, k), dim3(kST), 0, st, bt.jb, pass);
+            PCP_CHECK_LAUNCH(ctx);
+            hipLaunchKernelGGL(k_radix_scatter, dim3(gx, k), dim3(kST), 0, st, bt.jb, pass);
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        hipLaunchKernelGGL(k_seg_count, dim3(gx, k), dim3(kST), 0, st, bt.jb);
         PCP_CHECK_LAUNCH(ctx);
-        hipLaunchKernelGGL(k_radix_scatter, dim3(ntg), dim3(kST), 0, st,
-                           B.keys[cur].as<const uint32_t>(), (const float4 *)pay[cur],
-                           (const VoxParams *)vp, shift, S.ntp, (const uint32_t *)S.rhist,
-                           (const uint32_t *)tot, (const uint32_t *)gs,
-                           B.keys[cur ^ 1].as<uint32_t>(), pay[cur ^ 1]);
+        hipLaunchKernelGGL(k_seg_centroid, dim3(gx, k), dim3(kST), 0, st, bt.jb, res);
         PCP_CHECK_LAUNCH(ctx);
-        cur ^= 1;
     }
-    const uint32_t *keys = B.keys[cur].as<const uint32_t>();
-    hipLaunchKernelGGL(k_seg_count, dim3(ntg), dim3(kST), 0, st, keys, (const VoxParams *)vp,
-                       S.tcount, S.fhead);
-    PCP_CHECK_LAUNCH(ctx);
-    hipLaunchKernelGGL(k_seg_centroid, dim3(ntg), dim3(kST), 0, st, keys, (const float4 *)pay[cur],
-                       (const VoxParams *)vp, (const uint32_t *)S.tcount, (const uint32_t *)S.fhead,
-                       S.out4(), S.vidx(), S.vcnt(), S.res, slot);
+    return PCP_OK;
+}
+
+// transform + colour + concat of one batch (after every batch's chain: offsets need all counts)
+static int enqueue_emit(pcp_ctx *ctx, const Batch &bt, const uint32_t *res, float4 *out,
+                        hipStream_t st) {
+    if (!bt.max_n) return PCP_OK;
+    ProfScope ps(ctx, PCP_K_TRANSFORM, st);
+    const unsigned g = (unsigned)std::min<uint64_t>((bt.max_n + kFT - 1) / kFT, 2048);
+    hipLaunchKernelGGL(k_emit_rgb, dim3(g, (unsigned)bt.k), dim3(kFT), 0, st, bt.jb, res, out);
     PCP_CHECK_LAUNCH(ctx);
     return PCP_OK;
 }
 
-static int enqueue_emit(pcp_ctx *ctx, Scratch &S, uint64_t ncap, int slot, const Rigid &r,
-                        float4 *out, hipStream_t st) {
-    if (ncap == 0) return PCP_OK;
-    ProfScope ps(ctx, PCP_K_TRANSFORM, st);
-    const unsigned g = (unsigned)std::min<uint64_t>((ncap + kFT - 1) / kFT, 4096);
-    hipLaunchKernelGGL(k_emit_rgb, dim3(g), dim3(kFT), 0, st, (const float4 *)S.xyz(),
-                       (const float4 *)S.out4(), (const VoxParams *)(S.vp + slot),
-                       (const uint32_t *)S.res, slot, r, out);
-    PCP_CHECK_LAUNCH(ctx);
+static int enqueue_all(pcp_ctx *ctx, const std::vector<Batch> &bts, uint32_t *res,
+                       float4 *emit_out, hipStream_t st) {
+    for (const Batch &bt : bts) {
+        int rc = enqueue_chain(ctx, bt, res, st);
+        if (rc) return rc;
+    }
+    if (emit_out)
+        for (const Batch &bt : bts) {
+            int rc = enqueue_emit(ctx, bt, res, emit_out, st);
+            if (rc) return rc;
+        }
     return PCP_OK;
 }
 
 static int stage_cloud(pcp_ctx *ctx, const pcp_cloud_view &v, bool device_in, DevBuf &buf,
-                       CloudIn &c) {
+                       size_t off, CloudIn &c) {
     c.n = v.n;
     c.step = v.point_step;
     c.ox = v.off_x;
@@ -868,9 +1000,9 @@ static int stage_cloud(pcp_ctx *ctx, const pcp_cloud_view &v, bool device_in, De
         return PCP_OK;
     }
     const uint64_t bytes = v.n * (uint64_t)v.point_step;
-    PCP_HIP(ctx, buf.ensure(bytes));
-    PCP_HIP(ctx, hipMemcpyAsync(buf.p, v.data, bytes, hipMemcpyHostToDevice, ctx->stream));
-    c.raw = buf.as<const unsigned char>();
+    unsigned char *dst = buf.as<unsigned char>() + off;
+    PCP_HIP(ctx, hipMemcpyAsync(dst, v.data, bytes, hipMemcpyHostToDevice, ctx->stream));
+    c.raw = dst;
     return PCP_OK;
 }
 
@@ -880,14 +1012,34 @@ struct ResultInfo {
     uint32_t overflow;
 };
 
-static int read_result(pcp_ctx *ctx, const Scratch &S, int slot, ResultInfo &ri) {
+static int read_results(pcp_ctx *ctx, const uint32_t *res_d, int k, ResultInfo *ri) {
     uint32_t buf[3 * kMaxClouds];
-    PCP_HIP(ctx, hipMemcpyAsync(buf, S.res, sizeof(buf), hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipMemcpyAsync(buf, res_d, sizeof(buf), hipMemcpyDeviceToHost, ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    ri.n = buf[slot];
-    ri.m = buf[kMaxClouds + 2 * slot];
-    ri.overflow = buf[kMaxClouds + 2 * slot + 1];
+    for (int i = 0; i < k; ++i) {
+        ri[i].n = buf[i];
+        ri[i].m = buf[kMaxClouds + 2 * i];
+        ri[i].overflow = buf[kMaxClouds + 2 * i + 1];
+    }
     return PCP_OK;
+}
+
+// one host cloud through crop [-> voxel] (slot 0); results stay in ctx->fbuf[0]
+static int run_single(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b, float leaf,
+                      bool want_idx, CloudJob &J, ResultInfo &ri) {
+    VoxParams *vp;
+    uint32_t *res;
+    int rc = ensure_misc(ctx, vp, res);
+    if (rc) return rc;
+    if (ctx->fbuf.empty()) ctx->fbuf.resize(1);
+    PCP_HIP(ctx, ctx->f_in.ensure(in->n * (uint64_t)in->point_step + 256));
+    CloudIn c;
+    if ((rc = stage_cloud(ctx, *in, false, ctx->f_in, 0, c))) return rc;
+    std::vector<CloudJob> jobs(1);
+    if ((rc = make_job(ctx, 0, c, b, leaf, want_idx, Rigid{}, vp, jobs[0]))) return rc;
+    if ((rc = enqueue_all(ctx, batches_of(jobs), res, nullptr, ctx->stream))) return rc;
+    J = jobs[0];
+    return read_results(ctx, res, 1, &ri);
 }
 
 }  // namespace pcp
@@ -905,14 +1057,10 @@ int pcp_crop_box(pcp_ctx *ctx, const pcp_cloud_view *in, const double box[6], ui
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     *n_kept = 0;
     if (in->n == 0) return PCP_OK;
-    Scratch S;
-    if ((rc = ensure_scratch(ctx, 0, in->n, kept_idx != nullptr, S))) return rc;
-    CloudIn c;
-    if ((rc = stage_cloud(ctx, *in, false, ctx->f_in, c))) return rc;
     const Box b{box[0], box[1], box[2], box[3], box[4], box[5]};
-    if ((rc = enqueue_cloud(ctx, S, c, b, 0.0f, kept_idx != nullptr, 0, ctx->stream))) return rc;
+    CloudJob J;
     ResultInfo ri;
-    if ((rc = read_result(ctx, S, 0, ri))) return rc;
+    if ((rc = run_single(ctx, in, b, 0.0f, kept_idx != nullptr, J, ri))) return rc;
     *n_kept = ri.m;
     if ((kept_idx || out_xyz16) && ri.m > cap) {
         prof_resolve(ctx);
@@ -920,11 +1068,11 @@ int pcp_crop_box(pcp_ctx *ctx, const pcp_cloud_view *in, const double box[6], ui
                        (unsigned long long)cap);
     }
     if (kept_idx && ri.m)
-        PCP_HIP(ctx, hipMemcpyAsync(kept_idx, S.B->idx.p, (size_t)ri.m * 4, hipMemcpyDeviceToHost,
+        PCP_HIP(ctx, hipMemcpyAsync(kept_idx, J.kept_idx, (size_t)ri.m * 4, hipMemcpyDeviceToHost,
                                     ctx->stream));
     if (out_xyz16 && ri.m)
-        PCP_HIP(ctx, hipMemcpyAsync(out_xyz16, S.xyz(), (size_t)ri.m * 16,
-                                    hipMemcpyDeviceToHost, ctx->stream));
+        PCP_HIP(ctx, hipMemcpyAsync(out_xyz16, J.xyz, (size_t)ri.m * 16, hipMemcpyDeviceToHost,
+                                    ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     prof_resolve(ctx);
     return PCP_OK;
@@ -934,14 +1082,10 @@ static int crop_voxel_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b,
                            float *out_xyz16, uint32_t *voxel_idx, uint32_t *voxel_count,
                            uint64_t cap, uint64_t *n_out, uint64_t *n_cropped,
                            int32_t *passthrough) {
-    Scratch S;
-    int rc = ensure_scratch(ctx, 0, in->n, false, S);
-    if (rc) return rc;
-    CloudIn c;
-    if ((rc = stage_cloud(ctx, *in, false, ctx->f_in, c))) return rc;
-    if ((rc = enqueue_cloud(ctx, S, c, b, leaf, false, 0, ctx->stream))) return rc;
+    CloudJob J;
     ResultInfo ri;
-    if ((rc = read_result(ctx, S, 0, ri))) return rc;
+    int rc = run_single(ctx, in, b, leaf, false, J, ri);
+    if (rc) return rc;
     const bool vox = leaf > 0.0f && !ri.overflow;
     if (passthrough) *passthrough = (leaf > 0.0f && ri.overflow) ? 1 : 0;
     if (n_cropped) *n_cropped = ri.m;
@@ -952,14 +1096,14 @@ static int crop_voxel_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b,
                        (unsigned long long)cap);
     }
     if (ri.n) {
-        const void *src = vox ? (const void *)S.out4() : (const void *)S.xyz();
+        const void *src = vox ? (const void *)J.out4 : (const void *)J.xyz;
         PCP_HIP(ctx, hipMemcpyAsync(out_xyz16, src, (size_t)ri.n * 16, hipMemcpyDeviceToHost,
                                     ctx->stream));
         if (vox && voxel_idx)
-            PCP_HIP(ctx, hipMemcpyAsync(voxel_idx, S.vidx(), (size_t)ri.n * 4,
+            PCP_HIP(ctx, hipMemcpyAsync(voxel_idx, J.vidx, (size_t)ri.n * 4,
                                         hipMemcpyDeviceToHost, ctx->stream));
         if (vox && voxel_count)
-            PCP_HIP(ctx, hipMemcpyAsync(voxel_count, S.vcnt(), (size_t)ri.n * 4,
+            PCP_HIP(ctx, hipMemcpyAsync(voxel_count, J.vcnt, (size_t)ri.n * 4,
                                         hipMemcpyDeviceToHost, ctx->stream));
     }
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -1024,8 +1168,9 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, cons
     uint64_t base = 0;
     for (int i = 0; i < k; ++i) {
         if (clouds[i].n == 0) continue;
+        PCP_HIP(ctx, ctx->f_in.ensure(clouds[i].n * (uint64_t)clouds[i].point_step + 256));
         CloudIn c;
-        int rc = stage_cloud(ctx, clouds[i], false, ctx->f_in, c);
+        int rc = stage_cloud(ctx, clouds[i], false, ctx->f_in, 0, c);
         if (rc) return rc;
         const Rigid r = make_rigid(tf[i], rgb + 3 * i);
         {
@@ -1043,10 +1188,11 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, cons
     return PCP_OK;
 }
 
-// key of a captured filter_merge graph: everything baked into its nodes
+// key of a captured filter_merge graph: everything baked into its nodes and its job table
 static std::vector<uint8_t> fm_key(int k, const pcp_cloud_view *clouds, const double *boxes,
                                    float leaf, const pcp_rigid *tf, const uint8_t *rgb,
-                                   const void *out, uint64_t cap) {
+                                   const void *out, uint64_t cap,
+                                   const std::vector<CloudJob> &jobs) {
     std::vector<uint8_t> key;
     auto put = [&key](const void *p, size_t n) {
         const uint8_t *b = static_cast<const uint8_t *>(p);
@@ -1060,6 +1206,7 @@ static std::vector<uint8_t> fm_key(int k, const pcp_cloud_view *clouds, const do
     put(rgb, 3 * (size_t)k);
     put(&out, sizeof(out));
     put(&cap, sizeof(cap));
+    put(jobs.data(), jobs.size() * sizeof(CloudJob));   // every scratch pointer, the results
     return key;
 }
 
@@ -1075,6 +1222,8 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
         if (rc) return rc;
         upper += clouds[i].n;
     }
+    *n_out = 0;
+    if (k == 0) return PCP_OK;
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     const bool dev_in = flags & PCP_MEM_DEVICE_IN, dev_out = flags & PCP_MEM_DEVICE_OUT;
     if (dev_out && !out && upper) return set_err(ctx, PCP_E_INVALID, "pcp_filter_merge: null output");
@@ -1085,86 +1234,31 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
         PCP_HIP(ctx, ctx->out_d.ensure(upper * 32 + 32));
         obuf = ctx->out_d.as<float4>();
     }
-    // staging (host input): one region per cloud, so no buffer is reused while in flight
+    VoxParams *vp;
+    uint32_t *res;
+    int rc = ensure_misc(ctx, vp, res);
+    if (rc) return rc;
+    // staging (host input): one region per cloud
     std::vector<size_t> soff(k + 1, 0);
     for (int i = 0; i < k; ++i)
         soff[i + 1] = soff[i] + (dev_in ? 0 : align256(clouds[i].n * clouds[i].point_step));
     if (!dev_in) PCP_HIP(ctx, ctx->f_in.ensure(soff[k] + 256));
-    // per-cloud scratch and one side stream per cloud (clouds run as concurrent branches).
-    // Size fbuf once: Scratch keeps CloudBufs pointers, a later resize would invalidate them.
     if ((int)ctx->fbuf.size() < k) ctx->fbuf.resize(k);
-    std::vector<Scratch> S(k);
+    std::vector<CloudJob> jobs(k);
     for (int i = 0; i < k; ++i) {
-        int rc = ensure_scratch(ctx, i, clouds[i].n, false, S[i]);
-        if (rc) return rc;
+        CloudIn c;
+        if ((rc = stage_cloud(ctx, clouds[i], dev_in, ctx->f_in, soff[i], c))) return rc;
+        const double *bx = boxes + 6 * i;
+        const Box b{bx[0], bx[1], bx[2], bx[3], bx[4], bx[5]};
+        if ((rc = make_job(ctx, i, c, b, leaf, false, make_rigid(tf[i], rgb + 3 * i), vp, jobs[i])))
+            return rc;
     }
-    while ((int)ctx->side.size() < k) {
-        hipStream_t s2 = nullptr;
-        PCP_HIP(ctx, hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-        ctx->side.push_back(s2);
-        hipEvent_t e = nullptr;
-        PCP_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        ctx->side_ev.push_back(e);
-        PCP_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        ctx->emit_ev.push_back(e);
-    }
-    if (!ctx->fork_ev) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
-    // fork: every cloud's crop/voxel chain on its own stream; join; then the emits (they need
-    // every earlier cloud's count for their output offset)
-    auto enqueue_all = [&]() -> int {
-        PCP_HIP(ctx, hipEventRecord(ctx->fork_ev, ctx->stream));
-        for (int i = 0; i < k; ++i) {
-            hipStream_t si = ctx->side[i];
-            PCP_HIP(ctx, hipStreamWaitEvent(si, ctx->fork_ev, 0));
-            CloudIn c{};
-            c.n = clouds[i].n;
-            c.step = clouds[i].point_step;
-            c.ox = clouds[i].off_x;
-            c.oy = clouds[i].off_y;
-            c.oz = clouds[i].off_z;
-            c.raw = static_cast<const unsigned char *>(clouds[i].data);
-            if (!dev_in && c.n) {
-                unsigned char *dst = ctx->f_in.as<unsigned char>() + soff[i];
-                PCP_HIP(ctx, hipMemcpyAsync(dst, clouds[i].data, c.n * (uint64_t)c.step,
-                                            hipMemcpyHostToDevice, si));
-                c.raw = dst;
-            }
-            const double *bx = boxes + 6 * i;
-            const Box b{bx[0], bx[1], bx[2], bx[3], bx[4], bx[5]};
-            int r = enqueue_cloud(ctx, S[i], c, b, leaf, false, i, si);
-            if (r) return r;
-            PCP_HIP(ctx, hipEventRecord(ctx->side_ev[i], si));
-        }
-        if (dev_out && upper > cap) {   // sizes checked on the host afterwards
-            for (int i = 0; i < k; ++i) PCP_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[i], 0));
-            return PCP_OK;
-        }
-        // cloud i's emit needs the counts of clouds 0..i-1 (its offset in the concatenation):
-        // it runs on branch i once those chains are done, so emit 0 overlaps the later chains
-        for (int i = 0; i < k; ++i) {
-            hipStream_t si = ctx->side[i];
-            for (int j = 0; j < i; ++j) PCP_HIP(ctx, hipStreamWaitEvent(si, ctx->side_ev[j], 0));
-            int r = enqueue_emit(ctx, S[i], clouds[i].n, i, make_rigid(tf[i], rgb + 3 * i), obuf, si);
-            if (r) return r;
-            PCP_HIP(ctx, hipEventRecord(ctx->emit_ev[i], si));
-        }
-        for (int i = 0; i < k; ++i) PCP_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->emit_ev[i], 0));
-        return PCP_OK;
-    };
-    int rc = PCP_OK;
-    const bool graphable = dev_in && dev_out && upper <= cap && ctx->use_graphs;
+    const std::vector<Batch> bts = batches_of(jobs);
+    // the emit needs the sizes first when the output might not fit (device output only)
+    const bool emit_now = !(dev_out && upper > cap);
+    const bool graphable = dev_in && dev_out && emit_now && ctx->use_graphs;
     if (graphable) {
-        std::vector<uint8_t> key = fm_key(k, clouds, boxes, leaf, tf, rgb, out, cap);
-        std::vector<const void *> sp;
-        for (int i = 0; i < k; ++i) {
-            const CloudBufs &B = ctx->fbuf[i];
-            const void *v[] = {B.xyz.p, B.keys[0].p, B.keys[1].p, B.sparse.p, B.sparse_idx.p,
-                               B.hist.p, B.out.p};
-            sp.insert(sp.end(), v, v + 7);
-        }
-        sp.push_back(ctx->f_misc.p);
-        key.insert(key.end(), reinterpret_cast<const uint8_t *>(sp.data()),
-                   reinterpret_cast<const uint8_t *>(sp.data() + sp.size()));
+        std::vector<uint8_t> key = fm_key(k, clouds, boxes, leaf, tf, rgb, out, cap, jobs);
         if (!ctx->fm_exec || key != ctx->fm_key) {
             if (ctx->fm_exec) (void)hipGraphExecDestroy(ctx->fm_exec);
             if (ctx->fm_graph) (void)hipGraphDestroy(ctx->fm_graph);
@@ -1173,7 +1267,7 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
             ctx->fm_key.clear();
             PCP_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
             ctx->capturing = true;
-            rc = enqueue_all();
+            rc = enqueue_all(ctx, bts, res, obuf, ctx->stream);
             ctx->capturing = false;
             hipGraph_t g = nullptr;
             const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
@@ -1190,17 +1284,16 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
         PCP_HIP(ctx, hipGraphLaunch(ctx->fm_exec, ctx->stream));
     } else {
         ProfScope ps(ctx, PCP_K_FILTER_MERGE);
-        rc = enqueue_all();
+        rc = enqueue_all(ctx, bts, res, emit_now ? obuf : nullptr, ctx->stream);
         if (rc) return rc;
     }
-    uint32_t res[3 * kMaxClouds];
-    PCP_HIP(ctx, hipMemcpyAsync(res, ctx->f_misc.as<char>() + align256(kMaxClouds * sizeof(VoxParams)),
-                                sizeof(res), hipMemcpyDeviceToHost, ctx->stream));
-    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<ResultInfo> ri(k);
+    if ((rc = read_results(ctx, res, k, ri.data()))) return rc;
     uint64_t total = 0;
     for (int i = 0; i < k; ++i) {
-        if (n_per_cloud) n_per_cloud[i] = clouds[i].n ? res[i] : 0;
-        total += clouds[i].n ? res[i] : 0;
+        const uint64_t ni = clouds[i].n ? ri[i].n : 0;
+        if (n_per_cloud) n_per_cloud[i] = ni;
+        total += ni;
     }
     *n_out = total;
     if (total > cap) {
@@ -1208,13 +1301,9 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
         return set_err(ctx, PCP_E_CAPACITY, "pcp_filter_merge: need %llu, cap %llu",
                        (unsigned long long)total, (unsigned long long)cap);
     }
-    if (dev_out && upper > cap && total) {   // emits were deferred until the size was known
-        for (int i = 0; i < k; ++i) {
-            rc = enqueue_emit(ctx, S[i], clouds[i].n, i, make_rigid(tf[i], rgb + 3 * i), obuf,
-                              ctx->stream);
-            if (rc) return rc;
-        }
-    }
+    if (!emit_now && total)   // deferred until the size was known to fit
+        for (const Batch &bt : bts)
+            if ((rc = enqueue_emit(ctx, bt, res, obuf, ctx->stream))) return rc;
     if (!dev_out && total)
         PCP_HIP(ctx, hipMemcpyAsync(out, obuf, total * 32, hipMemcpyDeviceToHost, ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));

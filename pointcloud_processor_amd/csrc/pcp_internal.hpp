@@ -148,9 +148,6 @@ struct pcp_ctx {
     // filter/merge scratch
     pcp::DevBuf f_in, f_misc;
     std::vector<pcp::CloudBufs> fbuf;        // per-cloud scratch of the filter pipeline
-    std::vector<hipStream_t> side;           // per-cloud branch streams
-    std::vector<hipEvent_t> side_ev, emit_ev;
-    hipEvent_t fork_ev = nullptr;
     // captured filter_merge pipeline (device-resident inputs), replayed while its key matches
     hipGraph_t fm_graph = nullptr;
     hipGraphExec_t fm_exec = nullptr;
