@@ -184,7 +184,7 @@ def run_fan(args, torch, dist, world, rank, local):
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": _traffic_from_profiles("fan"),
-            "kernel": "k_raycast_fan", "avg_kernel_ms": avg_kernel_s * 1e3,
+            "kernel": "k_raycast_fan_w<0, 7>", "avg_kernel_ms": avg_kernel_s * 1e3,
             "alg_bytes_per_launch": alg_bytes,
             "model": "64 B/sample query + 12 B/point test (SURVEY 8d)",
             "diag": st,

@@ -46,6 +46,15 @@ GridView GridIndex::view() const {
     v.ncx = ncx;
     v.ncy = ncy;
     v.col_shift = col_shift;
+    v.flo_x = (float)v.lo_x;
+    v.flo_y = (float)v.lo_y;
+    v.flo_z = (float)v.lo_z;
+    v.finv_c = (float)v.inv_c;
+    v.fnx1 = (float)(nx - 1);
+    v.fny1 = (float)(ny - 1);
+    v.fnz1 = (float)(nz - 1);
+    const double bb[6] = {v.bx0, v.bx1, v.by0, v.by1, v.bz0, v.bz1};
+    for (int a = 0; a < 6; ++a) v.fb[a] = (float)bb[a];
     return v;
 }
 

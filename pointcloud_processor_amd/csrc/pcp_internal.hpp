@@ -73,6 +73,11 @@ struct GridView {               // POD passed to kernels by value
     // columns hold lo 255 / hi 0.  A corner outside its column's range is provably empty.
     const uint16_t *colmap;     // null when disabled (nz > 255 or too large for LDS)
     int32_t ncx, ncy, col_shift;
+    // float copies for the stencil-corner and clip arithmetic: their rounding (~1e-5 m) stays
+    // far inside the 1 mm query margin, so the skips remain exact (Terrain index)
+    float flo_x, flo_y, flo_z, finv_c;
+    float fnx1, fny1, fnz1;     // n - 1 per axis
+    float fb[6];                // clip box x0, x1, y0, y1, z0, z1
 };
 
 struct GridIndex {

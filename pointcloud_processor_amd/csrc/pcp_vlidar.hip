@@ -21,7 +21,17 @@ constexpr int kT = 256;
 // ---------------------------------------------------------------------------------------
 // FLANN L2_Simple<float>: result += diff*diff over x, y, z; returned iff result < r2
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ bool flann_within(float qx, float qy, float qz, const float4 &p,
+// a terrain point's x, y, z (the .w index is not needed by the test: 12-byte loads)
+struct P3 {
+    float x, y, z;
+};
+__device__ __forceinline__ P3 ld_p3(const float4 *pts, uint32_t i) {
+    const float *f = reinterpret_cast<const float *>(pts + i);
+    return P3{f[0], f[1], f[2]};
+}
+
+template <class PT>
+__device__ __forceinline__ bool flann_within(float qx, float qy, float qz, const PT &p,
                                              float r2) {
     const float d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
     float acc = 0.0f;
@@ -48,10 +58,28 @@ __device__ __forceinline__ bool stencil_cell3(const GridView &g, float qx, float
     return true;
 }
 
+// The same corner in float.  Exact in outcome: a corner off by one (the value within the float
+// error of a cell boundary) still holds every point within r of q while the error is below the
+// query margin m (the block keeps >= m of slack on the low side and c - 2r - m on the high
+// side); the rounding here is ~1e-5 m against m = 1e-3 m.  The same holds at the grid border,
+// where the off-by-one block is padding / outside (empty).
+__device__ __forceinline__ bool stencil_cell3_f(const GridView &g, float qx, float qy, float qz,
+                                                uint32_t &ix, uint32_t &iy, uint32_t &iz) {
+    const float fx = (qx - g.flo_x) * g.finv_c;
+    const float fy = (qy - g.flo_y) * g.finv_c;
+    const float fz = (qz - g.flo_z) * g.finv_c;
+    if (!(fx >= 0.0f && fx < g.fnx1 && fy >= 0.0f && fy < g.fny1 && fz >= 0.0f && fz < g.fnz1))
+        return false;
+    ix = (uint32_t)fx;
+    iy = (uint32_t)fy;
+    iz = (uint32_t)fz;
+    return true;
+}
+
 __device__ __forceinline__ bool stencil_cell(const GridView &g, float qx, float qy, float qz,
                                              uint32_t &lin) {
     uint32_t ix, iy, iz;
-    if (!stencil_cell3(g, qx, qy, qz, ix, iy, iz)) return false;
+    if (!stencil_cell3_f(g, qx, qy, qz, ix, iy, iz)) return false;
     const uint32_t nx = (uint32_t)g.nx, nxy = nx * (uint32_t)g.ny;
     lin = ix + nx * iy + nxy * iz;
     return true;
@@ -77,9 +105,9 @@ __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, fl
         b[r][2] = g.start[row + 2];
     }
     const uint32_t last = g.n_pts - 1;
-    float4 f[8];
+    P3 f[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = g.pts[min(b[i >> 1][i & 1], last)];
+    for (int i = 0; i < 8; ++i) f[i] = ld_p3(g.pts, min(b[i >> 1][i & 1], last));
     uint32_t live = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -97,8 +125,8 @@ __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, fl
         if (!(live & (1u << i))) continue;
         const uint32_t e = b[i >> 1][(i & 1) + 1];
         for (uint32_t k = b[i >> 1][i & 1] + 1; k < e; k += 2) {
-            const float4 p0 = g.pts[k];
-            const float4 p1 = g.pts[min(k + 1, e - 1)];
+            const P3 p0 = ld_p3(g.pts, k);
+            const P3 p1 = ld_p3(g.pts, min(k + 1, e - 1));
             if (STATS) cnt[2] += 1;
             if (flann_within(qx, qy, qz, p0, r2)) return true;
             float dz = qz - p0.z;
@@ -159,6 +187,39 @@ __device__ __forceinline__ void clip_k(const GridView &g, double px, double py, 
     khi = (int)fmin(fmax(kh, -1.0), (double)(K - 1));
 }
 
+// clip_k in float (approximate reciprocal): the interval is that of a box perturbed by ~1e-5 m;
+// samples it drops lie within that distance of the true clip box's outside, i.e. >= r + m -
+// 1e-5 from every point (the box is the point bbox inflated by r + m + 1e-6 |coord|): empty.
+__device__ __forceinline__ void clip_kf(const GridView &g, double px, double py, double pz,
+                                        double dx, double dy, double dz, int K, int &klo,
+                                        int &khi) {
+    float t0 = 0.0f, t1 = FLT_MAX;
+    const float p[3] = {(float)px, (float)py, (float)pz}, d[3] = {(float)dx, (float)dy, (float)dz};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float lo = g.fb[2 * a], hi = g.fb[2 * a + 1];
+        if (d[a] == 0.0f) {
+            if (p[a] < lo || p[a] > hi) t1 = -1.0f;
+        } else {
+            const float inv = __builtin_amdgcn_rcpf(d[a]);
+            const float ta = (lo - p[a]) * inv, tb = (hi - p[a]) * inv;
+            t0 = fmaxf(t0, fminf(ta, tb));
+            t1 = fminf(t1, fmaxf(ta, tb));
+        }
+    }
+    if (!(t0 <= t1)) {
+        klo = 0;
+        khi = -1;
+        return;
+    }
+    // one sample of slack each side (s_k = 0.5 + 0.3 k to ~1e-13, t0/t1 to float rounding)
+    const float inv_step = (float)(1.0 / kRayStep);
+    const float kl = ceilf((t0 - 0.5f) * inv_step) - 1.0f;
+    const float kh = floorf(fminf(t1, 1e30f) * inv_step - 0.5f * inv_step) + 1.0f;
+    klo = (int)fminf(fmaxf(kl, 0.0f), (float)K);
+    khi = (int)fminf(fmaxf(kh, -1.0f), (float)(K - 1));
+}
+
 // checkVisibilityWithRaycasting's march (virtual_lidar.cpp:765-797) from pos along unit dir.
 // Visits samples k with s_k < end; returns the first blocked k or -1.  Samples outside the
 // clip box have no point within r (skipped exactly).  s_k comes from ONE table read at klo and
@@ -166,13 +227,16 @@ __device__ __forceinline__ void clip_k(const GridView &g, double px, double py, 
 // processed 4 at a time: the 4 occupancy words are loaded together, then tested in order.
 // col (optional, LDS copy of g.colmap): a stencil corner outside its column's occupied z-range
 // is empty, decided from LDS without touching the occupancy bits in global memory.
-template <bool STATS, int B = 1>
+template <bool STATS, int B = 1, bool FC = true>
 __device__ __forceinline__ int march_t(const GridView &g, double px, double py, double pz,
                                        double dx, double dy, double dz,
                                        const double *__restrict__ steps, int K, double end,
                                        float r2, uint32_t *cnt, const uint16_t *col = nullptr) {
     int klo, khi;
-    clip_k(g, px, py, pz, dx, dy, dz, K, klo, khi);
+    if (FC)
+        clip_kf(g, px, py, pz, dx, dy, dz, K, klo, khi);
+    else
+        clip_k(g, px, py, pz, dx, dy, dz, K, klo, khi);
     if (klo > khi) return -1;
     double s = steps[klo];
     for (int k0 = klo; k0 <= khi; k0 += B) {
@@ -187,7 +251,8 @@ __device__ __forceinline__ int march_t(const GridView &g, double px, double py, 
             qz[i] = (float)(pz + dz * s);
             lin[i] = 0;
             uint32_t ix = 0, iy = 0, iz = 0;
-            bool in = vis[i] && stencil_cell3(g, qx[i], qy[i], qz[i], ix, iy, iz);
+            bool in = vis[i] && (FC ? stencil_cell3_f(g, qx[i], qy[i], qz[i], ix, iy, iz)
+                                    : stencil_cell3(g, qx[i], qy[i], qz[i], ix, iy, iz));
             if (in && col) {
                 const uint32_t zr = col[(iy >> g.col_shift) * (uint32_t)g.ncx + (ix >> g.col_shift)];
                 in = iz >= (zr & 255u) && iz <= (zr >> 8);
@@ -524,7 +589,7 @@ enum { FAN_PLAIN = 0, FAN_STATS = 1, FAN_STAMPS = 2 };
 // termination on near-flat terrain); blockIdx.y = pose.  Each wave writes its blocked-ray
 // count and its sample-query count to its own slot: the per-pose sums are formed by
 // k_fan_reduce in a fixed order (deterministic, no same-address atomics).
-template <int MODE, int B>
+template <int MODE, int B, bool FC = true>
 __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t rblock,
                                          const uint16_t *col) {
     const uint32_t ray = rblock * kT + threadIdx.x;
@@ -549,7 +614,7 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
             asm volatile("" ::"v"(dx), "v"(dy));
             t1 = __builtin_amdgcn_s_memtime();
         }
-        hit = march_t<MODE == FAN_STATS, B>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K,
+        hit = march_t<MODE == FAN_STATS, B, FC>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K,
                                             1e300, a.r2, cnt, col);
     }
     if (MODE == FAN_STAMPS) {
@@ -585,8 +650,23 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
 }
 
 // one block per (ray block, pose); no column map
-template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
-    fan_body<MODE, B>(a, blockIdx.y, blockIdx.x, nullptr);
+template <int MODE, int B, bool FC = true>
+__global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
+    fan_body<MODE, B, FC>(a, blockIdx.y, blockIdx.x, nullptr);
+}
+
+// A/B variants: occupancy forced to W waves per SIMD (register caps; SGPRs count too: a wave
+// slot needs ceil(sgpr/16)*16 + 16 of the 800 SGPRs per SIMD)
+template <int MODE, int W>
+__global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(W, W)))
+k_raycast_fan_w(FanArgs a) {
+    fan_body<MODE, 1, true>(a, blockIdx.y, blockIdx.x, nullptr);
+}
+
+// A/B variant: the column z-range map read from global memory (22 KB: L1-resident), so samples
+// below / above their column's points skip the occupancy word in L2
+template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan_gc(FanArgs a) {
+    fan_body<MODE, B>(a, blockIdx.y, blockIdx.x, a.g.colmap);
 }
 
 // persistent: a CU-filling grid strides over the (pose, ray block) items; each block stages the
@@ -981,10 +1061,16 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     } else {
         ProfScope ps(ctx, PCP_K_RAYCAST_FAN);
         // default: one block per (ray block, pose); PCP_FAN_BATCH selects A/B variants
+        // default: one block per (ray block, pose), capped at 7 waves/SIMD (the compiler's own
+        // choice, 106 SGPRs, admits only 6); PCP_FAN_BATCH selects the A/B variants
         switch (ctx->fan_batch) {
+        case 2: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 1>), grid, dim3(kT), 0, st, a); break;
         case 3: hipLaunchKernelGGL((k_raycast_fan_p<FAN_PLAIN, 1>), dim3(pgrid), dim3(kT), lds, st, a); break;
         case 4: hipLaunchKernelGGL((k_raycast_fan_p<FAN_PLAIN, 2>), dim3(pgrid), dim3(kT), lds, st, a); break;
-        default: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 1>), grid, dim3(kT), 0, st, a); break;
+        case 5: hipLaunchKernelGGL((k_raycast_fan_gc<FAN_PLAIN, 1>), grid, dim3(kT), 0, st, a); break;
+        case 7: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 1, false>), grid, dim3(kT), 0, st, a); break;
+        case 8: hipLaunchKernelGGL((k_raycast_fan_w<FAN_PLAIN, 8>), grid, dim3(kT), 0, st, a); break;
+        default: hipLaunchKernelGGL((k_raycast_fan_w<FAN_PLAIN, 7>), grid, dim3(kT), 0, st, a); break;
         }
         PCP_CHECK_LAUNCH(ctx);
     }
