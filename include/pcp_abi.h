@@ -170,6 +170,24 @@ int pcp_set_aux_cloud(pcp_ctx *ctx, const pcp_cloud_view *aux);
  * surface normals (float, computeCellSurfaceNormal :301-340), in grid order. */
 int pcp_set_cells(pcp_ctx *ctx, const double *xyz, const float *normals, uint64_t n);
 
+/* excavationAreaCallback (virtual_lidar.cpp:164-178) on the GPU: replaces the excavation
+ * KdTreeFLANN, computeTerrainNormals (:209-234: pcl::NormalEstimation, radius 1.5, viewpoint
+ * (0,0,0), then flipped to normal_z >= 0) and generateExcavationGrid3D (:236-287, with
+ * isPointNearExcavation :289-299 at radius 1.5 * grid_resolution and computeCellSurfaceNormal
+ * :301-340).  The valid cells, in the reference's loop order, with their surface normals become
+ * the context's scoring cells (as pcp_set_cells).  An empty area returns PCP_OK and keeps the
+ * previous cells (:168).  grid_bbox (nullable out): grid_min_x, grid_max_x, grid_min_y,
+ * grid_max_y, excavation_min_z, excavation_max_z after the margin; n_cells (nullable out).
+ * `area` is host memory (the PointCloud2 data blob). */
+int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
+                            int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells);
+/* the context's scoring cells: xyz (n x 3 double) and normals (n x 3 float), either nullable;
+ * *n_cells = count (PCP_E_CAPACITY when it exceeds cap). */
+int pcp_get_cells(pcp_ctx *ctx, double *xyz, float *normals, uint64_t cap, uint64_t *n_cells);
+/* terrain_normals_ of the last pcp_set_excavation_area, in input order (n x 3 float, NaN
+ * where fewer than 3 neighbours or a non-finite point). */
+int pcp_get_area_normals(pcp_ctx *ctx, float *normals, uint64_t cap, uint64_t *n);
+
 /* generateCandidatePositions + getGroundHeight (:550-625).  grid_bbox = {grid_min_x,
  * grid_max_x, grid_min_y, grid_max_y, excavation_min_z, excavation_max_z} after the
  * margin (:251-254).  zx120_pose5 = {x,y,z,pitch,yaw} from getZX120Position (:342-358).

@@ -115,6 +115,22 @@ void orc_raycast_fan(const orc_cloud *terrain, const double *poses5, int64_t n_p
 void orc_fan_tables(int32_t n_az, int32_t n_el, double el_min, double el_max,
                     double *ca, double *sa, double *ce, double *se);
 
+/* ---- excavation-area setup (pcp_oracle_setup.c) ------------------------------------------
+ * computeTerrainNormals (virtual_lidar.cpp:209-234): pcl::NormalEstimation, radius 1.5,
+ * viewpoint (0,0,0), then flipped to normal_z >= 0; < 3 neighbours -> NaN.  normals3: n x 3. */
+void orc_area_normals(const float *pts, int64_t n, int64_t stride_floats, double radius,
+                      float *normals3);
+
+/* generateExcavationGrid3D (:236-287) with isPointNearExcavation (radius 1.5 * resolution)
+ * and computeCellSurfaceNormal (:301-340) from area_normals3 (NULL: default (0,0,1)).
+ * Cells in the reference's loop order (rows i over y, columns j over x, layers k).  Returns
+ * the number of valid cells (writes at most cap); grid_bbox = x0, x1, y0, y1, z0, z1 after
+ * the margin; dims = grid_height, grid_width, layers. */
+int64_t orc_excavation_grid(const float *pts, int64_t n, int64_t stride_floats,
+                            double grid_resolution, int32_t vertical_layers,
+                            const float *area_normals3, double *cells_xyz, float *cells_nrm,
+                            int64_t cap, double grid_bbox[6], int32_t dims[3]);
+
 #ifdef __cplusplus
 }
 #endif

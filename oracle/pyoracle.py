@@ -56,6 +56,9 @@ _SIGS = [
     ("orc_raycast_fan", None, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                C.c_double, _P, _P, _P]),
     ("orc_fan_tables", None, [C.c_int32, C.c_int32, C.c_double, C.c_double, _P, _P, _P, _P]),
+    ("orc_area_normals", None, [_P, C.c_int64, C.c_int64, C.c_double, _P]),
+    ("orc_excavation_grid", C.c_int64, [_P, C.c_int64, C.c_int64, C.c_double, C.c_int32, _P, _P,
+                                        _P, C.c_int64, _P, _P]),
 ]
 
 _lib = None
@@ -198,3 +201,28 @@ def fan_tables(n_az, n_el, el_min, el_max):
     ca = np.empty(n_az); sa = np.empty(n_az); ce = np.empty(n_el); se = np.empty(n_el)
     lib().orc_fan_tables(n_az, n_el, el_min, el_max, _p(ca), _p(sa), _p(ce), _p(se))
     return ca, sa, ce, se
+
+
+def area_normals(pts, radius=1.5):
+    """computeTerrainNormals: (N, 3) float32, NaN where < 3 neighbours."""
+    a = _f32(pts)
+    out = np.empty((a.shape[0], 3), np.float32)
+    lib().orc_area_normals(_p(a), a.shape[0], a.shape[1], float(radius), _p(out))
+    return out
+
+
+def excavation_grid(pts, grid_resolution=0.1, vertical_layers=10, normals=None):
+    """generateExcavationGrid3D + computeCellSurfaceNormal -> (cells_xyz f64 (M,3),
+    cells_nrm f32 (M,3), grid_bbox f64 (6,), dims (gh, gw, layers))."""
+    a = _f32(pts)
+    nrm = None if normals is None else np.ascontiguousarray(normals, np.float32)
+    bbox = np.zeros(6, np.float64)
+    dims = np.zeros(3, np.int32)
+    n = lib().orc_excavation_grid(_p(a), a.shape[0], a.shape[1], float(grid_resolution),
+                                  int(vertical_layers), _p(nrm), None, None, 0, _p(bbox), _p(dims))
+    xyz = np.empty((max(n, 1), 3), np.float64)
+    cn = np.empty((max(n, 1), 3), np.float32)
+    lib().orc_excavation_grid(_p(a), a.shape[0], a.shape[1], float(grid_resolution),
+                              int(vertical_layers), _p(nrm), _p(xyz), _p(cn), n, _p(bbox),
+                              _p(dims))
+    return xyz[:n], cn[:n], bbox, tuple(int(d) for d in dims)

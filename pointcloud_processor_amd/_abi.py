@@ -108,6 +108,9 @@ _SIGS = [
     ("pcp_set_terrain", C.c_int, [_P, C.POINTER(CloudView)]),
     ("pcp_set_aux_cloud", C.c_int, [_P, C.POINTER(CloudView)]),
     ("pcp_set_cells", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("pcp_set_excavation_area", C.c_int, [_P, _P, C.c_double, C.c_int32, _P, _P]),
+    ("pcp_get_cells", C.c_int, [_P, _P, _P, C.c_uint64, _P]),
+    ("pcp_get_area_normals", C.c_int, [_P, _P, C.c_uint64, _P]),
     ("pcp_generate_candidates", C.c_int, [_P, _P, C.POINTER(VlParams), _P, _P, C.c_uint64,
                                           C.POINTER(C.c_uint64)]),
     ("pcp_score_poses", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams), _P, _P, _P,
@@ -336,6 +339,40 @@ class Context:
         self._check(self.lib.pcp_set_cells(self.h, _ptr(xyz), _ptr(nrm), xyz.shape[0]),
                     "pcp_set_cells")
         self.n_cells = xyz.shape[0]
+
+    def set_excavation_area(self, area: np.ndarray, grid_resolution: float = 0.1,
+                            vertical_layers: int = 10, point_step=None, offs=(0, 4, 8)):
+        """excavationAreaCallback: GPU normals + 3-D cell grid; the cells become the scoring
+        cells.  Returns (grid_bbox (6,), n_cells)."""
+        v = cloud_view(area, point_step, offs)
+        bbox = np.zeros(6, np.float64)
+        n = C.c_uint64()
+        self._check(self.lib.pcp_set_excavation_area(self.h, C.byref(v), float(grid_resolution),
+                                                      int(vertical_layers), _ptr(bbox),
+                                                      C.byref(n)), "pcp_set_excavation_area")
+        self.n_cells = n.value
+        return bbox, n.value
+
+    def get_cells(self):
+        n = C.c_uint64()
+        rc = self.lib.pcp_get_cells(self.h, None, None, 0, C.byref(n))
+        if rc not in (PCP_OK, PCP_E_CAPACITY):
+            self._check(rc, "pcp_get_cells")
+        xyz = np.empty((n.value, 3), np.float64)
+        nrm = np.empty((n.value, 3), np.float32)
+        self._check(self.lib.pcp_get_cells(self.h, _ptr(xyz), _ptr(nrm), n.value, C.byref(n)),
+                    "pcp_get_cells")
+        return xyz, nrm
+
+    def get_area_normals(self):
+        n = C.c_uint64()
+        rc = self.lib.pcp_get_area_normals(self.h, None, 0, C.byref(n))
+        if rc not in (PCP_OK, PCP_E_CAPACITY):
+            self._check(rc, "pcp_get_area_normals")
+        out = np.empty((n.value, 3), np.float32)
+        self._check(self.lib.pcp_get_area_normals(self.h, _ptr(out), n.value, C.byref(n)),
+                    "pcp_get_area_normals")
+        return out
 
     def terrain_info(self) -> dict:
         info = IndexInfo()

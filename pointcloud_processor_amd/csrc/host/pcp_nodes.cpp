@@ -157,6 +157,26 @@ void SimplifiedDualLidarOptimizer::zx120PointsCallback(const PointCloud2 &msg) {
     if (pcp_set_aux_cloud(dev_.ctx(), &v) != PCP_OK) err_ = dev_.error();
 }
 
+void SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg) {
+    pcp_cloud_view v;
+    std::string why;
+    if (!cloud_view(msg, v, &why)) {   // fromROSMsg would throw: logged, nothing rebuilt
+        err_ = "excavation area: " + why;
+        return;
+    }
+    if (msg.empty()) return;   // :168
+    double bb[6];
+    uint64_t n = 0;
+    if (pcp_set_excavation_area(dev_.ctx(), &v, p_.grid_resolution, p_.vertical_layers, bb, &n) !=
+        PCP_OK) {
+        err_ = dev_.error();   // "Failed to process excavation area" (:175-177)
+        return;
+    }
+    n_cells_ = n;
+    flags_.assign(n_cells_, 0);   // excavation_grid_3d_ rebuilt from fresh GridCells (:259)
+    std::memcpy(bbox_, bb, sizeof(bbox_));
+}
+
 void SimplifiedDualLidarOptimizer::setExcavationGrid(const std::vector<double> &xyz,
                                                      const std::vector<float> &normals,
                                                      const double grid_bbox[6]) {

@@ -131,10 +131,14 @@ class SimplifiedDualLidarOptimizer {
     explicit SimplifiedDualLidarOptimizer(Device &dev) : dev_(dev) {}
     SimplifiedDualLidarOptimizer(Device &dev, const Params &p) : dev_(dev), p_(p) {}
     Params &params() { return p_; }
+    // excavationAreaCallback (:164-178): GPU normals + 3-D cell grid from /excavation_area;
+    // an empty cloud keeps the previous grid (:168)
+    void excavationAreaCallback(const PointCloud2 &msg);
     void terrainCallback(const PointCloud2 &msg);       // :180-192
     void zx120PointsCallback(const PointCloud2 &msg);   // :194-207
-    // the valid cells of generateExcavationGrid3D (:236-287) with computeCellSurfaceNormal;
-    // grid_bbox = grid_min_x, grid_max_x, grid_min_y, grid_max_y, excavation_min_z/max_z
+    // cells computed elsewhere (tests, replays): the valid cells of generateExcavationGrid3D
+    // (:236-287) with computeCellSurfaceNormal; grid_bbox = grid_min_x, grid_max_x,
+    // grid_min_y, grid_max_y, excavation_min_z/max_z
     void setExcavationGrid(const std::vector<double> &xyz, const std::vector<float> &normals,
                            const double grid_bbox[6]);
     // runOptimization (:454-548); zx120_base = TF map -> zx120/base_link, nullptr = missing

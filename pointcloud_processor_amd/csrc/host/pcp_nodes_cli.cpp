@@ -229,13 +229,60 @@ static int cmd_replay(Device &dev, char **a) {
     return 0;
 }
 
+// area AREA.f32 N_AREA TERRAIN.f32 N_TERRAIN ZX120_BASE(x,y,z) NUM_CANDIDATES MAX_DISTANCE
+//      OUT_TOTAL.f64 OUT_CELLS.f64 OUT_NORMALS.f32
+// the virtual_lidar node from its /excavation_area message: excavationAreaCallback (GPU normals
+// + 3-D cell grid), terrainCallback, one runOptimization tick (no zx120 cloud)
+static int cmd_area(Device &dev, char **a) {
+    const auto ar = read_file(a[0]), t = read_file(a[2]);
+    const size_t an = std::strtoull(a[1], nullptr, 10), tn = std::strtoull(a[3], nullptr, 10);
+    const auto zxt = tuple(a[4]);
+    SimplifiedDualLidarOptimizer::Params p;
+    p.num_candidates = std::atoi(a[5]);
+    p.max_distance = std::strtod(a[6], nullptr);
+    SimplifiedDualLidarOptimizer node(dev, p);
+    node.excavationAreaCallback(cloud_from(ar, an, 32, "map"));
+    if (!node.lastError().empty()) {
+        std::fprintf(stderr, "area: %s\n", node.lastError().c_str());
+        return 1;
+    }
+    node.terrainCallback(cloud_from(t, tn, 32, "map"));
+    Transform zx;
+    zx.t[0] = zxt[0];
+    zx.t[1] = zxt[1];
+    zx.t[2] = zxt[2];
+    const auto r = node.runOptimization(&zx);
+    if (!r.ran) {
+        std::fprintf(stderr, "area: %s\n", node.lastError().c_str());
+        return 1;
+    }
+    std::vector<double> tot(r.candidates.size());
+    for (size_t i = 0; i < tot.size(); ++i) tot[i] = r.candidates[i].total_score;
+    write_file(a[7], tot.data(), tot.size() * 8);
+    uint64_t nc = 0;
+    pcp_get_cells(dev.ctx(), nullptr, nullptr, 0, &nc);
+    std::vector<double> xyz(nc * 3);
+    std::vector<float> nrm(nc * 3);
+    if (pcp_get_cells(dev.ctx(), xyz.data(), nrm.data(), nc, &nc) != PCP_OK) return 1;
+    write_file(a[8], xyz.data(), xyz.size() * 8);
+    write_file(a[9], nrm.data(), nrm.size() * 4);
+    std::printf("{\"n_cells\": %llu, \"n_candidates\": %zu, \"best_idx\": %lld}\n",
+                (unsigned long long)nc, r.candidates.size(), (long long)r.report.best_idx);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: pcp_nodes_cli filter|merge|vlidar|replay ...\n");
+        std::fprintf(stderr, "usage: pcp_nodes_cli filter|merge|vlidar|area|replay ...\n");
         return 2;
     }
     const std::string cmd = argv[1];
-    const int need = cmd == "filter" ? 8 : cmd == "merge" ? 7 : cmd == "vlidar" ? 14 : cmd == "replay" ? 8 : -1;
+    const int need = cmd == "filter"   ? 8
+                     : cmd == "merge"  ? 7
+                     : cmd == "vlidar" ? 14
+                     : cmd == "area"   ? 10
+                     : cmd == "replay" ? 8
+                                       : -1;
     if (need < 0 || argc - 2 < need) {
         std::fprintf(stderr, "bad arguments for %s\n", cmd.c_str());
         return 2;
@@ -245,6 +292,7 @@ int main(int argc, char **argv) {
         if (cmd == "filter") return cmd_filter(dev, argv + 2);
         if (cmd == "merge") return cmd_merge(dev, argv + 2);
         if (cmd == "vlidar") return cmd_vlidar(dev, argv + 2, argc - 2);
+        if (cmd == "area") return cmd_area(dev, argv + 2);
         return cmd_replay(dev, argv + 2);
     } catch (const std::exception &e) {
         std::fprintf(stderr, "%s\n", e.what());

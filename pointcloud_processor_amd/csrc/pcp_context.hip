@@ -269,6 +269,9 @@ void pcp_destroy(pcp_ctx *ctx) {
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     ctx->terrain.release();
     ctx->aux.release();
+    ctx->exc_norm.release();
+    ctx->exc_near.release();
+    ctx->area_nrm.release();
     DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage, &ctx->fan_tab,
                       &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,
                       &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->f_in,

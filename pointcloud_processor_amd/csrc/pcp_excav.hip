@@ -1,0 +1,485 @@
+// pcp_excav.hip -- virtual_lidar.cpp's excavation-area setup on gfx950:
+// excavationAreaCallback (:164-178) -> computeTerrainNormals (:209-234) and
+// generateExcavationGrid3D (:236-287) with isPointNearExcavation (:289-299) and
+// computeCellSurfaceNormal (:301-340).  The resulting cells become the context's scoring
+// cells (what pcp_set_cells would hold).
+//
+//  area normals : one block per area point; the 1.5 m neighbours (FLANN predicate) of the
+//                 point's stencil in a uniform grid sized for r = 1.5; shifted second moments in
+//                 double, covariance rounded to float, pcl::eigen33 restated in float,
+//                 viewpoint (0,0,0) flip, then the reference's flip to normal_z >= 0
+//  cell lattice : one thread per (i, j, k) lattice point, exact radius test (r = 1.5 res) on a
+//                 grid sized for that radius; one block compacts the hits in loop order
+//  cell normals : one block per cell; double-double sums of the neighbours' finite normals
+//                 (the reference's sequential double sum when that sum is exact, which it is
+//                 for these magnitudes), normalised when the norm exceeds 1e-6
+#pragma clang fp contract(off)
+
+#include <cfloat>
+#include <cmath>
+#include <vector>
+
+#include "pcp_internal.hpp"
+#include "pcp_stencil.hpp"
+
+namespace pcp {
+
+constexpr double kNormalRadius = 1.5;   // NORMAL_SEARCH_RADIUS (virtual_lidar.cpp:110)
+constexpr int kXT = 256;
+
+// the 2x2x2 stencil of q as 4 contiguous point ranges [lo, hi) (rows of 2 adjacent x-cells)
+__device__ __forceinline__ bool stencil_ranges(const GridView &g, float qx, float qy, float qz,
+                                               uint32_t (&lo)[4], uint32_t (&hi)[4]) {
+    uint32_t ix, iy, iz;
+    if (!stencil_cell3_f(g, qx, qy, qz, ix, iy, iz)) return false;
+    const uint32_t nx = (uint32_t)g.nx, nxy = nx * (uint32_t)g.ny;
+    const uint32_t lin = ix + nx * iy + nxy * iz;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t row = lin + (r & 1) * nx + (r >> 1) * nxy;
+        lo[r] = g.start[row];
+        hi[r] = g.start[row + 2];
+    }
+    return true;
+}
+
+template <int N>
+__device__ __forceinline__ void block_sum_d(double (&v)[N], double (*lds)[kXT / 64]) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int a = 0; a < N; ++a)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[a] += __shfl_xor(v[a], o, 64);
+    if (lane == 0)
+#pragma unroll
+        for (int a = 0; a < N; ++a) lds[a][wid] = v[a];
+    __syncthreads();
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+        double t = 0.0;
+        for (int w = 0; w < kXT / 64; ++w) t += lds[a][w];
+        v[a] = t;
+    }
+}
+
+// ---- pcl::eigen33, smallest eigenvalue's eigenvector (float, as PCL's Scalar) ---------------
+__device__ __forceinline__ void roots2(float b, float c, float r[3]) {
+    r[0] = 0.0f;
+    float d = (float)(b * b - 4.0 * c);
+    if (d < 0.0f) d = 0.0f;
+    const float sd = sqrtf(d);
+    r[2] = 0.5f * (b + sd);
+    r[1] = 0.5f * (b - sd);
+}
+
+__device__ __forceinline__ void roots3(const float m[3][3], float r[3]) {
+    const float c0 = m[0][0] * m[1][1] * m[2][2] + 2.0f * m[0][1] * m[0][2] * m[1][2] -
+                     m[0][0] * m[1][2] * m[1][2] - m[1][1] * m[0][2] * m[0][2] -
+                     m[2][2] * m[0][1] * m[0][1];
+    const float c1 = m[0][0] * m[1][1] - m[0][1] * m[0][1] + m[0][0] * m[2][2] -
+                     m[0][2] * m[0][2] + m[1][1] * m[2][2] - m[1][2] * m[1][2];
+    const float c2 = m[0][0] + m[1][1] + m[2][2];
+    if (fabsf(c0) < FLT_EPSILON) {
+        roots2(c2, c1, r);
+        return;
+    }
+    const float s_inv3 = (float)(1.0 / 3.0);
+    const float s_sqrt3 = sqrtf(3.0f);
+    const float c2_over_3 = c2 * s_inv3;
+    float a_over_3 = (c1 - c2 * c2_over_3) * s_inv3;
+    if (a_over_3 > 0.0f) a_over_3 = 0.0f;
+    const float half_b = 0.5f * (c0 + c2_over_3 * (2.0f * c2_over_3 * c2_over_3 - c1));
+    float q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
+    if (q > 0.0f) q = 0.0f;
+    const float rho = sqrtf(-a_over_3);
+    const float theta = atan2f(sqrtf(-q), half_b) * s_inv3;
+    const float ct = cosf(theta), st = sinf(theta);
+    r[0] = c2_over_3 + 2.0f * rho * ct;
+    r[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);
+    r[2] = c2_over_3 - rho * (ct - s_sqrt3 * st);
+    float t;
+    if (r[0] >= r[1]) {
+        t = r[0]; r[0] = r[1]; r[1] = t;
+    }
+    if (r[1] >= r[2]) {
+        t = r[1]; r[1] = r[2]; r[2] = t;
+        if (r[0] >= r[1]) {
+            t = r[0]; r[0] = r[1]; r[1] = t;
+        }
+    }
+    if (r[0] <= 0.0f) roots2(c2, c1, r);
+}
+
+__device__ __forceinline__ void cross3(const float a[3], const float b[3], float o[3]) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+__device__ __forceinline__ void eigen33_min(const float cov[3][3], float ev[3]) {
+    float scale = 0.0f;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) scale = fmaxf(scale, fabsf(cov[i][j]));
+    if (scale <= FLT_MIN) scale = 1.0f;
+    float m[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) m[i][j] = cov[i][j] / scale;
+    float r[3];
+    roots3(m, r);
+    for (int i = 0; i < 3; ++i) m[i][i] -= r[0];
+    float v1[3], v2[3], v3[3];
+    cross3(m[0], m[1], v1);
+    cross3(m[0], m[2], v2);
+    cross3(m[1], m[2], v3);
+    const float l1 = v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2];
+    const float l2 = v2[0] * v2[0] + v2[1] * v2[1] + v2[2] * v2[2];
+    const float l3 = v3[0] * v3[0] + v3[1] * v3[1] + v3[2] * v3[2];
+    const float *v = v3;
+    float l = l3;
+    if (l1 >= l2 && l1 >= l3) {
+        v = v1;
+        l = l1;
+    } else if (l2 >= l1 && l2 >= l3) {
+        v = v2;
+        l = l2;
+    }
+    const float s = sqrtf(l);
+    for (int a = 0; a < 3; ++a) ev[a] = v[a] / s;
+}
+
+// computeTerrainNormals: block per point (sorted index order; .w = input index)
+__global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, float *__restrict__ out) {
+    const uint32_t qi = blockIdx.x;
+    const float4 q = g.pts[qi];
+    const uint32_t orig = __float_as_uint(q.w);
+    uint32_t lo[4], hi[4];
+    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // xx xy xz yy yz zz x y z count
+    if (stencil_ranges(g, q.x, q.y, q.z, lo, hi)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            for (uint32_t k = lo[r] + threadIdx.x; k < hi[r]; k += kXT) {
+                const P3 p = ld_p3(g.pts, k);
+                if (!flann_within(q.x, q.y, q.z, p, r2)) continue;
+                // shifted by K = the first (nearest) neighbour = the query point itself
+                const double x = (double)(p.x - q.x), y = (double)(p.y - q.y),
+                             z = (double)(p.z - q.z);
+                acc[0] += x * x;
+                acc[1] += x * y;
+                acc[2] += x * z;
+                acc[3] += y * y;
+                acc[4] += y * z;
+                acc[5] += z * z;
+                acc[6] += x;
+                acc[7] += y;
+                acc[8] += z;
+                acc[9] += 1.0;
+            }
+    }
+    __shared__ double lds[10][kXT / 64];
+    block_sum_d(acc, lds);
+    if (threadIdx.x != 0) return;
+    float *o = out + 3 * (size_t)orig;
+    if (acc[9] < 3.0) {   // computePointNormal: < 3 neighbours -> NaN
+        o[0] = o[1] = o[2] = NAN;
+        return;
+    }
+    for (int a = 0; a < 9; ++a) acc[a] /= acc[9];
+    float cov[3][3];
+    cov[0][0] = (float)(acc[0] - acc[6] * acc[6]);
+    cov[0][1] = (float)(acc[1] - acc[6] * acc[7]);
+    cov[0][2] = (float)(acc[2] - acc[6] * acc[8]);
+    cov[1][1] = (float)(acc[3] - acc[7] * acc[7]);
+    cov[1][2] = (float)(acc[4] - acc[7] * acc[8]);
+    cov[2][2] = (float)(acc[5] - acc[8] * acc[8]);
+    cov[1][0] = cov[0][1];
+    cov[2][0] = cov[0][2];
+    cov[2][1] = cov[1][2];
+    float ev[3];
+    eigen33_min(cov, ev);
+    const float ct = (0.0f - q.x) * ev[0] + (0.0f - q.y) * ev[1] + (0.0f - q.z) * ev[2];
+    if (ct < 0.0f)
+        for (int a = 0; a < 3; ++a) ev[a] = -ev[a];
+    if (ev[2] < 0.0f)
+        for (int a = 0; a < 3; ++a) ev[a] = -ev[a];
+    o[0] = ev[0];
+    o[1] = ev[1];
+    o[2] = ev[2];
+}
+
+struct Lattice {
+    double x0, y0, z0, res, z_step;
+    int32_t gw, gh, layers;
+    uint32_t total;
+};
+
+__device__ __forceinline__ void lattice_xyz(const Lattice &L, uint32_t li, double &x, double &y,
+                                            double &z) {
+    const uint32_t k = li % (uint32_t)L.layers;
+    const uint32_t ij = li / (uint32_t)L.layers;
+    const uint32_t j = ij % (uint32_t)L.gw, i = ij / (uint32_t)L.gw;
+    x = L.x0 + (int)j * L.res;
+    y = L.y0 + (int)i * L.res;
+    z = L.z0 + (int)k * L.z_step + L.z_step / 2.0;
+}
+
+// isPointNearExcavation (radiusSearch(r) > 0) of every lattice point; linear index =
+// (i * gw + j) * layers + k, i.e. the reference's loop order
+__global__ void __launch_bounds__(kXT)
+k_lattice_flags(GridView g, float r2, Lattice L, uint8_t *__restrict__ flags) {
+    const uint32_t li = blockIdx.x * kXT + threadIdx.x;
+    if (li >= L.total) return;
+    double x, y, z;
+    lattice_xyz(L, li, x, y, z);
+    const float qx = (float)x, qy = (float)y, qz = (float)z;
+    uint32_t lo[4], hi[4];
+    bool hit = false;
+    if (stencil_ranges(g, qx, qy, qz, lo, hi)) {
+        for (int r = 0; r < 4 && !hit; ++r)
+            for (uint32_t k = lo[r]; k < hi[r]; ++k)
+                if (flann_within(qx, qy, qz, ld_p3(g.pts, k), r2)) {
+                    hit = true;
+                    break;
+                }
+    }
+    flags[li] = hit ? 1 : 0;
+}
+
+// one block: the flagged lattice points in order -> cells (double xyz); *n_out = count
+__global__ void __launch_bounds__(1024)
+k_lattice_compact(const uint8_t *__restrict__ flags, Lattice L, double *__restrict__ cells,
+                  uint32_t cap, uint32_t *__restrict__ n_out) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ uint32_t wc[16];
+    uint32_t run = 0;
+    for (uint32_t base = 0; base < L.total; base += 1024) {
+        const uint32_t li = base + threadIdx.x;
+        const bool f = li < L.total && flags[li];
+        const uint64_t bal = __ballot(f);
+        if (lane == 0) wc[wid] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+        for (int w = 0; w < 16; ++w) {
+            pre += w < wid ? wc[w] : 0u;
+            tot += wc[w];
+        }
+        if (f) {
+            const uint32_t d = run + pre + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+            if (d < cap) {
+                double x, y, z;
+                lattice_xyz(L, li, x, y, z);
+                cells[3 * (size_t)d] = x;
+                cells[3 * (size_t)d + 1] = y;
+                cells[3 * (size_t)d + 2] = z;
+            }
+        }
+        run += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *n_out = run;
+}
+
+// double-double accumulation (TwoSum): exact sums of these float addends
+struct DD {
+    double hi, lo;
+};
+__device__ __forceinline__ void dd_add(DD &a, double x) {
+    const double s = a.hi + x;
+    const double bb = s - a.hi;
+    const double err = (a.hi - (s - bb)) + (x - bb);
+    a.hi = s;
+    a.lo += err;
+}
+__device__ __forceinline__ DD dd_merge(DD a, DD b) {
+    dd_add(a, b.hi);
+    a.lo += b.lo;
+    return a;
+}
+
+// computeCellSurfaceNormal: block per cell, neighbours within 1.5 m of the float cell position
+__global__ void __launch_bounds__(kXT)
+k_cell_normals(GridView g, float r2, const double *__restrict__ cells,
+               const float *__restrict__ area_nrm, float *__restrict__ out) {
+    const uint32_t c = blockIdx.x;
+    const float qx = (float)cells[3 * (size_t)c], qy = (float)cells[3 * (size_t)c + 1],
+                qz = (float)cells[3 * (size_t)c + 2];
+    DD s[3] = {{0, 0}, {0, 0}, {0, 0}};
+    uint32_t valid = 0;
+    uint32_t lo[4], hi[4];
+    if (stencil_ranges(g, qx, qy, qz, lo, hi)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            for (uint32_t k = lo[r] + threadIdx.x; k < hi[r]; k += kXT) {
+                const float4 p = g.pts[k];
+                if (!flann_within(qx, qy, qz, p, r2)) continue;
+                const float *n = area_nrm + 3 * (size_t)__float_as_uint(p.w);
+                const float nx = n[0], ny = n[1], nz = n[2];
+                if (!(isfinite(nx) && isfinite(ny) && isfinite(nz))) continue;
+                dd_add(s[0], (double)nx);
+                dd_add(s[1], (double)ny);
+                dd_add(s[2], (double)nz);
+                ++valid;
+            }
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            DD t{__shfl_xor(s[a].hi, o, 64), __shfl_xor(s[a].lo, o, 64)};
+            s[a] = dd_merge(s[a], t);
+        }
+        valid += __shfl_xor(valid, o, 64);
+    }
+    __shared__ DD lds[3][kXT / 64];
+    __shared__ uint32_t lv[kXT / 64];
+    if (lane == 0) {
+        for (int a = 0; a < 3; ++a) lds[a][wid] = s[a];
+        lv[wid] = valid;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    DD t[3];
+    uint32_t nv = 0;
+    for (int a = 0; a < 3; ++a) {
+        t[a] = lds[a][0];
+        for (int w = 1; w < kXT / 64; ++w) t[a] = dd_merge(t[a], lds[a][w]);
+    }
+    for (int w = 0; w < kXT / 64; ++w) nv += lv[w];
+    float *o = out + 3 * (size_t)c;
+    o[0] = 0.0f;   // GridCell's default surface normal
+    o[1] = 0.0f;
+    o[2] = 1.0f;
+    if (nv == 0) return;
+    const double sx = t[0].hi + t[0].lo, sy = t[1].hi + t[1].lo, sz = t[2].hi + t[2].lo;
+    const double norm = sqrt(sx * sx + sy * sy + sz * sz);
+    if (norm > 1e-6) {
+        o[0] = (float)(sx / norm);
+        o[1] = (float)(sy / norm);
+        o[2] = (float)(sz / norm);
+    }
+}
+
+}  // namespace pcp
+
+using namespace pcp;
+
+extern "C" {
+
+int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
+                            int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells) {
+    if (!ctx) return PCP_E_INVALID;
+    int rc = check_view(ctx, area, "pcp_set_excavation_area");
+    if (rc) return rc;
+    if (!(grid_resolution > 0.0))
+        return set_err(ctx, PCP_E_INVALID, "pcp_set_excavation_area: grid_resolution must be > 0");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    if (n_cells) *n_cells = ctx->n_cells;
+    if (area->n == 0) return PCP_OK;   // :168, nothing is rebuilt; the previous cells stay
+    const double r_near = grid_resolution * 1.5;
+    if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius))) return rc;
+    if ((rc = build_index(ctx, ctx->exc_near, *area, r_near))) return rc;
+    const uint64_t n = area->n;
+    PCP_HIP(ctx, ctx->area_nrm.ensure(n * 3 * sizeof(float) + 16));
+    // non-finite points are not in the index: PCL gives them a NaN normal
+    PCP_HIP(ctx, hipMemsetAsync(ctx->area_nrm.p, 0xff, n * 3 * sizeof(float), ctx->stream));
+    ctx->area_n = n;
+    if (ctx->exc_norm.n_pts == 0) {   // no finite point: no lattice bounds, no cells
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        ctx->n_cells = 0;
+        if (n_cells) *n_cells = 0;
+        return PCP_OK;
+    }
+    const GridView gn = ctx->exc_norm.view(), gq = ctx->exc_near.view();
+    const float r2n = (float)(kNormalRadius * kNormalRadius), r2q = (float)(r_near * r_near);
+    hipLaunchKernelGGL(k_area_normals, dim3((unsigned)ctx->exc_norm.n_pts), dim3(kXT), 0,
+                       ctx->stream, gn, r2n,
+                       ctx->area_nrm.as<float>());
+    PCP_CHECK_LAUNCH(ctx);
+    // grid bounds (:239-256): min/max of the float coordinates as doubles, then the margin
+    const double *bmin = ctx->exc_norm.bmin, *bmax = ctx->exc_norm.bmax;
+    Lattice L;
+    const double x0 = bmin[0] - grid_resolution, x1 = bmax[0] + grid_resolution;
+    const double y0 = bmin[1] - grid_resolution, y1 = bmax[1] + grid_resolution;
+    const double z0 = bmin[2] - grid_resolution, z1 = bmax[2] + grid_resolution;
+    L.x0 = x0;
+    L.y0 = y0;
+    L.z0 = z0;
+    L.res = grid_resolution;
+    L.gw = (int)std::ceil((x1 - x0) / grid_resolution) + 1;
+    L.gh = (int)std::ceil((y1 - y0) / grid_resolution) + 1;
+    L.layers = vertical_layers;
+    L.z_step = (z1 - z0) / std::max(1, vertical_layers);
+    if (grid_bbox) {
+        const double bb[6] = {x0, x1, y0, y1, z0, z1};
+        for (int a = 0; a < 6; ++a) grid_bbox[a] = bb[a];
+    }
+    const uint64_t total = vertical_layers > 0 ? (uint64_t)L.gw * L.gh * vertical_layers : 0;
+    if (total >= (1ull << 31))
+        return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: %llu lattice points",
+                       (unsigned long long)total);
+    L.total = (uint32_t)total;
+    PCP_HIP(ctx, ctx->stage.ensure(total + 64));
+    PCP_HIP(ctx, ctx->cells_xyz.ensure(total * 3 * sizeof(double) + 16));
+    PCP_HIP(ctx, ctx->cells_nrm.ensure(total * 3 * sizeof(float) + 16));
+    PCP_HIP(ctx, ctx->out_c.ensure(64));
+    uint32_t *n_d = ctx->out_c.as<uint32_t>();
+    if (total) {
+        hipLaunchKernelGGL(k_lattice_flags, dim3((unsigned)((total + kXT - 1) / kXT)), dim3(kXT),
+                           0, ctx->stream, gq, r2q, L, ctx->stage.as<uint8_t>());
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    hipLaunchKernelGGL(k_lattice_compact, dim3(1), dim3(1024), 0, ctx->stream,
+                       (const uint8_t *)ctx->stage.as<uint8_t>(), L, ctx->cells_xyz.as<double>(),
+                       (uint32_t)total, n_d);
+    PCP_CHECK_LAUNCH(ctx);
+    uint32_t nc = 0;
+    PCP_HIP(ctx, hipMemcpyAsync(&nc, n_d, 4, hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (nc) {
+        hipLaunchKernelGGL(k_cell_normals, dim3(nc), dim3(kXT), 0, ctx->stream, gn, r2n,
+                           (const double *)ctx->cells_xyz.as<double>(),
+                           (const float *)ctx->area_nrm.as<float>(), ctx->cells_nrm.as<float>());
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->n_cells = nc;
+    if (n_cells) *n_cells = nc;
+    prof_resolve(ctx);
+    return PCP_OK;
+}
+
+int pcp_get_cells(pcp_ctx *ctx, double *xyz, float *normals, uint64_t cap, uint64_t *n_cells) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!n_cells) return set_err(ctx, PCP_E_INVALID, "pcp_get_cells: null n_cells");
+    *n_cells = ctx->n_cells;
+    if (ctx->n_cells > cap)
+        return set_err(ctx, PCP_E_CAPACITY, "pcp_get_cells: %llu cells, cap %llu",
+                       (unsigned long long)ctx->n_cells, (unsigned long long)cap);
+    if (!ctx->n_cells) return PCP_OK;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    if (xyz)
+        PCP_HIP(ctx, hipMemcpyAsync(xyz, ctx->cells_xyz.p, ctx->n_cells * 3 * sizeof(double),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+    if (normals)
+        PCP_HIP(ctx, hipMemcpyAsync(normals, ctx->cells_nrm.p, ctx->n_cells * 3 * sizeof(float),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return PCP_OK;
+}
+
+int pcp_get_area_normals(pcp_ctx *ctx, float *normals, uint64_t cap, uint64_t *n) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!n) return set_err(ctx, PCP_E_INVALID, "pcp_get_area_normals: null n");
+    *n = ctx->area_n;
+    if (ctx->area_n > cap)
+        return set_err(ctx, PCP_E_CAPACITY, "pcp_get_area_normals: %llu points, cap %llu",
+                       (unsigned long long)ctx->area_n, (unsigned long long)cap);
+    if (!ctx->area_n || !normals) return PCP_OK;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    PCP_HIP(ctx, hipMemcpyAsync(normals, ctx->area_nrm.p, ctx->area_n * 3 * sizeof(float),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return PCP_OK;
+}
+
+}  // extern "C"

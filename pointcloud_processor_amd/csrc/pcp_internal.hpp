@@ -141,6 +141,11 @@ struct pcp_ctx {
     uint64_t aux_cloud_n = 0;
     uint64_t n_cells = 0;
     pcp::DevBuf cells_xyz, cells_nrm;
+    // excavation area (pcp_set_excavation_area): indices for the normal radius (1.5 m) and the
+    // lattice test radius (1.5 * grid_resolution), and the per-point normals
+    pcp::GridIndex exc_norm, exc_near;
+    pcp::DevBuf area_nrm;
+    uint64_t area_n = 0;
     // scratch
     pcp::DevBuf stage, scratch[8];
     pcp::DevBuf fan_tab, poses_d, steps_d, out_a, out_b, out_c, out_d, stats_d;

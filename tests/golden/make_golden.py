@@ -116,6 +116,14 @@ def main():
                                          rep.blue, rep.yellow, rep.zx120_green, rep.zx120_red,
                                          rep.zx120_blue, rep.zx120_yellow], np.int64),
                         best_score=rep.best_score, zx120_total=rep.zx120_total_score)
+    # ---- excavation-area setup (computeTerrainNormals + generateExcavationGrid3D, :164-340)
+    from pointcloud_processor_amd import synth
+
+    area = np.ascontiguousarray(synth.terrain_scene(n_side=200, x0=-2.0, y0=-4.0).area[::3, :4])
+    anrm = O.area_normals(area, 1.5)
+    cxyz, cn, gbb, dims = O.excavation_grid(area, 0.1, 10, anrm)
+    np.savez_compressed(HERE / "excavation.npz", area=area, normals=anrm, cells=cxyz,
+                        cell_normals=cn, grid_bbox=gbb, dims=np.array(dims, np.int32))
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, f.stat().st_size)
 

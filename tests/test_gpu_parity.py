@@ -7,6 +7,7 @@ a relative 1e-12 per pose; candidate pitch/yaw (atan2) within 1e-12 rad.
 All calls go through the C ABI (pointcloud_processor_amd/_abi.py -> libpcp.so).
 """
 import math
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -16,6 +17,7 @@ from pointcloud_processor_amd import _abi, synth
 pytestmark = pytest.mark.gpu
 
 BOX = np.array([0.0, 15.0, -10.0, 10.0, -1.5, 10.0])   # pointcloud_filter.cpp:30-36,111-113
+GOLD = Path(__file__).resolve().parent / "golden"
 
 
 def _cloud(n, seed, step_floats=4, nan_frac=0.01):
@@ -338,3 +340,34 @@ def test_score_poses_edge_states(oracle, scene, cells, aux):
         ctx.set_cells(np.zeros((0, 3)), np.zeros((0, 3), np.float32))
         t, c, rep = ctx.score_poses(poses, zx, params, np.zeros(0, np.uint8))
         assert rep.best_idx == 0 and np.all(t == 0)
+
+
+# ---------------------------------------------------------------- excavation-area setup
+def test_excavation_area_setup(oracle, scene):
+    """pcp_set_excavation_area against the oracle: grid bounds and the valid cells (positions,
+    reference loop order) bit-exact; point normals within 2e-3 and cell normals within 1e-4
+    (PCL's float covariance sums, see test_oracle.test_excavation_vs_numpy); an empty area
+    keeps the previous cells (virtual_lidar.cpp:168)."""
+    d = np.load(GOLD / "excavation.npz")
+    ctx = _abi.Context(0)
+    try:
+        for area, ref in ((d["area"], None), (scene.area, "full")):
+            if ref is None:
+                r_n, r_xyz, r_cn, r_bb = d["normals"], d["cells"], d["cell_normals"], d["grid_bbox"]
+            else:
+                r_n = oracle.area_normals(area, 1.5)
+                r_xyz, r_cn, r_bb, _ = oracle.excavation_grid(area, 0.1, 10, r_n)
+            bb, n = ctx.set_excavation_area(area, 0.1, 10, point_step=area.shape[1] * 4)
+            np.testing.assert_array_equal(bb, r_bb)
+            assert n == r_xyz.shape[0]
+            xyz, cn = ctx.get_cells()
+            np.testing.assert_array_equal(xyz, r_xyz)
+            np.testing.assert_allclose(cn, r_cn, atol=1e-4)
+            an = ctx.get_area_normals()
+            fin = np.isfinite(r_n).all(1)
+            assert np.array_equal(np.isfinite(an).all(1), fin)
+            np.testing.assert_allclose(an[fin], r_n[fin], atol=2e-3)
+        bb, n2 = ctx.set_excavation_area(np.zeros((0, 4), np.float32), 0.1, 10)
+        assert n2 == n and np.array_equal(ctx.get_cells()[0], xyz)
+    finally:
+        ctx.close()

@@ -98,3 +98,32 @@ def test_streaming_replay(tmp_path, scene, cells):
                tmp_path / "n.f32", cells.xyz.shape[0], _t(cells.grid_bbox), 20, 60032)
     assert res["frames"] == 20 and res["merged_points"] > 0 and res["best_idx"] >= 0
     assert 0 < res["p50_ms"] <= res["p99_ms"]
+
+
+def test_excavation_area_node(tmp_path, oracle, small_scene):
+    """virtual_lidar from its /excavation_area message: the node's excavationAreaCallback (GPU
+    normals + cell grid) then one runOptimization tick, against the oracle pipeline.  Cells
+    bit-exact, cell normals within 1e-4; with the node's own cells and normals the per-candidate
+    totals match the oracle's reference loop to 1e-12 and the best index exactly."""
+    area = np.ascontiguousarray(small_scene.area)
+    terr = np.ascontiguousarray(small_scene.terrain)
+    area.tofile(tmp_path / "a.f32")
+    terr.tofile(tmp_path / "t.f32")
+    res = _run("area", tmp_path / "a.f32", area.shape[0], tmp_path / "t.f32", terr.shape[0],
+               "0,0,0", 36, 12.0, tmp_path / "tot.f64", tmp_path / "c.f64", tmp_path / "n.f32")
+    xyz = np.fromfile(tmp_path / "c.f64", np.float64).reshape(-1, 3)
+    cn = np.fromfile(tmp_path / "n.f32", np.float32).reshape(-1, 3)
+    r_n = oracle.area_normals(area, 1.5)
+    r_xyz, r_cn, bb, _ = oracle.excavation_grid(area, 0.1, 10, r_n)
+    assert res["n_cells"] == r_xyz.shape[0]
+    np.testing.assert_array_equal(xyz, r_xyz)
+    np.testing.assert_allclose(cn, r_cn, atol=1e-4)
+    T = oracle.Cloud(terr)
+    zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])   # getZX120Position offsets on (0, 0, 0)
+    params = oracle.vl_params(num_candidates=36, max_distance=12.0)
+    cand = oracle.generate_candidates(T, bb, params, zx)
+    flags = np.zeros(xyz.shape[0], np.uint8)
+    tot, _, rep = oracle.score_poses(T, None, xyz, cn, cand, zx, params, flags)
+    got = np.fromfile(tmp_path / "tot.f64", np.float64)
+    np.testing.assert_allclose(got, tot, rtol=1e-12, atol=0)
+    assert res["best_idx"] == rep.best_idx
