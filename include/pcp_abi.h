@@ -79,6 +79,8 @@ enum pcp_kernel_id {
     PCP_K_VOXEL,             /* voxel keying + sort + centroid                       */
     PCP_K_TRANSFORM,         /* SE(3) + RGB + concat                                  */
     PCP_K_FILTER_MERGE,      /* whole crop->voxel->transform pipeline (graph replay)   */
+    PCP_K_EXCAVATE,          /* excavated-terrain carve: heights + pit test + compaction */
+    PCP_K_EXCAV_SETUP,       /* excavation-area normals + cell grid                    */
     PCP_K_COUNT
 };
 int pcp_profile_enable(pcp_ctx *ctx, int enable);
@@ -181,6 +183,39 @@ int pcp_set_cells(pcp_ctx *ctx, const double *xyz, const float *normals, uint64_
  * `area` is host memory (the PointCloud2 data blob). */
 int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
                             int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells);
+/* ---- excavated_surface_generator.cpp (ExcavationTerrainGenerator) ------------------------ */
+typedef struct pcp_excavation_params {   /* excavated_surface_generator.cpp:29-51 */
+    double depth;                 /* excavation.depth 1.0 */
+    double slope_angle_deg;       /* excavation.slope_angle 75.0 */
+    double offset_x, offset_y;    /* excavation.offset_x/_y 4.0, 1.0 (zx120 base frame) */
+    double point_density;         /* excavation.point_density 0.05 */
+    double terrain_search_radius; /* excavation.terrain_search_radius 0.5 */
+    int32_t l_shape_enabled;      /* excavation.l_shape_enabled 1 */
+    double arm1_length, arm1_width, arm2_length, arm2_width;   /* 2.0 1.2 2.0 1.2 */
+    double width, length;         /* rectangle mode 1.2, 1.8 */
+} pcp_excavation_params;
+
+/* matchedCloudCallback (:259-326) with excavation enabled and the zx120 TF present
+ * (zx120_base = map -> zx120/base_link).  in: /matched_point_cloud, host memory (x/y/z float
+ * fields; the rgb float at byte 16 when point_step >= 20, else 0).  Outputs are PointXYZRGB
+ * records (32 B: x, y, z, 1, rgb, 0, 0, 0) in host buffers:
+ *   terrain_out: /excavated_terrain = the input points processExcavation keeps (:451-485,
+ *                input order) then generateExcavatedSurface's bottom and wall points (:487-584)
+ *   area_out:    /excavation_area = generateExcavationArea (:350-455)
+ * Every getTerrainHeight (:183-226) runs on the GPU against one index of the input (the
+ * reference rebuilds a KD-tree per call, once per input point).  pose_out (nullable): the
+ * excavation centre x, y, its terrain height, yaw (publishExcavationMarkers).  *_cap in
+ * records; PCP_E_CAPACITY with *n_* set when short.  A missing TF is the caller's branch
+ * (:276-279: the input is republished unchanged). */
+int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_params *p,
+                 const pcp_rigid *zx120_base, void *terrain_out, uint64_t terrain_cap,
+                 uint64_t *n_terrain, void *area_out, uint64_t area_cap, uint64_t *n_area,
+                 double pose_out[4]);
+
+/* upper bounds of pcp_excavate's record counts for an n-point input (host arithmetic only) */
+int pcp_excavate_bounds(const pcp_excavation_params *p, uint64_t n_in, uint64_t *terrain_cap,
+                        uint64_t *area_cap);
+
 /* the context's scoring cells: xyz (n x 3 double) and normals (n x 3 float), either nullable;
  * *n_cells = count (PCP_E_CAPACITY when it exceeds cap). */
 int pcp_get_cells(pcp_ctx *ctx, double *xyz, float *normals, uint64_t cap, uint64_t *n_cells);

@@ -131,6 +131,27 @@ int64_t orc_excavation_grid(const float *pts, int64_t n, int64_t stride_floats,
                             const float *area_normals3, double *cells_xyz, float *cells_nrm,
                             int64_t cap, double grid_bbox[6], int32_t dims[3]);
 
+/* ---- excavated_surface_generator.cpp (pcp_oracle_setup.c) -------------------------------- */
+typedef struct orc_exc_params {
+    double depth, slope_angle_deg, offset_x, offset_y, point_density, terrain_search_radius;
+    int32_t l_shape_enabled;
+    double arm1_length, arm1_width, arm2_length, arm2_width, width, length;
+} orc_exc_params;
+
+/* getTerrainHeight (:183-226) over the cloud (FLANN radius search from (x, y, 0), 2-D filter,
+ * mean z in result order; else the nearest point's z; else 0) */
+double orc_terrain_height(const float *pts, int64_t n, int64_t stride_floats, double x, double y,
+                          double radius);
+
+/* matchedCloudCallback with the TF present (:259-326): zx120 base transform t, q (x,y,z,w).
+ * keep[i] = 1 for the input points processExcavation keeps (:451-485); surf = the points
+ * generateExcavatedSurface appends (:487-584), area = generateExcavationArea's cloud
+ * (:350-455), both as (x, y, z, rgb-float) rows; pose_out = centre x, y, terrain z, yaw. */
+void orc_excavate(const float *pts, int64_t n, int64_t stride_floats, const orc_exc_params *p,
+                  const double t[3], const double q[4], uint8_t *keep, float *surf,
+                  int64_t cap_surf, int64_t *n_surf, float *area, int64_t cap_area,
+                  int64_t *n_area, double pose_out[4]);
+
 #ifdef __cplusplus
 }
 #endif

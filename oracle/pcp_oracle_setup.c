@@ -267,3 +267,269 @@ int64_t orc_excavation_grid(const float *pts, int64_t n, int64_t stride_floats,
     free(nb);
     return nc;
 }
+
+/* ==========================================================================================
+ * excavated_surface_generator.cpp (ExcavationTerrainGenerator) -- the carve in front of the
+ * ray-trace.  getTerrainHeight (:183-226) here is a brute-force restatement of the KdTreeFLANN
+ * it rebuilds per call: 3-D radius search from (x, y, 0) with FLANN's float predicate (non-
+ * finite points are not in the tree), a 2-D distance filter in double, the mean z summed in
+ * the distance-sorted result order; else the nearest point's z (nearestKSearch k = 1: smallest
+ * float distance, lowest index on a tie); else 0.
+ * ========================================================================================== */
+double orc_terrain_height(const float *pts, int64_t n, int64_t stride_floats, double x, double y,
+                          double radius) {
+    if (n <= 0) return 0.0;
+    const float qx = (float)x, qy = (float)y, qz = 0.0f;
+    nb_t *nb = (nb_t *)malloc(sizeof(nb_t) * (size_t)n);
+    const float r2 = (float)(radius * radius);
+    int64_t m = 0, best = -1;
+    float bestd = INFINITY;
+    for (int64_t i = 0; i < n; ++i) {
+        const float *p = pts + i * stride_floats;
+        if (!(isfinite(p[0]) && isfinite(p[1]) && isfinite(p[2]))) continue;
+        const float d0 = qx - p[0], d1 = qy - p[1], d2 = qz - p[2];
+        float acc = 0.0f;
+        acc = acc + d0 * d0;
+        acc = acc + d1 * d1;
+        acc = acc + d2 * d2;
+        if (acc < r2) {
+            nb[m].d = acc;
+            nb[m].i = i;
+            ++m;
+        }
+        if (acc < bestd) {
+            bestd = acc;
+            best = i;
+        }
+    }
+    qsort(nb, (size_t)m, sizeof(nb_t), nb_cmp);
+    double sum_z = 0.0;
+    int valid = 0;
+    for (int64_t t = 0; t < m; ++t) {
+        const float *p = pts + nb[t].i * stride_floats;
+        const double dx = p[0] - x, dy = p[1] - y;
+        if (sqrt(dx * dx + dy * dy) <= radius) {
+            sum_z += p[2];
+            ++valid;
+        }
+    }
+    free(nb);
+    if (valid > 0) return sum_z / valid;
+    if (best >= 0) return pts[best * stride_floats + 2];
+    return 0.0;
+}
+
+typedef struct {
+    double cx, cy, len, wid, min_x, max_x, min_y, max_y;
+} exc_box;
+
+/* getExcavationBoxes (:138-181) */
+static int exc_boxes(const orc_exc_params *p, exc_box b[2]) {
+    if (p->l_shape_enabled) {
+        b[0].cx = 0.0;
+        b[0].cy = -p->arm1_length / 2.0;
+        b[0].len = p->arm1_width;
+        b[0].wid = p->arm1_length;
+        b[1].cx = p->arm2_length / 2.0;
+        b[1].cy = -p->arm1_length + p->arm2_width / 2.0;
+        b[1].len = p->arm2_length;
+        b[1].wid = p->arm2_width;
+        for (int k = 0; k < 2; ++k) {
+            b[k].min_x = b[k].cx - b[k].len / 2.0;
+            b[k].max_x = b[k].cx + b[k].len / 2.0;
+            b[k].min_y = b[k].cy - b[k].wid / 2.0;
+            b[k].max_y = b[k].cy + b[k].wid / 2.0;
+        }
+        return 2;
+    }
+    b[0].cx = 0.0;
+    b[0].cy = 0.0;
+    b[0].len = p->length;
+    b[0].wid = p->width;
+    b[0].min_x = -p->length / 2.0;
+    b[0].max_x = p->length / 2.0;
+    b[0].min_y = -p->width / 2.0;
+    b[0].max_y = p->width / 2.0;
+    return 1;
+}
+
+/* isInsideAnyBox (:229-237) */
+static int inside_any(double x, double y, const exc_box *b, int nb) {
+    for (int k = 0; k < nb; ++k)
+        if (x >= b[k].min_x && x <= b[k].max_x && y >= b[k].min_y && y <= b[k].max_y) return 1;
+    return 0;
+}
+
+/* isOuterEdge (:240-258) */
+static int outer_edge(double x, double y, const exc_box *b, int nb, double tol) {
+    if (!inside_any(x, y, b, nb)) return 0;
+    int out = 0;
+    if (!inside_any(x + tol, y, b, nb)) out = 1;
+    if (!inside_any(x - tol, y, b, nb)) out = 1;
+    if (!inside_any(x, y + tol, b, nb)) out = 1;
+    if (!inside_any(x, y - tol, b, nb)) out = 1;
+    return out;
+}
+
+/* isInsideExcavationArea (:328-348) */
+static int inside_exc(double xl, double yl, double zrel, const exc_box *b, int nb,
+                      const orc_exc_params *p, double slope_rad) {
+    if (zrel < -p->depth || zrel > 0) return 0;
+    const double slope_offset = p->depth / tan(slope_rad);
+    const double slope_factor = (p->depth + zrel) / p->depth;
+    const double cur = slope_offset * slope_factor;
+    for (int k = 0; k < nb; ++k) {
+        const double dx = xl - b[k].cx, dy = yl - b[k].cy;
+        const double hl = b[k].len / 2.0 + cur, hw = b[k].wid / 2.0 + cur;
+        if (fabs(dx) <= hl && fabs(dy) <= hw) return 1;
+    }
+    return 0;
+}
+
+/* PointXYZRGB rgb float of (r, g, b), alpha 255 */
+static float pack_rgb(unsigned r, unsigned g, unsigned b) {
+    const uint32_t v = b | (g << 8) | (r << 16) | (255u << 24);
+    float f;
+    memcpy(&f, &v, 4);
+    return f;
+}
+
+static void put4(float *o, int64_t i, int64_t cap, double x, double y, double z, float rgb) {
+    if (i >= cap) return;
+    o[4 * i + 0] = (float)x;
+    o[4 * i + 1] = (float)y;
+    o[4 * i + 2] = (float)z;
+    o[4 * i + 3] = rgb;
+}
+
+void orc_excavate(const float *pts, int64_t n, int64_t stride_floats, const orc_exc_params *p,
+                  const double t[3], const double q[4], uint8_t *keep, float *surf,
+                  int64_t cap_surf, int64_t *n_surf, float *area, int64_t cap_area,
+                  int64_t *n_area, double pose_out[4]) {
+    /* tf2::Matrix3x3::setRotation (quaternion x, y, z, w) and Transform * (ox, oy, 0) */
+    const double qx = q[0], qy = q[1], qz = q[2], qw = q[3];
+    const double d = qx * qx + qy * qy + qz * qz + qw * qw;
+    const double s = 2.0 / d;
+    const double xs = qx * s, ys = qy * s, zs = qz * s;
+    const double wx = qw * xs, wy = qw * ys, wz = qw * zs;
+    const double xx = qx * xs, xy = qx * ys, xz = qx * zs;
+    const double yy = qy * ys, yz = qy * zs, zz = qz * zs;
+    const double m[3][3] = {{1.0 - (yy + zz), xy - wz, xz + wy},
+                            {xy + wz, 1.0 - (xx + zz), yz - wx},
+                            {xz - wy, yz + wx, 1.0 - (xx + yy)}};
+    const double ox = p->offset_x, oy = p->offset_y, oz = 0.0;
+    const double cx = (m[0][0] * ox + m[0][1] * oy + m[0][2] * oz) + t[0];
+    const double cy = (m[1][0] * ox + m[1][1] * oy + m[1][2] * oz) + t[1];
+    const double r = p->terrain_search_radius;
+    const double cz = orc_terrain_height(pts, n, stride_floats, cx, cy, r);
+    /* Matrix3x3::getRPY -> getEulerYPR, solution 1 */
+    double yaw;
+    if (fabs(m[2][0]) >= 1) {
+        yaw = 0.0;
+    } else {
+        const double pitch = -asin(m[2][0]);
+        yaw = atan2(m[1][0] / cos(pitch), m[0][0] / cos(pitch));
+    }
+    if (pose_out) {
+        pose_out[0] = cx;
+        pose_out[1] = cy;
+        pose_out[2] = cz;
+        pose_out[3] = yaw;
+    }
+    exc_box b[2];
+    const int nb = exc_boxes(p, b);
+    const double slope_rad = p->slope_angle_deg * M_PI / 180.0;
+    const double slope_offset = p->depth / tan(slope_rad);
+    /* processExcavation (:451-485): points provably outside every widened box keep without a
+     * terrain-height query (inside needs |dx| <= half + offset with offset <= slope_offset) */
+    const double cyw = cos(-yaw), syw = sin(-yaw);
+    for (int64_t i = 0; i < n; ++i) {
+        const float *pt = pts + i * stride_floats;
+        const double dx = pt[0] - cx, dy = pt[1] - cy;
+        const double xl = dx * cyw - dy * syw;
+        const double yl = dx * syw + dy * cyw;
+        int maybe = 0;
+        for (int k = 0; k < nb; ++k)
+            if (fabs(xl - b[k].cx) <= b[k].len / 2.0 + slope_offset &&
+                fabs(yl - b[k].cy) <= b[k].wid / 2.0 + slope_offset)
+                maybe = 1;
+        int inside = 0;
+        if (maybe) {
+            const double h = orc_terrain_height(pts, n, stride_floats, pt[0], pt[1], r);
+            inside = inside_exc(xl, yl, pt[2] - h, b, nb, p, slope_rad);
+        }
+        keep[i] = inside ? 0 : 1;
+    }
+    double mnx = DBL_MAX, mxx = -DBL_MAX, mny = DBL_MAX, mxy = -DBL_MAX;
+    for (int k = 0; k < nb; ++k) {
+        mnx = fmin(mnx, b[k].min_x);
+        mxx = fmax(mxx, b[k].max_x);
+        mny = fmin(mny, b[k].min_y);
+        mxy = fmax(mxy, b[k].max_y);
+    }
+    const double dens = p->point_density;
+    const int n_x = (int)((mxx - mnx) / dens) + 1;
+    const int n_y = (int)((mxy - mny) / dens) + 1;
+    const double cyaw = cos(yaw), syaw = sin(yaw);
+    /* generateExcavatedSurface (:487-584): bottom, then the outer-wall slopes */
+    int64_t ns = 0;
+    const float rgb_bottom = pack_rgb(0, 139, 0), rgb_slope = pack_rgb(144, 238, 144);
+    for (int i = 0; i <= n_x; ++i)
+        for (int j = 0; j <= n_y; ++j) {
+            const double xl = mnx + i * dens, yl = mny + j * dens;
+            if (!inside_any(xl, yl, b, nb)) continue;
+            const double xg = cx + xl * cyaw - yl * syaw;
+            const double yg = cy + xl * syaw + yl * cyaw;
+            const double h = orc_terrain_height(pts, n, stride_floats, xg, yg, r);
+            put4(surf, ns++, cap_surf, xg, yg, h - p->depth, rgb_bottom);
+        }
+    const int n_slope = (int)(slope_offset / dens) + 1;
+    for (int i = 0; i <= n_x; ++i)
+        for (int j = 0; j <= n_y; ++j) {
+            const double xl = mnx + i * dens, yl = mny + j * dens;
+            if (!outer_edge(xl, yl, b, nb, dens)) continue;
+            for (int k = 0; k <= n_slope; ++k) {
+                const double z_ratio = (double)k / n_slope;
+                const double off = slope_offset * z_ratio;
+                double ofx = 0.0, ofy = 0.0;
+                if (!inside_any(xl + dens, yl, b, nb)) ofx = off;
+                else if (!inside_any(xl - dens, yl, b, nb)) ofx = -off;
+                if (!inside_any(xl, yl + dens, b, nb)) ofy = off;
+                else if (!inside_any(xl, yl - dens, b, nb)) ofy = -off;
+                const double xs2 = xl + ofx, ys2 = yl + ofy;
+                const double xg = cx + xs2 * cyaw - ys2 * syaw;
+                const double yg = cy + xs2 * syaw + ys2 * cyaw;
+                const double h = orc_terrain_height(pts, n, stride_floats, xg, yg, r);
+                put4(surf, ns++, cap_surf, xg, yg, h - p->depth * (1.0 - z_ratio), rgb_slope);
+            }
+        }
+    *n_surf = ns;
+    /* generateExcavationArea (:350-455) */
+    int64_t na = 0;
+    const int n_depth = (int)(p->depth / dens);
+    const float rgb_abot = pack_rgb(255, 255, 0), rgb_aslope = pack_rgb(200, 200, 0);
+    for (int i = 0; i <= n_x; ++i)
+        for (int j = 0; j <= n_y; ++j) {
+            const double xl = mnx + i * dens, yl = mny + j * dens;
+            if (!inside_any(xl, yl, b, nb)) continue;
+            const double xg = cx + xl * cyaw - yl * syaw;
+            const double yg = cy + xl * syaw + yl * cyaw;
+            const double h = orc_terrain_height(pts, n, stride_floats, xg, yg, r);
+            put4(area, na++, cap_area, xg, yg, h - p->depth, rgb_abot);
+            if (!outer_edge(xl, yl, b, nb, dens)) continue;
+            for (int k = 1; k < n_depth; ++k) {
+                const double z_ratio = (double)k / n_depth;
+                const double off = slope_offset * z_ratio;
+                double ofx = 0.0, ofy = 0.0;
+                if (!inside_any(xl + dens, yl, b, nb)) ofx = off;
+                else if (!inside_any(xl - dens, yl, b, nb)) ofx = -off;
+                if (!inside_any(xl, yl + dens, b, nb)) ofy = off;
+                else if (!inside_any(xl, yl - dens, b, nb)) ofy = -off;
+                const double xs2 = xl + ofx, ys2 = yl + ofy;
+                const double xg2 = cx + xs2 * cyaw - ys2 * syaw;
+                const double yg2 = cy + xs2 * syaw + ys2 * cyaw;
+                put4(area, na++, cap_area, xg2, yg2, h - p->depth + k * dens, rgb_aslope);
+            }
+        }
+    *n_area = na;
+}

@@ -57,6 +57,10 @@ _SIGS = [
                                C.c_double, _P, _P, _P]),
     ("orc_fan_tables", None, [C.c_int32, C.c_int32, C.c_double, C.c_double, _P, _P, _P, _P]),
     ("orc_area_normals", None, [_P, C.c_int64, C.c_int64, C.c_double, _P]),
+    ("orc_terrain_height", C.c_double, [_P, C.c_int64, C.c_int64, C.c_double, C.c_double,
+                                        C.c_double]),
+    ("orc_excavate", None, [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P,
+                            C.c_int64, _P, _P]),
     ("orc_excavation_grid", C.c_int64, [_P, C.c_int64, C.c_int64, C.c_double, C.c_int32, _P, _P,
                                         _P, C.c_int64, _P, _P]),
 ]
@@ -226,3 +230,45 @@ def excavation_grid(pts, grid_resolution=0.1, vertical_layers=10, normals=None):
                               int(vertical_layers), _p(nrm), _p(xyz), _p(cn), n, _p(bbox),
                               _p(dims))
     return xyz[:n], cn[:n], bbox, tuple(int(d) for d in dims)
+
+
+class ExcParams(C.Structure):
+    _fields_ = [("depth", C.c_double), ("slope_angle_deg", C.c_double),
+                ("offset_x", C.c_double), ("offset_y", C.c_double),
+                ("point_density", C.c_double), ("terrain_search_radius", C.c_double),
+                ("l_shape_enabled", C.c_int32), ("arm1_length", C.c_double),
+                ("arm1_width", C.c_double), ("arm2_length", C.c_double),
+                ("arm2_width", C.c_double), ("width", C.c_double), ("length", C.c_double)]
+
+
+def exc_params(**kw):
+    """excavated_surface_generator.cpp:29-51 defaults."""
+    p = ExcParams(1.0, 75.0, 4.0, 1.0, 0.05, 0.5, 1, 2.0, 1.2, 2.0, 1.2, 1.2, 1.8)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def terrain_height(pts, x, y, radius=0.5):
+    a = _f32(pts)
+    return lib().orc_terrain_height(_p(a), a.shape[0], a.shape[1], float(x), float(y),
+                                    float(radius))
+
+
+def excavate(pts, t, q, params=None):
+    """-> keep (N,) bool, surf (S, 4) f32 rows x,y,z,rgb, area (A, 4), pose (cx, cy, cz, yaw)."""
+    a = _f32(pts)
+    p = params or exc_params()
+    t = np.ascontiguousarray(t, np.float64)
+    q = np.ascontiguousarray(q, np.float64)
+    keep = np.empty(max(a.shape[0], 1), np.uint8)
+    ns, na = C.c_int64(), C.c_int64()
+    pose = np.zeros(4, np.float64)
+    lib().orc_excavate(_p(a), a.shape[0], a.shape[1], C.byref(p), _p(t), _p(q), _p(keep), None,
+                       0, C.byref(ns), None, 0, C.byref(na), _p(pose))
+    surf = np.empty((max(ns.value, 1), 4), np.float32)
+    area = np.empty((max(na.value, 1), 4), np.float32)
+    lib().orc_excavate(_p(a), a.shape[0], a.shape[1], C.byref(p), _p(t), _p(q), _p(keep),
+                       _p(surf), ns.value, C.byref(ns), _p(area), na.value, C.byref(na),
+                       _p(pose))
+    return keep[:a.shape[0]].astype(bool), surf[:ns.value], area[:na.value], pose

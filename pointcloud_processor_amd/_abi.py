@@ -28,7 +28,8 @@ PCP_MEM_DEVICE_OUT = 2
 F_RANGE_Z, F_FOV_Z, F_VIS_Z, F_RANGE_M, F_FOV_M, F_VIS_M = 1, 2, 4, 8, 16, 32
 
 KERNELS = ["raycast_fan", "score_cells", "zx120_cells", "pose_sum", "cell_flags",
-           "candidates", "index_build", "crop", "voxel", "transform", "filter_merge"]
+           "candidates", "index_build", "crop", "voxel", "transform", "filter_merge", "excavate",
+           "excav_setup"]
 
 
 class PcpError(RuntimeError):
@@ -111,6 +112,8 @@ _SIGS = [
     ("pcp_set_excavation_area", C.c_int, [_P, _P, C.c_double, C.c_int32, _P, _P]),
     ("pcp_get_cells", C.c_int, [_P, _P, _P, C.c_uint64, _P]),
     ("pcp_get_area_normals", C.c_int, [_P, _P, C.c_uint64, _P]),
+    ("pcp_excavate", C.c_int, [_P, _P, _P, _P, _P, C.c_uint64, _P, _P, C.c_uint64, _P, _P]),
+    ("pcp_excavate_bounds", C.c_int, [_P, C.c_uint64, _P, _P]),
     ("pcp_generate_candidates", C.c_int, [_P, _P, C.POINTER(VlParams), _P, _P, C.c_uint64,
                                           C.POINTER(C.c_uint64)]),
     ("pcp_score_poses", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams), _P, _P, _P,
@@ -163,6 +166,23 @@ def cloud_view(arr: np.ndarray, point_step: int | None = None, offs=(0, 4, 8)) -
             raise ValueError("pass point_step for non (N,k) float32 clouds")
         point_step = arr.shape[1] * 4
     return CloudView(arr.ctypes.data if n else None, n, point_step, *offs)
+
+
+class ExcavationParams(C.Structure):
+    """pcp_excavation_params (excavated_surface_generator.cpp:29-51 defaults)."""
+    _fields_ = [("depth", C.c_double), ("slope_angle_deg", C.c_double),
+                ("offset_x", C.c_double), ("offset_y", C.c_double),
+                ("point_density", C.c_double), ("terrain_search_radius", C.c_double),
+                ("l_shape_enabled", C.c_int32), ("arm1_length", C.c_double),
+                ("arm1_width", C.c_double), ("arm2_length", C.c_double),
+                ("arm2_width", C.c_double), ("width", C.c_double), ("length", C.c_double)]
+
+
+def excavation_params(**kw) -> ExcavationParams:
+    p = ExcavationParams(1.0, 75.0, 4.0, 1.0, 0.05, 0.5, 1, 2.0, 1.2, 2.0, 1.2, 1.2, 1.8)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
 
 
 class Context:
@@ -373,6 +393,25 @@ class Context:
         self._check(self.lib.pcp_get_area_normals(self.h, _ptr(out), n.value, C.byref(n)),
                     "pcp_get_area_normals")
         return out
+
+    def excavate(self, cloud: np.ndarray, zx120_tf, params: ExcavationParams | None = None,
+                 point_step=None, offs=(0, 4, 8)):
+        """matchedCloudCallback: -> (excavated_terrain (N, 8) f32 PointXYZRGB records,
+        excavation_area (M, 8) f32, pose (cx, cy, cz, yaw))."""
+        v = cloud_view(cloud, point_step, offs)
+        p = params or excavation_params()
+        tf = Rigid((C.c_double * 3)(*zx120_tf[0]), (C.c_double * 4)(*zx120_tf[1]))
+        nt, na = C.c_uint64(), C.c_uint64()
+        pose = np.zeros(4, np.float64)
+        self._check(self.lib.pcp_excavate_bounds(C.byref(p), v.n, C.byref(nt), C.byref(na)),
+                    "pcp_excavate_bounds")
+        terr = np.empty((max(nt.value, 1), 8), np.float32)
+        area = np.empty((max(na.value, 1), 8), np.float32)
+        self._check(self.lib.pcp_excavate(self.h, C.byref(v), C.byref(p), C.byref(tf),
+                                          _ptr(terr), terr.shape[0], C.byref(nt), _ptr(area),
+                                          area.shape[0], C.byref(na), _ptr(pose)),
+                    "pcp_excavate")
+        return terr[:nt.value], area[:na.value], pose
 
     def terrain_info(self) -> dict:
         info = IndexInfo()

@@ -269,4 +269,49 @@ SimplifiedDualLidarOptimizer::Result SimplifiedDualLidarOptimizer::runOptimizati
     return r;
 }
 
+// ---- ExcavationTerrainGenerator ----------------------------------------------------------------
+ExcavationTerrainGenerator::Output ExcavationTerrainGenerator::matchedCloudCallback(
+    const PointCloud2 &msg, const Transform *zx120_base) {
+    Output o;
+    err_.clear();
+    if (!p_.enabled || !zx120_base) {   // :260-263, :276-279: republish the input
+        o.excavated_terrain = msg;
+        return o;
+    }
+    pcp_cloud_view v;
+    std::string why;
+    if (!cloud_view(msg, v, &why)) {
+        err_ = "excavated_surface_generator: " + why;
+        o.excavated_terrain = msg;
+        return o;
+    }
+    pcp_rigid tf;
+    for (int a = 0; a < 3; ++a) tf.t[a] = zx120_base->t[a];
+    for (int a = 0; a < 4; ++a) tf.q[a] = zx120_base->q[a];
+    uint64_t nt = 0, na = 0;
+    double pose[4];
+    if (pcp_excavate_bounds(&p_, v.n, &nt, &na) != PCP_OK) {
+        err_ = "excavated_surface_generator: bad parameters";
+        o.excavated_terrain = msg;
+        return o;
+    }
+    std::vector<uint8_t> terr(nt * 32), area(na * 32);
+    if (pcp_excavate(dev_.ctx(), &v, &p_, &tf, terr.data(), nt, &nt, area.data(), na, &na, pose) !=
+        PCP_OK) {
+        err_ = dev_.error();
+        o.excavated_terrain = msg;
+        return o;
+    }
+    o.excavated_terrain = make_xyzrgb_cloud(terr.data(), nt, "map");   // header kept, frame map
+    o.excavated_terrain.stamp = msg.stamp;
+    o.excavation_area = make_xyzrgb_cloud(area.data(), na, "map");
+    o.excavation_area.stamp = msg.stamp;
+    o.area_published = true;
+    o.center[0] = pose[0];
+    o.center[1] = pose[1];
+    o.center[2] = pose[2];
+    o.yaw = pose[3];
+    return o;
+}
+
 }  // namespace pcp

@@ -108,6 +108,34 @@ class GnssGicpMatcher {
     std::string err_;
 };
 
+// ---- excavated_surface_generator.cpp (ExcavationTerrainGenerator) --------------------------
+class ExcavationTerrainGenerator {
+   public:
+    struct Params : pcp_excavation_params {   // :29-51 defaults, excavation.enabled
+        bool enabled = true;
+        Params() : pcp_excavation_params{1.0, 75.0, 4.0, 1.0, 0.05, 0.5, 1, 2.0, 1.2, 2.0, 1.2,
+                                         1.2, 1.8} {}
+    };
+    struct Output {
+        PointCloud2 excavated_terrain;   // /excavated_terrain (frame map)
+        PointCloud2 excavation_area;     // /excavation_area (frame map); empty: not published
+        bool area_published = false;
+        double center[3] = {0, 0, 0}, yaw = 0;   // publishExcavationMarkers pose
+    };
+    explicit ExcavationTerrainGenerator(Device &dev) : dev_(dev) {}
+    ExcavationTerrainGenerator(Device &dev, const Params &p) : dev_(dev), p_(p) {}
+    Params &params() { return p_; }
+    // matchedCloudCallback (:259-326); zx120_base = TF map -> zx120/base_link, nullptr = the
+    // lookup threw: the input is republished unchanged (as when disabled, :260-263, :276-279)
+    Output matchedCloudCallback(const PointCloud2 &msg, const Transform *zx120_base);
+    const std::string &lastError() const { return err_; }
+
+   private:
+    Device &dev_;
+    Params p_;
+    std::string err_;
+};
+
 // ---- virtual_lidar.cpp (SimplifiedDualLidarOptimizer) --------------------------------------
 class SimplifiedDualLidarOptimizer {
    public:
@@ -144,6 +172,7 @@ class SimplifiedDualLidarOptimizer {
     // runOptimization (:454-548); zx120_base = TF map -> zx120/base_link, nullptr = missing
     Result runOptimization(const Transform *zx120_base);
     const std::vector<uint8_t> &cellFlags() const { return flags_; }
+    size_t lastCells() const { return n_cells_; }
     const std::string &lastError() const { return err_; }
 
    private:

@@ -184,8 +184,13 @@ static int cmd_replay(Device &dev, char **a) {
     const auto bbox = tuple(a[5]);
     const int frames = std::atoi(a[6]);
     const size_t npts = std::strtoull(a[7], nullptr, 10);
+    // chain = 1: the launch file's whole per-frame chain -- the merged cloud goes through
+    // excavated_surface_generator, whose /excavated_terrain and /excavation_area feed
+    // virtual_lidar every frame (terrain index, normals, cell grid rebuilt per frame)
+    const bool chain = a[8] && std::atoi(a[8]) != 0;
     SimplifiedScanMatcher filt(dev);
     GnssGicpMatcher merger(dev);
+    ExcavationTerrainGenerator gen(dev);
     SimplifiedDualLidarOptimizer vl(dev);
     vl.terrainCallback(cloud_from(t, tn, 32, "map"));
     std::vector<double> xyz(cn * 3);
@@ -198,7 +203,7 @@ static int cmd_replay(Device &dev, char **a) {
     const Transform zx_tf{{0.55, 0.4, 3.5}, {0.0, 0.21633, 0.0, 0.97632}};
     const Transform zx_base{{0.0, 0.0, 0.0}, {0, 0, 0, 1}};
     std::vector<double> lat;
-    size_t merged_n = 0, best = 0;
+    size_t merged_n = 0, best = 0, cells_n = cn;
     for (int f = 0; f < frames + 2; ++f) {
         auto rs = synth_scan(npts, 2.0, rng), zs = synth_scan(npts, 3.5, rng);
         PointCloud2 rm = make_xyz_cloud(rs.data(), npts, "four_wheel_robot/velodyne_link");
@@ -210,6 +215,16 @@ static int cmd_replay(Device &dev, char **a) {
         merger.robotCloudCallback(rf);
         merger.backhoeCloudCallback(zf);
         auto o = merger.processPointClouds(true, &robot_tf, &zx_tf);
+        if (chain) {
+            auto e = gen.matchedCloudCallback(o.merged, &zx_base);
+            if (!e.area_published) {
+                std::fprintf(stderr, "replay: carve failed: %s\n", gen.lastError().c_str());
+                return 1;
+            }
+            vl.excavationAreaCallback(e.excavation_area);
+            vl.terrainCallback(e.excavated_terrain);
+            cells_n = vl.lastCells();
+        }
         vl.zx120PointsCallback(zf);
         auto r = vl.runOptimization(&zx_base);
         const auto t1 = std::chrono::steady_clock::now();
@@ -223,9 +238,11 @@ static int cmd_replay(Device &dev, char **a) {
     }
     std::sort(lat.begin(), lat.end());
     auto q = [&lat](double p) { return lat[std::min(lat.size() - 1, (size_t)(p * lat.size()))]; };
-    std::printf("{\"frames\": %zu, \"points_per_scan\": %zu, \"p50_ms\": %.4f, \"p99_ms\": %.4f, "
-                "\"max_ms\": %.4f, \"merged_points\": %zu, \"best_idx\": %zu}\n",
-                lat.size(), npts, q(0.5), q(0.99), lat.back(), merged_n, best);
+    std::printf("{\"frames\": %zu, \"points_per_scan\": %zu, \"chain\": %d, \"p50_ms\": %.4f, "
+                "\"p99_ms\": %.4f, \"max_ms\": %.4f, \"merged_points\": %zu, \"cells\": %zu, "
+                "\"best_idx\": %zu}\n",
+                lat.size(), npts, chain ? 1 : 0, q(0.5), q(0.99), lat.back(), merged_n, cells_n,
+                best);
     return 0;
 }
 

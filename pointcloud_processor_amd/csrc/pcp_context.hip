@@ -272,6 +272,8 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->exc_norm.release();
     ctx->exc_near.release();
     ctx->area_nrm.release();
+    ctx->carve.release();
+    ctx->carve_buf.release();
     DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage, &ctx->fan_tab,
                       &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,
                       &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->f_in,
@@ -348,7 +350,8 @@ const char *pcp_kernel_name(int kid) {
     static const char *names[PCP_K_COUNT] = {"raycast_fan", "score_cells", "zx120_cells",
                                              "pose_sum",    "cell_flags",  "candidates",
                                              "index_build", "crop",        "voxel",
-                                             "transform",   "filter_merge"};
+                                             "transform",   "filter_merge", "excavate",
+                                             "excav_setup"};
     if (kid < 0 || kid >= PCP_K_COUNT) return "unknown";
     return names[kid];
 }

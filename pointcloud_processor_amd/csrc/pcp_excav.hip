@@ -375,6 +375,7 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     if (n_cells) *n_cells = ctx->n_cells;
     if (area->n == 0) return PCP_OK;   // :168, nothing is rebuilt; the previous cells stay
+    ProfScope prof(ctx, PCP_K_EXCAV_SETUP);
     const double r_near = grid_resolution * 1.5;
     if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius))) return rc;
     if ((rc = build_index(ctx, ctx->exc_near, *area, r_near))) return rc;

@@ -146,6 +146,9 @@ struct pcp_ctx {
     pcp::GridIndex exc_norm, exc_near;
     pcp::DevBuf area_nrm;
     uint64_t area_n = 0;
+    // excavated-terrain carve (pcp_excavate): index of the input cloud + scratch
+    pcp::GridIndex carve;
+    pcp::DevBuf carve_buf;
     // scratch
     pcp::DevBuf stage, scratch[8];
     pcp::DevBuf fan_tab, poses_d, steps_d, out_a, out_b, out_c, out_d, stats_d;

@@ -6,6 +6,7 @@ xyz exact (same float evaluation order); scores (double, through ocml acos/sin v
 a relative 1e-12 per pose; candidate pitch/yaw (atan2) within 1e-12 rad.
 All calls go through the C ABI (pointcloud_processor_amd/_abi.py -> libpcp.so).
 """
+import ctypes
 import math
 from pathlib import Path
 
@@ -18,6 +19,7 @@ pytestmark = pytest.mark.gpu
 
 BOX = np.array([0.0, 15.0, -10.0, 10.0, -1.5, 10.0])   # pointcloud_filter.cpp:30-36,111-113
 GOLD = Path(__file__).resolve().parent / "golden"
+C_u64, C_ref = ctypes.c_uint64, ctypes.byref
 
 
 def _cloud(n, seed, step_floats=4, nan_frac=0.01):
@@ -371,3 +373,53 @@ def test_excavation_area_setup(oracle, scene):
         assert n2 == n and np.array_equal(ctx.get_cells()[0], xyz)
     finally:
         ctx.close()
+
+
+# ---------------------------------------------------------------- excavated-terrain carve
+def _matched_cloud(seed=3):
+    """A /matched_point_cloud stand-in: a noisy 0.05 m lattice (PointXYZRGB, 32 B), a raised
+    block over the pit, a hole with a few points 0.8 m up (nearest-point fallbacks), NaNs."""
+    rng = np.random.default_rng(seed)
+    xs, ys = np.arange(-2.0, 9.0, 0.05), np.arange(-3.0, 6.0, 0.05)
+    X, Y = np.meshgrid(xs, ys)
+    P = np.stack([X.ravel(), Y.ravel(), rng.normal(0, 0.01, X.size)], 1)
+    hole = np.hypot(P[:, 0] - 5.0, P[:, 1] - 0.0) < 0.8
+    P = P[~hole]
+    block = np.stack(np.meshgrid(np.arange(4.0, 4.6, 0.05), np.arange(1.0, 1.6, 0.05),
+                                 np.array([0.3, 1.5])), -1).reshape(-1, 3)
+    lifted = np.array([[5.0, 0.0, 0.8], [5.1, 0.2, 0.8], [4.8, -0.3, 0.85]])
+    P = np.concatenate([P, block, lifted])
+    c = np.zeros((P.shape[0], 8), np.float32)
+    c[:, :3] = P
+    c[:, 4] = np.frombuffer(np.full(P.shape[0], 0xFF00FF00, np.uint32).tobytes(), np.float32)
+    c[rng.integers(0, P.shape[0], 20), 0] = np.nan
+    return c
+
+
+def test_excavate_matches_oracle(gpu, oracle):
+    """pcp_excavate against the CPU restatement: kept points (order, bytes), the generated
+    excavated surface and /excavation_area records, and the marker pose, all bit-exact."""
+    c = _matched_cloud()
+    yaw = math.radians(20.0)
+    t, q = (0.3, -0.2, 0.1), (0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2))
+    terr, area, pose = gpu.excavate(c, (t, q))
+    keep, surf, r_area, r_pose = oracle.excavate(c, t, q)
+    np.testing.assert_array_equal(pose, r_pose)
+    nk = int(keep.sum())
+    assert 0 < nk < c.shape[0] and terr.shape[0] == nk + surf.shape[0]
+    kept = c[keep]
+    np.testing.assert_array_equal(terr[:nk, :3].view(np.uint32), kept[:, :3].view(np.uint32))
+    np.testing.assert_array_equal(terr[:nk, 4].view(np.uint32), kept[:, 4].view(np.uint32))
+    np.testing.assert_array_equal(terr[nk:, [0, 1, 2, 4]].view(np.uint32), surf.view(np.uint32))
+    np.testing.assert_array_equal(area[:, [0, 1, 2, 4]].view(np.uint32), r_area.view(np.uint32))
+
+
+def test_excavate_bounds_hold(gpu):
+    """pcp_excavate_bounds caps every output the carve can produce (rectangle and L modes)."""
+    c = _matched_cloud(5)
+    for kw in ({}, {"l_shape_enabled": 0}, {"point_density": 0.1, "depth": 0.5}):
+        p = _abi.excavation_params(**kw)
+        terr, area, _ = gpu.excavate(c, ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0)), p)
+        nt, na = C_u64(), C_u64()
+        assert gpu.lib.pcp_excavate_bounds(C_ref(p), c.shape[0], C_ref(nt), C_ref(na)) == 0
+        assert terr.shape[0] <= nt.value and area.shape[0] <= na.value

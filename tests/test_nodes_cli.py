@@ -127,3 +127,17 @@ def test_excavation_area_node(tmp_path, oracle, small_scene):
     got = np.fromfile(tmp_path / "tot.f64", np.float64)
     np.testing.assert_allclose(got, tot, rtol=1e-12, atol=0)
     assert res["best_idx"] == rep.best_idx
+
+
+def test_streaming_replay_full_chain(tmp_path, scene, cells):
+    """C5 with the launch file's whole chain per frame: filter x2 -> merge ->
+    excavated_surface_generator (/excavated_terrain, /excavation_area) -> virtual_lidar
+    (terrain index, normals + cell grid, pose search)."""
+    np.ascontiguousarray(scene.terrain).tofile(tmp_path / "t.f32")
+    np.ascontiguousarray(cells.xyz).tofile(tmp_path / "c.f64")
+    np.ascontiguousarray(cells.normals).tofile(tmp_path / "n.f32")
+    res = _run("replay", tmp_path / "t.f32", scene.terrain.shape[0], tmp_path / "c.f64",
+               tmp_path / "n.f32", cells.xyz.shape[0], _t(cells.grid_bbox), 6, 60032, 1)
+    assert res["frames"] == 6 and res["chain"] == 1
+    assert res["cells"] > 0 and res["merged_points"] > 0 and res["best_idx"] >= 0
+    assert 0 < res["p50_ms"] <= res["p99_ms"]
