@@ -43,25 +43,6 @@ __device__ __forceinline__ bool stencil_ranges(const GridView &g, float qx, floa
     return true;
 }
 
-template <int N>
-__device__ __forceinline__ void block_sum_d(double (&v)[N], double (*lds)[kXT / 64]) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int a = 0; a < N; ++a)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v[a] += __shfl_xor(v[a], o, 64);
-    if (lane == 0)
-#pragma unroll
-        for (int a = 0; a < N; ++a) lds[a][wid] = v[a];
-    __syncthreads();
-#pragma unroll
-    for (int a = 0; a < N; ++a) {
-        double t = 0.0;
-        for (int w = 0; w < kXT / 64; ++w) t += lds[a][w];
-        v[a] = t;
-    }
-}
-
 // ---- pcl::eigen33, smallest eigenvalue's eigenvector (float, as PCL's Scalar) ---------------
 __device__ __forceinline__ void roots2(float b, float c, float r[3]) {
     r[0] = 0.0f;
@@ -147,13 +128,33 @@ __device__ __forceinline__ void eigen33_min(const float cov[3][3], float ev[3]) 
     for (int a = 0; a < 3; ++a) ev[a] = v[a] / s;
 }
 
-// computeTerrainNormals: block per point (sorted index order; .w = input index)
+// double-double accumulation (TwoSum): exact sums of these float addends
+struct DD {
+    double hi, lo;
+};
+__device__ __forceinline__ void dd_add(DD &a, double x) {
+    const double s = a.hi + x;
+    const double bb = s - a.hi;
+    const double err = (a.hi - (s - bb)) + (x - bb);
+    a.hi = s;
+    a.lo += err;
+}
+__device__ __forceinline__ DD dd_merge(DD a, DD b) {
+    dd_add(a, b.hi);
+    a.lo += b.lo;
+    return a;
+}
+
+// computeTerrainNormals: block per point (sorted index order; .w = input index).  The
+// second moments are double-double sums of exact float x float products: the exact sum for
+// these magnitudes, so the result does not depend on the (atomic) order of points in a cell.
 __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, float *__restrict__ out) {
     const uint32_t qi = blockIdx.x;
     const float4 q = g.pts[qi];
     const uint32_t orig = __float_as_uint(q.w);
     uint32_t lo[4], hi[4];
-    double acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // xx xy xz yy yz zz x y z count
+    DD acc[10];   // xx xy xz yy yz zz x y z count
+    for (int a = 0; a < 10; ++a) acc[a] = DD{0.0, 0.0};
     if (stencil_ranges(g, q.x, q.y, q.z, lo, hi)) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -163,34 +164,51 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
                 // shifted by K = the first (nearest) neighbour = the query point itself
                 const double x = (double)(p.x - q.x), y = (double)(p.y - q.y),
                              z = (double)(p.z - q.z);
-                acc[0] += x * x;
-                acc[1] += x * y;
-                acc[2] += x * z;
-                acc[3] += y * y;
-                acc[4] += y * z;
-                acc[5] += z * z;
-                acc[6] += x;
-                acc[7] += y;
-                acc[8] += z;
-                acc[9] += 1.0;
+                dd_add(acc[0], x * x);
+                dd_add(acc[1], x * y);
+                dd_add(acc[2], x * z);
+                dd_add(acc[3], y * y);
+                dd_add(acc[4], y * z);
+                dd_add(acc[5], z * z);
+                dd_add(acc[6], x);
+                dd_add(acc[7], y);
+                dd_add(acc[8], z);
+                acc[9].hi += 1.0;
             }
     }
-    __shared__ double lds[10][kXT / 64];
-    block_sum_d(acc, lds);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int a = 0; a < 10; ++a) {
+            const DD t{__shfl_xor(acc[a].hi, o, 64), __shfl_xor(acc[a].lo, o, 64)};
+            acc[a] = dd_merge(acc[a], t);
+        }
+    __shared__ DD lds[10][kXT / 64];
+    if (lane == 0)
+        for (int a = 0; a < 10; ++a) lds[a][wid] = acc[a];
+    __syncthreads();
     if (threadIdx.x != 0) return;
+    double v[10];
+    for (int a = 0; a < 10; ++a) {
+        DD t = lds[a][0];
+        for (int w = 1; w < kXT / 64; ++w) t = dd_merge(t, lds[a][w]);
+        v[a] = t.hi + t.lo;
+    }
     float *o = out + 3 * (size_t)orig;
-    if (acc[9] < 3.0) {   // computePointNormal: < 3 neighbours -> NaN
+    if (v[9] < 3.0) {   // computePointNormal: < 3 neighbours -> NaN
         o[0] = o[1] = o[2] = NAN;
         return;
     }
-    for (int a = 0; a < 9; ++a) acc[a] /= acc[9];
+    double acc2[9];
+    for (int a = 0; a < 9; ++a) acc2[a] = v[a] / v[9];
     float cov[3][3];
-    cov[0][0] = (float)(acc[0] - acc[6] * acc[6]);
-    cov[0][1] = (float)(acc[1] - acc[6] * acc[7]);
-    cov[0][2] = (float)(acc[2] - acc[6] * acc[8]);
-    cov[1][1] = (float)(acc[3] - acc[7] * acc[7]);
-    cov[1][2] = (float)(acc[4] - acc[7] * acc[8]);
-    cov[2][2] = (float)(acc[5] - acc[8] * acc[8]);
+    cov[0][0] = (float)(acc2[0] - acc2[6] * acc2[6]);
+    cov[0][1] = (float)(acc2[1] - acc2[6] * acc2[7]);
+    cov[0][2] = (float)(acc2[2] - acc2[6] * acc2[8]);
+    cov[1][1] = (float)(acc2[3] - acc2[7] * acc2[7]);
+    cov[1][2] = (float)(acc2[4] - acc2[7] * acc2[8]);
+    cov[2][2] = (float)(acc2[5] - acc2[8] * acc2[8]);
     cov[1][0] = cov[0][1];
     cov[2][0] = cov[0][2];
     cov[2][1] = cov[1][2];
@@ -278,23 +296,6 @@ k_lattice_compact(const uint8_t *__restrict__ flags, Lattice L, double *__restri
     if (threadIdx.x == 0) *n_out = run;
 }
 
-// double-double accumulation (TwoSum): exact sums of these float addends
-struct DD {
-    double hi, lo;
-};
-__device__ __forceinline__ void dd_add(DD &a, double x) {
-    const double s = a.hi + x;
-    const double bb = s - a.hi;
-    const double err = (a.hi - (s - bb)) + (x - bb);
-    a.hi = s;
-    a.lo += err;
-}
-__device__ __forceinline__ DD dd_merge(DD a, DD b) {
-    dd_add(a, b.hi);
-    a.lo += b.lo;
-    return a;
-}
-
 // computeCellSurfaceNormal: block per cell, neighbours within 1.5 m of the float cell position
 __global__ void __launch_bounds__(kXT)
 k_cell_normals(GridView g, float r2, const double *__restrict__ cells,
@@ -377,8 +378,8 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     if (area->n == 0) return PCP_OK;   // :168, nothing is rebuilt; the previous cells stay
     ProfScope prof(ctx, PCP_K_EXCAV_SETUP);
     const double r_near = grid_resolution * 1.5;
-    if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius))) return rc;
-    if ((rc = build_index(ctx, ctx->exc_near, *area, r_near))) return rc;
+    if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius, false))) return rc;
+    if ((rc = build_index(ctx, ctx->exc_near, *area, r_near, false))) return rc;
     const uint64_t n = area->n;
     PCP_HIP(ctx, ctx->area_nrm.ensure(n * 3 * sizeof(float) + 16));
     // non-finite points are not in the index: PCL gives them a NaN normal

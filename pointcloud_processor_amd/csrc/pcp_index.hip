@@ -172,21 +172,24 @@ k_cell_scatter(const float4 *__restrict__ xyz, uint64_t n, const uint32_t *__res
 }
 
 // points of each cell in descending z: lets a query stop scanning a cell at the first point
-// that is more than r below it (exact early exit, see scan_stencil)
+// that is more than r below it (exact early exit, see scan_stencil).  One thread per point:
+// position = cell start + the cell's points ahead of it (higher z, or equal z and earlier), so
+// a cell of n points costs n^2 compares spread over n threads -- the 3 m cells of a 1.5 m
+// radius index hold thousands of points (a per-cell insertion sort took 250 ms there).
 __global__ void __launch_bounds__(kThreads)
-k_cell_sort_z(const uint32_t *__restrict__ start, uint64_t ncell, float4 *__restrict__ pts) {
-    const uint64_t c = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (c >= ncell) return;
+k_cell_rank_z(const float4 *__restrict__ in, uint64_t n, CellMap m,
+              const uint32_t *__restrict__ start, float4 *__restrict__ out) {
+    const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (k >= n) return;
+    const float4 p = in[k];
+    const uint32_t c = cell_of(m, p.x, p.y, p.z);
     const uint32_t s = start[c], e = start[c + 1];
-    for (uint32_t i = s + 1; i < e; ++i) {   // insertion sort (cells hold few points)
-        const float4 v = pts[i];
-        uint32_t j = i;
-        while (j > s && pts[j - 1].z < v.z) {
-            pts[j] = pts[j - 1];
-            --j;
-        }
-        pts[j] = v;
+    uint32_t rank = 0;
+    for (uint32_t j = s; j < e; ++j) {
+        const float z = in[j].z;
+        rank += (z > p.z || (z == p.z && j < (uint32_t)k)) ? 1u : 0u;
     }
+    out[s + rank] = p;
 }
 
 // dilated occupancy: bit for lower corner (ix,iy,iz) = any point in the 2x2x2 block
@@ -239,7 +242,7 @@ k_colmap(const uint32_t *__restrict__ occ2, CellMap m, int shift, int ncx, int n
     colmap[c] = (uint16_t)(lo | (hi << 8));
 }
 
-int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q) {
+int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort) {
     const uint64_t n = v.n;
     hipStream_t st = ctx->stream;
     ProfScope prof(ctx, PCP_K_INDEX_BUILD);
@@ -324,15 +327,20 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q)
     PCP_HIP(ctx, hipMemcpyAsync(ctx->scratch[3].p, g.start.p, ncell * sizeof(uint32_t),
                                 hipMemcpyDeviceToDevice, st));
     PCP_HIP(ctx, g.pts.ensure((size_t)nfin * sizeof(float4)));
+    // (with zsort the scatter lands in a temporary and the rank pass writes g.pts)
+    if (zsort) PCP_HIP(ctx, ctx->scratch[5].ensure((size_t)nfin * sizeof(float4)));
+    float4 *scat = zsort ? ctx->scratch[5].as<float4>() : g.pts.as<float4>();
     hipLaunchKernelGGL(k_cell_scatter, dim3(gridn), dim3(kThreads), 0, st,
                        ctx->scratch[0].as<const float4>(), n, ctx->scratch[2].as<const uint32_t>(),
-                       ctx->scratch[3].as<uint32_t>(), g.pts.as<float4>());
+                       ctx->scratch[3].as<uint32_t>(), scat);
     PCP_CHECK_LAUNCH(ctx);
-    // 7. descending z inside each cell
-    hipLaunchKernelGGL(k_cell_sort_z, dim3((unsigned)((ncell + kThreads - 1) / kThreads)),
-                       dim3(kThreads), 0, st, g.start.as<const uint32_t>(), ncell,
-                       g.pts.as<float4>());
-    PCP_CHECK_LAUNCH(ctx);
+    // 7. descending z inside each cell (the ray-march indices only)
+    if (zsort) {
+        hipLaunchKernelGGL(k_cell_rank_z, dim3((unsigned)((nfin + kThreads - 1) / kThreads)),
+                           dim3(kThreads), 0, st, (const float4 *)scat, (uint64_t)nfin, m,
+                           g.start.as<const uint32_t>(), g.pts.as<float4>());
+        PCP_CHECK_LAUNCH(ctx);
+    }
     // 8. dilated occupancy
     const uint64_t nw = (ncell + 31) / 32;
     PCP_HIP(ctx, g.occ2.ensure(nw * sizeof(uint32_t)));

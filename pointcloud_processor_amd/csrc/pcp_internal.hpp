@@ -200,7 +200,10 @@ struct ProfScope {
 void prof_resolve(pcp_ctx *ctx);   // after a stream sync
 
 // index ----------------------------------------------------------------------------------
-int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q);
+// zsort: points of each cell in descending z (needed by scan_stencil's early exit: the
+// terrain and aux indices); the other indices' queries are order-free
+int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
+                bool zsort = true);
 
 // scan: exclusive prefix sum of n uint32 values into out (n + 1 entries, out[n] = total).
 // tmp must hold scan_tmp_bytes(n).
