@@ -212,6 +212,26 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
                  uint64_t *n_terrain, void *area_out, uint64_t area_cap, uint64_t *n_area,
                  double pose_out[4]);
 
+/* ---- calc_drivable_area.cpp (the occupancy-grid node) -------------------------------------- */
+typedef struct pcp_drivable_params {   /* calc_drivable_area.cpp:20-26 */
+    double grid_resolution;            /* 1.0 */
+    double map_width, map_height;      /* 100, 100 */
+    double max_gradient;               /* 0.3 */
+    int32_t min_points_per_cell;       /* 10 */
+    double start_clear_radius;         /* 3.0 */
+} pcp_drivable_params;
+
+/* robotCloudCallback (:67-226): the robot's filtered cloud (host memory, sensor frame) through
+ * tf2::doTransform(cloud_to_map) (Eigen float), binned into the grid centred on (robot_x,
+ * robot_y) (map -> four_wheel_robot/base_link); start_x/y = the first robot position (the
+ * node's state).  grid (dims[1] rows of dims[0] int8, row-major over y): 0 free, 100 obstacle,
+ * -1 unknown -- nav_msgs/OccupancyGrid.data; origin = the grid's lower-left corner.  An empty
+ * cloud publishes nothing (:119-123): PCP_OK, grid untouched. */
+int pcp_drivable_area(pcp_ctx *ctx, const pcp_cloud_view *cloud, const pcp_rigid *cloud_to_map,
+                      double robot_x, double robot_y, double start_x, double start_y,
+                      const pcp_drivable_params *p, int8_t *grid, uint64_t cap, int32_t dims[2],
+                      double origin[2]);
+
 /* upper bounds of pcp_excavate's record counts for an n-point input (host arithmetic only) */
 int pcp_excavate_bounds(const pcp_excavation_params *p, uint64_t n_in, uint64_t *terrain_cap,
                         uint64_t *area_cap);

@@ -152,6 +152,14 @@ void orc_excavate(const float *pts, int64_t n, int64_t stride_floats, const orc_
                   int64_t cap_surf, int64_t *n_surf, float *area, int64_t cap_area,
                   int64_t *n_area, double pose_out[4]);
 
+/* calc_drivable_area.cpp robotCloudCallback (:67-226): grid gh rows x gw int8 (0 / 100 / -1),
+ * dims = gw, gh; origin = robot - map/2.  t, q: cloud frame -> map (x, y, z, w). */
+void orc_drivable_area(const float *pts, int64_t n, int64_t stride_floats, const double t[3],
+                       const double q[4], double robot_x, double robot_y, double start_x,
+                       double start_y, double res, double map_w, double map_h,
+                       double max_gradient, int32_t min_points, double clear_r, int8_t *grid,
+                       int32_t dims[2], double origin[2]);
+
 #ifdef __cplusplus
 }
 #endif

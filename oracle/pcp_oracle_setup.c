@@ -533,3 +533,70 @@ void orc_excavate(const float *pts, int64_t n, int64_t stride_floats, const orc_
         }
     *n_area = na;
 }
+
+/* ==========================================================================================
+ * calc_drivable_area.cpp robotCloudCallback (:67-226): tf2::doTransform (Eigen float, the
+ * order of orc_transform_rgb), (int) truncating bins, per-cell z lists, then the rules.
+ * ========================================================================================== */
+void orc_drivable_area(const float *pts, int64_t n, int64_t stride_floats, const double t[3],
+                       const double q[4], double robot_x, double robot_y, double start_x,
+                       double start_y, double res, double map_w, double map_h,
+                       double max_gradient, int32_t min_points, double clear_r, int8_t *grid,
+                       int32_t dims[2], double origin[2]) {
+    const int gw = (int)(map_w / res), gh = (int)(map_h / res);
+    dims[0] = gw;
+    dims[1] = gh;
+    const double ox = robot_x - map_w / 2.0, oy = robot_y - map_h / 2.0;
+    origin[0] = ox;
+    origin[1] = oy;
+    if (n <= 0 || gw <= 0 || gh <= 0) return;
+    const int64_t nc = (int64_t)gw * gh;
+    int64_t *cnt = (int64_t *)calloc((size_t)nc, sizeof(int64_t));
+    float *zmin = (float *)malloc(sizeof(float) * (size_t)nc);
+    float *zmax = (float *)malloc(sizeof(float) * (size_t)nc);
+    /* Eigen::Quaternionf(w,x,y,z).toRotationMatrix() + translation, in float */
+    const float qx = (float)q[0], qy = (float)q[1], qz = (float)q[2], qw = (float)q[3];
+    const float tx = 2.0f * qx, ty = 2.0f * qy, tz = 2.0f * qz;
+    const float twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    const float txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    const float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    const float m[3][3] = {{1.0f - (tyy + tzz), txy - twz, txz + twy},
+                           {txy + twz, 1.0f - (txx + tzz), tyz - twx},
+                           {txz - twy, tyz + twx, 1.0f - (txx + tyy)}};
+    const float T[3] = {(float)t[0], (float)t[1], (float)t[2]};
+    for (int64_t i = 0; i < n; ++i) {
+        const float *p = pts + i * stride_floats;
+        float o[3];
+        for (int a = 0; a < 3; ++a) o[a] = ((m[a][0] * p[0] + m[a][1] * p[1]) + m[a][2] * p[2]) + T[a];
+        if (!isfinite(o[0]) || !isfinite(o[1]) || !isfinite(o[2])) continue;
+        const int gx = (int)((o[0] - ox) / res), gy = (int)((o[1] - oy) / res);
+        if (gx >= 0 && gx < gw && gy >= 0 && gy < gh) {
+            const int64_t c = (int64_t)gy * gw + gx;
+            if (cnt[c] == 0) {
+                zmin[c] = zmax[c] = o[2];
+            } else {
+                if (o[2] < zmin[c]) zmin[c] = o[2];   /* std::min_element: first smallest */
+                if (zmax[c] < o[2]) zmax[c] = o[2];   /* std::max_element: first largest */
+            }
+            ++cnt[c];
+        }
+    }
+    for (int y = 0; y < gh; ++y)
+        for (int x = 0; x < gw; ++x) {
+            const int64_t c = (int64_t)y * gw + x;
+            const double cx = ox + (x + 0.5) * res, cy = oy + (y + 0.5) * res;
+            const double dist = sqrt(pow(cx - start_x, 2) + pow(cy - start_y, 2));
+            if (dist <= clear_r) {
+                grid[c] = 0;
+            } else if (cnt[c] == 0 || (size_t)cnt[c] < (size_t)min_points) {
+                grid[c] = -1;
+            } else {
+                float g = 0.0f;
+                if (cnt[c] >= 2) g = (zmax[c] - zmin[c]) / res;
+                grid[c] = g > max_gradient ? 100 : 0;
+            }
+        }
+    free(cnt);
+    free(zmin);
+    free(zmax);
+}

@@ -59,6 +59,9 @@ _SIGS = [
     ("orc_area_normals", None, [_P, C.c_int64, C.c_int64, C.c_double, _P]),
     ("orc_terrain_height", C.c_double, [_P, C.c_int64, C.c_int64, C.c_double, C.c_double,
                                         C.c_double]),
+    ("orc_drivable_area", None, [_P, C.c_int64, C.c_int64, _P, _P, C.c_double, C.c_double,
+                                 C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
+                                 C.c_double, C.c_int32, C.c_double, _P, _P, _P]),
     ("orc_excavate", None, [_P, C.c_int64, C.c_int64, _P, _P, _P, _P, _P, C.c_int64, _P, _P,
                             C.c_int64, _P, _P]),
     ("orc_excavation_grid", C.c_int64, [_P, C.c_int64, C.c_int64, C.c_double, C.c_int32, _P, _P,
@@ -272,3 +275,19 @@ def excavate(pts, t, q, params=None):
                        _p(surf), ns.value, C.byref(ns), _p(area), na.value, C.byref(na),
                        _p(pose))
     return keep[:a.shape[0]].astype(bool), surf[:ns.value], area[:na.value], pose
+
+
+def drivable_area(pts, t, q, robot_xy, start_xy, res=1.0, map_w=100.0, map_h=100.0,
+                  max_gradient=0.3, min_points=10, clear_r=3.0):
+    """calc_drivable_area: -> grid (gh, gw) int8, origin (2,)."""
+    a = _f32(pts)
+    gw, gh = int(map_w / res), int(map_h / res)
+    grid = np.zeros((max(gh, 1), max(gw, 1)), np.int8)
+    dims = np.zeros(2, np.int32)
+    origin = np.zeros(2, np.float64)
+    lib().orc_drivable_area(_p(a), a.shape[0], a.shape[1], _p(np.asarray(t, np.float64)),
+                            _p(np.asarray(q, np.float64)), float(robot_xy[0]),
+                            float(robot_xy[1]), float(start_xy[0]), float(start_xy[1]),
+                            float(res), float(map_w), float(map_h), float(max_gradient),
+                            int(min_points), float(clear_r), _p(grid), _p(dims), _p(origin))
+    return grid[:gh, :gw], origin

@@ -114,6 +114,8 @@ _SIGS = [
     ("pcp_get_area_normals", C.c_int, [_P, _P, C.c_uint64, _P]),
     ("pcp_excavate", C.c_int, [_P, _P, _P, _P, _P, C.c_uint64, _P, _P, C.c_uint64, _P, _P]),
     ("pcp_excavate_bounds", C.c_int, [_P, C.c_uint64, _P, _P]),
+    ("pcp_drivable_area", C.c_int, [_P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double,
+                                    _P, _P, C.c_uint64, _P, _P]),
     ("pcp_generate_candidates", C.c_int, [_P, _P, C.POINTER(VlParams), _P, _P, C.c_uint64,
                                           C.POINTER(C.c_uint64)]),
     ("pcp_score_poses", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams), _P, _P, _P,
@@ -180,6 +182,20 @@ class ExcavationParams(C.Structure):
 
 def excavation_params(**kw) -> ExcavationParams:
     p = ExcavationParams(1.0, 75.0, 4.0, 1.0, 0.05, 0.5, 1, 2.0, 1.2, 2.0, 1.2, 1.2, 1.8)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class DrivableParams(C.Structure):
+    """pcp_drivable_params (calc_drivable_area.cpp:20-26 defaults)."""
+    _fields_ = [("grid_resolution", C.c_double), ("map_width", C.c_double),
+                ("map_height", C.c_double), ("max_gradient", C.c_double),
+                ("min_points_per_cell", C.c_int32), ("start_clear_radius", C.c_double)]
+
+
+def drivable_params(**kw) -> DrivableParams:
+    p = DrivableParams(1.0, 100.0, 100.0, 0.3, 10, 3.0)
     for k, v in kw.items():
         setattr(p, k, v)
     return p
@@ -412,6 +428,23 @@ class Context:
                                           area.shape[0], C.byref(na), _ptr(pose)),
                     "pcp_excavate")
         return terr[:nt.value], area[:na.value], pose
+
+    def drivable_area(self, cloud: np.ndarray, cloud_to_map, robot_xy, start_xy,
+                      params: DrivableParams | None = None, point_step=None, offs=(0, 4, 8)):
+        """calc_drivable_area robotCloudCallback -> (grid (h, w) int8, origin (2,))."""
+        v = cloud_view(cloud, point_step, offs)
+        p = params or drivable_params()
+        tf = Rigid((C.c_double * 3)(*cloud_to_map[0]), (C.c_double * 4)(*cloud_to_map[1]))
+        gw, gh = int(p.map_width / p.grid_resolution), int(p.map_height / p.grid_resolution)
+        grid = np.zeros((max(gh, 1), max(gw, 1)), np.int8)
+        dims = np.zeros(2, np.int32)
+        origin = np.zeros(2, np.float64)
+        self._check(self.lib.pcp_drivable_area(self.h, C.byref(v), C.byref(tf), float(robot_xy[0]),
+                                               float(robot_xy[1]), float(start_xy[0]),
+                                               float(start_xy[1]), C.byref(p), _ptr(grid),
+                                               grid.size, _ptr(dims), _ptr(origin)),
+                    "pcp_drivable_area")
+        return grid[:dims[1], :dims[0]], origin
 
     def terrain_info(self) -> dict:
         info = IndexInfo()

@@ -314,4 +314,45 @@ ExcavationTerrainGenerator::Output ExcavationTerrainGenerator::matchedCloudCallb
     return o;
 }
 
+// ---- DrivableAreaMapper ---------------------------------------------------------------------------
+bool DrivableAreaMapper::robotCloudCallback(const PointCloud2 &msg, const Transform *cloud_to_map,
+                                            const Transform *robot_base, OccupancyGrid &out) {
+    err_.clear();
+    if (!cloud_to_map) return false;   // "Transform ... not available yet"
+    pcp_cloud_view v;
+    std::string why;
+    if (!cloud_view(msg, v, &why)) {
+        err_ = "calc_drivable_area: " + why;
+        return false;
+    }
+    if (msg.empty()) return false;   // "Received empty point cloud"
+    if (!robot_base) return false;   // "Could not get robot transform"
+    const double rx = robot_base->t[0], ry = robot_base->t[1];
+    if (!start_set_) {   // :134-141
+        start_x_ = rx;
+        start_y_ = ry;
+        start_set_ = true;
+    }
+    pcp_rigid tf;
+    for (int a = 0; a < 3; ++a) tf.t[a] = cloud_to_map->t[a];
+    for (int a = 0; a < 4; ++a) tf.q[a] = cloud_to_map->q[a];
+    const int gw = (int)(p_.map_width / p_.grid_resolution);
+    const int gh = (int)(p_.map_height / p_.grid_resolution);
+    out.data.assign((size_t)std::max(gw, 0) * (size_t)std::max(gh, 0), -1);
+    int32_t dims[2];
+    double origin[2];
+    if (pcp_drivable_area(dev_.ctx(), &v, &tf, rx, ry, start_x_, start_y_, &p_, out.data.data(),
+                          out.data.size(), dims, origin) != PCP_OK) {
+        err_ = dev_.error();
+        return false;
+    }
+    out.frame_id = "map";
+    out.resolution = p_.grid_resolution;
+    out.width = (uint32_t)dims[0];
+    out.height = (uint32_t)dims[1];
+    out.origin_x = origin[0];
+    out.origin_y = origin[1];
+    return true;
+}
+
 }  // namespace pcp

@@ -136,6 +136,35 @@ class ExcavationTerrainGenerator {
     std::string err_;
 };
 
+// ---- calc_drivable_area.cpp (its class is also named SimplifiedScanMatcher upstream) --------
+struct OccupancyGrid {   // nav_msgs::msg::OccupancyGrid (the fields the node fills)
+    std::string frame_id = "map";
+    double resolution = 0;
+    uint32_t width = 0, height = 0;
+    double origin_x = 0, origin_y = 0;   // orientation w = 1
+    std::vector<int8_t> data;            // 0 free, 100 obstacle, -1 unknown
+};
+
+class DrivableAreaMapper {
+   public:
+    explicit DrivableAreaMapper(Device &dev) : dev_(dev) { p_ = pcp_drivable_params{1.0, 100.0, 100.0, 0.3, 10, 3.0}; }
+    DrivableAreaMapper(Device &dev, const pcp_drivable_params &p) : dev_(dev), p_(p) {}
+    // robotCloudCallback (:67-226): cloud_to_map = the TF of the cloud's frame (nullptr: not
+    // available, skipped :76-96), robot_base = map -> four_wheel_robot/base_link (nullptr:
+    // skipped :127-131).  Returns false when nothing is published (also an empty cloud).
+    bool robotCloudCallback(const PointCloud2 &msg, const Transform *cloud_to_map,
+                            const Transform *robot_base, OccupancyGrid &out);
+    bool startSet() const { return start_set_; }
+    const std::string &lastError() const { return err_; }
+
+   private:
+    Device &dev_;
+    pcp_drivable_params p_;
+    bool start_set_ = false;   // start_position_initialized_
+    double start_x_ = 0, start_y_ = 0;
+    std::string err_;
+};
+
 // ---- virtual_lidar.cpp (SimplifiedDualLidarOptimizer) --------------------------------------
 class SimplifiedDualLidarOptimizer {
    public:

@@ -423,3 +423,30 @@ def test_excavate_bounds_hold(gpu):
         nt, na = C_u64(), C_u64()
         assert gpu.lib.pcp_excavate_bounds(C_ref(p), c.shape[0], C_ref(nt), C_ref(na)) == 0
         assert terr.shape[0] <= nt.value and area.shape[0] <= na.value
+
+
+# ---------------------------------------------------------------- drivable-area grid
+@pytest.mark.parametrize("kw", [{}, {"grid_resolution": 0.5, "map_width": 60.0, "map_height": 40.0,
+                                     "min_points_per_cell": 3, "max_gradient": 0.2}])
+def test_drivable_area_matches_oracle(gpu, oracle, kw):
+    """calc_drivable_area (robotCloudCallback :67-226) against the CPU restatement: the int8
+    occupancy grid and its origin bit-exact (start-clear disc, unknown, obstacle, free)."""
+    rng = np.random.default_rng(11)
+    n = 200_000
+    c = np.zeros((n, 4), np.float32)
+    c[:, 0] = rng.uniform(-45, 45, n)
+    c[:, 1] = rng.uniform(-45, 45, n)
+    c[:, 2] = rng.normal(-1.5, 0.05, n)
+    steep = (c[:, 0] > 5) & (c[:, 0] < 15)
+    c[steep, 2] += rng.uniform(0, 1.5, steep.sum())
+    c[rng.integers(0, n, 50), 1] = np.nan
+    yaw = math.radians(25.0)
+    t, q = (3.0, -2.0, 1.8), (0.0, 0.05, math.sin(yaw / 2), math.cos(yaw / 2))
+    p = _abi.drivable_params(**kw)
+    grid, origin = gpu.drivable_area(c, (t, q), (3.0, -2.0), (1.0, 0.5), p)
+    ref, r_origin = oracle.drivable_area(c, t, q, (3.0, -2.0), (1.0, 0.5), p.grid_resolution,
+                                         p.map_width, p.map_height, p.max_gradient,
+                                         p.min_points_per_cell, p.start_clear_radius)
+    np.testing.assert_array_equal(origin, r_origin)
+    np.testing.assert_array_equal(grid, ref)
+    assert {-1, 0, 100} <= set(np.unique(grid).tolist())
