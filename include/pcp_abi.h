@@ -65,6 +65,14 @@ int pcp_dev_alloc(pcp_ctx *ctx, uint64_t bytes, void **dptr);
 int pcp_dev_free(pcp_ctx *ctx, void *dptr);
 int pcp_memcpy_h2d(pcp_ctx *ctx, void *dst, const void *src, uint64_t bytes);
 int pcp_memcpy_d2h(pcp_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+/* Pinned (page-locked) host memory for PointCloud2 data blobs: the node shell deserializes
+ * into / publishes from these, so every H2D/D2H of the calls above runs as direct DMA instead
+ * of the runtime's pageable staging.  pcp_host_register pins an existing buffer in place
+ * (unregister before freeing it). */
+int pcp_host_alloc(pcp_ctx *ctx, uint64_t bytes, void **hptr);
+int pcp_host_free(pcp_ctx *ctx, void *hptr);
+int pcp_host_register(pcp_ctx *ctx, void *hptr, uint64_t bytes);
+int pcp_host_unregister(pcp_ctx *ctx, void *hptr);
 
 /* ---- in-library kernel timing (HIP events on the ctx stream) ------------------------ */
 enum pcp_kernel_id {

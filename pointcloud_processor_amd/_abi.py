@@ -91,6 +91,10 @@ _SIGS = [
     ("pcp_dev_free", C.c_int, [_P, _P]),
     ("pcp_memcpy_h2d", C.c_int, [_P, _P, _P, C.c_uint64]),
     ("pcp_memcpy_d2h", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("pcp_host_alloc", C.c_int, [_P, C.c_uint64, _P]),
+    ("pcp_host_free", C.c_int, [_P, _P]),
+    ("pcp_host_register", C.c_int, [_P, _P, C.c_uint64]),
+    ("pcp_host_unregister", C.c_int, [_P, _P]),
     ("pcp_profile_enable", C.c_int, [_P, C.c_int]),
     ("pcp_profile_reset", C.c_int, [_P]),
     ("pcp_profile_get", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
@@ -445,6 +449,13 @@ class Context:
                                                grid.size, _ptr(dims), _ptr(origin)),
                     "pcp_drivable_area")
         return grid[:dims[1], :dims[0]], origin
+
+    def host_register(self, arr: np.ndarray):
+        """Pin a (contiguous) numpy array in place; unregister before it is freed."""
+        self._check(self.lib.pcp_host_register(self.h, _ptr(arr), arr.nbytes), "pcp_host_register")
+
+    def host_unregister(self, arr: np.ndarray):
+        self._check(self.lib.pcp_host_unregister(self.h, _ptr(arr)), "pcp_host_unregister")
 
     def terrain_info(self) -> dict:
         info = IndexInfo()

@@ -296,6 +296,32 @@ int pcp_synchronize(pcp_ctx *ctx) {
     return PCP_OK;
 }
 
+int pcp_host_alloc(pcp_ctx *ctx, uint64_t bytes, void **hptr) {
+    if (!ctx || !hptr) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    PCP_HIP(ctx, hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocDefault));
+    return PCP_OK;
+}
+
+int pcp_host_free(pcp_ctx *ctx, void *hptr) {
+    if (!ctx) return PCP_E_INVALID;
+    if (hptr) PCP_HIP(ctx, hipHostFree(hptr));
+    return PCP_OK;
+}
+
+int pcp_host_register(pcp_ctx *ctx, void *hptr, uint64_t bytes) {
+    if (!ctx || !hptr || !bytes) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    PCP_HIP(ctx, hipHostRegister(hptr, bytes, hipHostRegisterDefault));
+    return PCP_OK;
+}
+
+int pcp_host_unregister(pcp_ctx *ctx, void *hptr) {
+    if (!ctx || !hptr) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipHostUnregister(hptr));
+    return PCP_OK;
+}
+
 int pcp_dev_alloc(pcp_ctx *ctx, uint64_t bytes, void **dptr) {
     if (!ctx || !dptr) return PCP_E_INVALID;
     PCP_HIP(ctx, hipSetDevice(ctx->device));
