@@ -196,6 +196,46 @@ def run_fan(args, torch, dist, world, rank, local):
     return out
 
 
+def _pcie_inclusive(ctx, clouds, box, tfs, n_in, cap, reps=5):
+    """Host-buffer filter_merge (the PointCloud2 boundary: H2D of the raw clouds, the same
+    pipeline, D2H of the merged cloud), pageable numpy buffers vs the same buffers pinned in
+    place with pcp_host_register.  Reported beside `value`, never as it."""
+    import numpy as np
+
+    rgbs = [(255, 0, 0), (0, 0, 255)]
+    out = np.empty((cap, 8), np.float32)
+    res = {"unit": "input points/s", "reps": reps,
+           "h2d_bytes": int(sum(c.nbytes for c in clouds))}
+
+    def timed():
+        ctx.filter_merge(clouds, [box, box], 0.05, tfs, rgbs, out=out)   # warm
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            got, _ = ctx.filter_merge(clouds, [box, box], 0.05, tfs, rgbs, out=out)
+        dt = (time.perf_counter() - t0) / reps
+        return dt, got.shape[0]
+
+    dt, n_out = timed()
+    res["pageable_ms"] = dt * 1e3
+    res["pageable"] = n_in / dt
+    res["d2h_bytes"] = int(n_out * 32)
+    pinned = []
+    try:
+        for a in clouds + [out]:
+            ctx.host_register(a)
+            pinned.append(a)
+        dt, _ = timed()
+        res["pinned_ms"] = dt * 1e3
+        res["pinned"] = n_in / dt
+        res["pinned_link_gbs"] = (res["h2d_bytes"] + res["d2h_bytes"]) / dt / 1e9
+    except RuntimeError as e:           # pinning refused (e.g. locked-memory limit)
+        res["pinned_error"] = str(e)
+    finally:
+        for a in pinned:
+            ctx.host_unregister(a)
+    return res
+
+
 def run_filter(args, torch, dist, world, rank, local):
     """C3: crop + voxel(0.05) + transform on a 10M-pt dual-LiDAR frame, inputs in HBM."""
     import math
@@ -250,6 +290,7 @@ def run_filter(args, torch, dist, world, rank, local):
                                  cap)
     stages = {k: ectx.profile_get(k)[0] / 3 for k in ("crop", "voxel", "transform", "filter_merge")}
     ectx.close()
+    pcie = _pcie_inclusive(ctx, clouds, box, tfs, n_in, cap)
     alg = 12.0 * n_in + 16.0 * n_out
     res = {
         "metric": "crop+voxel+transform points/s (C3)", "value": n_in * args.steps / dt,
@@ -266,6 +307,7 @@ def run_filter(args, torch, dist, world, rank, local):
                      "kernel": "filter_merge graph (all stages)", "avg_kernel_ms": step_dev_ms,
                      "eager_stage_ms": stages,
                      "model": "12 B/input point + 16 B/output point (SURVEY 8d)"},
+        "pcie_inclusive": pcie,
     }
     for p in dptr + [out_d]:
         ctx.dev_free(p)

@@ -234,7 +234,7 @@ typedef struct pcp_drivable_params {   /* calc_drivable_area.cpp:20-26 */
  * robot_y) (map -> four_wheel_robot/base_link); start_x/y = the first robot position (the
  * node's state).  grid (dims[1] rows of dims[0] int8, row-major over y): 0 free, 100 obstacle,
  * -1 unknown -- nav_msgs/OccupancyGrid.data; origin = the grid's lower-left corner.  An empty
- * cloud publishes nothing (:119-123): PCP_OK, grid untouched. */
+ * cloud publishes nothing (:107-111): PCP_OK, grid untouched. */
 int pcp_drivable_area(pcp_ctx *ctx, const pcp_cloud_view *cloud, const pcp_rigid *cloud_to_map,
                       double robot_x, double robot_y, double start_x, double start_y,
                       const pcp_drivable_params *p, int8_t *grid, uint64_t cap, int32_t dims[2],

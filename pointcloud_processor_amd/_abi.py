@@ -333,11 +333,19 @@ class Context:
                     "pcp_transform_concat")
         return out[: n.value].copy()
 
-    def filter_merge(self, clouds, boxes, leaf, tfs, rgbs):
+    def filter_merge(self, clouds, boxes, leaf, tfs, rgbs, out=None):
+        """Host-buffer filter_merge.  ``out`` (optional, float32 [>= total, 8], e.g. a
+        host_register-ed array for pinned D2H) receives the merged cloud; a view of it is
+        returned in that case, a fresh copy otherwise."""
         k = len(clouds)
         views = (CloudView * max(k, 1))(*[cloud_view(c) for c in clouds])
         total = sum(c.shape[0] for c in clouds)
-        out = np.empty((max(total, 1), 8), np.float32)
+        own = out is None
+        if own:
+            out = np.empty((max(total, 1), 8), np.float32)
+        elif (out.dtype != np.float32 or out.ndim != 2 or out.shape[1] != 8
+              or out.shape[0] < total or not out.flags.c_contiguous):
+            raise ValueError("filter_merge: out must be C-contiguous float32 [>= total, 8]")
         rgb = np.ascontiguousarray(np.asarray(rgbs, np.uint8).reshape(-1))
         bx = np.ascontiguousarray(np.asarray(boxes, np.float64).reshape(-1))
         n = C.c_uint64()
@@ -345,7 +353,8 @@ class Context:
         self._check(self.lib.pcp_filter_merge(self.h, k, views, _ptr(bx), C.c_float(leaf),
                                               self._rigids(tfs), _ptr(rgb), _ptr(out), total,
                                               C.byref(n), _ptr(per), 0), "pcp_filter_merge")
-        return out[: n.value].copy(), per[:k].copy()
+        res = out[: n.value].copy() if own else out[: n.value]
+        return res, per[:k].copy()
 
     def filter_merge_device(self, views, boxes, leaf, tfs, rgbs, out_dev: int, cap: int):
         """Device-resident pipeline (benchmark): views hold device pointers."""

@@ -151,7 +151,7 @@ class DrivableAreaMapper {
     DrivableAreaMapper(Device &dev, const pcp_drivable_params &p) : dev_(dev), p_(p) {}
     // robotCloudCallback (:67-226): cloud_to_map = the TF of the cloud's frame (nullptr: not
     // available, skipped :76-96), robot_base = map -> four_wheel_robot/base_link (nullptr:
-    // skipped :127-131).  Returns false when nothing is published (also an empty cloud).
+    // skipped :114-126).  Returns false when nothing is published (also an empty cloud).
     bool robotCloudCallback(const PointCloud2 &msg, const Transform *cloud_to_map,
                             const Transform *robot_base, OccupancyGrid &out);
     bool startSet() const { return start_set_; }

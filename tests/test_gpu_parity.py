@@ -192,6 +192,40 @@ def test_filter_merge_device_graph_replay(gpu, oracle):
                                   np.concatenate(parts)[:, :5].view(np.uint32))
 
 
+def test_filter_merge_pinned_staging(gpu):
+    """PointCloud2 boundary with page-locked buffers: clouds and the output pinned in place
+    (pcp_host_register) and a pcp_host_alloc block must give the pageable path's bytes."""
+    a = synth.lidar_cloud(120_000, seed=9)
+    b = synth.lidar_cloud(80_000, seed=10, sensor_height=3.5)
+    tfs = _tfs()
+    rgbs = [(255, 0, 0), (0, 0, 255)]
+    ref, per_ref = gpu.filter_merge([a, b], [BOX, BOX], 0.05, tfs, rgbs)
+    out = np.empty((a.shape[0] + b.shape[0], 8), np.float32)
+    for x in (a, b, out):
+        gpu.host_register(x)
+    try:
+        got, per = gpu.filter_merge([a, b], [BOX, BOX], 0.05, tfs, rgbs, out=out)
+        assert list(per) == list(per_ref)
+        np.testing.assert_array_equal(got[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
+    finally:
+        for x in (a, b, out):
+            gpu.host_unregister(x)
+    # a pinned allocation from the library, filled in place and used as the input cloud
+    hp = ctypes.c_void_p()
+    assert gpu.lib.pcp_host_alloc(gpu.h, a.nbytes, C_ref(hp)) == 0 and hp.value
+    try:
+        pinned = np.ctypeslib.as_array(ctypes.cast(hp, ctypes.POINTER(ctypes.c_float)),
+                                       shape=a.shape)
+        pinned[:] = a
+        got, per = gpu.filter_merge([pinned, b], [BOX, BOX], 0.05, tfs, rgbs)
+        assert list(per) == list(per_ref)
+        np.testing.assert_array_equal(got[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
+    finally:
+        assert gpu.lib.pcp_host_free(gpu.h, hp) == 0
+    with pytest.raises(ValueError):                       # output too small
+        gpu.filter_merge([a, b], [BOX, BOX], 0.05, tfs, rgbs, out=out[:10])
+
+
 # ---------------------------------------------------------------------------------- virtual_lidar
 @pytest.fixture(scope="module")
 def loaded(gpu, oracle, scene, cells, aux):
