@@ -328,7 +328,7 @@ bool DrivableAreaMapper::robotCloudCallback(const PointCloud2 &msg, const Transf
     if (msg.empty()) return false;   // "Received empty point cloud"
     if (!robot_base) return false;   // "Could not get robot transform"
     const double rx = robot_base->t[0], ry = robot_base->t[1];
-    if (!start_set_) {   // :134-141
+    if (!start_set_) {   // :132-138
         start_x_ = rx;
         start_y_ = ry;
         start_set_ = true;

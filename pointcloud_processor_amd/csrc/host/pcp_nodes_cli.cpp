@@ -5,6 +5,7 @@
 //   pcp_nodes_cli merge   ROBOT.f32 RN ZX.f32 ZN TR(7) TZ(7) OUT.f32        (t xyz, q xyzw)
 //   pcp_nodes_cli vlidar  TERRAIN.f32 TN AUX.f32 AN CELLS.f64 NORMALS.f32 CN BBOX(6) ZXT(3) NUMC
 //                         MAXD OUT_TOTALS.f64 OUT_FLAGS.u8 OUT_REPORT.txt [TICKS]
+//   pcp_nodes_cli drivable IN.f32 N STEP TF(7) R1(2) R2(2) OUT.i8
 //   pcp_nodes_cli replay  TERRAIN.f32 TN CELLS.f64 NORMALS.f32 CN BBOX(6) FRAMES POINTS
 //
 // Tuples are comma-separated doubles.  .f32 clouds are PointXYZRGB-like records of STEP bytes
@@ -288,9 +289,44 @@ static int cmd_area(Device &dev, char **a) {
     return 0;
 }
 
+// calc_drivable_area: two robotCloudCallback frames of the same cloud at robot positions R1, R2
+// (the first one fixes the start-clear centre), plus the skipped cases (no TF, empty cloud)
+static int cmd_drivable(Device &dev, char **a) {
+    const auto raw = read_file(a[0]);
+    const size_t n = std::strtoull(a[1], nullptr, 10);
+    const uint32_t step = (uint32_t)std::strtoul(a[2], nullptr, 10);
+    const Transform tf = tf_from(tuple(a[3]));
+    const auto r1 = tuple(a[4]), r2 = tuple(a[5]);
+    DrivableAreaMapper node(dev);
+    const PointCloud2 msg = cloud_from(raw, n, step, "four_wheel_robot/velodyne_link");
+    OccupancyGrid g1, g2, skip;
+    Transform b1, b2;
+    b1.t[0] = r1[0];
+    b1.t[1] = r1[1];
+    b2.t[0] = r2[0];
+    b2.t[1] = r2[1];
+    if (node.robotCloudCallback(msg, nullptr, &b1, skip) || node.startSet()) return 3;
+    if (node.robotCloudCallback(msg, &tf, nullptr, skip) || node.startSet()) return 4;
+    if (node.robotCloudCallback(cloud_from(raw, 0, step, msg.frame_id), &tf, &b1, skip) ||
+        node.startSet())
+        return 5;
+    if (!node.robotCloudCallback(msg, &tf, &b1, g1) || !node.robotCloudCallback(msg, &tf, &b2, g2)) {
+        std::fprintf(stderr, "drivable: %s\n", node.lastError().c_str());
+        return 1;
+    }
+    std::vector<int8_t> both(g1.data);
+    both.insert(both.end(), g2.data.begin(), g2.data.end());
+    write_file(a[6], both.data(), both.size());
+    std::printf("{\"width\": %u, \"height\": %u, \"resolution\": %.17g, "
+                "\"origin1\": [%.17g, %.17g], \"origin2\": [%.17g, %.17g]}\n",
+                g1.width, g1.height, g1.resolution, g1.origin_x, g1.origin_y, g2.origin_x,
+                g2.origin_y);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: pcp_nodes_cli filter|merge|vlidar|area|replay ...\n");
+        std::fprintf(stderr, "usage: pcp_nodes_cli filter|merge|vlidar|area|drivable|replay ...\n");
         return 2;
     }
     const std::string cmd = argv[1];
@@ -298,6 +334,7 @@ int main(int argc, char **argv) {
                      : cmd == "merge"  ? 7
                      : cmd == "vlidar" ? 14
                      : cmd == "area"   ? 10
+                     : cmd == "drivable" ? 7
                      : cmd == "replay" ? 8
                                        : -1;
     if (need < 0 || argc - 2 < need) {
@@ -310,6 +347,7 @@ int main(int argc, char **argv) {
         if (cmd == "merge") return cmd_merge(dev, argv + 2);
         if (cmd == "vlidar") return cmd_vlidar(dev, argv + 2, argc - 2);
         if (cmd == "area") return cmd_area(dev, argv + 2);
+        if (cmd == "drivable") return cmd_drivable(dev, argv + 2);
         return cmd_replay(dev, argv + 2);
     } catch (const std::exception &e) {
         std::fprintf(stderr, "%s\n", e.what());

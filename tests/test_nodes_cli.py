@@ -141,3 +141,29 @@ def test_streaming_replay_full_chain(tmp_path, scene, cells):
     assert res["frames"] == 6 and res["chain"] == 1
     assert res["cells"] > 0 and res["merged_points"] > 0 and res["best_idx"] >= 0
     assert 0 < res["p50_ms"] <= res["p99_ms"]
+
+
+def test_drivable_area_node(tmp_path, oracle):
+    """DrivableAreaMapper::robotCloudCallback (calc_drivable_area.cpp:67-226): the skipped
+    callbacks leave the start unset; the first published frame fixes the start-clear centre,
+    which the second frame (robot moved) keeps. Grids and origins bit-exact vs the oracle."""
+    rng = np.random.default_rng(4)
+    n = 120_000
+    c = np.zeros((n, 4), np.float32)
+    c[:, 0] = rng.uniform(-40, 40, n)
+    c[:, 1] = rng.uniform(-40, 40, n)
+    c[:, 2] = rng.normal(-1.6, 0.04, n)
+    wall = (c[:, 1] > 8) & (c[:, 1] < 12)
+    c[wall, 2] += rng.uniform(0, 2.0, wall.sum())
+    c.tofile(tmp_path / "in.f32")
+    yaw = math.radians(-40.0)
+    tf = [5.0, 1.0, 1.9, 0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2)]
+    r1, r2 = (5.0, 1.0), (12.25, -6.5)
+    res = _run("drivable", tmp_path / "in.f32", n, 16, _t(tf), _t(r1), _t(r2), tmp_path / "g.i8")
+    w, h = res["width"], res["height"]
+    assert (w, h, res["resolution"]) == (100, 100, 1.0)
+    got = np.fromfile(tmp_path / "g.i8", np.int8).reshape(2, h, w)
+    for k, (r, key) in enumerate(((r1, "origin1"), (r2, "origin2"))):
+        ref, origin = oracle.drivable_area(c, tf[:3], tf[3:], r, r1)
+        np.testing.assert_array_equal(res[key], origin)
+        np.testing.assert_array_equal(got[k], ref)
