@@ -79,13 +79,27 @@ def _traffic_from_profiles(workload_key: str):
         return None
 
 
-def cpu_baseline_fan(terrain, poses, fan, budget_s: float):
-    """The oracle (CPU restatement, single thread = the reference's executor) on a bounded
-    sample: the first k poses of this workload, whole fans, until ~budget_s elapsed."""
+def _host_cpu():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"model": model, "nproc": os.cpu_count(), "affinity": share}
+
+
+def cpu_baseline_fan(terrain, poses, fan, budget_s: float, threads: int = 1):
+    """The oracle (CPU restatement) on a bounded sample: the first k poses of this workload,
+    whole fans, until ~budget_s elapsed.  threads = 1 is the reference's single-threaded
+    executor; threads > 1 is the OpenMP variant SURVEY 8d asks for beside it."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle
 
-    pyoracle.set_threads(1)
+    pyoracle.set_threads(threads)
     T = pyoracle.Cloud(terrain)
     units = 0
     k = 0
@@ -96,9 +110,11 @@ def cpu_baseline_fan(terrain, poses, fan, budget_s: float):
         units += int(u.sum())
         k += 1
     dt = time.perf_counter() - t0
-    return {"value": units / dt, "unit": "ray-hit tests/s", "cores": 1, "kind": "port",
+    pyoracle.set_threads(1)
+    return {"value": units / dt, "unit": "ray-hit tests/s", "cores": threads, "kind": "port",
             "sample": f"{k} of {len(poses)} poses x full {fan.n_az}x{fan.n_el} fan, "
-                      f"{units} sample queries in {dt:.1f} s (oracle/pcp_oracle.c, 1 thread)"}
+                      f"{units} sample queries in {dt:.1f} s (oracle/pcp_oracle.c, "
+                      f"{threads} thread{'s' if threads > 1 else ''})"}
 
 
 def run_fan(args, torch, dist, world, rank, local):
@@ -184,7 +200,7 @@ def run_fan(args, torch, dist, world, rank, local):
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": _traffic_from_profiles("fan"),
-            "kernel": "k_raycast_fan_w<0, 7>", "avg_kernel_ms": avg_kernel_s * 1e3,
+            "kernel": "k_raycast_fan<0, 64, true>", "avg_kernel_ms": avg_kernel_s * 1e3,
             "alg_bytes_per_launch": alg_bytes,
             "model": "64 B/sample query + 12 B/point test (SURVEY 8d)",
             "diag": st,
@@ -192,6 +208,11 @@ def run_fan(args, torch, dist, world, rank, local):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_fan(scene.terrain, poses, fan, args.cpu_seconds)
+        host = _host_cpu()
+        mt = max(1, min(16, host["affinity"] or 1))     # the box's CPU share is 16
+        out["cpu_baseline_mt"] = cpu_baseline_fan(scene.terrain, poses, fan,
+                                                  args.cpu_seconds / 2, threads=mt)
+        out["cpu_baseline_mt"]["host"] = host
     ctx.close()
     return out
 
@@ -290,7 +311,7 @@ def run_filter(args, torch, dist, world, rank, local):
                                  cap)
     stages = {k: ectx.profile_get(k)[0] / 3 for k in ("crop", "voxel", "transform", "filter_merge")}
     ectx.close()
-    pcie = _pcie_inclusive(ctx, clouds, box, tfs, n_in, cap)
+    pcie = None if args.no_pcie else _pcie_inclusive(ctx, clouds, box, tfs, n_in, cap)
     alg = 12.0 * n_in + 16.0 * n_out
     res = {
         "metric": "crop+voxel+transform points/s (C3)", "value": n_in * args.steps / dt,
@@ -359,6 +380,8 @@ def main():
     ap.add_argument("--filter-points", type=int, default=10_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="filter mode: skip the host-buffer (PCIe-inclusive) measurement")
     args = ap.parse_args()
     torch, dist, world, rank, local = _dist_init(args.gpus)
     fn = {"fan": run_fan, "filter": run_filter, "cells": run_cells}[args.mode]

@@ -283,9 +283,9 @@ typedef struct pcp_fan_params {
 int pcp_raycast_fan(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
                     uint32_t *blocked, uint64_t *units, int16_t *first_hit, int64_t *best_idx);
 
-/* Diagnostic build of the same march (not for timing): stats[0] = samples visited after the
- * exact clip, stats[1] = samples whose 2x2x2 stencil is occupied (directory reads),
- * stats[2] = point tests.  Used to state the roofline's algorithmic bytes. */
+/* Diagnostic build of the same march (not for timing): stats[0] = samples probed after the
+ * exact clip, stats[1] = samples whose 2x2x2 stencil survives the z-band probe and is scanned
+ * (directory reads), stats[2] = point tests.  Used to state the roofline's algorithmic bytes. */
 int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
                           const pcp_fan_params *fan, uint64_t stats[3]);
 

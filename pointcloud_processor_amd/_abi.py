@@ -518,7 +518,7 @@ def _fan_stats(self, poses5, fan):
     st = np.zeros(3, np.uint64)
     self._check(self.lib.pcp_raycast_fan_stats(self.h, _ptr(poses), poses.shape[0], C.byref(fan),
                                                _ptr(st)), "pcp_raycast_fan_stats")
-    return {"samples_visited": int(st[0]), "occupied_stencils": int(st[1]),
+    return {"samples_visited": int(st[0]), "scanned_stencils": int(st[1]),
             "point_tests": int(st[2])}
 
 

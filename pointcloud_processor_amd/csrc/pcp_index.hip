@@ -3,6 +3,7 @@
 //   pts   : float4[n]   x, y, z, bitcast(original point index), sorted by cell
 //   start : u32[ncell+1] prefix offsets (cell c holds pts[start[c] .. start[c+1]) )
 //   occ2  : u32[(ncell+31)/32] dilated occupancy (bit c = any point in cells c + {0,1}^3)
+//   occz  : u16[ncell] z band of the same 2x2x2 block (z-sorted indices: the march's probe)
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -42,10 +43,6 @@ GridView GridIndex::view() const {
     v.by1 = bmax[1] + rb;
     v.bz0 = bmin[2] - rb;
     v.bz1 = bmax[2] + rb;
-    v.colmap = colmap_ok ? colmap.as<const uint16_t>() : nullptr;
-    v.ncx = ncx;
-    v.ncy = ncy;
-    v.col_shift = col_shift;
     v.flo_x = (float)v.lo_x;
     v.flo_y = (float)v.lo_y;
     v.flo_z = (float)v.lo_z;
@@ -55,6 +52,9 @@ GridView GridIndex::view() const {
     v.fnz1 = (float)(nz - 1);
     const double bb[6] = {v.bx0, v.bx1, v.by0, v.by1, v.bz0, v.bz1};
     for (int a = 0; a < 6; ++a) v.fb[a] = (float)bb[a];
+    v.occz = occz_ok ? occz.as<const uint16_t>() : nullptr;
+    v.fzoff = (float)(rm * v.inv_c);
+    v.fzt = (float)((r_q + 2e-3) * v.inv_c);
     return v;
 }
 
@@ -184,12 +184,56 @@ k_cell_rank_z(const float4 *__restrict__ in, uint64_t n, CellMap m,
     const float4 p = in[k];
     const uint32_t c = cell_of(m, p.x, p.y, p.z);
     const uint32_t s = start[c], e = start[c + 1];
+    // descending z, ties by original index (.w): the layout does not depend on the order
+    // in which the scatter's atomics placed the points
+    const uint32_t ok = __float_as_uint(p.w);
     uint32_t rank = 0;
     for (uint32_t j = s; j < e; ++j) {
-        const float z = in[j].z;
-        rank += (z > p.z || (z == p.z && j < (uint32_t)k)) ? 1u : 0u;
+        const float4 q = in[j];
+        rank += (q.z > p.z || (q.z == p.z && __float_as_uint(q.w) < ok)) ? 1u : 0u;
     }
     out[s + rank] = p;
+}
+
+// z band per stencil corner (z-sorted cells: a cell's first point is its highest, its last
+// the lowest).  Rounded outwards by one extra step and clamped to the open-ended codes, so
+// zb + lo*kZq*c <= every point z <= zb + hi*kZq*c holds for the block's points whatever the
+// rounding of their cell assignment (zb = the block's floor, oz + iz*c).
+__global__ void __launch_bounds__(kThreads)
+k_occz(const uint32_t *__restrict__ start, const float4 *__restrict__ pts, CellMap m, double c,
+       uint64_t ncell, uint16_t *__restrict__ occz) {
+    const uint64_t lin = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (lin >= ncell) return;
+    const int ix = (int)(lin % m.nx);
+    const int iy = (int)((lin / m.nx) % m.ny);
+    const int iz = (int)(lin / ((uint64_t)m.nx * m.ny));
+    float zmax = -FLT_MAX, zmin = FLT_MAX;
+    bool any = false;
+    for (int dz = 0; dz < 2; ++dz)
+        for (int dy = 0; dy < 2; ++dy) {
+            const int y = iy + dy, z = iz + dz;
+            if (y >= m.ny || z >= m.nz) continue;
+            const uint64_t row = (uint64_t)m.nx * ((uint64_t)y + (uint64_t)m.ny * z);
+            for (int dx = 0; dx < 2 && ix + dx < m.nx; ++dx) {
+                const uint32_t s = start[row + ix + dx], e = start[row + ix + dx + 1];
+                if (s < e) {
+                    any = true;
+                    zmax = fmaxf(zmax, pts[s].z);
+                    zmin = fminf(zmin, pts[e - 1].z);
+                }
+            }
+        }
+    if (!any) {
+        occz[lin] = 0x00FFu;
+        return;
+    }
+    const double zb = m.oz + (double)iz * c;
+    const double step = (double)kZq * c;
+    const double h = ceil(((double)zmax - zb) / step) + 1.0;
+    const double l = floor(((double)zmin - zb) / step) - 1.0;
+    const uint32_t hi = h >= 255.0 ? 255u : (uint32_t)fmax(h, 1.0);
+    const uint32_t lo = l <= 0.0 ? 0u : (uint32_t)fmin(l, 254.0);
+    occz[lin] = (uint16_t)(lo | (hi << 8));
 }
 
 // dilated occupancy: bit for lower corner (ix,iy,iz) = any point in the 2x2x2 block
@@ -220,31 +264,13 @@ k_occ2(const uint32_t *__restrict__ start, CellMap m, uint64_t ncell, uint32_t *
     occ2[w] = bits;
 }
 
-// column z-range map over the dilated occupancy (one thread per column)
-__global__ void __launch_bounds__(kThreads)
-k_colmap(const uint32_t *__restrict__ occ2, CellMap m, int shift, int ncx, int ncy,
-         uint16_t *__restrict__ colmap) {
-    const int c = blockIdx.x * kThreads + threadIdx.x;
-    if (c >= ncx * ncy) return;
-    const int cx = c % ncx, cy = c / ncx;
-    int lo = 255, hi = 0;
-    const int x0 = cx << shift, y0 = cy << shift;
-    const int x1 = min(x0 + (1 << shift), m.nx), y1 = min(y0 + (1 << shift), m.ny);
-    for (int iz = 0; iz < m.nz; ++iz)
-        for (int iy = y0; iy < y1; ++iy)
-            for (int ix = x0; ix < x1; ++ix) {
-                const uint64_t lin = (uint64_t)ix + (uint64_t)m.nx * ((uint64_t)iy + (uint64_t)m.ny * iz);
-                if ((occ2[lin >> 5] >> (lin & 31)) & 1u) {
-                    lo = min(lo, iz);
-                    hi = max(hi, iz);
-                }
-            }
-    colmap[c] = (uint16_t)(lo | (hi << 8));
-}
-
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort) {
     const uint64_t n = v.n;
     hipStream_t st = ctx->stream;
+    // the query kernels address points and cells with 32-bit byte offsets (pcp_stencil.hpp)
+    if (n >= (1ull << 28))
+        return set_err(ctx, PCP_E_INVALID, "index cloud of %llu points exceeds 2^28",
+                       (unsigned long long)n);
     ProfScope prof(ctx, PCP_K_INDEX_BUILD);
     // 1. stage the raw AoS bytes (the PointCloud2 data blob)
     const uint64_t raw_bytes = n * (uint64_t)v.point_step;
@@ -282,7 +308,11 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         PCP_HIP(ctx, g.occ2.ensure(16));
         PCP_HIP(ctx, hipMemsetAsync(g.start.p, 0, 16, st));
         PCP_HIP(ctx, hipMemsetAsync(g.occ2.p, 0, 16, st));
-        g.colmap_ok = false;
+        // one empty z band (lo 255, hi 0) for the single cell
+        PCP_HIP(ctx, g.occz.ensure(16));
+        PCP_HIP(ctx, hipMemsetAsync(g.occz.p, 0xFF, 1, st));
+        PCP_HIP(ctx, hipMemsetAsync(static_cast<char *>(g.occz.p) + 1, 0, 1, st));
+        g.occz_ok = zsort;
         return PCP_OK;
     }
     for (int a = 0; a < 3; ++a) {
@@ -347,27 +377,15 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     hipLaunchKernelGGL(k_occ2, dim3((unsigned)((nw + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                        st, g.start.as<const uint32_t>(), m, ncell, g.occ2.as<uint32_t>());
     PCP_CHECK_LAUNCH(ctx);
-    // 9. column z-range map (fits the LDS budget of the persistent fan kernel: <= 32 KiB)
-    g.colmap_ok = false;
-    if (g.nz <= 255) {
-        for (int sh = 2; sh <= 6; ++sh) {
-            const int ncx = (g.nx + (1 << sh) - 1) >> sh, ncy = (g.ny + (1 << sh) - 1) >> sh;
-            if ((size_t)ncx * ncy * 2 <= 32768) {
-                g.ncx = ncx;
-                g.ncy = ncy;
-                g.col_shift = sh;
-                g.colmap_ok = true;
-                break;
-            }
-        }
-    }
-    if (g.colmap_ok) {
-        const int nc = g.ncx * g.ncy;
-        PCP_HIP(ctx, g.colmap.ensure((size_t)nc * 2 + 16));
-        hipLaunchKernelGGL(k_colmap, dim3((nc + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
-                           g.occ2.as<const uint32_t>(), m, g.col_shift, g.ncx, g.ncy,
-                           g.colmap.as<uint16_t>());
+    // 8b. z band per stencil corner (the fan march's probe), z-sorted indices only
+    g.occz_ok = false;
+    if (zsort) {
+        PCP_HIP(ctx, g.occz.ensure(ncell * sizeof(uint16_t)));
+        hipLaunchKernelGGL(k_occz, dim3((unsigned)((ncell + kThreads - 1) / kThreads)),
+                           dim3(kThreads), 0, st, g.start.as<const uint32_t>(),
+                           g.pts.as<const float4>(), m, c, ncell, g.occz.as<uint16_t>());
         PCP_CHECK_LAUNCH(ctx);
+        g.occz_ok = true;
     }
     PCP_HIP(ctx, hipStreamSynchronize(st));
     return PCP_OK;

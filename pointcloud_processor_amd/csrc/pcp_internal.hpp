@@ -68,17 +68,19 @@ struct GridView {               // POD passed to kernels by value
     uint32_t n_pts;
     // tight bbox of the points, inflated by r_q + margin: samples outside are empty
     double bx0, bx1, by0, by1, bz0, bz1;
-    // column z-range map: for each column of 2^col_shift x 2^col_shift stencil corners, the
-    // lowest (low byte) and highest (high byte) corner z-index whose occ2 bit is set; empty
-    // columns hold lo 255 / hi 0.  A corner outside its column's range is provably empty.
-    const uint16_t *colmap;     // null when disabled (nz > 255 or too large for LDS)
-    int32_t ncx, ncy, col_shift;
     // float copies for the stencil-corner and clip arithmetic: their rounding (~1e-5 m) stays
     // far inside the 1 mm query margin, so the skips remain exact (Terrain index)
     float flo_x, flo_y, flo_z, finv_c;
     float fnx1, fny1, fnz1;     // n - 1 per axis
     float fb[6];                // clip box x0, x1, y0, y1, z0, z1
+    // z band of each stencil corner's 2x2x2 block (z-sorted indices only, else null): u16 =
+    // lo | hi << 8, the block's lowest / highest point z as conservative steps of kZq cells
+    // above the block's floor (lo 0 = unbounded below, hi 255 = unbounded above; lo > hi =
+    // empty block).  fzoff = (r_q + m) / c (stencil-corner offset), fzt = (r_q + 2 mm) / c.
+    const uint16_t *occz;
+    float fzoff, fzt;
 };
+constexpr float kZq = 2.0f / 250.0f;   // z band step, cells (2 cells = 250 steps)
 
 struct GridIndex {
     bool present = false;        // a tree exists (KdTreeFLANN::Ptr non-null)
@@ -87,16 +89,15 @@ struct GridIndex {
     double c = 0.0;
     int32_t nx = 0, ny = 0, nz = 0;
     double bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
-    DevBuf pts, start, occ2, colmap;
-    int32_t ncx = 0, ncy = 0, col_shift = 0;
-    bool colmap_ok = false;
+    DevBuf pts, start, occ2, occz;
+    bool occz_ok = false;
     GridView view() const;
     void release() {
         pts.release();
         start.release();
         occ2.release();
-        colmap.release();
-        colmap_ok = false;
+        occz.release();
+        occz_ok = false;
         present = false;
         n_pts = 0;
     }
@@ -157,7 +158,7 @@ struct pcp_ctx {
     double steps_end = -1e300;               // cached step table
     int steps_K = 0;
     int num_cus = 256;                       // multiprocessors of the device
-    int fan_batch = 1;                       // tuning knob (PCP_FAN_BATCH), A/B only
+    int fan_batch = 0;                       // fan kernel variant (PCP_FAN_BATCH), A/B only
     // filter/merge scratch
     pcp::DevBuf f_in, f_misc;
     std::vector<pcp::CloudBufs> fbuf;        // per-cloud scratch of the filter pipeline

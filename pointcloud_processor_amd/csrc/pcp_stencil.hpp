@@ -46,4 +46,43 @@ __device__ __forceinline__ bool stencil_cell3_f(const GridView &g, float qx, flo
     return true;
 }
 
+// The same test as one predicate (no short-circuit chain: one exec mask instead of three nested
+// branches).  The indices are only meaningful when it returns true.
+__device__ __forceinline__ bool stencil_cell3_fb(const GridView &g, float qx, float qy, float qz,
+                                                 uint32_t &ix, uint32_t &iy, uint32_t &iz) {
+    const float fx = (qx - g.flo_x) * g.finv_c;
+    const float fy = (qy - g.flo_y) * g.finv_c;
+    const float fz = (qz - g.flo_z) * g.finv_c;
+    const bool ok = (fx >= 0.0f) & (fx < g.fnx1) & (fy >= 0.0f) & (fy < g.fny1) & (fz >= 0.0f) &
+                    (fz < g.fnz1);
+    ix = ok ? (uint32_t)fx : 0u;
+    iy = ok ? (uint32_t)fy : 0u;
+    iz = ok ? (uint32_t)fz : 0u;
+    return ok;
+}
+
+// Loads at 32-bit byte offsets from a kernel-argument base: one voffset VGPR and the base in
+// SGPRs (global_load ... v, s[base:base+1]) instead of a 64-bit address add per load.  Valid
+// while the arrays stay below 4 GiB: build_index caps an index at 2^28 points and 2^25 cells.
+__device__ __forceinline__ uint32_t ld_u32o(const uint32_t *base, uint32_t i) {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + (i << 2));
+}
+// three consecutive directory entries (cells c, c+1, c+2 of one stencil row) in ONE load
+// instruction: one L1 tag lookup per lane instead of three (the fan kernel is bound by the
+// texture address / data path, one tag lookup per distinct line per lane and instruction)
+struct U3 {
+    uint32_t a, b, c;
+};
+__device__ __forceinline__ U3 ld_u3o(const uint32_t *base, uint32_t i) {
+    return *reinterpret_cast<const U3 *>(reinterpret_cast<const char *>(base) + (i << 2));
+}
+__device__ __forceinline__ uint32_t ld_u16o(const uint16_t *base, uint32_t i) {
+    return *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(base) + (i << 1));
+}
+__device__ __forceinline__ P3 ld_p3o(const float4 *pts, uint32_t i) {
+    const float *f =
+        reinterpret_cast<const float *>(reinterpret_cast<const char *>(pts) + (i << 4));
+    return P3{f[0], f[1], f[2]};
+}
+
 }  // namespace pcp

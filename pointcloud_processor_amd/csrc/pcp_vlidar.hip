@@ -19,30 +19,15 @@ namespace pcp {
 
 constexpr int kT = 256;
 
-// Lower-corner cell of the 2x2x2 stencil of a query (q - r - margin).  False when the corner
-// falls outside [0, n-2]^3: then the stencil holds only padding / outside cells and no point
-// can be within r (exact skip, see DESIGN.md "Terrain index").
-__device__ __forceinline__ bool stencil_cell3(const GridView &g, float qx, float qy, float qz,
-                                              uint32_t &ix, uint32_t &iy, uint32_t &iz) {
-    const double fx = ((double)qx - g.lo_x) * g.inv_c;
-    const double fy = ((double)qy - g.lo_y) * g.inv_c;
-    const double fz = ((double)qz - g.lo_z) * g.inv_c;
-    if (!(fx >= 0.0 && fx < (double)(g.nx - 1) && fy >= 0.0 && fy < (double)(g.ny - 1) &&
-          fz >= 0.0 && fz < (double)(g.nz - 1)))
-        return false;
-    ix = (uint32_t)fx;
-    iy = (uint32_t)fy;
-    iz = (uint32_t)fz;
-    return true;
-}
-
+// Lower-corner cell of the 2x2x2 stencil of a query (q - r - margin), as one linear index.
+// False when the corner falls outside [0, n-2]^3: then the stencil holds only padding /
+// outside cells and no point can be within r (exact skip, see DESIGN.md "Terrain index").
 __device__ __forceinline__ bool stencil_cell(const GridView &g, float qx, float qy, float qz,
                                              uint32_t &lin) {
     uint32_t ix, iy, iz;
-    if (!stencil_cell3_f(g, qx, qy, qz, ix, iy, iz)) return false;
-    const uint32_t nx = (uint32_t)g.nx, nxy = nx * (uint32_t)g.ny;
-    lin = ix + nx * iy + nxy * iz;
-    return true;
+    const bool ok = stencil_cell3_fb(g, qx, qy, qz, ix, iy, iz);
+    lin = ix + (uint32_t)g.nx * (iy + (uint32_t)g.ny * iz);
+    return ok;
 }
 
 // Exact point tests of an occupied stencil: 2 x 2 rows (y, z) x 2 cells (x) = 8 runs.  Points
@@ -50,8 +35,10 @@ __device__ __forceinline__ bool stencil_cell(const GridView &g, float qx, float 
 // and fl(dz*dz) >= r2: FLANN's accumulator ((0 + dx^2) + dy^2) + dz^2 is >= fl(dz^2) (adding
 // non-negative floats never decreases), and every later point of the run has a larger dz, so
 // none of them can be within r (exact).
-// Latency shape: round 1 = the 12 directory entries; round 2 = the first point of all 8 runs
-// (independent loads; most runs end here); only runs that continue are walked, 2 points/step.
+// Latency shape: round 1 = the 4 rows' directory entries (one 12-byte load per row: cells c,
+// c+1 and the end of c+1); round 2 = the first point of all 8 runs (independent loads; an empty
+// run reads point 0, one line shared by every such lane); only runs that continue are walked,
+// 2 points per step.  Loads use 32-bit offsets from the kernel-argument bases.
 template <bool STATS>
 __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, float qx, float qy,
                                              float qz, float r2, uint32_t *cnt) {
@@ -59,15 +46,17 @@ __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, fl
     uint32_t b[4][3];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const uint32_t row = lin + (r & 1) * nx + (r >> 1) * nxy;
-        b[r][0] = g.start[row];
-        b[r][1] = g.start[row + 1];
-        b[r][2] = g.start[row + 2];
+        const U3 u = ld_u3o(g.start, lin + (r & 1) * nx + (r >> 1) * nxy);
+        b[r][0] = u.a;
+        b[r][1] = u.b;
+        b[r][2] = u.c;
     }
-    const uint32_t last = g.n_pts - 1;
     P3 f[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = ld_p3(g.pts, min(b[i >> 1][i & 1], last));
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t k = b[i >> 1][i & 1];
+        f[i] = ld_p3o(g.pts, k < b[i >> 1][(i & 1) + 1] ? k : 0u);
+    }
     uint32_t live = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -85,8 +74,8 @@ __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, fl
         if (!(live & (1u << i))) continue;
         const uint32_t e = b[i >> 1][(i & 1) + 1];
         for (uint32_t k = b[i >> 1][i & 1] + 1; k < e; k += 2) {
-            const P3 p0 = ld_p3(g.pts, k);
-            const P3 p1 = ld_p3(g.pts, min(k + 1, e - 1));
+            const P3 p0 = ld_p3o(g.pts, k);
+            const P3 p1 = ld_p3o(g.pts, min(k + 1, e - 1));
             if (STATS) cnt[2] += 1;
             if (flann_within(qx, qy, qz, p0, r2)) return true;
             float dz = qz - p0.z;
@@ -102,49 +91,12 @@ __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, fl
 }
 
 // KdTreeFLANN::radiusSearch(q, r) > 0 for r <= the index's stencil radius.
-template <bool STATS>
-__device__ __forceinline__ bool stencil_any_t(const GridView &g, float qx, float qy, float qz,
-                                              float r2, uint32_t *cnt) {
-    uint32_t lin;
-    if (!stencil_cell(g, qx, qy, qz, lin)) return false;
-    if (!((g.occ2[lin >> 5] >> (lin & 31)) & 1u)) return false;
-    if (STATS) cnt[1] += 1;
-    return scan_stencil<STATS>(g, lin, qx, qy, qz, r2, cnt);
-}
-
 __device__ __forceinline__ bool stencil_any(const GridView &g, float qx, float qy, float qz,
                                             float r2) {
-    return stencil_any_t<false>(g, qx, qy, qz, r2, nullptr);
-}
-
-// sample index range [klo, khi] whose positions can lie in the index's clip box
-__device__ __forceinline__ void clip_k(const GridView &g, double px, double py, double pz,
-                                       double dx, double dy, double dz, int K, int &klo,
-                                       int &khi) {
-    double t0 = 0.0, t1 = 1e300;
-    const double p[3] = {px, py, pz}, d[3] = {dx, dy, dz};
-    const double lo[3] = {g.bx0, g.by0, g.bz0}, hi[3] = {g.bx1, g.by1, g.bz1};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        if (d[a] == 0.0) {
-            if (p[a] < lo[a] || p[a] > hi[a]) t1 = -1.0;
-        } else {
-            const double inv = 1.0 / d[a];
-            const double ta = (lo[a] - p[a]) * inv, tb = (hi[a] - p[a]) * inv;
-            t0 = fmax(t0, fmin(ta, tb));
-            t1 = fmin(t1, fmax(ta, tb));
-        }
-    }
-    if (!(t0 <= t1)) {
-        klo = 0;
-        khi = -1;
-        return;
-    }
-    // s_k = 0.5 + 0.3 k up to ~1e-13 and t0/t1 are within a few ulps: widen by one sample
-    const double kl = ceil((t0 - 0.5) / kRayStep) - 1.0;
-    const double kh = floor((t1 - 0.5) / kRayStep) + 1.0;
-    klo = (int)fmin(fmax(kl, 0.0), (double)K);
-    khi = (int)fmin(fmax(kh, -1.0), (double)(K - 1));
+    uint32_t lin;
+    if (!stencil_cell(g, qx, qy, qz, lin)) return false;
+    if (!((ld_u32o(g.occ2, lin >> 5) >> (lin & 31)) & 1u)) return false;
+    return scan_stencil<false>(g, lin, qx, qy, qz, r2, nullptr);
 }
 
 // clip_k in float (approximate reciprocal): the interval is that of a box perturbed by ~1e-5 m;
@@ -180,64 +132,75 @@ __device__ __forceinline__ void clip_kf(const GridView &g, double px, double py,
     khi = (int)fminf(fmaxf(kh, -1.0f), (float)(K - 1));
 }
 
-// checkVisibilityWithRaycasting's march (virtual_lidar.cpp:765-797) from pos along unit dir.
-// Visits samples k with s_k < end; returns the first blocked k or -1.  Samples outside the
-// clip box have no point within r (skipped exactly).  s_k comes from ONE table read at klo and
-// then the same repeated addition that built the table (identical doubles).  Samples are
-// processed 4 at a time: the 4 occupancy words are loaded together, then tested in order.
-// col (optional, LDS copy of g.colmap): a stencil corner outside its column's occupied z-range
-// is empty, decided from LDS without touching the occupancy bits in global memory.
-template <bool STATS, int B = 1, bool FC = true>
-__device__ __forceinline__ int march_t(const GridView &g, double px, double py, double pz,
-                                       double dx, double dy, double dz,
-                                       const double *__restrict__ steps, int K, double end,
-                                       float r2, uint32_t *cnt, const uint16_t *col = nullptr) {
+// checkVisibilityWithRaycasting's march (virtual_lidar.cpp:765-797) from pos along unit dir:
+// the samples s_k < end in order, returns the first blocked k or -1.
+//  * Samples outside the clip box have no point within r (clip_kf, exact skip).
+//  * Probe: sample k's stencil-corner coordinates (cell units) are A + D k, one fma per axis,
+//    instead of the double query point q_k = float(p + d s_k).  Their error against the exact
+//    corner arithmetic is ~1e-5 m, far inside the 1 mm query margin that already absorbs the
+//    float corner: a block found empty from the approximate corner holds no point
+//    within r of q_k.
+//  * ZB (the z-sorted terrain index): the probe reads the corner block's z band (GridView.occz)
+//    and skips q_k when it lies >= r + 2 mm above the block's highest point or below its lowest
+//    -- then dz alone exceeds r for every point of the block, so FLANN's float sum does too.
+//    Without ZB the probe reads the block's occupancy bit.
+//  * A surviving sample computes q_k exactly (s_k is the step table entry: the table was built
+//    by the same repeated additions the reference performs) and scans the block of its exact
+//    corner, so every point test is the reference's test.
+// STATS counts probes, scanned stencils and point tests into cnt[0..2].
+template <bool STATS, bool ZB = true>
+__device__ __forceinline__ int march(const GridView &g, double px, double py, double pz,
+                                     double dx, double dy, double dz,
+                                     const double *__restrict__ steps, int K, double end,
+                                     float r2, uint32_t *cnt = nullptr) {
     int klo, khi;
-    if (FC)
-        clip_kf(g, px, py, pz, dx, dy, dz, K, klo, khi);
-    else
-        clip_k(g, px, py, pz, dx, dy, dz, K, klo, khi);
+    clip_kf(g, px, py, pz, dx, dy, dz, K, klo, khi);
+    if (end < 1e299) {   // s_k < end: k <= (end - 0.5) / 0.3, with one sample of slack
+        const double ke = floor((end - 0.5) / kRayStep) + 1.0;
+        khi = (int)fmin((double)khi, fmax(ke, -1.0));
+    }
     if (klo > khi) return -1;
-    double s = steps[klo];
-    for (int k0 = klo; k0 <= khi; k0 += B) {
-        float qx[B], qy[B], qz[B];
-        uint32_t lin[B], word[B];
-        bool vis[B];
-#pragma unroll
-        for (int i = 0; i < B; ++i) {
-            vis[i] = (k0 + i <= khi) && (s < end);
-            qx[i] = (float)(px + dx * s);
-            qy[i] = (float)(py + dy * s);
-            qz[i] = (float)(pz + dz * s);
-            lin[i] = 0;
-            uint32_t ix = 0, iy = 0, iz = 0;
-            bool in = vis[i] && (FC ? stencil_cell3_f(g, qx[i], qy[i], qz[i], ix, iy, iz)
-                                    : stencil_cell3(g, qx[i], qy[i], qz[i], ix, iy, iz));
-            if (in && col) {
-                const uint32_t zr = col[(iy >> g.col_shift) * (uint32_t)g.ncx + (ix >> g.col_shift)];
-                in = iz >= (zr & 255u) && iz <= (zr >> 8);
-            }
-            lin[i] = ix + (uint32_t)g.nx * (iy + (uint32_t)g.ny * iz);
-            word[i] = in ? g.occ2[lin[i] >> 5] : 0u;
-            s = s + kRayStep;
+    const float fdx = (float)dx, fdy = (float)dy, fdz = (float)dz;
+    const float sc = (float)kRayStep * g.finv_c, h = 0.5f * g.finv_c;   // s_k = 0.5 + 0.3 k
+    const float Dx = fdx * sc, Dy = fdy * sc, Dz = fdz * sc;
+    const float Ax = ((float)px - g.flo_x) * g.finv_c + fdx * h;
+    const float Ay = ((float)py - g.flo_y) * g.finv_c + fdy * h;
+    const float Az = ((float)pz - g.flo_z) * g.finv_c + fdz * h;
+    const uint32_t nx = (uint32_t)g.nx, ny = (uint32_t)g.ny;
+    for (int k = klo; k <= khi; ++k) {
+        const float kf = (float)k;
+        const float fx = __builtin_fmaf(Dx, kf, Ax);
+        const float fy = __builtin_fmaf(Dy, kf, Ay);
+        const float fz = __builtin_fmaf(Dz, kf, Az);
+        const bool ok = (fx >= 0.0f) & (fx < g.fnx1) & (fy >= 0.0f) & (fy < g.fny1) &
+                        (fz >= 0.0f) & (fz < g.fnz1);
+        const uint32_t izc = ok ? (uint32_t)fz : 0u;
+        const uint32_t lin = ok ? (uint32_t)fx + nx * ((uint32_t)fy + ny * izc) : 0u;
+        bool cand;
+        if (ZB) {
+            const uint32_t zz = ok ? ld_u16o(g.occz, lin) : 0x00FFu;
+            const uint32_t lo = zz & 255u, hi = zz >> 8;
+            const float u = fz - (float)izc + g.fzoff;          // (q_z - block floor) / c
+            cand = (lo <= hi) & ((hi == 255u) | (u - (float)hi * kZq < g.fzt)) &
+                   ((lo == 0u) | ((float)lo * kZq - u < g.fzt));
+        } else {
+            const uint32_t word = ok ? ld_u32o(g.occ2, lin >> 5) : 0u;
+            cand = (word >> (lin & 31u)) & 1u;
         }
-#pragma unroll
-        for (int i = 0; i < B; ++i) {
-            if (STATS && vis[i]) cnt[0] += 1;
-            if ((word[i] >> (lin[i] & 31)) & 1u) {
-                if (STATS) cnt[1] += 1;
-                if (scan_stencil<STATS>(g, lin[i], qx[i], qy[i], qz[i], r2, cnt)) return k0 + i;
-            }
+        if (STATS) cnt[0] += 1;
+        if (cand) {
+            const double s = steps[k];
+            if (!(s < end)) return -1;       // every later sample is beyond end too
+            if (STATS) cnt[1] += 1;
+            const float qx = (float)(px + dx * s);
+            const float qy = (float)(py + dy * s);
+            const float qz = (float)(pz + dz * s);
+            uint32_t l2;
+            if (stencil_cell(g, qx, qy, qz, l2) && scan_stencil<STATS>(g, l2, qx, qy, qz, r2, cnt))
+                return k;
         }
-        if (!vis[B - 1]) break;
     }
     return -1;
-}
-
-__device__ __forceinline__ int march(const GridView &g, double px, double py, double pz, double dx,
-                                     double dy, double dz, const double *__restrict__ steps, int K,
-                                     double end, float r2) {
-    return march_t<false>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, nullptr);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -279,7 +242,8 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
     } else if (!E.terrain_present) {
         visible = true;   // (:721, :727, :750)
     } else {
-        visible = march(E.terrain, px, py, pz, ndx, ndy, ndz, E.steps, E.K, end, E.r2_ray) < 0;
+        visible = march<false>(E.terrain, px, py, pz, ndx, ndy, ndz, E.steps, E.K, end,
+                               E.r2_ray) < 0;
     }
     if (!visible) return 0.0;
     bits |= 4u;
@@ -532,29 +496,30 @@ struct FanArgs {
     int uniform_el;        // every wave lies in one elevation ring
     uint32_t rays;
     uint32_t waves;        // waves per pose = ceil(rays / 64)
-    uint32_t items;        // P * ceil(rays / 256) work items of the persistent kernel
-    uint32_t *queue;       // persistent kernel's work-queue head
     float r2;
     int present;
     int16_t *first_hit;
-    uint32_t *wave_blocked;        // [P][waves] per-wave partials (no atomics)
-    uint32_t *wave_units;
-    unsigned long long *stats;     // MODE 1: samples visited, occupied stencils, point tests
+    // per-wave partials {blocked, units}, one 8-byte store per wave (no atomics).  Wave w of
+    // pose p is launch item b = w * P + p; its slot groups the items by XCD (item b runs on XCD
+    // b % 8), so each XCD's L2 fills whole lines before they leave: slot = (b % 8) * per + b / 8
+    uint2 *wave_part;
+    uint32_t P, per_xcd;
+    unsigned long long *stats;     // MODE 1: probes, scanned stencils, point tests
                                    // MODE 2: per-wave s_memtime stamps [P*waves][4]
 };
 
 enum { FAN_PLAIN = 0, FAN_STATS = 1, FAN_STAMPS = 2 };
 
 // one lane = one ray; 64 consecutive azimuths of one elevation ring per wave (coherent
-// termination on near-flat terrain); blockIdx.y = pose.  Each wave writes its blocked-ray
-// count and its sample-query count to its own slot: the per-pose sums are formed by
-// k_fan_reduce in a fixed order (deterministic, no same-address atomics).
-template <int MODE, int B, bool FC = true>
-__device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t rblock,
-                                         const uint16_t *col) {
-    const uint32_t ray = rblock * kT + threadIdx.x;
+// termination on near-flat terrain).  Each wave writes its blocked-ray count and its
+// sample-query count to its own slot: the per-pose sums are formed by k_fan_reduce in a fixed
+// order (deterministic, no same-address atomics).
+template <int MODE, int BS, bool ZB = true>
+__device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t rblock) {
+    const uint32_t ray = rblock * BS + threadIdx.x;
+    const uint32_t wid = ray >> 6;
     const bool active = ray < a.rays;
-    const uint32_t wslot = (uint32_t)p * a.waves + (ray >> 6);
+    const uint32_t wslot = p * a.waves + wid;
     unsigned long long t0 = 0, t1 = 0, t2 = 0;
     if (MODE == FAN_STAMPS) t0 = __builtin_amdgcn_s_memtime();
     int hit = -1;
@@ -574,8 +539,8 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
             asm volatile("" ::"v"(dx), "v"(dy));
             t1 = __builtin_amdgcn_s_memtime();
         }
-        hit = march_t<MODE == FAN_STATS, B, FC>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K,
-                                            1e300, a.r2, cnt, col);
+        hit = march<MODE == FAN_STATS, ZB>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K,
+                                           1e300, a.r2, cnt);
     }
     if (MODE == FAN_STAMPS) {
         asm volatile("" ::"v"(hit));
@@ -586,20 +551,22 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
     uint32_t u = active ? (hit >= 0 ? (uint32_t)hit + 1u : (uint32_t)a.K) : 0u;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o, 64);
-    if ((threadIdx.x & 63) == 0 && (ray >> 6) < a.waves) {
-        a.wave_blocked[wslot] = (uint32_t)__popcll(bal);
-        a.wave_units[wslot] = u;
+    if ((threadIdx.x & 63) == 0 && wid < a.waves) {
+        const uint32_t b = wid * a.P + p;
+        a.wave_part[(size_t)(b & 7u) * a.per_xcd + (b >> 3)] =
+            make_uint2((uint32_t)__popcll(bal), u);
     }
-    if (MODE == FAN_STATS) {
+    if (MODE == FAN_STATS) {   // per-wave slots [3][P * waves], summed by k_sum_u64
+        const size_t nw = (size_t)gridDim.x * (BS / 64);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             unsigned long long v = cnt[q];
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if ((threadIdx.x & 63) == 0) atomicAdd(&a.stats[q], v);
+            if ((threadIdx.x & 63) == 0 && wid < a.waves) a.stats[q * nw + wslot] = v;
         }
     }
-    if (MODE == FAN_STAMPS && (threadIdx.x & 63) == 0 && (ray >> 6) < a.waves) {
+    if (MODE == FAN_STAMPS && (threadIdx.x & 63) == 0 && wid < a.waves) {
         const unsigned long long t3 = __builtin_amdgcn_s_memtime();
         unsigned long long *o = a.stats + 4 * (size_t)wslot;
         o[0] = t0;
@@ -609,67 +576,54 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
     }
 }
 
-// one block per (ray block, pose); no column map
-template <int MODE, int B, bool FC = true>
-__global__ void __launch_bounds__(kT) k_raycast_fan(FanArgs a) {
-    fan_body<MODE, B, FC>(a, blockIdx.y, blockIdx.x, nullptr);
+// The fan kernel: one wave per workgroup (a finished wave's slot refills without waiting for
+// the rest of a workgroup), 1-D grid interleaving the poses (block b = ray block b / P of pose
+// b % P: the waves in flight at any time march the same ring of many poses), capped at 7 waves
+// per SIMD (94 SGPRs; the compiler's own choice, 106, admits only 6).
+template <int MODE, int BS = 64, bool ZB = true>
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(7, 7)))
+k_raycast_fan(FanArgs a, uint32_t P) {
+    fan_body<MODE, BS, ZB>(a, blockIdx.x % P, blockIdx.x / P);
 }
 
-// A/B variants: occupancy forced to W waves per SIMD (register caps; SGPRs count too: a wave
-// slot needs ceil(sgpr/16)*16 + 16 of the 800 SGPRs per SIMD)
-template <int MODE, int W>
-__global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(W, W)))
-k_raycast_fan_w(FanArgs a) {
-    fan_body<MODE, 1, true>(a, blockIdx.y, blockIdx.x, nullptr);
+// A/B: pose-major 2-D grid (blockIdx.y = pose), BS-thread workgroups
+template <int BS, bool ZB>
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(7, 7)))
+k_raycast_fan_pm(FanArgs a) {
+    fan_body<FAN_PLAIN, BS, ZB>(a, blockIdx.y, blockIdx.x);
 }
 
-// A/B variant: the column z-range map read from global memory (22 KB: L1-resident), so samples
-// below / above their column's points skip the occupancy word in L2
-template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan_gc(FanArgs a) {
-    fan_body<MODE, B>(a, blockIdx.y, blockIdx.x, a.g.colmap);
-}
-
-// persistent: a CU-filling grid strides over the (pose, ray block) items; each block stages the
-// column z-range map in LDS once (dynamic LDS, 16-B aligned base per the LDS guideline)
-template <int MODE, int B> __global__ void __launch_bounds__(kT) k_raycast_fan_p(FanArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint16_t s_col[];
-    const uint16_t *col = nullptr;
-    if (a.g.colmap) {
-        const uint32_t n16 = ((uint32_t)(a.g.ncx * a.g.ncy) + 7) / 8;   // uint4 chunks
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.g.colmap);
-        uint4 *dst = reinterpret_cast<uint4 *>(s_col);
-        for (uint32_t k = threadIdx.x; k < n16; k += kT) dst[k] = src[k];
-        __syncthreads();
-        col = s_col;
-    }
-    const uint32_t per_pose = (a.rays + kT - 1) / kT;
-    // dynamic work queue: chunks of 8 items from one head word (zeroed before every launch);
-    // every block exits once the head passes the item count, whatever the residency
-    __shared__ uint32_t s_chunk;
-    for (;;) {
-        if (threadIdx.x == 0) s_chunk = atomicAdd(a.queue, 8u);
-        __syncthreads();
-        const uint32_t c0 = s_chunk;
-        __syncthreads();
-        if (c0 >= a.items) break;
-        const uint32_t c1 = min(c0 + 8u, a.items);
-        for (uint32_t w = c0; w < c1; ++w) {
-            const uint32_t p = w / per_pose;
-            fan_body<MODE, B>(a, p, w - p * per_pose, col);
-        }
+// out[q] = sum of in[q * n .. (q + 1) * n) (one block per q)
+__global__ void __launch_bounds__(1024)
+k_sum_u64(const unsigned long long *__restrict__ in, size_t n, unsigned long long *__restrict__ out) {
+    const unsigned long long *row = in + (size_t)blockIdx.x * n;
+    unsigned long long v = 0;
+    for (size_t k = threadIdx.x; k < n; k += 1024) v += row[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __shared__ unsigned long long sw[16];
+    if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < 16; ++w) t += sw[w];
+        out[blockIdx.x] = t;
     }
 }
 
-// per-pose sums of the per-wave partials, fixed order
+// per-pose sums of the per-wave partials: one block per pose, fixed order (integer sums:
+// exact and deterministic)
 __global__ void __launch_bounds__(kT)
-k_fan_reduce(const uint32_t *__restrict__ wb, const uint32_t *__restrict__ wu, uint32_t waves,
+k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves, uint32_t P, uint32_t per_xcd,
              uint32_t *__restrict__ blocked, unsigned long long *__restrict__ units) {
     const uint32_t p = blockIdx.x;
     uint32_t b = 0;
     unsigned long long u = 0;
     for (uint32_t w = threadIdx.x; w < waves; w += kT) {
-        b += wb[(size_t)p * waves + w];
-        u += wu[(size_t)p * waves + w];
+        const uint32_t it = w * P + p;
+        const uint2 v = part[(size_t)(it & 7u) * per_xcd + (it >> 3)];
+        b += v.x;
+        u += v.y;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -963,9 +917,15 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     }
     PCP_HIP(ctx, ctx->poses_d.ensure(pose8.size() * sizeof(double)));
     const uint32_t waves = (rays + 63) / 64;
+    if ((uint64_t)waves * (uint64_t)P >= (1ull << 31))
+        return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: %d poses x %u rays exceed one launch",
+                       P, rays);
     PCP_HIP(ctx, ctx->out_c.ensure((size_t)P * (sizeof(uint32_t) + sizeof(uint64_t)) + 64));
-    PCP_HIP(ctx, ctx->out_b.ensure((size_t)P * waves * 2 * sizeof(uint32_t) + 64));
-    const size_t stats_bytes = stamps ? (size_t)P * waves * 4 * sizeof(uint64_t) : 64 * sizeof(uint64_t);
+    PCP_HIP(ctx, ctx->out_b.ensure(((size_t)P * waves + 8) * sizeof(uint2)));
+    // stamps: 4 per wave; stats: 3 per wave + the 3 sums
+    const size_t stats_bytes = stamps  ? (size_t)P * waves * 4 * sizeof(uint64_t)
+                               : stats ? ((size_t)P * waves * 3 + 3) * sizeof(uint64_t)
+                                       : 64 * sizeof(uint64_t);
     PCP_HIP(ctx, ctx->stats_d.ensure(stats_bytes));
     PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pose8.data(), pose8.size() * sizeof(double),
                                 hipMemcpyHostToDevice, st));
@@ -978,7 +938,10 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     }
     FanArgs a{};
     a.present = ctx->terrain.present ? 1 : 0;
-    if (a.present) a.g = ctx->terrain.view();
+    if (a.present) {
+        a.g = ctx->terrain.view();
+        if (!a.g.occz) return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: terrain index has no z bands");
+    }
     const double *tab = ctx->fan_tab.as<const double>();
     a.ca = tab;
     a.sa = tab + fan->n_az;
@@ -991,51 +954,40 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     a.uniform_el = (fan->n_az % 64 == 0) ? 1 : 0;
     a.rays = rays;
     a.waves = waves;
+    a.P = (uint32_t)P;
     a.r2 = (float)(kRayRadius * kRayRadius);
     a.first_hit = fh_d;
-    a.wave_blocked = ctx->out_b.as<uint32_t>();
-    a.wave_units = a.wave_blocked + (size_t)P * waves;
+    a.per_xcd = (uint32_t)(((uint64_t)waves * P + 7) / 8);
+    a.wave_part = ctx->out_b.as<uint2>();
     a.stats = ctx->stats_d.as<unsigned long long>();
-    const dim3 grid((rays + kT - 1) / kT, P);
-    const uint32_t per_pose = (rays + kT - 1) / kT;
-    a.items = per_pose * (uint32_t)P;
-    // persistent launch: 6 blocks per CU (the SGPR budget admits 6), column map in LDS
-    const size_t lds = a.g.colmap ? ((size_t)a.g.ncx * a.g.ncy * 2 + 15) / 16 * 16 : 0;
-    int occ_blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_blocks, k_raycast_fan_p<FAN_PLAIN, 1>, kT,
-                                                     lds) != hipSuccess || occ_blocks < 1)
-        occ_blocks = 4;
-    const unsigned pgrid = std::min<unsigned>(a.items, (unsigned)ctx->num_cus * (unsigned)occ_blocks);
-    PCP_HIP(ctx, ctx->out_a.ensure(256));
-    a.queue = ctx->out_a.as<uint32_t>();
-    PCP_HIP(ctx, hipMemsetAsync(a.queue, 0, 16, st));
+    const dim3 grid1(waves * (uint32_t)P);           // 64-thread blocks, pose-interleaved
     if (stats) {
-        PCP_HIP(ctx, hipMemsetAsync(a.stats, 0, 4 * sizeof(uint64_t), st));
-        hipLaunchKernelGGL((k_raycast_fan<FAN_STATS, 1>), grid, dim3(kT), 0, st, a);
+        hipLaunchKernelGGL((k_raycast_fan<FAN_STATS>), grid1, dim3(64), 0, st, a, (uint32_t)P);
         PCP_CHECK_LAUNCH(ctx);
-        PCP_HIP(ctx, hipMemcpyAsync(stats, a.stats, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        const size_t nw = (size_t)P * waves;
+        hipLaunchKernelGGL(k_sum_u64, dim3(3), dim3(1024), 0, st,
+                           (const unsigned long long *)a.stats, nw, a.stats + 3 * nw);
+        PCP_CHECK_LAUNCH(ctx);
+        PCP_HIP(ctx, hipMemcpyAsync(stats, a.stats + 3 * nw, 3 * sizeof(uint64_t),
+                                    hipMemcpyDeviceToHost, st));
     } else if (stamps) {
-        hipLaunchKernelGGL((k_raycast_fan<FAN_STAMPS, 1>), grid, dim3(kT), 0, st, a);
+        hipLaunchKernelGGL((k_raycast_fan<FAN_STAMPS>), grid1, dim3(64), 0, st, a, (uint32_t)P);
         PCP_CHECK_LAUNCH(ctx);
         PCP_HIP(ctx, hipMemcpyAsync(stamps, a.stats, stats_bytes, hipMemcpyDeviceToHost, st));
     } else {
         ProfScope ps(ctx, PCP_K_RAYCAST_FAN);
-        // default: one block per (ray block, pose); PCP_FAN_BATCH selects A/B variants
-        // default: one block per (ray block, pose), capped at 7 waves/SIMD (the compiler's own
-        // choice, 106 SGPRs, admits only 6); PCP_FAN_BATCH selects the A/B variants
+        // PCP_FAN_BATCH selects the A/B variants of DESIGN.md §6b
+        const dim3 grid128((rays + 127) / 128, P);
         switch (ctx->fan_batch) {
-        case 2: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 1>), grid, dim3(kT), 0, st, a); break;
-        case 3: hipLaunchKernelGGL((k_raycast_fan_p<FAN_PLAIN, 1>), dim3(pgrid), dim3(kT), lds, st, a); break;
-        case 4: hipLaunchKernelGGL((k_raycast_fan_p<FAN_PLAIN, 2>), dim3(pgrid), dim3(kT), lds, st, a); break;
-        case 5: hipLaunchKernelGGL((k_raycast_fan_gc<FAN_PLAIN, 1>), grid, dim3(kT), 0, st, a); break;
-        case 7: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 1, false>), grid, dim3(kT), 0, st, a); break;
-        case 8: hipLaunchKernelGGL((k_raycast_fan_w<FAN_PLAIN, 8>), grid, dim3(kT), 0, st, a); break;
-        default: hipLaunchKernelGGL((k_raycast_fan_w<FAN_PLAIN, 7>), grid, dim3(kT), 0, st, a); break;
+        case 1: hipLaunchKernelGGL((k_raycast_fan_pm<128, true>), grid128, dim3(128), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 64, false>), grid1, dim3(64), 0, st, a, (uint32_t)P); break;
+        default: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN>), grid1, dim3(64), 0, st, a, (uint32_t)P); break;
         }
         PCP_CHECK_LAUNCH(ctx);
     }
-    hipLaunchKernelGGL(k_fan_reduce, dim3(P), dim3(kT), 0, st, (const uint32_t *)a.wave_blocked,
-                       (const uint32_t *)a.wave_units, waves, blocked_d, units_d);
+    hipLaunchKernelGGL(k_fan_reduce, dim3(P), dim3(kT), 0, st,
+                       (const uint2 *)a.wave_part, waves, (uint32_t)P, a.per_xcd, blocked_d,
+                       units_d);
     PCP_CHECK_LAUNCH(ctx);
     std::vector<uint64_t> u_h(P);
     PCP_HIP(ctx, hipMemcpyAsync(blocked, blocked_d, (size_t)P * sizeof(uint32_t),

@@ -11,7 +11,7 @@ import torch  # noqa: F401,E402
 
 from pointcloud_processor_amd import _abi, synth  # noqa: E402
 
-variants = [int(v) for v in (sys.argv[1:] or ["1", "2", "4"])]
+variants = [int(v) for v in (sys.argv[1:] or ["0", "1", "2"])]
 sc = synth.terrain_scene()
 p = sc.area[:, :3].astype(np.float64)
 bb = np.array([p[:, 0].min() - .1, p[:, 0].max() + .1, p[:, 1].min() - .1, p[:, 1].max() + .1,
@@ -38,7 +38,8 @@ for rnd in range(12):
             times[v].append(ms / n)
         if ref is None:
             ref = (b, u)
-        assert np.array_equal(b, ref[0]) and np.array_equal(u, ref[1]), v
+        if v < 90:      # >= 90: timing experiments that skip work (results differ)
+            assert np.array_equal(b, ref[0]) and np.array_equal(u, ref[1]), v
 for v in variants:
     t = np.array(times[v])
     print(f"batch={v}: median {np.median(t):.4f} ms  min {t.min():.4f} ms")

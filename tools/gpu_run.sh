@@ -46,8 +46,8 @@ if [ "$WHAT" = traffic ]; then
   step pmc_fan_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fan_fetch -o pmc --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
   step pmc_fan_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_fan_write -o pmc --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
   export PCP_NO_GRAPHS=1   # every pipeline kernel its own dispatch: 1 + 3 + 3 = 7 pipeline runs
-  step pmc_flt_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_flt_fetch -o pmc --output-format csv -- python3 bench.py --mode filter --steps 3 --warmup 1
-  step pmc_flt_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_flt_write -o pmc --output-format csv -- python3 bench.py --mode filter --steps 3 --warmup 1
+  step pmc_flt_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_flt_fetch -o pmc --output-format csv -- python3 bench.py --mode filter --steps 3 --warmup 1 --no-pcie
+  step pmc_flt_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_flt_write -o pmc --output-format csv -- python3 bench.py --mode filter --steps 3 --warmup 1 --no-pcie
   unset PCP_NO_GRAPHS
 fi
 echo "=== done"
