@@ -2,7 +2,7 @@
 """Benchmark of the virtual-LiDAR pose search (BASELINE.json metric, configs[1]).
 
 A step = one pass of the hot path over one batch: the candidate poses of this rank (256 per
-GPU: BASELINE configs[1] at N=1, 4096 over 8 GPUs = configs[3]) each cast the dense
+GPU: BASELINE configs[1] at N=1; --poses-per-gpu 512 on 8 GPUs = configs[3]'s 4096) each cast the dense
 1024 x 256 azimuth x elevation fan against the 1M-point excavation terrain with the
 reference's march rule (virtual_lidar.cpp:765-797), plus ONE collective: all-reduce(MIN)
 of the per-pose blocked-ray counts (RCCL over xGMI when N > 1), then the argmin.
