@@ -303,6 +303,69 @@ def test_raycast_fan_full_size_two_poses(gpu, oracle, loaded, scene, cells):
     np.testing.assert_array_equal(units, r_units)
 
 
+def _clutter_cloud(seed=17):
+    """A volumetric cloud (not a surface): a noisy floor, a dense box of random points, a thin
+    vertical wall and a few isolated points -- cells hold many points spread in z, so the z
+    bands are wide and the run walks go deep."""
+    rng = np.random.default_rng(seed)
+    floor = np.c_[rng.uniform(-6, 6, (60_000, 2)), rng.normal(-1.0, 0.02, 60_000)]
+    box = rng.uniform([-1.5, -1.5, -1.0], [1.5, 1.5, 1.5], (50_000, 3))
+    wall = np.c_[np.full(8_000, 3.0) + rng.normal(0, 0.01, 8_000), rng.uniform(-4, 4, 8_000),
+                 rng.uniform(-1, 2, 8_000)]
+    iso = rng.uniform([-6, -6, -1], [6, 6, 3], (300, 3))
+    pts = np.concatenate([floor, box, wall, iso]).astype(np.float32)
+    out = np.zeros((pts.shape[0], 4), np.float32)
+    out[:, :3] = pts
+    return out
+
+
+@pytest.mark.parametrize("n_az,n_el", [(100, 37), (64, 3)])
+def test_raycast_fan_clutter_and_odd_fans(oracle, n_az, n_el):
+    """Fan sizes that are not multiples of the 64-lane wave (a ring spans waves, partial last
+    wave), against a volumetric cloud; poses inside the box, at its edge, above, below the
+    floor and far outside.  First hits, blocked counts and ray-hit tests bit-exact."""
+    cloud = _clutter_cloud()
+    ctx = _abi.Context(0)
+    try:
+        ctx.set_terrain(cloud)
+        poses = np.array([[0.0, 0.0, 0.2, 0.0, 0.3], [1.5, -1.5, 1.5, 0.0, -2.0],
+                          [-4.0, 2.0, 2.5, 0.0, 1.0], [0.5, 4.0, -1.5, 0.0, 0.0],
+                          [40.0, 40.0, 0.0, 0.0, 0.0], [2.9, 0.0, 0.5, 0.0, 3.1]])
+        fan = _abi.fan_params(n_az=n_az, n_el=n_el)
+        blocked, units, fh, best = ctx.raycast_fan(poses, fan, want_first_hit=True)
+        T = oracle.Cloud(cloud)
+        r_blocked, r_units, r_fh = oracle.raycast_fan(T, poses, n_az, n_el, fan.el_min,
+                                                      fan.el_max, fan.max_distance)
+        np.testing.assert_array_equal(fh, r_fh)
+        np.testing.assert_array_equal(blocked, r_blocked)
+        np.testing.assert_array_equal(units, r_units)
+        assert best == int(np.argmin(r_blocked))
+        assert blocked[4] == 0 and blocked[0] > 0
+    finally:
+        ctx.close()
+
+
+def test_raycast_fan_without_terrain_and_empty(oracle):
+    """No terrain tree: every ray runs to the end unblocked (the reference's visible = true);
+    zero poses: nothing to do, best index -1; an all-NaN terrain: an empty tree."""
+    ctx = _abi.Context(0)
+    try:
+        fan = _abi.fan_params(n_az=128, n_el=16)
+        poses = np.array([[0.0, 0.0, 1.0, 0.0, 0.0], [3.0, 1.0, 2.0, 0.0, 1.0]])
+        K = len(_abi.step_table(fan.max_distance - 0.08))
+        blocked, units, _, best = ctx.raycast_fan(poses, fan)
+        assert blocked.tolist() == [0, 0] and units.tolist() == [128 * 16 * K] * 2
+        assert best == 0
+        b0, u0, _, best0 = ctx.raycast_fan(np.zeros((0, 5)), fan)
+        assert b0.size == 0 and u0.size == 0 and best0 == -1
+        nan_cloud = np.full((1000, 4), np.nan, np.float32)
+        ctx.set_terrain(nan_cloud)
+        blocked, units, fh, _ = ctx.raycast_fan(poses, fan, want_first_hit=True)
+        assert blocked.tolist() == [0, 0] and (fh == -1).all()
+    finally:
+        ctx.close()
+
+
 def _rel_close(a, b, tol=1e-12):
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     return np.all(np.abs(a - b) <= tol * np.maximum(1.0, np.abs(b)))
@@ -335,6 +398,37 @@ def test_score_poses_matches_reference_loop(gpu, oracle, loaded, scene, cells):
                                            scene.zx120_pose5, oracle.vl_params(), flags_r)
     np.testing.assert_array_equal(flags_g, flags_r)
     assert rep2.best_idx == r_rep2.best_idx
+
+
+def test_score_poses_clutter(oracle):
+    """Reference-mode scoring against the volumetric cloud: visibility marches that end at the
+    cell (s_k < L - 0.08), cells inside the clutter, behind the wall and in the open."""
+    cloud = _clutter_cloud(23)
+    rng = np.random.default_rng(5)
+    xyz = np.c_[rng.uniform(-5, 5, (400, 2)), rng.uniform(-1, 1.5, 400)]
+    nrm = rng.normal(size=(400, 3)).astype(np.float32)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    ctx = _abi.Context(0)
+    try:
+        ctx.set_terrain(cloud)
+        ctx.set_cells(xyz, nrm)
+        params = _abi.default_vl_params()
+        poses = np.array([[0.0, 0.0, 2.5, -0.6, 0.0], [-4.0, -4.0, 1.0, -0.2, 0.8],
+                          [4.5, 0.0, 0.5, 0.0, 3.1], [0.0, 5.0, 3.0, -1.2, -1.57]])
+        zx = np.array([-5.0, 5.0, 2.0, -0.5, -0.7])
+        flags_g = np.zeros(400, np.uint8)
+        flags_r = flags_g.copy()
+        tot, cov, rep = ctx.score_poses(poses, zx, params, flags_g)
+        T = oracle.Cloud(cloud)
+        r_tot, r_cov, r_rep = oracle.score_poses(T, None, xyz, nrm, poses, zx, oracle.vl_params(),
+                                                 flags_r)
+        np.testing.assert_array_equal(flags_g, flags_r)
+        np.testing.assert_array_equal(cov, r_cov)
+        assert _rel_close(tot, r_tot)
+        assert rep.best_idx == r_rep.best_idx
+        assert 0 < cov.min() and cov.max() < 400
+    finally:
+        ctx.close()
 
 
 def test_score_poses_edge_states(oracle, scene, cells, aux):
