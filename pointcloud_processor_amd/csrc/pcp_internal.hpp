@@ -50,6 +50,29 @@ struct DevBuf {
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+// pinned (page-locked) host staging buffer (grow-only): small per-call H2D / D2H transfers
+// from it skip the runtime's pageable staging copy
+struct PinnedBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes < 4096 ? 4096 : bytes;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
 // ---------------------------------------------------------------------------------------
 // Uniform-grid spatial index (replaces pcl::KdTreeFLANN).  Points sorted by cell, cell
 // start offsets (prefix sum, ncell+1 entries), and a dilated occupancy bitmask: bit of
@@ -153,6 +176,7 @@ struct pcp_ctx {
     // scratch
     pcp::DevBuf stage, scratch[8];
     pcp::DevBuf fan_tab, poses_d, steps_d, out_a, out_b, out_c, out_d, stats_d;
+    pcp::PinnedBuf fan_host;                 // pinned staging of poses in / counts out
     int32_t fan_naz = -1, fan_nel = -1;      // cached fan direction tables
     double fan_elmin = 0.0, fan_elmax = 0.0;
     double steps_end = -1e300;               // cached step table

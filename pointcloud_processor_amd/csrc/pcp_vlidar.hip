@@ -906,16 +906,18 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     int K = 0;
     int rc = ensure_steps(ctx, fan->max_distance - kVisRadius, &K);
     if (rc) return rc;
-    std::vector<double> pose8((size_t)P * 8);
+    // pinned staging: poses in (P x 8 doubles), then {units u64[P], blocked u32[P]} out
+    PCP_HIP(ctx, ctx->fan_host.ensure((size_t)P * (8 * sizeof(double) + 12) + 64));
+    double *pose8 = ctx->fan_host.as<double>();
     for (int k = 0; k < P; ++k) {
         const double *s = poses5 + 5 * (size_t)k;
-        double *d = pose8.data() + 8 * (size_t)k;
+        double *d = pose8 + 8 * (size_t)k;
         for (int q = 0; q < 5; ++q) d[q] = s[q];
         d[5] = std::cos(s[4]);
         d[6] = std::sin(s[4]);
         d[7] = 0.0;
     }
-    PCP_HIP(ctx, ctx->poses_d.ensure(pose8.size() * sizeof(double)));
+    PCP_HIP(ctx, ctx->poses_d.ensure((size_t)P * 8 * sizeof(double)));
     const uint32_t waves = (rays + 63) / 64;
     if ((uint64_t)waves * (uint64_t)P >= (1ull << 31))
         return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: %d poses x %u rays exceed one launch",
@@ -927,7 +929,7 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
                                : stats ? ((size_t)P * waves * 3 + 3) * sizeof(uint64_t)
                                        : 64 * sizeof(uint64_t);
     PCP_HIP(ctx, ctx->stats_d.ensure(stats_bytes));
-    PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pose8.data(), pose8.size() * sizeof(double),
+    PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pose8, (size_t)P * 8 * sizeof(double),
                                 hipMemcpyHostToDevice, st));
     unsigned long long *units_d = ctx->out_c.as<unsigned long long>();
     uint32_t *blocked_d = reinterpret_cast<uint32_t *>(units_d + P);
@@ -989,16 +991,16 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
                        (const uint2 *)a.wave_part, waves, (uint32_t)P, a.per_xcd, blocked_d,
                        units_d);
     PCP_CHECK_LAUNCH(ctx);
-    std::vector<uint64_t> u_h(P);
-    PCP_HIP(ctx, hipMemcpyAsync(blocked, blocked_d, (size_t)P * sizeof(uint32_t),
-                                hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipMemcpyAsync(u_h.data(), units_d, (size_t)P * sizeof(uint64_t),
-                                hipMemcpyDeviceToHost, st));
+    // units and blocked are adjacent on the device: one copy into the pinned block
+    uint64_t *u_h = reinterpret_cast<uint64_t *>(pose8 + 8 * (size_t)P);
+    const uint32_t *b_h = reinterpret_cast<const uint32_t *>(u_h + P);
+    PCP_HIP(ctx, hipMemcpyAsync(u_h, units_d, (size_t)P * 12, hipMemcpyDeviceToHost, st));
     if (first_hit)
         PCP_HIP(ctx, hipMemcpyAsync(first_hit, fh_d, (size_t)P * rays * sizeof(int16_t),
                                     hipMemcpyDeviceToHost, st));
     PCP_HIP(ctx, hipStreamSynchronize(st));
     prof_resolve(ctx);
+    std::memcpy(blocked, b_h, (size_t)P * sizeof(uint32_t));
     if (units)
         for (int k = 0; k < P; ++k) units[k] = u_h[k];
     if (best_idx) {
