@@ -153,6 +153,28 @@ def test_filter_merge_pipeline(gpu, oracle):
     np.testing.assert_array_equal(out[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
 
 
+def test_filter_merge_full_c3_frame(gpu, oracle):
+    """The whole C3 frame of bench.py --mode filter (2 x 5 M LiDAR-like points, crop + voxel
+    0.05 + transform + colour): every output record bit-exact against the oracle."""
+    import math
+
+    a = synth.lidar_cloud(5_000_000, sensor_height=2.0, seed=1)
+    b = synth.lidar_cloud(5_000_000, sensor_height=3.5, seed=2)
+    yaw = math.radians(30.0)
+    tfs = [((8.0, -3.0, 0.0), (0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2))),
+           ((0.55, 0.4, 3.5), (0.0, math.sin(0.4363 / 2), 0.0, math.cos(0.4363 / 2)))]
+    rgbs = [(255, 0, 0), (0, 0, 255)]
+    out, per = gpu.filter_merge([a, b], [BOX, BOX], 0.05, tfs, rgbs)
+    parts = []
+    for c, tf, rgb in zip([a, b], tfs, rgbs):
+        k = oracle.crop_box(c, BOX)
+        v, _, _, _ = oracle.voxel_grid(c[k], 0.05)
+        parts.append(oracle.transform_rgb(v, *tf, rgb))
+    ref = np.concatenate(parts)
+    assert list(per) == [p.shape[0] for p in parts]
+    np.testing.assert_array_equal(out[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
+
+
 def test_filter_merge_device_graph_replay(gpu, oracle):
     """Device-resident inputs: the pipeline is captured into a hipGraph and replayed; every
     replay must equal the eager host-path result and the oracle."""
@@ -364,6 +386,32 @@ def test_raycast_fan_without_terrain_and_empty(oracle):
         assert blocked.tolist() == [0, 0] and (fh == -1).all()
     finally:
         ctx.close()
+
+
+def test_raycast_fan_full_c2_workload(gpu, oracle, loaded, scene):
+    """The whole headline workload of bench.py (BASELINE configs[1]: 256 candidate poses x the
+    1024 x 256 fan on the 1M-point terrain), every first hit bit-exact against the oracle
+    (67 M rays; the oracle's OpenMP build takes a few seconds on the box's 16 cores)."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    T, _ = loaded
+    poses, _ = bench._poses_for(gpu, bench._grid_bbox(scene.area), scene.zx120_pose5, 256)
+    fan = _abi.fan_params()
+    blocked, units, fh, best = gpu.raycast_fan(poses, fan, want_first_hit=True)
+    oracle.set_threads(16)
+    try:
+        r_blocked, r_units, r_fh = oracle.raycast_fan(T, poses, 1024, 256, fan.el_min,
+                                                      fan.el_max, fan.max_distance)
+    finally:
+        oracle.set_threads(1)
+    assert np.array_equal(blocked, r_blocked) and np.array_equal(units, r_units)
+    bad = np.count_nonzero(fh != r_fh)
+    assert bad == 0, f"{bad} of {fh.size} first hits differ"
+    assert best == int(np.argmin(r_blocked))
 
 
 def _rel_close(a, b, tol=1e-12):
