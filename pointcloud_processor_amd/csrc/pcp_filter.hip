@@ -27,7 +27,10 @@ constexpr int kCropItems = 16;      // points per thread per crop tile
 constexpr int kCropTile = kFT * kCropItems;
 constexpr int kST = 512;            // threads of the sort-tile kernels (8 waves)
 constexpr int kSW = kST / 64;
-constexpr int kSortItems = 8;       // keys per thread per sort tile
+#ifndef PCP_SORT_ITEMS
+#define PCP_SORT_ITEMS 8
+#endif
+constexpr int kSortItems = PCP_SORT_ITEMS;   // keys per thread per sort tile
 constexpr int kSortTile = kST * kSortItems;
 constexpr int kGroup = 16;          // sort tiles per prefix group (radix digit prefix sums)
 constexpr int kDigitBits = 9;       // radix digit: 512 bins, 3 passes for the C3 crop box
@@ -149,7 +152,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds) {
 template <int J, int W>
 __device__ __forceinline__ uint32_t round_offsets(const uint64_t (&bal)[J], uint32_t (*wo)[W]) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    static_assert(J * W == 64, "one wave scans the (round, wave) counts");
+    static_assert(J * W <= 64, "one wave scans the (round, wave) counts");
     if (lane == 0)
 #pragma unroll
         for (int j = 0; j < J; ++j) wo[j][wid] = (uint32_t)__popcll(bal[j]);
@@ -157,14 +160,15 @@ __device__ __forceinline__ uint32_t round_offsets(const uint64_t (&bal)[J], uint
     __shared__ uint32_t tot;
     if (threadIdx.x < 64) {
         const int j = threadIdx.x / W, w = threadIdx.x % W;
-        const uint32_t v = wo[j][w];
+        const bool in = threadIdx.x < J * W;
+        const uint32_t v = in ? wo[j][w] : 0u;
         uint32_t incl = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t u = __shfl_up(incl, o, 64);
             if (threadIdx.x >= o) incl += u;
         }
-        wo[j][w] = incl - v;
+        if (in) wo[j][w] = incl - v;
         if (threadIdx.x == 63) tot = incl;
     }
     __syncthreads();
@@ -906,9 +910,10 @@ static int enqueue_chain(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream
     }
     if (bt.max_passes > 0) {
         ProfScope ps(ctx, PCP_K_VOXEL, st);
-        // sort-tile kernels: LDS admits one block per CU; the clouds share the CUs
+        // sort-tile kernels: LDS admits 8192 / kSortTile blocks per CU; the clouds share the CUs
+        const unsigned per_cu = (unsigned)std::max(1, 8192 / kSortTile);
         const unsigned gx = std::max(1u, std::min<unsigned>(
-                                             bt.max_nt, (unsigned)std::max(ctx->num_cus, 1) / k));
+                                             bt.max_nt, per_cu * (unsigned)std::max(ctx->num_cus, 1) / k));
         for (int pass = 0; pass < bt.max_passes; ++pass) {
             hipLaunchKernelGGL(k_radix_hist, dim3(gx, k), dim3(kST), 0, st, bt.jb, pass);
             PCP_CHECK_LAUNCH(ctx);
