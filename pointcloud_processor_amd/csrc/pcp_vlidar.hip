@@ -580,8 +580,8 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
 // the rest of a workgroup), 1-D grid interleaving the poses (block b = ray block b / P of pose
 // b % P: the waves in flight at any time march the same ring of many poses), capped at 7 waves
 // per SIMD (94 SGPRs; the compiler's own choice, 106, admits only 6).
-template <int MODE, int BS = 64, bool ZB = true>
-__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(7, 7)))
+template <int MODE, int BS = 64, bool ZB = true, int W = 7>
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(W, W)))
 k_raycast_fan(FanArgs a, uint32_t P) {
     fan_body<MODE, BS, ZB>(a, blockIdx.x % P, blockIdx.x / P);
 }
