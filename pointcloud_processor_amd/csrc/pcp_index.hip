@@ -113,20 +113,46 @@ k_extract(const unsigned char *__restrict__ raw, uint64_t n, uint32_t step, uint
     }
 }
 
-__global__ void k_bbox_final(const float *__restrict__ part, const uint32_t *__restrict__ part_n,
-                             int nb, float *__restrict__ out, uint32_t *__restrict__ out_n) {
-    if (threadIdx.x != 0) return;
+// order-free reduction of the k_extract partials (min / max / count), one block
+__global__ void __launch_bounds__(kThreads)
+k_bbox_final(const float *__restrict__ part, const uint32_t *__restrict__ part_n, int nb,
+             float *__restrict__ out, uint32_t *__restrict__ out_n) {
     float r[6] = {FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
     uint32_t c = 0;
-    for (int b = 0; b < nb; ++b) {
+    for (int b = threadIdx.x; b < nb; b += kThreads) {
         for (int a = 0; a < 3; ++a) {
             r[a] = fminf(r[a], part[b * 6 + a]);
             r[3 + a] = fmaxf(r[3 + a], part[b * 6 + 3 + a]);
         }
         c += part_n[b];
     }
-    for (int a = 0; a < 6; ++a) out[a] = r[a];
-    *out_n = c;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            r[a] = fminf(r[a], __shfl_xor(r[a], o, 64));
+            r[3 + a] = fmaxf(r[3 + a], __shfl_xor(r[3 + a], o, 64));
+        }
+        c += __shfl_xor(c, o, 64);
+    }
+    __shared__ float s[6][kThreads / 64];
+    __shared__ uint32_t sc[kThreads / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) {
+        for (int a = 0; a < 6; ++a) s[a][w] = r[a];
+        sc[w] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int ww = 1; ww < kThreads / 64; ++ww) {
+        for (int a = 0; a < 3; ++a) {
+            s[a][0] = fminf(s[a][0], s[a][ww]);
+            s[3 + a][0] = fmaxf(s[3 + a][0], s[3 + a][ww]);
+        }
+        sc[0] += sc[ww];
+    }
+    for (int a = 0; a < 6; ++a) out[a] = s[a][0];
+    *out_n = sc[0];
 }
 
 struct CellMap {
@@ -288,7 +314,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
                        part, part_n);
     PCP_CHECK_LAUNCH(ctx);
     float *bb_d = ctx->stats_d.as<float>();
-    hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(64), 0, st, part, part_n, nb, bb_d,
+    hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(kThreads), 0, st, part, part_n, nb, bb_d,
                        reinterpret_cast<uint32_t *>(bb_d + 8));
     PCP_CHECK_LAUNCH(ctx);
     float bb_h[10];

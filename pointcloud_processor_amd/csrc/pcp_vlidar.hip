@@ -18,6 +18,11 @@
 namespace pcp {
 
 constexpr int kT = 256;
+#ifndef PCP_CELL_PROBES
+// z-band probes issued per round in the cell-scoring march (build knob; 4 measured 130 vs 132
+// us per 256-pose k_score_cells: that march is not probe-latency bound)
+#define PCP_CELL_PROBES 1
+#endif
 
 // Lower-corner cell of the 2x2x2 stencil of a query (q - r - margin), as one linear index.
 // False when the corner falls outside [0, n-2]^3: then the stencil holds only padding /
@@ -148,7 +153,7 @@ __device__ __forceinline__ void clip_kf(const GridView &g, double px, double py,
 //    by the same repeated additions the reference performs) and scans the block of its exact
 //    corner, so every point test is the reference's test.
 // STATS counts probes, scanned stencils and point tests into cnt[0..2].
-template <bool STATS, bool ZB = true>
+template <bool STATS, bool ZB = true, int NB = 1>
 __device__ __forceinline__ int march(const GridView &g, double px, double py, double pz,
                                      double dx, double dy, double dz,
                                      const double *__restrict__ steps, int K, double end,
@@ -167,6 +172,49 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
     const float Ay = ((float)py - g.flo_y) * g.finv_c + fdy * h;
     const float Az = ((float)pz - g.flo_z) * g.finv_c + fdz * h;
     const uint32_t nx = (uint32_t)g.nx, ny = (uint32_t)g.ny;
+    if (NB > 1 && ZB) {
+        // latency-bound callers (few rays in flight): NB probes per round as independent loads,
+        // then taken in sample order -- the same samples, candidates and scans as below
+        for (int k0 = klo; k0 <= khi; k0 += NB) {
+            uint32_t zz[NB], izs[NB];
+            float fzs[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const float kf = (float)(k0 + b);
+                const float fx = __builtin_fmaf(Dx, kf, Ax);
+                const float fy = __builtin_fmaf(Dy, kf, Ay);
+                const float fz = __builtin_fmaf(Dz, kf, Az);
+                const bool ok = (k0 + b <= khi) & (fx >= 0.0f) & (fx < g.fnx1) & (fy >= 0.0f) &
+                                (fy < g.fny1) & (fz >= 0.0f) & (fz < g.fnz1);
+                const uint32_t izc = ok ? (uint32_t)fz : 0u;
+                const uint32_t lin = ok ? (uint32_t)fx + nx * ((uint32_t)fy + ny * izc) : 0u;
+                zz[b] = ok ? ld_u16o(g.occz, lin) : 0x00FFu;
+                izs[b] = izc;
+                fzs[b] = fz;
+            }
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int k = k0 + b;
+                const uint32_t lo = zz[b] & 255u, hi = zz[b] >> 8;
+                const float u = fzs[b] - (float)izs[b] + g.fzoff;
+                const bool cand = (lo <= hi) & ((hi == 255u) | (u - (float)hi * kZq < g.fzt)) &
+                                  ((lo == 0u) | ((float)lo * kZq - u < g.fzt));
+                if (STATS && k <= khi) cnt[0] += 1;
+                if (cand) {
+                    const double s = steps[k];
+                    if (!(s < end)) return -1;
+                    if (STATS) cnt[1] += 1;
+                    const float qx = (float)(px + dx * s);
+                    const float qy = (float)(py + dy * s);
+                    const float qz = (float)(pz + dz * s);
+                    uint32_t l2;
+                    if (stencil_cell(g, qx, qy, qz, l2) && scan_stencil<STATS>(g, l2, qx, qy, qz, r2, cnt))
+                        return k;
+                }
+            }
+        }
+        return -1;
+    }
     for (int k = klo; k <= khi; ++k) {
         const float kf = (float)k;
         const float fx = __builtin_fmaf(Dx, kf, Ax);
@@ -242,8 +290,8 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
     } else if (!E.terrain_present) {
         visible = true;   // (:721, :727, :750)
     } else {
-        visible = march<false>(E.terrain, px, py, pz, ndx, ndy, ndz, E.steps, E.K, end,
-                               E.r2_ray) < 0;
+        visible = march<false, true, PCP_CELL_PROBES>(E.terrain, px, py, pz, ndx, ndy, ndz,
+                                                      E.steps, E.K, end, E.r2_ray) < 0;
     }
     if (!visible) return 0.0;
     bits |= 4u;
@@ -253,58 +301,99 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
     return fmax(0.0, score);
 }
 
-__global__ void __launch_bounds__(kT)
-k_zx120_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict__ cn, int C,
-              double zx, double zy, double zz, double zpitch, double *__restrict__ score_z,
-              uint8_t *__restrict__ zbits) {
-    const int c = blockIdx.x * kT + threadIdx.x;
-    if (c >= C) return;
-    uint32_t bits;
-    const double s = eval_cell(E, zx, zy, zz, zpitch, cxyz[3 * c], cxyz[3 * c + 1], cxyz[3 * c + 2],
-                               cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], true, bits);
-    score_z[c] = s;
-    zbits[c] = (uint8_t)bits;
-}
-
-// one thread per (cell c, pose p); comb/mbits laid out [p][c] (coalesced writes)
+// one thread per (cell c, row r): rows r < P are the candidate poses (evaluatePosition's
+// score_mobile, written [p][c], coalesced), row P is the pose-invariant zx120 evaluation
+// (score_zx120 and its result bits) -- one launch, so the zx120 row does not run alone on a
+// handful of CUs.  std::max(score_zx120, score_mobile) is applied by k_row_sum.
 __global__ void __launch_bounds__(kT)
 k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict__ cn, int C,
-              const double *__restrict__ poses5, const double *__restrict__ score_z,
-              double *__restrict__ comb, uint8_t *__restrict__ mbits) {
+              const double *__restrict__ poses5, int P, const double *__restrict__ zx5,
+              double *__restrict__ sm_out, uint8_t *__restrict__ mbits,
+              double *__restrict__ score_z, uint8_t *__restrict__ zbits) {
     const int c = blockIdx.x * kT + threadIdx.x;
     const int p = blockIdx.y;
     if (c >= C) return;
-    const double *P = poses5 + 5 * (size_t)p;
+    const bool zrow = p == P;
+    const double *Q = zrow ? zx5 : poses5 + 5 * (size_t)p;
     uint32_t bits;
-    const double sm = eval_cell(E, P[0], P[1], P[2], P[3], cxyz[3 * c], cxyz[3 * c + 1],
-                                cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], false, bits);
-    const double sz = score_z[c];
-    comb[(size_t)p * C + c] = (sz < sm) ? sm : sz;   // std::max(score_zx120, score_mobile)
-    mbits[(size_t)p * C + c] = (uint8_t)bits;
+    const double s = eval_cell(E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1],
+                               cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], zrow, bits);
+    if (zrow) {
+        score_z[c] = s;
+        zbits[c] = (uint8_t)bits;
+    } else {
+        sm_out[(size_t)p * C + c] = s;
+        mbits[(size_t)p * C + c] = (uint8_t)bits;
+    }
 }
 
-// ordered sequential sum per row (evaluatePosition :634-645): one wave per row, every lane
-// carries the same running sum so the addition order is exactly the cell order.
-__global__ void __launch_bounds__(kT)
-k_row_sum(const double *__restrict__ rows, int C, int R, double *__restrict__ total,
-          int32_t *__restrict__ covered) {
-    const int r = blockIdx.x * (kT / 64) + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (r >= R) return;
-    const double *row = rows + (size_t)r * C;
+// ordered sequential sum per row (evaluatePosition :634-645): total_score += s for s > 0 in cell
+// order, s = std::max(score_zx120, score_mobile) = (sz < sm) ? sm : sz for a pose row, sz for
+// the zx120 row (r == P).  One wave per row: the lanes stage 512 values at a time in LDS (the
+// next 512 already loading into registers), lane 0 adds them in order -- the chain is the adds.
+constexpr int kSumChunk = 512;
+__global__ void __launch_bounds__(64)
+k_row_sum(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
+          double *__restrict__ total, int32_t *__restrict__ covered) {
+    const int r = blockIdx.x;
+    const int lane = threadIdx.x;
+    const double *row = sm + (size_t)r * C;
+    __shared__ __attribute__((aligned(16))) double buf[kSumChunk];
+    constexpr int kPer = kSumChunk / 64;
+    double v[kPer];
+    int32_t cov = 0;   // order-free: each lane counts its own positive values
+    // x > 0 ? x : +0.0 -- adding +0.0 to the (non-negative) running sum leaves it bit-identical,
+    // so lane 0's unconditional adds are the reference's `if (x > 0) total += x`
+    auto load = [&](int base) {
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const int c = base + q * 64 + lane;
+            double x = 0.0;
+            if (c < C) {
+                const double sz = score_z[c];
+                if (r < P) {
+                    const double m = row[c];
+                    x = (sz < m) ? m : sz;
+                } else {
+                    x = sz;
+                }
+            }
+            const bool pos = x > 0;
+            cov += pos ? 1 : 0;
+            v[q] = pos ? x : 0.0;
+        }
+    };
     double acc = 0.0;
-    int32_t cov = 0;
-    for (int base = 0; base < C; base += 64) {
-        const double v = (base + lane < C) ? row[base + lane] : 0.0;
-        const int m = min(64, C - base);
-        for (int j = 0; j < m; ++j) {
-            const double x = __shfl(v, j, 64);
-            if (x > 0) {
-                acc += x;
-                ++cov;
+    load(0);
+    for (int base = 0; base < C; base += kSumChunk) {
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) buf[q * 64 + lane] = v[q];
+        __syncthreads();
+        if (base + kSumChunk < C) load(base + kSumChunk);   // in flight during the sum
+        if (lane == 0) {   // the chain: dependent adds only; LDS reads run one group ahead
+            const int m = (min(kSumChunk, C - base) + 15) & ~15;   // zero padding adds +0.0
+            const double2 *b2 = reinterpret_cast<const double2 *>(buf);
+            double2 cur[8], nxt[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) cur[q] = b2[q];
+            for (int j = 0; j < m; j += 16) {
+                if (j + 16 < m) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) nxt[q] = b2[(j + 16) / 2 + q];
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    acc += cur[q].x;
+                    acc += cur[q].y;
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
             }
         }
+        __syncthreads();
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cov += __shfl_xor(cov, o, 64);
     if (lane == 0) {
         total[r] = acc;
         covered[r] = cov;
@@ -322,47 +411,54 @@ __global__ void __launch_bounds__(kT)
 k_cell_flags(const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbits, int C, int P,
              uint8_t *__restrict__ flags, int32_t *__restrict__ stats) {
     const int c = blockIdx.x * kT + threadIdx.x;
-    if (c >= C) return;
-    uint32_t f = flags[c];
-    const uint32_t z = zbits[c];
-    f = (z & 1u) ? (f | PCP_F_RANGE_Z) : (f & ~PCP_F_RANGE_Z);
-    if (z & 1u) f = (z & 2u) ? (f | PCP_F_FOV_Z) : (f & ~PCP_F_FOV_Z);
-    if ((z & 3u) == 3u) f = (z & 4u) ? (f | PCP_F_VIS_Z) : (f & ~PCP_F_VIS_Z);
-    // evaluateZX120Only statistics use the zx120 flags right after its evaluation (:377-397)
-    const bool zr = f & PCP_F_RANGE_Z, zf = f & PCP_F_FOV_Z, zv = f & PCP_F_VIS_Z;
-    if (P > 0) {
-        const uint32_t last = mbits[(size_t)(P - 1) * C + c];
-        f = (last & 1u) ? (f | PCP_F_RANGE_M) : (f & ~PCP_F_RANGE_M);
-        for (int p = P - 1; p >= 0; --p) {
-            const uint32_t b = mbits[(size_t)p * C + c];
-            if (b & 1u) {
-                f = (b & 2u) ? (f | PCP_F_FOV_M) : (f & ~PCP_F_FOV_M);
-                break;
+    __shared__ int32_t bst[S_N];
+    if (threadIdx.x < S_N) bst[threadIdx.x] = 0;
+    __syncthreads();
+    if (c < C) {
+        uint32_t f = flags[c];
+        const uint32_t z = zbits[c];
+        f = (z & 1u) ? (f | PCP_F_RANGE_Z) : (f & ~PCP_F_RANGE_Z);
+        if (z & 1u) f = (z & 2u) ? (f | PCP_F_FOV_Z) : (f & ~PCP_F_FOV_Z);
+        if ((z & 3u) == 3u) f = (z & 4u) ? (f | PCP_F_VIS_Z) : (f & ~PCP_F_VIS_Z);
+        // evaluateZX120Only statistics use the zx120 flags right after its evaluation (:377-397)
+        const bool zr = f & PCP_F_RANGE_Z, zf = f & PCP_F_FOV_Z, zv = f & PCP_F_VIS_Z;
+        if (P > 0) {
+            // the last pose that reached each assignment, newest first, 16 poses per round of
+            // independent loads (coalesced over the cells of the block)
+            const uint32_t lastb = mbits[(size_t)(P - 1) * C + c];
+            f = (lastb & 1u) ? (f | PCP_F_RANGE_M) : (f & ~PCP_F_RANGE_M);
+            int fov_from = -1, vis_from = -1;   // pose whose bits set the flag
+            for (int p0 = P - 1; p0 >= 0 && (fov_from < 0 || vis_from < 0); p0 -= 16) {
+                uint32_t b[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    b[q] = (p0 - q >= 0) ? mbits[(size_t)(p0 - q) * C + c] : 0u;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    if (fov_from < 0 && (b[q] & 1u)) fov_from = p0 - q, f = (b[q] & 2u) ? (f | PCP_F_FOV_M) : (f & ~PCP_F_FOV_M);
+                    if (vis_from < 0 && (b[q] & 3u) == 3u) vis_from = p0 - q, f = (b[q] & 4u) ? (f | PCP_F_VIS_M) : (f & ~PCP_F_VIS_M);
+                }
+                if (p0 - 15 <= 0) break;
             }
         }
-        for (int p = P - 1; p >= 0; --p) {
-            const uint32_t b = mbits[(size_t)p * C + c];
-            if ((b & 3u) == 3u) {
-                f = (b & 4u) ? (f | PCP_F_VIS_M) : (f & ~PCP_F_VIS_M);
-                break;
-            }
-        }
+        flags[c] = (uint8_t)f;
+        atomicAdd(&bst[S_TOTAL], 1);
+        if (zr) atomicAdd(&bst[S_ZR], 1);
+        if (zf) atomicAdd(&bst[S_ZF], 1);
+        if (zv) atomicAdd(&bst[S_ZV], 1);
+        if (!zr) atomicAdd(&bst[S_ZB], 1);
+        else if (!zf) atomicAdd(&bst[S_ZY], 1);
+        else if (!zv) atomicAdd(&bst[S_ZRED], 1);
+        else atomicAdd(&bst[S_ZG], 1);
+        const bool mr = f & PCP_F_RANGE_M, mf = f & PCP_F_FOV_M, mv = f & PCP_F_VIS_M;
+        const bool zr2 = f & PCP_F_RANGE_Z, zf2 = f & PCP_F_FOV_Z, zv2 = f & PCP_F_VIS_Z;
+        if (!zr2 && !mr) atomicAdd(&bst[S_B], 1);
+        else if (!zf2 && !mf) atomicAdd(&bst[S_Y], 1);
+        else if (!zv2 && !mv) atomicAdd(&bst[S_RED], 1);
+        else atomicAdd(&bst[S_G], 1);
     }
-    flags[c] = (uint8_t)f;
-    atomicAdd(&stats[S_TOTAL], 1);
-    if (zr) atomicAdd(&stats[S_ZR], 1);
-    if (zf) atomicAdd(&stats[S_ZF], 1);
-    if (zv) atomicAdd(&stats[S_ZV], 1);
-    if (!zr) atomicAdd(&stats[S_ZB], 1);
-    else if (!zf) atomicAdd(&stats[S_ZY], 1);
-    else if (!zv) atomicAdd(&stats[S_ZRED], 1);
-    else atomicAdd(&stats[S_ZG], 1);
-    const bool mr = f & PCP_F_RANGE_M, mf = f & PCP_F_FOV_M, mv = f & PCP_F_VIS_M;
-    const bool zr2 = f & PCP_F_RANGE_Z, zf2 = f & PCP_F_FOV_Z, zv2 = f & PCP_F_VIS_Z;
-    if (!zr2 && !mr) atomicAdd(&stats[S_B], 1);
-    else if (!zf2 && !mf) atomicAdd(&stats[S_Y], 1);
-    else if (!zv2 && !mv) atomicAdd(&stats[S_RED], 1);
-    else atomicAdd(&stats[S_G], 1);
+    __syncthreads();
+    if (threadIdx.x < S_N && bst[threadIdx.x]) atomicAdd(&stats[threadIdx.x], bst[threadIdx.x]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -776,7 +872,7 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     VisEnv E = make_env(ctx, p, ctx->steps_d.as<const double>(), K);
     // buffers
     const size_t pc = (size_t)P * (size_t)C;
-    PCP_HIP(ctx, ctx->poses_d.ensure((size_t)P * 5 * sizeof(double) + 16));
+    PCP_HIP(ctx, ctx->poses_d.ensure((size_t)(P + 1) * 5 * sizeof(double) + 16));
     PCP_HIP(ctx, ctx->out_a.ensure(pc * sizeof(double) + (size_t)C * sizeof(double) + 64));
     PCP_HIP(ctx, ctx->out_b.ensure(pc + (size_t)C * 2 + 64));
     PCP_HIP(ctx, ctx->out_c.ensure((size_t)(P + 1) * (sizeof(double) + sizeof(int32_t)) + 64));
@@ -791,32 +887,26 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     int32_t *stats = ctx->stats_d.as<int32_t>();
     if (P) PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, poses5, (size_t)P * 5 * sizeof(double),
                                        hipMemcpyHostToDevice, st));
+    // the zx120 pose rides behind the candidates (row P of k_score_cells)
+    PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.as<double>() + 5 * (size_t)P, zx, 5 * sizeof(double),
+                                hipMemcpyHostToDevice, st));
     if (C) PCP_HIP(ctx, hipMemcpyAsync(flags_d, cell_flags, C, hipMemcpyHostToDevice, st));
     PCP_HIP(ctx, hipMemsetAsync(stats, 0, 64 * sizeof(int32_t), st));
     const unsigned cb = (unsigned)((C + kT - 1) / kT);
     if (C) {
         {
-            ProfScope ps(ctx, PCP_K_ZX120_CELLS);
-            hipLaunchKernelGGL(k_zx120_cells, dim3(cb), dim3(kT), 0, st, E,
-                               ctx->cells_xyz.as<const double>(), ctx->cells_nrm.as<const float>(),
-                               C, zx[0], zx[1], zx[2], zx[3], score_z, zbits);
-            PCP_CHECK_LAUNCH(ctx);
-        }
-        if (P) {
             ProfScope ps(ctx, PCP_K_SCORE_CELLS);
-            hipLaunchKernelGGL(k_score_cells, dim3(cb, P), dim3(kT), 0, st, E,
+            hipLaunchKernelGGL(k_score_cells, dim3(cb, P + 1), dim3(kT), 0, st, E,
                                ctx->cells_xyz.as<const double>(), ctx->cells_nrm.as<const float>(),
-                               C, ctx->poses_d.as<const double>(), (const double *)score_z, comb,
-                               mbits);
+                               C, ctx->poses_d.as<const double>(), P,
+                               ctx->poses_d.as<const double>() + 5 * (size_t)P, comb, mbits,
+                               score_z, zbits);
             PCP_CHECK_LAUNCH(ctx);
         }
         {
             ProfScope ps(ctx, PCP_K_POSE_SUM);
-            if (P)
-                hipLaunchKernelGGL(k_row_sum, dim3((P + 3) / 4), dim3(kT), 0, st,
-                                   (const double *)comb, C, P, tot_d, cov_d);
-            hipLaunchKernelGGL(k_row_sum, dim3(1), dim3(kT), 0, st, (const double *)score_z, C, 1,
-                               tot_d + P, cov_d + P);
+            hipLaunchKernelGGL(k_row_sum, dim3(P + 1), dim3(64), 0, st, (const double *)comb,
+                               (const double *)score_z, C, P, tot_d, cov_d);
             PCP_CHECK_LAUNCH(ctx);
         }
         {

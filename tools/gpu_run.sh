@@ -18,7 +18,7 @@ step() {  # name, seconds, command...
 }
 WHAT=${1:-all}
 if [ "$WHAT" = all ] || [ "$WHAT" = test ]; then
-  step pytest_gpu 900 python -m pytest tests -q -m gpu -rf
+  step pytest_gpu 900 python -u -m pytest tests -v -m gpu -rf --timeout 300 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
