@@ -141,7 +141,8 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # PCP_LIB: another build of the same library (A/B timing of kernel variants)
+    p = Path(path) if path else Path(os.environ.get("PCP_LIB", LIB_PATH))
     if not p.exists():
         raise OSError(f"libpcp.so not found at {p}: run __graft_entry__.build() "
                       f"(make -C pointcloud_processor_amd/csrc)")
