@@ -454,7 +454,7 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     const uint64_t n = in->n;
     // ---- index of the input (radius = terrain_search_radius); the raw records stay staged
     // in ctx->stage (build_index's H2D copy) for the per-point passes below
-    if ((rc = build_index(ctx, ctx->carve, *in, p->terrain_search_radius, false))) return rc;
+    if ((rc = build_index(ctx, ctx->carve, *in, p->terrain_search_radius, false, false))) return rc;
     const GridView g = ctx->carve.view();
     CarveArgs a{};
     a.raw = ctx->stage.as<const unsigned char>();

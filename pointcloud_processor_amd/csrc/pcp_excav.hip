@@ -378,8 +378,8 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     if (area->n == 0) return PCP_OK;   // :168, nothing is rebuilt; the previous cells stay
     ProfScope prof(ctx, PCP_K_EXCAV_SETUP);
     const double r_near = grid_resolution * 1.5;
-    if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius, false))) return rc;
-    if ((rc = build_index(ctx, ctx->exc_near, *area, r_near, false))) return rc;
+    if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius, false, false))) return rc;
+    if ((rc = build_index(ctx, ctx->exc_near, *area, r_near, false, false))) return rc;
     const uint64_t n = area->n;
     PCP_HIP(ctx, ctx->area_nrm.ensure(n * 3 * sizeof(float) + 16));
     // non-finite points are not in the index: PCL gives them a NaN normal

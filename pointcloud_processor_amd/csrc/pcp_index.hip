@@ -19,7 +19,7 @@ GridView GridIndex::view() const {
     GridView v{};
     v.pts = pts.as<const float4>();
     v.start = start.as<const uint32_t>();
-    v.occ2 = occ2.as<const uint32_t>();
+    v.occ2 = occ2_ok ? occ2.as<const uint32_t>() : nullptr;
     v.c = c;
     v.inv_c = c > 0 ? 1.0 / c : 0.0;
     v.ox = bmin[0] - c;   // one padding cell below the points
@@ -171,6 +171,20 @@ __device__ __forceinline__ uint32_t cell_of(const CellMap &m, float x, float y, 
     return (uint32_t)ix + (uint32_t)m.nx * ((uint32_t)iy + (uint32_t)m.ny * (uint32_t)iz);
 }
 
+// the active lanes of the wave holding the same 32-bit key as this lane.  Big cells (the 1.5 m
+// normal index is a 3 m grid) put many points of a wave into one cell, where per-lane atomics on
+// one counter serialize; one atomic per group of equal keys avoids that.
+__device__ __forceinline__ uint64_t peer_mask(uint32_t key) {
+    uint64_t same = __ballot(1);
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+        const bool bit = (key >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        same &= bit ? bb : ~bb;
+    }
+    return same;
+}
+
 __global__ void __launch_bounds__(kThreads)
 k_cell_count(const float4 *__restrict__ xyz, uint64_t n, CellMap m, uint32_t *__restrict__ cid,
              uint32_t *__restrict__ count) {
@@ -183,7 +197,9 @@ k_cell_count(const float4 *__restrict__ xyz, uint64_t n, CellMap m, uint32_t *__
     }
     const uint32_t c = cell_of(m, p.x, p.y, p.z);
     cid[i] = c;
-    atomicAdd(&count[c], 1u);
+    const uint64_t peers = peer_mask(c);
+    if ((threadIdx.x & 63) == (uint32_t)(__ffsll((long long)peers) - 1))
+        atomicAdd(&count[c], (uint32_t)__popcll(peers));
 }
 
 __global__ void __launch_bounds__(kThreads)
@@ -193,8 +209,14 @@ k_cell_scatter(const float4 *__restrict__ xyz, uint64_t n, const uint32_t *__res
     if (i >= n) return;
     const uint32_t c = cid[i];
     if (c == 0xFFFFFFFFu) return;
-    const uint32_t pos = atomicAdd(&cursor[c], 1u);
-    out[pos] = xyz[i];
+    // one atomic per group of lanes sharing the cell (the order inside a cell is free: z-sorted
+    // indices re-rank by (z, index), the others are queried order-free)
+    const uint64_t peers = peer_mask(c);
+    const int lane = threadIdx.x & 63, leader = __ffsll((long long)peers) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&cursor[c], (uint32_t)__popcll(peers));
+    base = __shfl(base, leader, 64);
+    out[base + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull))] = xyz[i];
 }
 
 // points of each cell in descending z: lets a query stop scanning a cell at the first point
@@ -290,7 +312,8 @@ k_occ2(const uint32_t *__restrict__ start, CellMap m, uint64_t ncell, uint32_t *
     occ2[w] = bits;
 }
 
-int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort) {
+int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort,
+                bool occ) {
     const uint64_t n = v.n;
     hipStream_t st = ctx->stream;
     // the query kernels address points and cells with 32-bit byte offsets (pcp_stencil.hpp)
@@ -334,6 +357,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         PCP_HIP(ctx, g.occ2.ensure(16));
         PCP_HIP(ctx, hipMemsetAsync(g.start.p, 0, 16, st));
         PCP_HIP(ctx, hipMemsetAsync(g.occ2.p, 0, 16, st));
+        g.occ2_ok = true;
         // one empty z band (lo 255, hi 0) for the single cell
         PCP_HIP(ctx, g.occz.ensure(16));
         PCP_HIP(ctx, hipMemsetAsync(g.occz.p, 0xFF, 1, st));
@@ -397,12 +421,16 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
                            g.start.as<const uint32_t>(), g.pts.as<float4>());
         PCP_CHECK_LAUNCH(ctx);
     }
-    // 8. dilated occupancy
-    const uint64_t nw = (ncell + 31) / 32;
-    PCP_HIP(ctx, g.occ2.ensure(nw * sizeof(uint32_t)));
-    hipLaunchKernelGGL(k_occ2, dim3((unsigned)((nw + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                       st, g.start.as<const uint32_t>(), m, ncell, g.occ2.as<uint32_t>());
-    PCP_CHECK_LAUNCH(ctx);
+    // 8. dilated occupancy (one pass over every cell: only for indices that stencil_any queries)
+    g.occ2_ok = false;
+    if (occ) {
+        const uint64_t nw = (ncell + 31) / 32;
+        PCP_HIP(ctx, g.occ2.ensure(nw * sizeof(uint32_t)));
+        hipLaunchKernelGGL(k_occ2, dim3((unsigned)((nw + kThreads - 1) / kThreads)), dim3(kThreads),
+                           0, st, g.start.as<const uint32_t>(), m, ncell, g.occ2.as<uint32_t>());
+        PCP_CHECK_LAUNCH(ctx);
+        g.occ2_ok = true;
+    }
     // 8b. z band per stencil corner (the fan march's probe), z-sorted indices only
     g.occz_ok = false;
     if (zsort) {
@@ -430,7 +458,8 @@ int pcp_set_terrain(pcp_ctx *ctx, const pcp_cloud_view *terrain) {
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     ctx->terrain_cloud_n = terrain->n;
     if (terrain->n == 0) return PCP_OK;   // terrainCallback: no rebuild on an empty cloud
-    rc = build_index(ctx, ctx->terrain, *terrain, kRayRadius);
+    // the march probes the z bands; occupancy bits only for the fan's A/B variant 2
+    rc = build_index(ctx, ctx->terrain, *terrain, kRayRadius, true, ctx->fan_batch == 2);
     prof_resolve(ctx);
     return rc;
 }

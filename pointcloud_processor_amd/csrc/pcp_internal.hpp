@@ -114,6 +114,7 @@ struct GridIndex {
     double bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
     DevBuf pts, start, occ2, occz;
     bool occz_ok = false;
+    bool occ2_ok = false;        // occ2 built (only indices queried by stencil_any need it)
     GridView view() const;
     void release() {
         pts.release();
@@ -227,8 +228,9 @@ void prof_resolve(pcp_ctx *ctx);   // after a stream sync
 // index ----------------------------------------------------------------------------------
 // zsort: points of each cell in descending z (needed by scan_stencil's early exit: the
 // terrain and aux indices); the other indices' queries are order-free
+// occ: build the dilated occupancy bits (stencil_any: the aux index; the fan's A/B variant 2)
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
-                bool zsort = true);
+                bool zsort = true, bool occ = true);
 
 // scan: exclusive prefix sum of n uint32 values into out (n + 1 entries, out[n] = total).
 // tmp must hold scan_tmp_bytes(n).

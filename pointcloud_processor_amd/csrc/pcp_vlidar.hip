@@ -1033,6 +1033,8 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     if (a.present) {
         a.g = ctx->terrain.view();
         if (!a.g.occz) return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: terrain index has no z bands");
+        if (ctx->fan_batch == 2 && !a.g.occ2)
+            return set_err(ctx, PCP_E_STATE, "pcp_raycast_fan: variant 2 needs a terrain set with PCP_FAN_BATCH=2");
     }
     const double *tab = ctx->fan_tab.as<const double>();
     a.ca = tab;
