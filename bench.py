@@ -79,6 +79,11 @@ def _traffic_from_profiles(workload_key: str):
         return None
 
 
+def _gbs(nbytes, seconds):
+    """Bytes per launch / launch time in GB/s (None when either is unknown)."""
+    return nbytes / seconds / 1e9 if nbytes and seconds else None
+
+
 def _host_cpu():
     model = None
     try:
@@ -200,6 +205,11 @@ def run_fan(args, torch, dist, world, rank, local):
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": _traffic_from_profiles("fan"),
+            # the survey's model charges 64 B to every sample query the reference would make;
+            # the kernel skips ~95 % of them exactly, so frac > 1.  What it really moves:
+            "traffic_gbs": _gbs(_traffic_from_profiles("fan"), avg_kernel_s),
+            "limiter": "vector-memory address/data path of dependent L2 gathers (TA 83 %, TD "
+                       "93 % busy, profiles/r01_fan_pmc.txt), not HBM",
             "kernel": "k_raycast_fan<0, 64, true>", "avg_kernel_ms": avg_kernel_s * 1e3,
             "alg_bytes_per_launch": alg_bytes,
             "model": "64 B/sample query + 12 B/point test (SURVEY 8d)",
@@ -325,6 +335,9 @@ def run_filter(args, torch, dist, world, rank, local):
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": alg / (step_dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic": _traffic_from_profiles("filter"),
+                     "traffic_gbs": _gbs(_traffic_from_profiles("filter"), step_dev_ms * 1e-3),
+                     "limiter": "crop streams at ~4.8 TB/s; the voxel stage (sort of the ~1 M "
+                                "cropped points) is launch- and latency-bound",
                      "kernel": "filter_merge graph (all stages)", "avg_kernel_ms": step_dev_ms,
                      "eager_stage_ms": stages,
                      "model": "12 B/input point + 16 B/output point (SURVEY 8d)"},
