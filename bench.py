@@ -38,8 +38,11 @@ def _dist_init(n_gpus: int):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        # one process per GPU over RCCL; PCP_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
+        backend = os.environ.get("PCP_DIST_BACKEND",
+                                 "nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
+            local = local % max(torch.cuda.device_count(), 1)
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
     return torch, (dist if world > 1 else None), world, rank, local
