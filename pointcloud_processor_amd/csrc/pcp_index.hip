@@ -287,29 +287,28 @@ k_occz(const uint32_t *__restrict__ start, const float4 *__restrict__ pts, CellM
 // dilated occupancy: bit for lower corner (ix,iy,iz) = any point in the 2x2x2 block
 __global__ void __launch_bounds__(kThreads)
 k_occ2(const uint32_t *__restrict__ start, CellMap m, uint64_t ncell, uint32_t *__restrict__ occ2) {
-    const uint64_t w = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    const uint64_t nw = (ncell + 31) / 32;
-    if (w >= nw) return;
-    uint32_t bits = 0;
-    const uint64_t sxy = (uint64_t)m.nx * m.ny;
-    for (int b = 0; b < 32; ++b) {
-        const uint64_t c = w * 32 + b;
-        if (c >= ncell) break;
+    // one thread per cell (its 4 block rows are independent loads), a wave's 64 bits by ballot
+    const uint64_t c = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    bool any = false;
+    if (c < ncell) {
         const int ix = (int)(c % m.nx);
         const int iy = (int)((c / m.nx) % m.ny);
-        const int iz = (int)(c / sxy);
-        bool any = false;
-        for (int dz = 0; dz < 2 && !any; ++dz)
-            for (int dy = 0; dy < 2 && !any; ++dy) {
-                const int y = iy + dy, z = iz + dz;
-                if (y >= m.ny || z >= m.nz) continue;
+        const int iz = (int)(c / ((uint64_t)m.nx * m.ny));
+        const int x1 = min(ix + 2, m.nx);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int y = iy + (r & 1), z = iz + (r >> 1);
+            if (y < m.ny && z < m.nz) {
                 const uint64_t row = (uint64_t)m.nx * ((uint64_t)y + (uint64_t)m.ny * z);
-                const int x1 = min(ix + 2, m.nx);
-                if (start[row + x1] > start[row + ix]) any = true;
+                any |= start[row + x1] > start[row + ix];
             }
-        if (any) bits |= 1u << b;
+        }
     }
-    occ2[w] = bits;
+    const uint64_t bits = __ballot(any);
+    const uint64_t w = c >> 5;   // the wave's first word (64-cell aligned)
+    const uint64_t nw = (ncell + 31) / 32;
+    if ((threadIdx.x & 63) == 0 && w < nw) occ2[w] = (uint32_t)bits;
+    if ((threadIdx.x & 63) == 0 && w + 1 < nw) occ2[w + 1] = (uint32_t)(bits >> 32);
 }
 
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort,
@@ -426,8 +425,9 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     if (occ) {
         const uint64_t nw = (ncell + 31) / 32;
         PCP_HIP(ctx, g.occ2.ensure(nw * sizeof(uint32_t)));
-        hipLaunchKernelGGL(k_occ2, dim3((unsigned)((nw + kThreads - 1) / kThreads)), dim3(kThreads),
-                           0, st, g.start.as<const uint32_t>(), m, ncell, g.occ2.as<uint32_t>());
+        hipLaunchKernelGGL(k_occ2, dim3((unsigned)((ncell + kThreads - 1) / kThreads)),
+                           dim3(kThreads), 0, st, g.start.as<const uint32_t>(), m, ncell,
+                           g.occ2.as<uint32_t>());
         PCP_CHECK_LAUNCH(ctx);
         g.occ2_ok = true;
     }
