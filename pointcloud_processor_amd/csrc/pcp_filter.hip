@@ -23,8 +23,12 @@
 namespace pcp {
 
 constexpr int kFT = 256;            // threads per block
-constexpr int kCropItems = 16;      // points per thread per crop tile
-constexpr int kCropTile = kFT * kCropItems;
+#ifndef PCP_CROP_THREADS
+#define PCP_CROP_THREADS 256
+#endif
+constexpr int kCT = PCP_CROP_THREADS;   // threads of a crop block (build knob)
+constexpr int kCropTile = 4096;         // points per crop tile
+constexpr int kCropItems = kCropTile / kCT;   // points per thread per crop tile
 constexpr int kST = 512;            // threads of the sort-tile kernels (8 waves)
 constexpr int kSW = kST / 64;
 #ifndef PCP_SORT_ITEMS
@@ -73,7 +77,7 @@ __device__ __forceinline__ void load_xyz(const CloudIn &c, uint64_t i, float &x,
     }
 }
 
-// a crop tile's points: item j of thread t is base + j*kFT + t (coalesced); indices past the
+// a crop tile's points: item j of thread t is base + j*kCT + t (coalesced); indices past the
 // end are clamped to the last point (the caller masks them)
 template <bool PXYZ16>
 __device__ __forceinline__ void load_tile(const CloudIn &c, uint64_t base, float (&x)[kCropItems],
@@ -81,7 +85,7 @@ __device__ __forceinline__ void load_tile(const CloudIn &c, uint64_t base, float
     const uint64_t last = c.n - 1;
 #pragma unroll
     for (int j = 0; j < kCropItems; ++j) {
-        const uint64_t i = min(base + (uint64_t)j * kFT + threadIdx.x, last);
+        const uint64_t i = min(base + (uint64_t)j * kCT + threadIdx.x, last);
         if constexpr (PXYZ16) {
             const float4 v = reinterpret_cast<const float4 *>(c.raw)[i];
             x[j] = v.x;
@@ -229,7 +233,7 @@ struct JobBatch {
 
 // ---- crop: one read of the input; stable compaction of each tile into its own slot of a
 //      sparse buffer (kept count + bbox partial per tile); k_compact_keys closes the gaps ----
-__global__ void __launch_bounds__(kFT) k_crop_tile(const JobBatch jobs) {
+__global__ void __launch_bounds__(kCT) k_crop_tile(const JobBatch jobs) {
     const CloudJob &J = jobs.j[blockIdx.y];
     if (blockIdx.x >= J.nb) return;
     const CloudIn c = J.in;
@@ -251,12 +255,12 @@ __global__ void __launch_bounds__(kFT) k_crop_tile(const JobBatch jobs) {
     uint32_t keep = 0;
 #pragma unroll
     for (int j = 0; j < kCropItems; ++j) {
-        const uint64_t i = base + (uint64_t)j * kFT + threadIdx.x;
+        const uint64_t i = base + (uint64_t)j * kCT + threadIdx.x;
         const bool k = i < c.n && in_box(b, x[j], y[j], z[j]);
         keep |= (k ? 1u : 0u) << j;
         bal[j] = __ballot(k);
     }
-    __shared__ uint32_t wo[kCropItems][kFT / 64];
+    __shared__ uint32_t wo[kCropItems][kCT / 64];
     const uint32_t tot = round_offsets(bal, wo);
     if (threadIdx.x == 0) counts[blockIdx.x] = tot;
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
@@ -265,7 +269,7 @@ __global__ void __launch_bounds__(kFT) k_crop_tile(const JobBatch jobs) {
         if (!((keep >> j) & 1u)) continue;
         const uint32_t d = wo[j][wid] + (uint32_t)__popcll(bal[j] & lanemask_lt(lane));
         sparse[base + d] = make_float4(x[j], y[j], z[j], 1.0f);
-        if (sparse_idx) sparse_idx[base + d] = (uint32_t)(base + (uint64_t)j * kFT + threadIdx.x);
+        if (sparse_idx) sparse_idx[base + d] = (uint32_t)(base + (uint64_t)j * kCT + threadIdx.x);
         mn[0] = fminf(mn[0], x[j]); mx[0] = fmaxf(mx[0], x[j]);
         mn[1] = fminf(mn[1], y[j]); mx[1] = fmaxf(mx[1], y[j]);
         mn[2] = fminf(mn[2], z[j]); mx[2] = fmaxf(mx[2], z[j]);
@@ -279,7 +283,7 @@ __global__ void __launch_bounds__(kFT) k_crop_tile(const JobBatch jobs) {
             mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
         }
     }
-    __shared__ float s[6][kFT / 64];
+    __shared__ float s[6][kCT / 64];
     if (lane == 0)
         for (int a = 0; a < 3; ++a) {
             s[a][wid] = mn[a];
@@ -289,7 +293,7 @@ __global__ void __launch_bounds__(kFT) k_crop_tile(const JobBatch jobs) {
     if (threadIdx.x < 6) {
         const int a = threadIdx.x;
         float v = s[a][0];
-        for (int w = 1; w < kFT / 64; ++w) v = (a < 3) ? fminf(v, s[a][w]) : fmaxf(v, s[a][w]);
+        for (int w = 1; w < kCT / 64; ++w) v = (a < 3) ? fminf(v, s[a][w]) : fmaxf(v, s[a][w]);
         part[blockIdx.x * 6 + a] = v;
     }
 }
@@ -897,7 +901,7 @@ static int enqueue_chain(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream
     {
         ProfScope ps(ctx, PCP_K_CROP, st);
         if (bt.max_nb) {
-            hipLaunchKernelGGL(k_crop_tile, dim3(bt.max_nb, k), dim3(kFT), 0, st, bt.jb);
+            hipLaunchKernelGGL(k_crop_tile, dim3(bt.max_nb, k), dim3(kCT), 0, st, bt.jb);
             PCP_CHECK_LAUNCH(ctx);
         }
         hipLaunchKernelGGL(k_vox_params, dim3(1, k), dim3(kFT), 0, st, bt.jb, res,
