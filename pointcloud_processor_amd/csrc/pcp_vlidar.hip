@@ -290,8 +290,15 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
     } else if (!E.terrain_present) {
         visible = true;   // (:721, :727, :750)
     } else {
+#if defined(PCP_CELL_EXP) && PCP_CELL_EXP == 1   // A/B timing only: no march
+        visible = end > 1e300;
+#elif defined(PCP_CELL_EXP) && PCP_CELL_EXP == 2  // A/B timing only: probes, a candidate = hit
+        visible = march<false, true, PCP_CELL_PROBES>(E.terrain, px, py, pz, ndx, ndy, ndz,
+                                                      E.steps, E.K, end, 1e30f) < 0;
+#else
         visible = march<false, true, PCP_CELL_PROBES>(E.terrain, px, py, pz, ndx, ndy, ndz,
                                                       E.steps, E.K, end, E.r2_ray) < 0;
+#endif
     }
     if (!visible) return 0.0;
     bits |= 4u;
