@@ -241,11 +241,15 @@ __device__ __forceinline__ void lattice_xyz(const Lattice &L, uint32_t li, doubl
 }
 
 // isPointNearExcavation (radiusSearch(r) > 0) of every lattice point; linear index =
-// (i * gw + j) * layers + k, i.e. the reference's loop order
+// (i * gw + j) * layers + k, i.e. the reference's loop order.  One wave per lattice point: the
+// lanes split the block's candidate points and stop at the first round that finds one (a point
+// far from the area would otherwise walk hundreds of candidates on one lane)
+constexpr int kLatWaves = kXT / 64;
 __global__ void __launch_bounds__(kXT)
 k_lattice_flags(GridView g, float r2, Lattice L, uint8_t *__restrict__ flags) {
-    const uint32_t li = blockIdx.x * kXT + threadIdx.x;
-    if (li >= L.total) return;
+    const uint32_t li = blockIdx.x * kLatWaves + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (li >= L.total) return;   // uniform per wave
     double x, y, z;
     lattice_xyz(L, li, x, y, z);
     const float qx = (float)x, qy = (float)y, qz = (float)z;
@@ -253,13 +257,13 @@ k_lattice_flags(GridView g, float r2, Lattice L, uint8_t *__restrict__ flags) {
     bool hit = false;
     if (stencil_ranges(g, qx, qy, qz, lo, hi)) {
         for (int r = 0; r < 4 && !hit; ++r)
-            for (uint32_t k = lo[r]; k < hi[r]; ++k)
-                if (flann_within(qx, qy, qz, ld_p3(g.pts, k), r2)) {
-                    hit = true;
-                    break;
-                }
+            for (uint32_t k0 = lo[r]; k0 < hi[r] && !hit; k0 += 64) {
+                const uint32_t k = k0 + lane;
+                const bool w = k < hi[r] && flann_within(qx, qy, qz, ld_p3(g.pts, k), r2);
+                hit = __ballot(w) != 0ull;
+            }
     }
-    flags[li] = hit ? 1 : 0;
+    if (lane == 0) flags[li] = hit ? 1 : 0;
 }
 
 // one block: the flagged lattice points in order -> cells (double xyz); *n_out = count
@@ -426,7 +430,7 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     PCP_HIP(ctx, ctx->out_c.ensure(64));
     uint32_t *n_d = ctx->out_c.as<uint32_t>();
     if (total) {
-        hipLaunchKernelGGL(k_lattice_flags, dim3((unsigned)((total + kXT - 1) / kXT)), dim3(kXT),
+        hipLaunchKernelGGL(k_lattice_flags, dim3((unsigned)((total + kLatWaves - 1) / kLatWaves)), dim3(kXT),
                            0, ctx->stream, gq, r2q, L, ctx->stage.as<uint8_t>());
         PCP_CHECK_LAUNCH(ctx);
     }
