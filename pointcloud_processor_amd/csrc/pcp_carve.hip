@@ -104,9 +104,13 @@ __global__ void __launch_bounds__(kCT)
 k_heights(GridView g, float r2, double radius, const double2 *__restrict__ qxy,
           const uint32_t *__restrict__ nq_dev, uint32_t nq_fixed, double *__restrict__ h,
           uint32_t *__restrict__ fb_list, uint32_t *__restrict__ fb_count) {
+    // one wave per query: the lanes split the stencil's candidate points (a query used to walk
+    // hundreds of them on one lane).  The z sum is double-double, exact at these magnitudes, so
+    // the lanes' partial sums merge to the same value in any order.
     const uint32_t nq = nq_fixed + (nq_dev ? *nq_dev : 0u);
-    const uint32_t q = blockIdx.x * kCT + threadIdx.x;
-    if (q >= nq) return;
+    const uint32_t q = blockIdx.x * (kCT / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (q >= nq) return;   // uniform per wave
     const double2 xy = qxy[q];
     const float qx = (float)xy.x, qy = (float)xy.y, qz = 0.0f;
     DDs s{0.0, 0.0};
@@ -118,7 +122,7 @@ k_heights(GridView g, float r2, double radius, const double2 *__restrict__ qxy,
         for (int r = 0; r < 4; ++r) {
             const uint32_t row = lin + (r & 1) * nx + (r >> 1) * nxy;
             const uint32_t lo = g.start[row], hi = g.start[row + 2];
-            for (uint32_t k = lo; k < hi; ++k) {
+            for (uint32_t k = lo + lane; k < hi; k += 64) {
                 const P3 p = ld_p3(g.pts, k);
                 if (!flann_within(qx, qy, qz, p, r2)) continue;
                 const double dx = (double)p.x - xy.x, dy = (double)p.y - xy.y;
@@ -129,6 +133,14 @@ k_heights(GridView g, float r2, double radius, const double2 *__restrict__ qxy,
             }
         }
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double oh = __shfl_xor(s.hi, o, 64), ol = __shfl_xor(s.lo, o, 64);
+        dds_add(s, oh);
+        s.lo += ol;
+        valid += __shfl_xor(valid, o, 64);
+    }
+    if (lane != 0) return;
     if (valid > 0) {
         h[q] = (s.hi + s.lo) / (double)valid;
     } else {
@@ -503,7 +515,7 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
         hipLaunchKernelGGL(k_carve_cand, dim3(gn), dim3(kCT), 0, st, a, qxy, qidx, ctr, G);
         PCP_CHECK_LAUNCH(ctx);
     }
-    const unsigned gq = (unsigned)((nq_max + kCT - 1) / kCT);
+    const unsigned gq = (unsigned)((nq_max + kCT / 64 - 1) / (kCT / 64));   // a wave per query
     hipLaunchKernelGGL(k_heights, dim3(gq), dim3(kCT), 0, st, g, r2, p->terrain_search_radius,
                        (const double2 *)qxy, (const uint32_t *)ctr, G, h, fb_list, ctr + 1);
     PCP_CHECK_LAUNCH(ctx);
