@@ -117,6 +117,27 @@ def test_crop_voxel_pipeline(gpu, oracle, leaf):
     np.testing.assert_array_equal(out[:, :3], r_xyz)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_crop_voxel_random_boxes(gpu, oracle, seed):
+    """Random boxes, leaf sizes and clouds with a third of the coordinates on the 0.05 grid (box
+    faces and voxel boundaries), through the GPU crop + voxel against the oracle."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(1, 300_000))
+    a = rng.uniform(-6, 6, (n, 4)).astype(np.float32)
+    k = n // 3
+    a[:k, :3] = (np.round(a[:k, :3] / np.float32(0.05)) * np.float32(0.05)).astype(np.float32)
+    lo = rng.uniform(-5, 1, 3)
+    box = np.array([lo[0], lo[0] + rng.uniform(0, 8), lo[1], lo[1] + rng.uniform(0, 8),
+                    lo[2], lo[2] + rng.uniform(0, 8)])
+    box[::2] = np.round(box[::2] / 0.05) * 0.05      # faces on the grid too
+    leaf = float(rng.choice([0.0, 0.05, 0.1, 0.2, 0.37]))
+    out, ncrop = gpu.crop_voxel(a, box, leaf)
+    kept = oracle.crop_box(a, box)
+    assert ncrop == kept.size
+    ref = oracle.voxel_grid(a[kept], leaf)[0] if leaf > 0 and kept.size else a[kept, :3]
+    np.testing.assert_array_equal(out[:, :3], ref)
+
+
 # ---------------------------------------------------------------------------------- merger
 def _tfs():
     yaw = math.radians(30.0)
@@ -306,6 +327,27 @@ def test_raycast_fan_first_hit_exact(gpu, oracle, loaded, scene, cells):
     d = np.where(fh >= 0, steps[np.maximum(fh, 0)], np.nan)
     rd = np.where(r_fh >= 0, steps[np.maximum(r_fh, 0)], np.nan)
     np.testing.assert_allclose(d, rd, atol=1e-4, equal_nan=True)
+
+
+def test_raycast_fan_random_poses(gpu, oracle, loaded, scene):
+    """Poses anywhere around the terrain: inside and outside its bbox, below the ground, in
+    the pit, at any pitch/yaw; odd fan sizes and elevation limits."""
+    T, _ = loaded
+    rng = np.random.default_rng(7)
+    pts = scene.terrain[:, :3]
+    lo, hi = pts.min(0) - 3.0, pts.max(0) + 3.0
+    poses = np.column_stack([rng.uniform(lo[0], hi[0], 24), rng.uniform(lo[1], hi[1], 24),
+                             rng.uniform(lo[2] - 1.0, hi[2] + 3.0, 24),
+                             rng.uniform(-1.5, 1.5, 24), rng.uniform(-np.pi, np.pi, 24)])
+    for n_az, n_el, el_lo, el_hi, dmax in ((96, 17, -80.0, 80.0, 15.0), (130, 9, -17.0, 6.0, 7.5)):
+        fan = _abi.fan_params(n_az=n_az, n_el=n_el, el_min_deg=el_lo, el_max_deg=el_hi,
+                              max_distance=dmax)
+        blocked, units, fh, _ = gpu.raycast_fan(poses, fan, want_first_hit=True)
+        r_blocked, r_units, r_fh = oracle.raycast_fan(T, poses, n_az, n_el, fan.el_min,
+                                                      fan.el_max, dmax)
+        np.testing.assert_array_equal(fh, r_fh)
+        np.testing.assert_array_equal(blocked, r_blocked)
+        np.testing.assert_array_equal(units, r_units)
 
 
 def test_raycast_fan_full_size_two_poses(gpu, oracle, loaded, scene, cells):
