@@ -275,6 +275,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->carve.release();
     ctx->carve_buf.release();
     ctx->fan_host.release();
+    ctx->res_host.release();
     DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage, &ctx->fan_tab,
                       &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,
                       &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->f_in,

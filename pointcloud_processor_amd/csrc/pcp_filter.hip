@@ -984,8 +984,11 @@ struct ResultInfo {
 };
 
 static int read_results(pcp_ctx *ctx, const uint32_t *res_d, int k, ResultInfo *ri) {
-    uint32_t buf[3 * kMaxClouds];
-    PCP_HIP(ctx, hipMemcpyAsync(buf, res_d, sizeof(buf), hipMemcpyDeviceToHost, ctx->stream));
+    // pinned landing buffer: the per-frame size readback is one small DMA, no staging copy
+    PCP_HIP(ctx, ctx->res_host.ensure(3 * kMaxClouds * sizeof(uint32_t)));
+    uint32_t *buf = ctx->res_host.as<uint32_t>();
+    PCP_HIP(ctx, hipMemcpyAsync(buf, res_d, 3 * kMaxClouds * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     for (int i = 0; i < k; ++i) {
         ri[i].n = buf[i];

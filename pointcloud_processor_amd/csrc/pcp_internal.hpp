@@ -178,6 +178,7 @@ struct pcp_ctx {
     pcp::DevBuf stage, scratch[8];
     pcp::DevBuf fan_tab, poses_d, steps_d, out_a, out_b, out_c, out_d, stats_d;
     pcp::PinnedBuf fan_host;                 // pinned staging of poses in / counts out
+    pcp::PinnedBuf res_host;                 // pinned landing of the filter chain's sizes
     int32_t fan_naz = -1, fan_nel = -1;      // cached fan direction tables
     double fan_elmin = 0.0, fan_elmax = 0.0;
     double steps_end = -1e300;               // cached step table

@@ -897,7 +897,15 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     // the zx120 pose rides behind the candidates (row P of k_score_cells)
     PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.as<double>() + 5 * (size_t)P, zx, 5 * sizeof(double),
                                 hipMemcpyHostToDevice, st));
-    if (C) PCP_HIP(ctx, hipMemcpyAsync(flags_d, cell_flags, C, hipMemcpyHostToDevice, st));
+    // pinned staging: [totals f64 (P+1) | covered i32 (P+1)] [stats] [cell flags]
+    const size_t tc_bytes = (size_t)(P + 1) * (sizeof(double) + sizeof(int32_t));
+    const size_t st_off = (tc_bytes + 15) & ~(size_t)15, fl_off = st_off + 64 * sizeof(int32_t);
+    PCP_HIP(ctx, ctx->res_host.ensure(fl_off + (size_t)C + 16));
+    char *pin = ctx->res_host.as<char>();
+    if (C) {
+        std::memcpy(pin + fl_off, cell_flags, C);
+        PCP_HIP(ctx, hipMemcpyAsync(flags_d, pin + fl_off, C, hipMemcpyHostToDevice, st));
+    }
     PCP_HIP(ctx, hipMemsetAsync(stats, 0, 64 * sizeof(int32_t), st));
     const unsigned cb = (unsigned)((C + kT - 1) / kT);
     if (C) {
@@ -926,16 +934,15 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
         PCP_HIP(ctx, hipMemsetAsync(tot_d, 0, (size_t)(P + 1) * sizeof(double), st));
         PCP_HIP(ctx, hipMemsetAsync(cov_d, 0, (size_t)(P + 1) * sizeof(int32_t), st));
     }
-    std::vector<double> tot_h(P + 1);
-    std::vector<int32_t> cov_h(P + 1);
-    int32_t st_h[S_N];
-    PCP_HIP(ctx, hipMemcpyAsync(tot_h.data(), tot_d, (size_t)(P + 1) * sizeof(double),
-                                hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipMemcpyAsync(cov_h.data(), cov_d, (size_t)(P + 1) * sizeof(int32_t),
-                                hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipMemcpyAsync(st_h, stats, sizeof(st_h), hipMemcpyDeviceToHost, st));
-    if (C) PCP_HIP(ctx, hipMemcpyAsync(cell_flags, flags_d, C, hipMemcpyDeviceToHost, st));
+    // totals and covered counts are adjacent on the device: one copy into the pinned block
+    const double *tot_h = reinterpret_cast<const double *>(pin);
+    const int32_t *cov_h = reinterpret_cast<const int32_t *>(tot_h + (P + 1));
+    const int32_t *st_h = reinterpret_cast<const int32_t *>(pin + st_off);
+    PCP_HIP(ctx, hipMemcpyAsync(pin, tot_d, tc_bytes, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipMemcpyAsync(pin + st_off, stats, S_N * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    if (C) PCP_HIP(ctx, hipMemcpyAsync(pin + fl_off, flags_d, C, hipMemcpyDeviceToHost, st));
     PCP_HIP(ctx, hipStreamSynchronize(st));
+    if (C) std::memcpy(cell_flags, pin + fl_off, C);
     prof_resolve(ctx);
     // runOptimization candidate loop (:464-475): strict '>' keeps the first maximum
     double best = -INFINITY;
