@@ -536,8 +536,7 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     std::vector<double> hg(G);
     uint32_t cnt[4];
     PCP_HIP(ctx, hipMemcpyAsync(hg.data(), h, G * sizeof(double), hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipMemcpyAsync(cnt, ctr, sizeof(cnt), hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipStreamSynchronize(st));
+    if (int rc0 = read_small(ctx, cnt, ctr, sizeof(cnt), st)) return rc0;   // also waits for hg
     const uint64_t nkept = n ? cnt[2] : 0;
     if (pose_out) {
         pose_out[0] = cx;

@@ -43,6 +43,15 @@ int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what) {
     return PCP_OK;
 }
 
+int read_small(pcp_ctx *ctx, void *dst, const void *src_d, size_t bytes, hipStream_t st) {
+    if (bytes > 4096) return set_err(ctx, PCP_E_INVALID, "read_small: %zu bytes", bytes);
+    PCP_HIP(ctx, ctx->small_host.ensure(4096));
+    PCP_HIP(ctx, hipMemcpyAsync(ctx->small_host.p, src_d, bytes, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    std::memcpy(dst, ctx->small_host.p, bytes);
+    return PCP_OK;
+}
+
 void fan_tables(int32_t n_az, int32_t n_el, double el_min, double el_max, double *ca, double *sa,
                 double *ce, double *se) {
     // identical expression order to oracle/pcp_oracle.c:orc_fan_tables (glibc libm)
@@ -276,6 +285,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->carve_buf.release();
     ctx->fan_host.release();
     ctx->res_host.release();
+    ctx->small_host.release();
     DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage, &ctx->fan_tab,
                       &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,
                       &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->f_in,

@@ -439,8 +439,7 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
                        (uint32_t)total, n_d);
     PCP_CHECK_LAUNCH(ctx);
     uint32_t nc = 0;
-    PCP_HIP(ctx, hipMemcpyAsync(&nc, n_d, 4, hipMemcpyDeviceToHost, ctx->stream));
-    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc0 = read_small(ctx, &nc, n_d, 4, ctx->stream)) return rc0;
     if (nc) {
         hipLaunchKernelGGL(k_cell_normals, dim3(nc), dim3(kXT), 0, ctx->stream, gn, r2n,
                            (const double *)ctx->cells_xyz.as<double>(),

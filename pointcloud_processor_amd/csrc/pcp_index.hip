@@ -340,8 +340,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
                        reinterpret_cast<uint32_t *>(bb_d + 8));
     PCP_CHECK_LAUNCH(ctx);
     float bb_h[10];
-    PCP_HIP(ctx, hipMemcpyAsync(bb_h, bb_d, sizeof(bb_h), hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipStreamSynchronize(st));
+    if (int rc0 = read_small(ctx, bb_h, bb_d, sizeof(bb_h), st)) return rc0;
     uint32_t nfin;
     memcpy(&nfin, &bb_h[8], 4);
     g.present = true;

@@ -179,6 +179,7 @@ struct pcp_ctx {
     pcp::DevBuf fan_tab, poses_d, steps_d, out_a, out_b, out_c, out_d, stats_d;
     pcp::PinnedBuf fan_host;                 // pinned staging of poses in / counts out
     pcp::PinnedBuf res_host;                 // pinned landing of the filter chain's sizes
+    pcp::PinnedBuf small_host;               // pinned landing of small size readbacks
     int32_t fan_naz = -1, fan_nel = -1;      // cached fan direction tables
     double fan_elmin = 0.0, fan_elmax = 0.0;
     double steps_end = -1e300;               // cached step table
@@ -240,6 +241,10 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
 
 // validate a cloud view
 int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what);
+
+// a small (<= 4 KB) device -> host readback through pinned memory; synchronizes the stream
+// (a pageable destination costs a staging copy per call)
+int read_small(pcp_ctx *ctx, void *dst, const void *src_d, size_t bytes, hipStream_t st);
 
 // fan tables (shared definition with the oracle's orc_fan_tables)
 void fan_tables(int32_t n_az, int32_t n_el, double el_min, double el_max, double *ca,

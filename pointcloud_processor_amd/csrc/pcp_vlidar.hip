@@ -829,18 +829,22 @@ int pcp_generate_candidates(pcp_ctx *ctx, const double bb[6], const pcp_vl_param
         PCP_CHECK_LAUNCH(ctx);
     }
     uint32_t nh = 0;
-    PCP_HIP(ctx, hipMemcpyAsync(&nh, n_d, 4, hipMemcpyDeviceToHost, ctx->stream));
-    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc0 = read_small(ctx, &nh, n_d, 4, ctx->stream)) return rc0;
     *n_out = nh;
     if (nh > cap) {
         prof_resolve(ctx);
         return set_err(ctx, PCP_E_CAPACITY, "pcp_generate_candidates: need %u poses, cap %llu", nh,
                        (unsigned long long)cap);
     }
-    if (nh)
-        PCP_HIP(ctx, hipMemcpyAsync(poses5, ctx->out_b.p, (size_t)nh * 5 * sizeof(double),
-                                    hipMemcpyDeviceToHost, ctx->stream));
-    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const size_t pbytes = (size_t)nh * 5 * sizeof(double);
+    if (nh && pbytes <= 4096) {   // the usual lattice (~100 poses): through pinned memory
+        if (int rc0 = read_small(ctx, poses5, ctx->out_b.p, pbytes, ctx->stream)) return rc0;
+    } else {
+        if (nh)
+            PCP_HIP(ctx, hipMemcpyAsync(poses5, ctx->out_b.p, pbytes, hipMemcpyDeviceToHost,
+                                        ctx->stream));
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     prof_resolve(ctx);
     return PCP_OK;
 }
@@ -892,16 +896,17 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     double *tot_d = ctx->out_c.as<double>();
     int32_t *cov_d = reinterpret_cast<int32_t *>(tot_d + (P + 1));
     int32_t *stats = ctx->stats_d.as<int32_t>();
-    if (P) PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, poses5, (size_t)P * 5 * sizeof(double),
-                                       hipMemcpyHostToDevice, st));
-    // the zx120 pose rides behind the candidates (row P of k_score_cells)
-    PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.as<double>() + 5 * (size_t)P, zx, 5 * sizeof(double),
-                                hipMemcpyHostToDevice, st));
-    // pinned staging: [totals f64 (P+1) | covered i32 (P+1)] [stats] [cell flags]
+    // pinned staging: [totals f64 (P+1) | covered i32 (P+1)] [stats] [cell flags] [poses + zx120]
     const size_t tc_bytes = (size_t)(P + 1) * (sizeof(double) + sizeof(int32_t));
     const size_t st_off = (tc_bytes + 15) & ~(size_t)15, fl_off = st_off + 64 * sizeof(int32_t);
-    PCP_HIP(ctx, ctx->res_host.ensure(fl_off + (size_t)C + 16));
+    const size_t po_off = (fl_off + (size_t)C + 15) & ~(size_t)15;
+    const size_t po_bytes = (size_t)(P + 1) * 5 * sizeof(double);
+    PCP_HIP(ctx, ctx->res_host.ensure(po_off + po_bytes + 16));
     char *pin = ctx->res_host.as<char>();
+    // the candidates, then the zx120 pose behind them (row P of k_score_cells): one upload
+    if (P) std::memcpy(pin + po_off, poses5, (size_t)P * 5 * sizeof(double));
+    std::memcpy(pin + po_off + (size_t)P * 5 * sizeof(double), zx, 5 * sizeof(double));
+    PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pin + po_off, po_bytes, hipMemcpyHostToDevice, st));
     if (C) {
         std::memcpy(pin + fl_off, cell_flags, C);
         PCP_HIP(ctx, hipMemcpyAsync(flags_d, pin + fl_off, C, hipMemcpyHostToDevice, st));
