@@ -339,35 +339,42 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
 
 // ordered sequential sum per row (evaluatePosition :634-645): total_score += s for s > 0 in cell
 // order, s = std::max(score_zx120, score_mobile) = (sz < sm) ? sm : sz for a pose row, sz for
-// the zx120 row (r == P).  One wave per row: the lanes stage 512 values at a time in LDS (the
-// next 512 already loading into registers), lane 0 adds them in order -- the chain is the adds.
+// the zx120 row (r == P).  One wave per row: each lane holds 8 of the next 512 values in
+// registers (the following 512 already loading), and the wave walks them in cell order with
+// v_readlane into scalar registers, every lane carrying the same running sum -- no LDS round
+// trip in the chain, which is the dependent adds alone.
 constexpr int kSumChunk = 512;
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const uint64_t b = __double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __global__ void __launch_bounds__(64)
 k_row_sum(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
           double *__restrict__ total, int32_t *__restrict__ covered) {
     const int r = blockIdx.x;
     const int lane = threadIdx.x;
     const double *row = sm + (size_t)r * C;
-    __shared__ __attribute__((aligned(16))) double buf[kSumChunk];
     constexpr int kPer = kSumChunk / 64;
-    double v[kPer];
+    double v[kPer], wz[kPer], wm[kPer];
     int32_t cov = 0;   // order-free: each lane counts its own positive values
-    // x > 0 ? x : +0.0 -- adding +0.0 to the (non-negative) running sum leaves it bit-identical,
-    // so lane 0's unconditional adds are the reference's `if (x > 0) total += x`
+    // raw loads only: the values they feed are formed after the chain that overlaps them
     auto load = [&](int base) {
 #pragma unroll
         for (int q = 0; q < kPer; ++q) {
             const int c = base + q * 64 + lane;
-            double x = 0.0;
-            if (c < C) {
-                const double sz = score_z[c];
-                if (r < P) {
-                    const double m = row[c];
-                    x = (sz < m) ? m : sz;
-                } else {
-                    x = sz;
-                }
-            }
+            wz[q] = c < C ? score_z[c] : 0.0;
+            wm[q] = (c < C && r < P) ? row[c] : 0.0;
+        }
+    };
+    // x > 0 ? x : +0.0 -- adding +0.0 to the (non-negative) running sum leaves it bit-identical,
+    // so the unconditional adds are the reference's `if (x > 0) total += x`
+    auto form = [&]() {
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const double sz = wz[q], m = wm[q];
+            const double x = r < P ? ((sz < m) ? m : sz) : sz;
             const bool pos = x > 0;
             cov += pos ? 1 : 0;
             v[q] = pos ? x : 0.0;
@@ -375,32 +382,23 @@ k_row_sum(const double *__restrict__ sm, const double *__restrict__ score_z, int
     };
     double acc = 0.0;
     load(0);
+    form();
     for (int base = 0; base < C; base += kSumChunk) {
+        const bool more = base + kSumChunk < C;
+        if (more) load(base + kSumChunk);   // in flight during the chain
 #pragma unroll
-        for (int q = 0; q < kPer; ++q) buf[q * 64 + lane] = v[q];
-        __syncthreads();
-        if (base + kSumChunk < C) load(base + kSumChunk);   // in flight during the sum
-        if (lane == 0) {   // the chain: dependent adds only; LDS reads run one group ahead
-            const int m = (min(kSumChunk, C - base) + 15) & ~15;   // zero padding adds +0.0
-            const double2 *b2 = reinterpret_cast<const double2 *>(buf);
-            double2 cur[8], nxt[8];
+        for (int q = 0; q < kPer; ++q) {
+            if (base + q * 64 >= C) break;   // wave-uniform; the tail's zero lanes add +0.0
 #pragma unroll
-            for (int q = 0; q < 8; ++q) cur[q] = b2[q];
-            for (int j = 0; j < m; j += 16) {
-                if (j + 16 < m) {
+            for (int l = 0; l < 64; l += 8) {   // 8 readlanes ahead of their adds
+                double t[8];
 #pragma unroll
-                    for (int q = 0; q < 8; ++q) nxt[q] = b2[(j + 16) / 2 + q];
-                }
+                for (int i = 0; i < 8; ++i) t[i] = readlane_f64(v[q], l + i);
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    acc += cur[q].x;
-                    acc += cur[q].y;
-                }
-#pragma unroll
-                for (int q = 0; q < 8; ++q) cur[q] = nxt[q];
+                for (int i = 0; i < 8; ++i) acc += t[i];
             }
         }
-        __syncthreads();
+        if (more) form();
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cov += __shfl_xor(cov, o, 64);
