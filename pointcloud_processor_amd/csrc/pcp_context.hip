@@ -257,6 +257,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (!ctx) return PCP_E_NOMEM;
     ctx->device = device;
     if (const char *fb = std::getenv("PCP_FAN_BATCH")) ctx->fan_batch = std::atoi(fb);
+    if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)

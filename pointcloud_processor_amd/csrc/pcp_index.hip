@@ -4,6 +4,8 @@
 //   start : u32[ncell+1] prefix offsets (cell c holds pts[start[c] .. start[c+1]) )
 //   occ2  : u32[(ncell+31)/32] dilated occupancy (bit c = any point in cells c + {0,1}^3)
 //   occz  : u16[ncell] z band of the same 2x2x2 block (z-sorted indices: the march's probe)
+//   bstart: u32[ncell+1], bpts: float4[8 n] (terrain): each stencil corner's 2x2x2 block as
+//           one run in descending z (every point appears in the blocks of its 8 corners)
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -53,6 +55,8 @@ GridView GridIndex::view() const {
     const double bb[6] = {v.bx0, v.bx1, v.by0, v.by1, v.bz0, v.bz1};
     for (int a = 0; a < 6; ++a) v.fb[a] = (float)bb[a];
     v.occz = occz_ok ? occz.as<const uint16_t>() : nullptr;
+    v.bstart = blk_ok ? bstart.as<const uint32_t>() : nullptr;
+    v.bpts = blk_ok ? bpts.as<const float4>() : nullptr;
     v.fzoff = (float)(rm * v.inv_c);
     v.fzt = (float)((r_q + 2e-3) * v.inv_c);
     return v;
@@ -311,6 +315,87 @@ k_occ2(const uint32_t *__restrict__ start, CellMap m, uint64_t ncell, uint32_t *
     if ((threadIdx.x & 63) == 0 && w + 1 < nw) occ2[w + 1] = (uint32_t)(bits >> 32);
 }
 
+// points per stencil corner's 2x2x2 block (0 for corners on the upper border: stencil_cell
+// never returns them)
+__global__ void __launch_bounds__(kThreads)
+k_blk_count(const uint32_t *__restrict__ start, CellMap m, uint64_t ncell,
+            uint32_t *__restrict__ cnt) {
+    const uint64_t lin = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (lin >= ncell) return;
+    const int ix = (int)(lin % m.nx);
+    const int iy = (int)((lin / m.nx) % m.ny);
+    const int iz = (int)(lin / ((uint64_t)m.nx * m.ny));
+    uint32_t n = 0;
+    if (ix < m.nx - 1 && iy < m.ny - 1 && iz < m.nz - 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint64_t row = lin + (uint64_t)(r & 1) * m.nx + (uint64_t)(r >> 1) * m.nx * m.ny;
+            n += start[row + 2] - start[row];
+        }
+    }
+    cnt[lin] = n;
+}
+
+// (z descending, original index ascending) -- the order of k_cell_rank_z, as one comparison
+__device__ __forceinline__ bool zbefore(float az, uint32_t ai, float bz, uint32_t bi) {
+    return az > bz || (az == bz && ai < bi);
+}
+
+// block-major fill, one thread per point p of cell C (cells already z-sorted): p's place in
+// corner K's block is the number of block points ahead of it = the sum over K's 8 cells D of
+// rank_D(p) (points of D ahead of p; its own position for D = C).  The 27 cells around C cover
+// the blocks of all 8 corners that contain C; their ranks are counted once and summed per corner.
+// Consecutive threads are consecutive points of one cell, so a wave reads the same neighbour
+// runs (shared lines).
+__global__ void __launch_bounds__(kThreads)
+k_blk_fill(const float4 *__restrict__ pts, uint64_t n, const uint32_t *__restrict__ start,
+           CellMap m, const uint32_t *__restrict__ bstart, float4 *__restrict__ bpts) {
+    const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (k >= n) return;
+    const float4 p = pts[k];
+    const uint32_t pi = __float_as_uint(p.w);
+    const uint32_t c = cell_of(m, p.x, p.y, p.z);
+    const int nx = m.nx, ny = m.ny, nz = m.nz;
+    const int ix = (int)(c % (uint32_t)nx);
+    const int iy = (int)((c / (uint32_t)nx) % (uint32_t)ny);
+    const int iz = (int)(c / ((uint32_t)nx * (uint32_t)ny));
+    const uint32_t nxy = (uint32_t)nx * (uint32_t)ny;
+    uint32_t rk[27];   // rank of p in cell C + (dx, dy, dz), index (dz+1)*9 + (dy+1)*3 + (dx+1)
+#pragma unroll
+    for (int t = 0; t < 27; ++t) {
+        const int dx = t % 3 - 1, dy = (t / 3) % 3 - 1, dz = t / 9 - 1;
+        uint32_t r = 0;
+        if (dx == 0 && dy == 0 && dz == 0) {
+            r = (uint32_t)k - start[c];
+        } else if (ix + dx >= 0 && ix + dx < nx && iy + dy >= 0 && iy + dy < ny && iz + dz >= 0 &&
+                   iz + dz < nz) {
+            const uint32_t d = (uint32_t)((int)c + dx + dy * nx + dz * (int)nxy);
+            const uint32_t s = start[d], e = start[d + 1];
+            // descending z: the points ahead of p form a prefix of the run
+            for (uint32_t j = s; j < e; ++j) {
+                const float4 q = pts[j];
+                if (!zbefore(q.z, __float_as_uint(q.w), p.z, pi)) break;
+                ++r;
+            }
+        }
+        rk[t] = r;
+    }
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {   // corner K = C - (ax, ay, az)
+        const int ax = a & 1, ay = (a >> 1) & 1, az = a >> 2;
+        const int kx = ix - ax, ky = iy - ay, kz = iz - az;
+        if (kx < 0 || ky < 0 || kz < 0 || kx >= nx - 1 || ky >= ny - 1 || kz >= nz - 1) continue;
+        uint32_t pos = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {   // the block's cells K + (bx, by, bz) = C + (b - a)
+            const int dx = (b & 1) - ax, dy = ((b >> 1) & 1) - ay, dz = (b >> 2) - az;
+            pos += rk[(dz + 1) * 9 + (dy + 1) * 3 + (dx + 1)];
+        }
+        const uint32_t K = c - (uint32_t)ax - (uint32_t)ay * (uint32_t)nx - (uint32_t)az * nxy;
+        bpts[bstart[K] + pos] = p;
+    }
+}
+
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort,
                 bool occ) {
     const uint64_t n = v.n;
@@ -361,6 +446,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         PCP_HIP(ctx, hipMemsetAsync(g.occz.p, 0xFF, 1, st));
         PCP_HIP(ctx, hipMemsetAsync(static_cast<char *>(g.occz.p) + 1, 0, 1, st));
         g.occz_ok = zsort;
+        g.blk_ok = false;
         return PCP_OK;
     }
     for (int a = 0; a < 3; ++a) {
@@ -440,8 +526,48 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         PCP_CHECK_LAUNCH(ctx);
         g.occz_ok = true;
     }
+    g.blk_ok = false;
     PCP_HIP(ctx, hipStreamSynchronize(st));
     return PCP_OK;
+}
+
+// block-major copy: count per corner -> prefix -> fill (every point lands in the blocks of its
+// 8 corners, ~8 n entries; not built past the 2^28 point cap -- the scans fall back to the
+// per-cell runs)
+int build_blocks(pcp_ctx *ctx, GridIndex &g) {
+    if (g.blk_ok || !g.present || !g.occz_ok || g.n_pts == 0) return PCP_OK;
+    hipStream_t st = ctx->stream;
+    ProfScope prof(ctx, PCP_K_INDEX_BUILD);
+    const GridView gv = g.view();
+    const CellMap m{gv.ox, gv.oy, gv.oz, gv.inv_c, g.nx, g.ny, g.nz};
+    const uint64_t ncell = (uint64_t)g.nx * (uint64_t)g.ny * (uint64_t)g.nz;
+    PCP_HIP(ctx, ctx->scratch[3].ensure((ncell + 1) * sizeof(uint32_t)));
+    PCP_HIP(ctx, ctx->scratch[4].ensure(scan_tmp_bytes(ncell) + (ncell + 1) * sizeof(uint32_t)));
+    uint32_t *cnt = ctx->scratch[3].as<uint32_t>();
+    hipLaunchKernelGGL(k_blk_count, dim3((unsigned)((ncell + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, st, g.start.as<const uint32_t>(), m, ncell, cnt);
+    PCP_CHECK_LAUNCH(ctx);
+    PCP_HIP(ctx, g.bstart.ensure((ncell + 1) * sizeof(uint32_t)));
+    int rc = exclusive_scan_u32(ctx, cnt, g.bstart.as<uint32_t>(), ncell, ctx->scratch[4].p);
+    if (rc) return rc;
+    uint32_t nb_tot = 0;
+    if ((rc = read_small(ctx, &nb_tot, g.bstart.as<uint32_t>() + ncell, 4, st))) return rc;
+    if (nb_tot == 0 || nb_tot >= (1u << 28)) return PCP_OK;
+    PCP_HIP(ctx, g.bpts.ensure((size_t)nb_tot * sizeof(float4)));
+    const uint64_t n = g.n_pts;
+    hipLaunchKernelGGL(k_blk_fill, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads),
+                       0, st, g.pts.as<const float4>(), n, g.start.as<const uint32_t>(), m,
+                       g.bstart.as<const uint32_t>(), g.bpts.as<float4>());
+    PCP_CHECK_LAUNCH(ctx);
+    g.blk_ok = true;
+    return PCP_OK;
+}
+
+int terrain_blocks_before_query(pcp_ctx *ctx) {
+    if (ctx->terrain_blocks <= 0 || ctx->terrain.blk_ok || !ctx->terrain.present) return PCP_OK;
+    ++ctx->terrain_queries;
+    if (ctx->terrain_blocks == 1 && ctx->terrain_queries < 2) return PCP_OK;
+    return build_blocks(ctx, ctx->terrain);
 }
 
 }  // namespace pcp
@@ -459,6 +585,7 @@ int pcp_set_terrain(pcp_ctx *ctx, const pcp_cloud_view *terrain) {
     if (terrain->n == 0) return PCP_OK;   // terrainCallback: no rebuild on an empty cloud
     // the march probes the z bands; occupancy bits only for the fan's A/B variant 2
     rc = build_index(ctx, ctx->terrain, *terrain, kRayRadius, true, ctx->fan_batch == 2);
+    ctx->terrain_queries = 0;
     prof_resolve(ctx);
     return rc;
 }

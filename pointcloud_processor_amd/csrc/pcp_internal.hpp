@@ -102,6 +102,11 @@ struct GridView {               // POD passed to kernels by value
     // empty block).  fzoff = (r_q + m) / c (stencil-corner offset), fzt = (r_q + 2 mm) / c.
     const uint16_t *occz;
     float fzoff, fzt;
+    // block-major copy (null unless built): the points of each stencil corner's 2x2x2 block in
+    // one run, descending z -- bpts[bstart[lin] .. bstart[lin + 1]); one directory load and one
+    // early exit per scan instead of 4 + 8
+    const uint32_t *bstart;
+    const float4 *bpts;
 };
 constexpr float kZq = 2.0f / 250.0f;   // z band step, cells (2 cells = 250 steps)
 
@@ -112,8 +117,9 @@ struct GridIndex {
     double c = 0.0;
     int32_t nx = 0, ny = 0, nz = 0;
     double bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
-    DevBuf pts, start, occ2, occz;
+    DevBuf pts, start, occ2, occz, bstart, bpts;
     bool occz_ok = false;
+    bool blk_ok = false;         // block-major copy built (bstart / bpts)
     bool occ2_ok = false;        // occ2 built (only indices queried by stencil_any need it)
     GridView view() const;
     void release() {
@@ -121,7 +127,10 @@ struct GridIndex {
         start.release();
         occ2.release();
         occz.release();
+        bstart.release();
+        bpts.release();
         occz_ok = false;
+        blk_ok = false;
         present = false;
         n_pts = 0;
     }
@@ -186,6 +195,8 @@ struct pcp_ctx {
     int steps_K = 0;
     int num_cus = 256;                       // multiprocessors of the device
     int fan_batch = 0;                       // fan kernel variant (PCP_FAN_BATCH), A/B only
+    int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
+    int terrain_queries = 0;                 // queries since the last pcp_set_terrain
     // filter/merge scratch
     pcp::DevBuf f_in, f_misc;
     std::vector<pcp::CloudBufs> fbuf;        // per-cloud scratch of the filter pipeline
@@ -233,6 +244,12 @@ void prof_resolve(pcp_ctx *ctx);   // after a stream sync
 // occ: build the dilated occupancy bits (stencil_any: the aux index; the fan's A/B variant 2)
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
                 bool zsort = true, bool occ = true);
+// the block-major copy of a z-sorted index (GridView.bstart / bpts); no-op when built
+int build_blocks(pcp_ctx *ctx, GridIndex &g);
+// before a terrain query: build the terrain's block copy per PCP_TERRAIN_BLOCKS (0 never,
+// 1 at the second query after pcp_set_terrain -- a terrain that is queried once, as in the
+// per-frame chain, does not pay for it --, 2 at the first)
+int terrain_blocks_before_query(pcp_ctx *ctx);
 
 // scan: exclusive prefix sum of n uint32 values into out (n + 1 entries, out[n] = total).
 // tmp must hold scan_tmp_bytes(n).

@@ -76,6 +76,12 @@ struct U3 {
 __device__ __forceinline__ U3 ld_u3o(const uint32_t *base, uint32_t i) {
     return *reinterpret_cast<const U3 *>(reinterpret_cast<const char *>(base) + (i << 2));
 }
+// two consecutive directory entries (a block's start and end) in one load
+__device__ __forceinline__ uint2 ld_u2o(const uint32_t *base, uint32_t i) {
+    const uint32_t *p =
+        reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + (i << 2));
+    return make_uint2(p[0], p[1]);
+}
 __device__ __forceinline__ uint32_t ld_u16o(const uint16_t *base, uint32_t i) {
     return *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(base) + (i << 1));
 }

@@ -668,3 +668,35 @@ def test_drivable_area_matches_oracle(gpu, oracle, kw):
     np.testing.assert_array_equal(origin, r_origin)
     np.testing.assert_array_equal(grid, ref)
     assert {-1, 0, 100} <= set(np.unique(grid).tolist())
+
+
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, monkeypatch):
+    """PCP_TERRAIN_BLOCKS=0 scans the per-cell runs, =2 the block-major copy from the first
+    query on (the default, 1, switches at the second query): both bit-exact on the fan and the
+    reference-mode scoring."""
+    monkeypatch.setenv("PCP_TERRAIN_BLOCKS", mode)
+    ctx = _abi.Context(0)
+    try:
+        ctx.set_terrain(scene.terrain, point_step=32)
+        ctx.set_aux_cloud(aux, point_step=32)
+        ctx.set_cells(cells.xyz, cells.normals)
+        T, A = oracle.Cloud(scene.terrain), oracle.Cloud(aux)
+        params = _abi.default_vl_params()
+        poses = ctx.generate_candidates(cells.grid_bbox, params, scene.zx120_pose5)
+        fan = _abi.fan_params(n_az=128, n_el=48)
+        _, _, fh, _ = ctx.raycast_fan(poses[:5], fan, want_first_hit=True)
+        _, _, r_fh = oracle.raycast_fan(T, poses[:5], 128, 48, fan.el_min, fan.el_max,
+                                        fan.max_distance)
+        np.testing.assert_array_equal(fh, r_fh)
+        flags_g = np.zeros(cells.xyz.shape[0], np.uint8)
+        flags_r = flags_g.copy()
+        tot, cov, rep = ctx.score_poses(poses, scene.zx120_pose5, params, flags_g)
+        r_tot, r_cov, r_rep = oracle.score_poses(T, A, cells.xyz, cells.normals, poses,
+                                                 scene.zx120_pose5, oracle.vl_params(), flags_r)
+        np.testing.assert_array_equal(flags_g, flags_r)
+        np.testing.assert_array_equal(cov, r_cov)
+        assert _rel_close(tot, r_tot)
+        assert rep.best_idx == r_rep.best_idx
+    finally:
+        ctx.close()
