@@ -700,3 +700,33 @@ def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, monkeypatch):
         assert rep.best_idx == r_rep.best_idx
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_terrain_block_copy_dense_and_tiny(oracle, mode, monkeypatch):
+    """Block-major copy on awkward terrains: 20 k points packed into a 0.3 m cube (blocks of
+    thousands of points, ties in z) next to a sparse plane, and a one-point terrain."""
+    monkeypatch.setenv("PCP_TERRAIN_BLOCKS", mode)
+    rng = np.random.default_rng(11)
+    dense = np.column_stack([rng.uniform(2.0, 2.3, 20_000), rng.uniform(-0.15, 0.15, 20_000),
+                             np.round(rng.uniform(0.0, 0.3, 20_000), 2)])
+    gx, gy = np.meshgrid(np.arange(-3.0, 6.0, 0.07), np.arange(-3.0, 3.0, 0.07))
+    plane = np.column_stack([gx.ravel(), gy.ravel(), rng.normal(-0.5, 0.01, gx.size)])
+    poses = np.array([[0.0, 0.0, 1.0, -0.3, 0.0], [4.5, 0.5, 0.8, 0.0, np.pi],
+                      [2.15, 0.0, 0.15, 0.0, 0.3], [-2.0, -2.0, 2.5, -0.8, 0.7]])
+    fan = _abi.fan_params(n_az=96, n_el=40, el_min_deg=-80.0, el_max_deg=60.0, max_distance=9.0)
+    for pts in (np.vstack([dense, plane]), np.array([[1.0, 0.2, 0.4]])):
+        cloud = np.zeros((pts.shape[0], 8), np.float32)
+        cloud[:, :3] = pts
+        ctx = _abi.Context(0)
+        try:
+            ctx.set_terrain(cloud, point_step=32)
+            for _ in range(2):   # mode 1 would switch paths between these two calls
+                blocked, units, fh, _ = ctx.raycast_fan(poses, fan, want_first_hit=True)
+                r_blocked, r_units, r_fh = oracle.raycast_fan(oracle.Cloud(cloud), poses, 96, 40,
+                                                              fan.el_min, fan.el_max, 9.0)
+                np.testing.assert_array_equal(fh, r_fh)
+                np.testing.assert_array_equal(blocked, r_blocked)
+                np.testing.assert_array_equal(units, r_units)
+        finally:
+            ctx.close()
