@@ -98,22 +98,26 @@ __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, fl
 // The same test over the block-major copy: the block's points are one run in descending z,
 // so one directory load, then 2 points per step until a point lies r below q (exact: every
 // later point is lower still) -- a single early exit instead of one per cell.
+#ifndef PCP_BLK_STEP
+#define PCP_BLK_STEP 2   // block-walk points per step (build knob)
+#endif
 template <bool STATS>
 __device__ __forceinline__ bool scan_block(const GridView &g, uint32_t lin, float qx, float qy,
                                            float qz, float r2, uint32_t *cnt) {
     const uint2 se = ld_u2o(g.bstart, lin);
-    for (uint32_t k = se.x; k < se.y; k += 2) {
-        const P3 p0 = ld_p3o(g.bpts, k);
-        const P3 p1 = ld_p3o(g.bpts, min(k + 1, se.y - 1));
-        if (STATS) cnt[2] += 1;
-        if (flann_within(qx, qy, qz, p0, r2)) return true;
-        float dz = qz - p0.z;
-        if (dz >= 0.0f && dz * dz >= r2) return false;
-        if (k + 1 >= se.y) return false;
-        if (STATS) cnt[2] += 1;
-        if (flann_within(qx, qy, qz, p1, r2)) return true;
-        dz = qz - p1.z;
-        if (dz >= 0.0f && dz * dz >= r2) return false;
+    const uint32_t e = se.y;
+    for (uint32_t k = se.x; k < e; k += PCP_BLK_STEP) {
+        P3 p[PCP_BLK_STEP];   // independent loads (the tail repeats the last entry)
+#pragma unroll
+        for (int i = 0; i < PCP_BLK_STEP; ++i) p[i] = ld_p3o(g.bpts, min(k + i, e - 1));
+#pragma unroll
+        for (int i = 0; i < PCP_BLK_STEP; ++i) {
+            if (i > 0 && k + i >= e) return false;
+            if (STATS) cnt[2] += 1;
+            if (flann_within(qx, qy, qz, p[i], r2)) return true;
+            const float dz = qz - p[i].z;
+            if (dz >= 0.0f && dz * dz >= r2) return false;
+        }
     }
     return false;
 }
