@@ -96,10 +96,12 @@ __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, fl
 }
 
 // The same test over the block-major copy: the block's points are one run in descending z,
-// so one directory load, then 2 points per step until a point lies r below q (exact: every
-// later point is lower still) -- a single early exit instead of one per cell.
+// so one directory load, then one point per step until a point lies r below q (exact: every
+// later point is lower still) -- a single early exit instead of one per cell.  (2, 3 or 4
+// independent loads per step measured 1-2 % slower: the loads past the exit are wasted on the
+// bound vector-memory path.)
 #ifndef PCP_BLK_STEP
-#define PCP_BLK_STEP 2   // block-walk points per step (build knob)
+#define PCP_BLK_STEP 1   // block-walk points per step (build knob)
 #endif
 template <bool STATS>
 __device__ __forceinline__ bool scan_block(const GridView &g, uint32_t lin, float qx, float qy,
