@@ -349,7 +349,7 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
 // (score_zx120 and its result bits) -- one launch, so the zx120 row does not run alone on a
 // handful of CUs.  std::max(score_zx120, score_mobile) is applied by k_row_sum.
 #ifndef PCP_SCORE_WAVES
-#define PCP_SCORE_WAVES 5   // waves per SIMD of k_score_cells (build knob)
+#define PCP_SCORE_WAVES 6   // waves per SIMD of k_score_cells (build knob)
 #endif
 __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(PCP_SCORE_WAVES, 8)))
 k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict__ cn, int C,
