@@ -10,8 +10,15 @@ of the per-pose blocked-ray counts (RCCL over xGMI when N > 1), then the argmin.
 value = ray-hit tests/s: sample queries the reference would execute (samples up to and
 including the first hit, else all), summed over all ranks, / max-over-ranks wall time.
 Inputs (terrain index, direction tables, poses) are resident in HBM before timing starts.
+The same line carries the rest of the metric ("+ candidate poses/sec (whole node)"):
+poses_per_s_reference_mode (runOptimization over the excavation cells, virtual_lidar.cpp:
+454-548) and c3 (crop + voxel + transform frame, BASELINE configs[2]), each its own timed loop
+of K steps, and CPU baselines (the oracle restatement, 1 thread and the host's CPU share) for
+all three on rank 0 at N = 1.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fan|filter|cells]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode all|fan|filter|cells]
+
+--gpus N without WORLD_SIZE starts N ranks itself (one process per GPU).
 """
 from __future__ import annotations
 
@@ -29,6 +36,36 @@ METRIC = "ray-hit tests/sec + candidate poses/sec (whole node), 1M-pt terrain"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: 8 TB/s spec
 
 
+def _self_launch(n: int) -> int:
+    """--gpus N without a launcher: start N ranks of this script (one process per GPU, as
+    torch.distributed.run would), before this process touches the GPU.  Rank 0 prints the
+    JSON line; the exit code is the worst rank's."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] +
+                                      sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, p.wait())
+            if rc:
+                break
+    finally:
+        for p in procs:   # a failed rank leaves the others stuck in a collective
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def _dist_init(n_gpus: int):
     import torch
     import torch.distributed as dist
@@ -36,16 +73,20 @@ def _dist_init(n_gpus: int):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}")
+    backend = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # one process per GPU over RCCL; PCP_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
-        backend = os.environ.get("PCP_DIST_BACKEND",
-                                 "nccl" if torch.cuda.is_available() else "gloo")
-        if torch.cuda.is_available():
-            local = local % max(torch.cuda.device_count(), 1)
+        # one process per GPU over RCCL; with fewer GPUs than ranks (a rehearsal on a 1-GPU
+        # box) the ranks share devices and the collective runs over gloo
+        ndev = torch.cuda.device_count()
+        backend = os.environ.get("PCP_DIST_BACKEND", "nccl" if ndev >= world else "gloo")
+        if ndev:
+            local = local % ndev
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
-    return torch, (dist if world > 1 else None), world, rank, local
+    return torch, (dist if world > 1 else None), world, rank, local, backend
 
 
 def _poses_for(ctx, grid_bbox, zx, total: int):
@@ -88,6 +129,8 @@ def _gbs(nbytes, seconds):
 
 
 def _host_cpu():
+    """The host's CPU share: affinity list, cgroup quota, and the threads the MT baselines
+    use (min of the two: threads beyond the quota only time-slice)."""
     model = None
     try:
         for line in open("/proc/cpuinfo"):
@@ -96,27 +139,43 @@ def _host_cpu():
                 break
     except OSError:
         pass
-    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    return {"model": model, "nproc": os.cpu_count(), "affinity": share}
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"model": model, "nproc": os.cpu_count(), "affinity": aff,
+            "cgroup_quota_cores": quota, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "threads_used": threads}
+
+
+def _oracle():
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle
+
+    return pyoracle
 
 
 def cpu_baseline_fan(terrain, poses, fan, budget_s: float, threads: int = 1):
     """The oracle (CPU restatement) on a bounded sample: the first k poses of this workload,
     whole fans, until ~budget_s elapsed.  threads = 1 is the reference's single-threaded
     executor; threads > 1 is the OpenMP variant SURVEY 8d asks for beside it."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import pyoracle
-
+    pyoracle = _oracle()
     pyoracle.set_threads(threads)
     T = pyoracle.Cloud(terrain)
     units = 0
     k = 0
+    chunk = 1 if threads == 1 else max(1, threads // 16)
     t0 = time.perf_counter()
     while k < len(poses) and time.perf_counter() - t0 < budget_s:
-        _, u, _ = pyoracle.raycast_fan(T, poses[k:k + 1], fan.n_az, fan.n_el, fan.el_min,
+        _, u, _ = pyoracle.raycast_fan(T, poses[k:k + chunk], fan.n_az, fan.n_el, fan.el_min,
                                        fan.el_max, fan.max_distance, want_first_hit=False)
         units += int(u.sum())
-        k += 1
+        k += min(chunk, len(poses) - k)
     dt = time.perf_counter() - t0
     pyoracle.set_threads(1)
     return {"value": units / dt, "unit": "ray-hit tests/s", "cores": threads, "kind": "port",
@@ -125,29 +184,55 @@ def cpu_baseline_fan(terrain, poses, fan, budget_s: float, threads: int = 1):
                       f"{threads} thread{'s' if threads > 1 else ''})"}
 
 
-def run_fan(args, torch, dist, world, rank, local):
+def cpu_baseline_cells(terrain, aux, cells, poses, zx, budget_s: float, threads: int = 1):
+    """runOptimization's candidate loop on the CPU: 1 thread = the reference's own loop
+    (orc_score_poses, flags and all); threads > 1 = per-pose totals over OpenMP."""
+    pyoracle = _oracle()
     import numpy as np
 
-    from pointcloud_processor_amd import _abi, synth
+    T, A = pyoracle.Cloud(terrain), pyoracle.Cloud(aux)
+    prm = pyoracle.vl_params()
+    flags = np.zeros(cells.xyz.shape[0], np.uint8)
+    chunk = 1 if threads == 1 else threads
+    pyoracle.set_threads(threads)
+    k = 0
+    t0 = time.perf_counter()
+    while k < len(poses) and time.perf_counter() - t0 < budget_s:
+        sel = poses[k:k + chunk]
+        if threads == 1:
+            pyoracle.score_poses(T, A, cells.xyz, cells.normals, sel, zx, prm, flags)
+        else:
+            pyoracle.score_totals(T, A, cells.xyz, cells.normals, sel, zx, prm)
+        k += sel.shape[0]
+    dt = time.perf_counter() - t0
+    pyoracle.set_threads(1)
+    return {"value": k / dt, "unit": "poses/s", "cores": threads, "kind": "port",
+            "sample": f"{k} of {len(poses)} poses x {cells.xyz.shape[0]} cells in {dt:.1f} s "
+                      f"({'orc_score_poses' if threads == 1 else 'orc_score_totals, OpenMP'})"}
 
-    ctx = _abi.Context(local)
-    scene = synth.terrain_scene()
-    ctx.set_terrain(scene.terrain, point_step=32)
-    bbox = _grid_bbox(scene.area)
-    from pointcloud_processor_amd import dist as pd
 
-    P_total = args.poses_per_gpu * world
-    poses_all, nc = _poses_for(ctx, bbox, scene.zx120_pose5, P_total)
-    lo, hi = pd.shard(P_total, world, rank)
-    poses = np.ascontiguousarray(poses_all[lo:hi])
-    fan = _abi.fan_params(n_az=args.n_az, n_el=args.n_el)
-    on_gpu = torch.cuda.is_available()
-    dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
+def cpu_baseline_c3(clouds, box, leaf, tfs):
+    """processCloudSimple (crop + VoxelGrid) per cloud, then processRobotCloud's transform +
+    colour, on the CPU restatement: one whole C3 frame, one thread (PCL's path)."""
+    pyoracle = _oracle()
+    n_in = sum(c.shape[0] for c in clouds)
+    t0 = time.perf_counter()
+    n_out = 0
+    for c, (t, q), rgb in zip(clouds, tfs, [(255, 0, 0), (0, 0, 255)]):
+        kept = pyoracle.crop_box(c, box)
+        vox, _, _, _ = pyoracle.voxel_grid(c[kept], leaf)
+        out = pyoracle.transform_rgb(vox, t, q, rgb)
+        n_out += out.shape[0]
+    dt = time.perf_counter() - t0
+    return {"value": n_in / dt, "unit": "input points/s", "cores": 1, "kind": "port",
+            "sample": f"one whole frame: {n_in} input points -> {n_out} merged in {dt:.2f} s "
+                      "(oracle crop_box + voxel_grid + transform_rgb)"}
 
-    def step():
-        blocked, units, _, _ = ctx.raycast_fan(poses, fan)
-        keys, best = pd.reduce_fan(blocked, lo, hi, P_total, dist, dev)   # the one collective
-        return int(units.sum()), best, keys
+
+def _timed(step, args, dist, on_gpu, dev):
+    """W untimed warmup steps, then exactly K steps between barrier + synchronize on both
+    sides; -> (max-over-ranks seconds, sum-over-ranks units, last step's result)."""
+    import torch
 
     def barrier_sync():
         if dist is not None:
@@ -157,75 +242,173 @@ def run_fan(args, torch, dist, world, rank, local):
 
     for _ in range(args.warmup):
         step()
-    ctx.profile(True)
-    ctx.profile_reset()
     barrier_sync()
     t0 = time.perf_counter()
-    units_local = 0
-    best = -1
+    units = 0.0
+    res = None
     for _ in range(args.steps):
-        u, best, keys = step()
-        units_local += u
+        u, res = step()
+        units += u
     barrier_sync()
     dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    uu = torch.tensor([units], dtype=torch.float64)
+    if dist is not None:
+        t, uu = t.to(dev), uu.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(uu, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(uu.item()), res
+
+
+def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
+    """Roofline of k_raycast_fan from the kernel's own request counts:
+    requested bytes = 2 B per z-band probe + 16 B per scanned block (8-B directory entry +
+    8-B step) + 16 B per point test + 16 B per ray (azimuth table) + 8 B per wave partial.
+    These are the bytes the kernel's loads and stores ask for (served by L1/L2/MALL: the 1M-pt
+    terrain's working set is cache-resident); the HBM-side bytes are the PMC `traffic`."""
+    st = ctx.raycast_fan_stats(poses, fan)
+    rays = poses.shape[0] * fan.n_az * fan.n_el
+    waves = poses.shape[0] * ((fan.n_az * fan.n_el + 63) // 64)
+    req = 2.0 * st["samples_visited"] + 16.0 * st["scanned_stencils"] + 16.0 * st["point_tests"] \
+        + 16.0 * rays \
+        + 8.0 * waves
+    ref_model = 64.0 * units_per_launch + 12.0 * st["point_tests"]
+    traffic = _traffic_from_profiles("fan")
+    achieved = _gbs(req, avg_kernel_s)
+    return {
+        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS if achieved else None,
+        "traffic": traffic,
+        "traffic_gbs": _gbs(traffic, avg_kernel_s),
+        "traffic_frac": (_gbs(traffic, avg_kernel_s) or 0.0) / HBM_PEAK_GBS if traffic else None,
+        "kernel": "k_raycast_fan<0, 64, true>", "avg_kernel_ms": avg_kernel_s * 1e3,
+        "requested_bytes_per_launch": req,
+        "model": "requested bytes: 2 B/probe + 16 B/scan + 16 B/point test + 16 B/ray + "
+                 "8 B/wave (pcp_raycast_fan_stats counts); traffic = PMC FETCH(x2)+WRITE per "
+                 "launch (profiles/pmc_traffic.json)",
+        "limiter": "vector-memory gather path (TA/TD busy, L1 tag lookups per instruction; "
+                   "profiles/r02_fan_pmc*.txt), not HBM: the terrain lives in L2/MALL",
+        "alg_reference_bytes_per_launch": ref_model,
+        "alg_reference_bytes_frac": (ref_model / avg_kernel_s / 1e9 / HBM_PEAK_GBS)
+        if avg_kernel_s else None,
+        "alg_reference_model": "SURVEY 8d: 64 B per reference sample query + 12 B per point "
+                               "test; > 1 because the kernel skips ~95 % of the sample "
+                               "queries exactly (DESIGN.md §5)",
+        "diag": st,
+    }
+
+
+def run_all(args, torch, dist, world, rank, local, backend):
+    """Default line: the C2 fan (value), reference-mode scoring of the same node
+    (runOptimization, poses/s) and the C3 filter frame, each timed as its own loop of K steps
+    with the barrier / max-over-ranks discipline; CPU baselines on rank 0 at N = 1."""
+    import numpy as np
+
+    from pointcloud_processor_amd import _abi, synth
+    from pointcloud_processor_amd import dist as pd
+
+    on_gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", local) if (on_gpu and backend != "gloo") else torch.device("cpu")
+    ctx = _abi.Context(local)
+    scene = synth.terrain_scene()
+    ctx.set_terrain(scene.terrain, point_step=32)
+    P_total = args.poses_per_gpu * world
+    poses_all, nc = _poses_for(ctx, _grid_bbox(scene.area), scene.zx120_pose5, P_total)
+    lo, hi = pd.shard(P_total, world, rank)
+    poses = np.ascontiguousarray(poses_all[lo:hi])
+    fan = _abi.fan_params(n_az=args.n_az, n_el=args.n_el)
+
+    # ---- C2 / C4: the fan (the headline) -------------------------------------------------
+    best = {}
+
+    def fan_step():
+        blocked, units, _, _ = ctx.raycast_fan(poses, fan)
+        keys, b = pd.reduce_fan(blocked, lo, hi, P_total, dist, dev)   # the one collective
+        best["fan"] = b
+        return int(units.sum()), keys
+
+    ctx.profile(True)
+    ctx.profile_reset()
+    dt, units_all, _ = _timed(fan_step, args, dist, on_gpu, dev)
     ctx.profile(False)
     k_ms, k_n = ctx.profile_get("raycast_fan")
-    # max-over-ranks time, sum-over-ranks units
-    t = torch.tensor([dt], dtype=torch.float64)
-    u = torch.tensor([units_local], dtype=torch.float64)
-    if dist is not None:
-        t = t.to(dev); u = u.to(dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(u, op=dist.ReduceOp.SUM)
-    dt_max, units_all = float(t.item()), float(u.item())
-    # diagnostic (untimed): algorithmic bytes of one launch
-    st = ctx.raycast_fan_stats(poses, fan)
-    units_per_launch = units_local / max(args.steps, 1)
-    alg_bytes = 64.0 * units_per_launch + 12.0 * st["point_tests"]
     avg_kernel_s = (k_ms / max(k_n, 1)) * 1e-3
-    achieved = alg_bytes / avg_kernel_s / 1e9 if avg_kernel_s > 0 else None
+    units_per_launch = units_all / max(world, 1) / max(args.steps, 1)
     out = {
         "metric": METRIC,
-        "value": units_all / dt_max,
+        "value": units_all / dt,
         "unit": "ray-hit tests/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": dt_max / max(args.steps, 1) * 1e3,
+        "ms_per_step": dt / max(args.steps, 1) * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64 march / f32 point test",
         "data": "synthetic (seeded T1M L-pit terrain, reference candidate lattice)",
         "config": {"workload": "C2: 1M-pt L-shape excavation terrain, 1024x256 ray fan, "
-                               f"{args.poses_per_gpu} candidate poses per GPU",
+                               f"{args.poses_per_gpu} candidate poses per GPU"
+                               + (" (C4 at 8 GPUs x 512)" if args.poses_per_gpu == 512 else ""),
                    "terrain_points": int(scene.terrain.shape[0]),
                    "poses_total": P_total, "fan": [args.n_az, args.n_el],
-                   "num_candidates_lattice": nc, "parallelism": f"pose-shard x{world}"},
-        "poses_per_s": P_total * args.steps / dt_max,
-        "best_pose": best,
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": _traffic_from_profiles("fan"),
-            # the survey's model charges 64 B to every sample query the reference would make;
-            # the kernel skips ~95 % of them exactly, so frac > 1.  What it really moves:
-            "traffic_gbs": _gbs(_traffic_from_profiles("fan"), avg_kernel_s),
-            "limiter": "vector-memory address/data path of dependent L2 gathers (TA 83 %, TD "
-                       "93 % busy, profiles/r01_fan_pmc.txt), not HBM",
-            "kernel": "k_raycast_fan<0, 64, true>", "avg_kernel_ms": avg_kernel_s * 1e3,
-            "alg_bytes_per_launch": alg_bytes,
-            "model": "64 B/sample query + 12 B/point test (SURVEY 8d)",
-            "diag": st,
-        },
+                   "num_candidates_lattice": nc, "parallelism": f"pose-shard x{world}",
+                   "collective": None if dist is None else f"all_reduce(MIN) over {backend}"},
+        "poses_per_s": P_total * args.steps / dt,
+        "best_pose": best["fan"],
+        "roofline": _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if dist is not None and backend == "gloo" and on_gpu:
+        out["rehearsal"] = (f"{world} ranks on {torch.cuda.device_count()} GPU(s): collective "
+                            "over gloo, ranks share devices")
+    host = _host_cpu()
+    cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    if cpu:
         out["cpu_baseline"] = cpu_baseline_fan(scene.terrain, poses, fan, args.cpu_seconds)
-        host = _host_cpu()
-        mt = max(1, min(16, host["affinity"] or 1))     # the box's CPU share is 16
         out["cpu_baseline_mt"] = cpu_baseline_fan(scene.terrain, poses, fan,
-                                                  args.cpu_seconds / 2, threads=mt)
+                                                  args.cpu_seconds / 2,
+                                                  threads=host["threads_used"])
         out["cpu_baseline_mt"]["host"] = host
+
+    # ---- reference mode: runOptimization over the excavation cells (poses/s) -----------
+    if not args.fan_only:
+        cells = synth.excavation_cells(scene.area)
+        aux = synth.aux_cloud()
+        ctx.set_aux_cloud(aux, point_step=32)
+        ctx.set_cells(cells.xyz, cells.normals)
+        cposes_all, cnc = _poses_for(ctx, cells.grid_bbox, scene.zx120_pose5, P_total)
+        cposes = np.ascontiguousarray(cposes_all[lo:hi])
+        params = _abi.default_vl_params()
+        flags = np.zeros(cells.xyz.shape[0], np.uint8)
+
+        def cells_step():
+            tot, cov, rep = ctx.score_poses(cposes, scene.zx120_pose5, params, flags)
+            _, b, _ = pd.reduce_scores(tot, lo, hi, P_total, dist, dev)   # the one collective
+            best["cells"] = b
+            return cposes.shape[0], tot
+
+        ctx.profile(True)
+        ctx.profile_reset()
+        cdt, cunits, _ = _timed(cells_step, args, dist, on_gpu, dev)
+        ctx.profile(False)
+        kern = {k: ctx.profile_get(k)[0] / max(ctx.profile_get(k)[1], 1)
+                for k in ("score_cells", "pose_sum", "cell_flags")}
+        out["poses_per_s_reference_mode"] = cunits / cdt
+        out["reference_mode"] = {
+            "workload": f"runOptimization: {P_total} candidate poses x {cells.xyz.shape[0]} "
+                        "cells, visibility by ray march (virtual_lidar.cpp:454-548)",
+            "value": cunits / cdt, "unit": "poses/s", "ms_per_step": cdt / args.steps * 1e3,
+            "best_pose": best["cells"], "num_candidates_lattice": cnc,
+            "kernel_avg_ms": kern, "dtype": "f64",
+        }
+        if cpu:
+            out["reference_mode"]["cpu_baseline"] = cpu_baseline_cells(
+                scene.terrain, aux, cells, cposes, scene.zx120_pose5, args.cpu_seconds / 2)
+            out["reference_mode"]["cpu_baseline_mt"] = cpu_baseline_cells(
+                scene.terrain, aux, cells, cposes, scene.zx120_pose5, args.cpu_seconds / 2,
+                threads=host["threads_used"])
+        out["c3"] = run_filter(args, torch, dist, world, rank, local, backend, embedded=True,
+                               cpu=cpu)
     ctx.close()
     return out
 
@@ -270,14 +453,18 @@ def _pcie_inclusive(ctx, clouds, box, tfs, n_in, cap, reps=5):
     return res
 
 
-def run_filter(args, torch, dist, world, rank, local):
-    """C3: crop + voxel(0.05) + transform on a 10M-pt dual-LiDAR frame, inputs in HBM."""
+def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=False, cpu=False):
+    """C3: crop + voxel(0.05) + transform on a 10M-pt dual-LiDAR frame, inputs in HBM.  Every
+    rank runs its own frame (replicas); value = input points of all ranks / max-over-ranks
+    time."""
     import math
 
     import numpy as np
 
     from pointcloud_processor_amd import _abi, synth
 
+    on_gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", local) if (on_gpu and backend != "gloo") else torch.device("cpu")
     ctx = _abi.Context(local)
     n_each = args.filter_points // 2
     clouds = [synth.lidar_cloud(n_each, sensor_height=2.0, seed=1 + 2 * rank),
@@ -295,93 +482,80 @@ def run_filter(args, torch, dist, world, rank, local):
            ((0.55, 0.4, 3.5), (0.0, math.sin(0.4363 / 2), 0.0, math.cos(0.4363 / 2)))]
     cap = sum(c.shape[0] for c in clouds)
     out_d = ctx.dev_alloc(cap * 32)
+    n_in = sum(c.shape[0] for c in clouds)
+    last = {}
 
     def step():
-        return ctx.filter_merge_device(views, [box, box], 0.05, tfs, [(255, 0, 0), (0, 0, 255)],
-                                       out_d, cap)
+        n_out, per = ctx.filter_merge_device(views, [box, box], 0.05, tfs,
+                                             [(255, 0, 0), (0, 0, 255)], out_d, cap)
+        last["n_out"], last["per"] = n_out, per
+        return n_in, n_out
 
-    for _ in range(args.warmup):
-        n_out, per = step()
     ctx.profile(True)
     ctx.profile_reset()
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        n_out, per = step()
-    dt = time.perf_counter() - t0
+    dt, units_all, _ = _timed(step, args, dist, on_gpu, dev)
     ctx.profile(False)
     g_ms, g_n = ctx.profile_get("filter_merge")
-    n_in = sum(c.shape[0] for c in clouds)
     step_dev_ms = g_ms / max(g_n, 1)
-    # per-stage breakdown from one eager (non-graph) context, untimed
-    os.environ["PCP_NO_GRAPHS"] = "1"
-    ectx = _abi.Context(local)
-    os.environ.pop("PCP_NO_GRAPHS")
-    ectx.profile(True)
-    for _ in range(3):
-        ectx.filter_merge_device(views, [box, box], 0.05, tfs, [(255, 0, 0), (0, 0, 255)], out_d,
-                                 cap)
-    stages = {k: ectx.profile_get(k)[0] / 3 for k in ("crop", "voxel", "transform", "filter_merge")}
-    ectx.close()
-    pcie = None if args.no_pcie else _pcie_inclusive(ctx, clouds, box, tfs, n_in, cap)
+    n_out = last["n_out"]
+    stages = None
+    pcie = None
+    if not embedded:
+        # per-stage breakdown from one eager (non-graph) context, untimed
+        os.environ["PCP_NO_GRAPHS"] = "1"
+        ectx = _abi.Context(local)
+        os.environ.pop("PCP_NO_GRAPHS")
+        ectx.profile(True)
+        for _ in range(3):
+            ectx.filter_merge_device(views, [box, box], 0.05, tfs, [(255, 0, 0), (0, 0, 255)],
+                                     out_d, cap)
+        stages = {k: ectx.profile_get(k)[0] / 3 for k in ("crop", "voxel", "transform",
+                                                          "filter_merge")}
+        ectx.close()
+        pcie = None if args.no_pcie else _pcie_inclusive(ctx, clouds, box, tfs, n_in, cap)
     alg = 12.0 * n_in + 16.0 * n_out
+    traffic = _traffic_from_profiles("filter")
     res = {
-        "metric": "crop+voxel+transform points/s (C3)", "value": n_in * args.steps / dt,
+        "metric": "crop+voxel+transform points/s (C3)", "value": units_all / dt,
         "unit": "input points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / max(args.steps, 1) * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic 2 x LiDAR-like clouds, point_step 16, resident in HBM",
-        "config": {"workload": f"C3: crop+voxel(0.05)+transform, {n_in} pts", "n_out": n_out,
-                   "per_cloud": [int(x) for x in per], "graph": True},
+        "config": {"workload": f"C3: crop+voxel(0.05)+transform, {n_in} pts per GPU",
+                   "n_out": n_out, "per_cloud": [int(x) for x in last["per"]], "graph": True},
         "roofline": {"bound": "hbm", "achieved": alg / (step_dev_ms * 1e-3) / 1e9,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": alg / (step_dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": _traffic_from_profiles("filter"),
-                     "traffic_gbs": _gbs(_traffic_from_profiles("filter"), step_dev_ms * 1e-3),
+                     "traffic": traffic,
+                     "traffic_gbs": _gbs(traffic, step_dev_ms * 1e-3),
                      "limiter": "crop streams at ~4.8 TB/s; the voxel stage (sort of the ~1 M "
                                 "cropped points) is launch- and latency-bound",
                      "kernel": "filter_merge graph (all stages)", "avg_kernel_ms": step_dev_ms,
-                     "eager_stage_ms": stages,
                      "model": "12 B/input point + 16 B/output point (SURVEY 8d)"},
-        "pcie_inclusive": pcie,
     }
+    if stages is not None:
+        res["roofline"]["eager_stage_ms"] = stages
+    if pcie is not None:
+        res["pcie_inclusive"] = pcie
+    if cpu or (not embedded and rank == 0 and world == 1 and not args.no_cpu_baseline):
+        res["cpu_baseline"] = cpu_baseline_c3(clouds, np.array(box), 0.05, tfs)
     for p in dptr + [out_d]:
         ctx.dev_free(p)
     ctx.close()
     return res
 
 
-def run_cells(args, torch, dist, world, rank, local):
-    """Reference-mode scoring (runOptimization) for the same poses: poses/s."""
-    import numpy as np
-
-    from pointcloud_processor_amd import _abi, synth
-
-    ctx = _abi.Context(local)
-    scene = synth.terrain_scene()
-    cells = synth.excavation_cells(scene.area)
-    ctx.set_terrain(scene.terrain, point_step=32)
-    ctx.set_aux_cloud(synth.aux_cloud(), point_step=32)
-    ctx.set_cells(cells.xyz, cells.normals)
-    P_total = args.poses_per_gpu * world
-    poses_all, nc = _poses_for(ctx, cells.grid_bbox, scene.zx120_pose5, P_total)
-    poses = np.ascontiguousarray(poses_all[rank * args.poses_per_gpu:(rank + 1) * args.poses_per_gpu])
-    params = _abi.default_vl_params()
-    flags = np.zeros(cells.xyz.shape[0], np.uint8)
-    for _ in range(args.warmup):
-        ctx.score_poses(poses, scene.zx120_pose5, params, flags)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tot, cov, rep = ctx.score_poses(poses, scene.zx120_pose5, params, flags)
-    dt = time.perf_counter() - t0
-    ctx.close()
-    return {"metric": "candidate poses/sec (reference cell scoring)",
-            "value": P_total * args.steps / dt, "unit": "poses/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic", "config": {"workload": f"{P_total} poses x {cells.xyz.shape[0]} cells"},
-            "best_pose": int(rep.best_idx)}
+def run_cells(args, torch, dist, world, rank, local, backend=None):
+    """Reference-mode scoring (runOptimization) alone: poses/s."""
+    a = argparse.Namespace(**vars(args))
+    out = run_all(a, torch, dist, world, rank, local, backend)
+    rm = out["reference_mode"]
+    return {"metric": "candidate poses/sec (reference cell scoring)", "value": rm["value"],
+            "unit": "poses/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": rm["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": rm["workload"]}, "best_pose": rm["best_pose"],
+            "detail": rm}
 
 
 def main():
@@ -389,7 +563,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=["fan", "filter", "cells"], default="fan")
+    ap.add_argument("--mode", choices=["all", "fan", "filter", "cells", "launch-check"],
+                    default="all",
+                    help="all (default): the fan line with reference-mode scoring and C3 as "
+                         "extra keys; fan: the fan alone (profiling); filter: C3 with PCIe and "
+                         "stage breakdown; cells: reference mode alone")
     ap.add_argument("--poses-per-gpu", type=int, default=256)
     ap.add_argument("--n-az", type=int, default=1024)
     ap.add_argument("--n-el", type=int, default=256)
@@ -399,9 +577,21 @@ def main():
     ap.add_argument("--no-pcie", action="store_true",
                     help="filter mode: skip the host-buffer (PCIe-inclusive) measurement")
     args = ap.parse_args()
-    torch, dist, world, rank, local = _dist_init(args.gpus)
-    fn = {"fan": run_fan, "filter": run_filter, "cells": run_cells}[args.mode]
-    out = fn(args, torch, dist, world, rank, local)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
+    args.fan_only = args.mode == "fan"
+    torch, dist, world, rank, local, backend = _dist_init(args.gpus)
+    if args.mode == "launch-check":   # the launch path alone (CPU test): ranks + one collective
+        t = torch.tensor([float(rank)])
+        if dist is not None:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        out = {"n_gpus": world, "backend": backend, "rank_sum": float(t.item())}
+    elif args.mode == "filter":
+        out = run_filter(args, torch, dist, world, rank, local, backend)
+    elif args.mode == "cells":
+        out = run_cells(args, torch, dist, world, rank, local, backend)
+    else:
+        out = run_all(args, torch, dist, world, rank, local, backend)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

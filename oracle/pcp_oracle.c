@@ -510,6 +510,41 @@ void orc_score_poses(const orc_cloud *terrain, const orc_cloud *aux, int64_t aux
     }
 }
 
+/* The candidate loop's per-pose totals alone (evaluatePosition :627-654 for every pose),
+ * OpenMP over poses -- the CPU baseline's multi-threaded variant.  The flags a pose writes
+ * never feed a score, so each thread keeps its own scratch flags; totals and covered counts
+ * are those of orc_score_poses. */
+void orc_score_totals(const orc_cloud *terrain, const orc_cloud *aux, int64_t aux_n,
+                      const double *cxyz, const float *cn, int64_t C,
+                      const double *poses5, int64_t P, const double zx120[5],
+                      const orc_vl_params *p, double *total_score, int32_t *covered)
+{
+    vl_env E = {terrain, aux, aux_n, p->max_distance};
+#ifdef _OPENMP
+#pragma omp parallel num_threads(g_threads)
+#endif
+    {
+        uint8_t *fl = (uint8_t *)calloc((size_t)(C > 0 ? C : 1), 1);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t k = 0; k < P; ++k) {
+            const double *pose = poses5 + 5 * k;
+            double total = 0.0;
+            int32_t cov = 0;
+            for (int64_t i = 0; i < C; ++i) {
+                const double sz = eval_cell(&E, zx120, cxyz + 3 * i, cn + 3 * i, &fl[i], 1);
+                const double sm = eval_cell(&E, pose, cxyz + 3 * i, cn + 3 * i, &fl[i], 0);
+                const double comb = sz > sm ? sz : sm;
+                if (comb > 0) { cov++; total += comb; }
+            }
+            total_score[k] = total;
+            covered[k] = cov;
+        }
+        free(fl);
+    }
+}
+
 /* ================================================================================ */
 /* Fan raycast (BASELINE configs[1]) using the :765-797 march rule                   */
 /* ================================================================================ */

@@ -99,6 +99,11 @@ void orc_score_poses(const orc_cloud *terrain, const orc_cloud *aux, int64_t aux
                      const double *poses5, int64_t n_poses, const double zx120[5],
                      const orc_vl_params *p, uint8_t *cell_flags,
                      double *total_score, int32_t *covered, orc_vl_report *rep);
+/* per-pose totals/covered only (no flags), OpenMP over poses: the CPU baseline's MT leg */
+void orc_score_totals(const orc_cloud *terrain, const orc_cloud *aux, int64_t aux_n,
+                      const double *cells_xyz, const float *cells_nrm, int64_t n_cells,
+                      const double *poses5, int64_t n_poses, const double zx120[5],
+                      const orc_vl_params *p, double *total_score, int32_t *covered);
 
 /* Dense azimuth x elevation fan (BASELINE configs[1]): per pose, ray
  * (az_i, el_j) with local dir (cos el cos a_i, cos el sin a_i, sin el), a_i = 2*pi*i/n_az,

@@ -53,6 +53,8 @@ _SIGS = [
                                             C.c_int64]),
     ("orc_score_poses", None, [_P, _P, C.c_int64, _P, _P, C.c_int64, _P, C.c_int64, _P,
                                C.POINTER(VlParams), _P, _P, _P, C.POINTER(VlReport)]),
+    ("orc_score_totals", None, [_P, _P, C.c_int64, _P, _P, C.c_int64, _P, C.c_int64, _P,
+                                C.POINTER(VlParams), _P, _P]),
     ("orc_raycast_fan", None, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                C.c_double, _P, _P, _P]),
     ("orc_fan_tables", None, [C.c_int32, C.c_int32, C.c_double, C.c_double, _P, _P, _P, _P]),
@@ -190,6 +192,22 @@ def score_poses(terrain: Cloud | None, aux: Cloud | None, cells_xyz, cells_nrm, 
                           aux.n if aux else 0, _p(cx), _p(cn), cx.shape[0], _p(poses), P, _p(zx),
                           C.byref(params), _p(cell_flags), _p(tot), _p(cov), C.byref(rep))
     return tot[:P].copy(), cov[:P].copy(), rep
+
+
+def score_totals(terrain: Cloud | None, aux: Cloud | None, cells_xyz, cells_nrm, poses5,
+                 zx120_pose5, params):
+    """Per-pose total_score / covered of the candidate loop (no flags), OpenMP over poses."""
+    cx = np.ascontiguousarray(cells_xyz, np.float64).reshape(-1, 3)
+    cn = np.ascontiguousarray(cells_nrm, np.float32).reshape(-1, 3)
+    poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+    zx = np.ascontiguousarray(zx120_pose5, np.float64)
+    P = poses.shape[0]
+    tot = np.empty(max(P, 1), np.float64)
+    cov = np.empty(max(P, 1), np.int32)
+    lib().orc_score_totals(terrain.h if terrain else None, aux.h if aux else None,
+                           aux.n if aux else 0, _p(cx), _p(cn), cx.shape[0], _p(poses), P,
+                           _p(zx), C.byref(params), _p(tot), _p(cov))
+    return tot[:P].copy(), cov[:P].copy()
 
 
 def raycast_fan(terrain: Cloud, poses5, n_az, n_el, el_min, el_max, max_distance,

@@ -405,6 +405,14 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         return set_err(ctx, PCP_E_INVALID, "index cloud of %llu points exceeds 2^28",
                        (unsigned long long)n);
     ProfScope prof(ctx, PCP_K_INDEX_BUILD);
+    // Invalidate everything derived from the previous cloud first: an early return below (e.g.
+    // an allocation failure after the new geometry is written) must not leave the old block
+    // copy or z bands paired with the new grid.  present is set again only on success.
+    g.present = false;
+    g.occz_ok = false;
+    g.occ2_ok = false;
+    g.blk_ok = false;
+    g.blk_fail = false;
     // 1. stage the raw AoS bytes (the PointCloud2 data blob)
     const uint64_t raw_bytes = n * (uint64_t)v.point_step;
     PCP_HIP(ctx, ctx->stage.ensure(raw_bytes));
@@ -428,7 +436,6 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     if (int rc0 = read_small(ctx, bb_h, bb_d, sizeof(bb_h), st)) return rc0;
     uint32_t nfin;
     memcpy(&nfin, &bb_h[8], 4);
-    g.present = true;
     g.r_q = r_q;
     g.n_pts = nfin;
     if (nfin == 0) {   // a tree over zero valid points: never returns neighbours
@@ -446,7 +453,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         PCP_HIP(ctx, hipMemsetAsync(g.occz.p, 0xFF, 1, st));
         PCP_HIP(ctx, hipMemsetAsync(static_cast<char *>(g.occz.p) + 1, 0, 1, st));
         g.occz_ok = zsort;
-        g.blk_ok = false;
+        g.present = true;
         return PCP_OK;
     }
     for (int a = 0; a < 3; ++a) {
@@ -526,8 +533,8 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         PCP_CHECK_LAUNCH(ctx);
         g.occz_ok = true;
     }
-    g.blk_ok = false;
     PCP_HIP(ctx, hipStreamSynchronize(st));
+    g.present = true;
     return PCP_OK;
 }
 
@@ -535,7 +542,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
 // 8 corners, ~8 n entries; not built past the 2^28 point cap -- the scans fall back to the
 // per-cell runs)
 int build_blocks(pcp_ctx *ctx, GridIndex &g) {
-    if (g.blk_ok || !g.present || !g.occz_ok || g.n_pts == 0) return PCP_OK;
+    if (g.blk_ok || g.blk_fail || !g.present || !g.occz_ok || g.n_pts == 0) return PCP_OK;
     hipStream_t st = ctx->stream;
     ProfScope prof(ctx, PCP_K_INDEX_BUILD);
     const GridView gv = g.view();
@@ -552,8 +559,18 @@ int build_blocks(pcp_ctx *ctx, GridIndex &g) {
     if (rc) return rc;
     uint32_t nb_tot = 0;
     if ((rc = read_small(ctx, &nb_tot, g.bstart.as<uint32_t>() + ncell, 4, st))) return rc;
-    if (nb_tot == 0 || nb_tot >= (1u << 28)) return PCP_OK;
-    PCP_HIP(ctx, g.bpts.ensure((size_t)nb_tot * sizeof(float4)));
+    if (nb_tot == 0 || nb_tot >= (1u << 28)) {   // past the 32-bit offset cap: never retry
+        g.blk_fail = true;
+        return PCP_OK;
+    }
+    // the copy is an optional speed-up: if it cannot be allocated, the queries keep the
+    // per-cell runs (scan_stencil) instead of failing, and no later query retries
+    if (g.bpts.ensure((size_t)nb_tot * sizeof(float4)) != hipSuccess) {
+        (void)hipGetLastError();
+        g.bpts.release();
+        g.blk_fail = true;
+        return PCP_OK;
+    }
     const uint64_t n = g.n_pts;
     hipLaunchKernelGGL(k_blk_fill, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads),
                        0, st, g.pts.as<const float4>(), n, g.start.as<const uint32_t>(), m,
@@ -564,7 +581,9 @@ int build_blocks(pcp_ctx *ctx, GridIndex &g) {
 }
 
 int terrain_blocks_before_query(pcp_ctx *ctx) {
-    if (ctx->terrain_blocks <= 0 || ctx->terrain.blk_ok || !ctx->terrain.present) return PCP_OK;
+    if (ctx->terrain_blocks <= 0 || ctx->terrain.blk_ok || ctx->terrain.blk_fail ||
+        !ctx->terrain.present)
+        return PCP_OK;
     ++ctx->terrain_queries;
     if (ctx->terrain_blocks == 1 && ctx->terrain_queries < 2) return PCP_OK;
     return build_blocks(ctx, ctx->terrain);

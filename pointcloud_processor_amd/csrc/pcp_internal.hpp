@@ -120,6 +120,8 @@ struct GridIndex {
     DevBuf pts, start, occ2, occz, bstart, bpts;
     bool occz_ok = false;
     bool blk_ok = false;         // block-major copy built (bstart / bpts)
+    bool blk_fail = false;       // copy unavailable for this index (size cap or allocation
+                                 // failure): the scans keep the per-cell runs, no retry
     bool occ2_ok = false;        // occ2 built (only indices queried by stencil_any need it)
     GridView view() const;
     void release() {
@@ -131,6 +133,8 @@ struct GridIndex {
         bpts.release();
         occz_ok = false;
         blk_ok = false;
+        blk_fail = false;
+        occ2_ok = false;
         present = false;
         n_pts = 0;
     }

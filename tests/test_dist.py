@@ -111,3 +111,32 @@ def test_two_rank_gloo_matches_single_process():
         np.testing.assert_array_equal(vec, s["total"])     # golden: one process, all poses
         assert bidx == int(s["report"][0])
         assert bscore == float(s["best_score"])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_self_launch(n):
+    """`bench.py --gpus N` with no launcher starts N ranks itself (one process per GPU): the
+    line reports n_gpus = N and one collective over all ranks ran (gloo here, no GPU)."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n),
+                        "--mode", "launch-check"], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["rank_sum"] == n * (n - 1) / 2
+
+
+def test_bench_rejects_mismatched_world():
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2",
+                        "--mode", "launch-check"], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

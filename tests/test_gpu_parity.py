@@ -456,6 +456,79 @@ def test_raycast_fan_full_c2_workload(gpu, oracle, loaded, scene):
     assert best == int(np.argmin(r_blocked))
 
 
+def test_c4_sharded_4096_poses(gpu, oracle, loaded, scene):
+    """BASELINE configs[3]: 4096 candidate poses split into 8 contiguous shards of 512 (one
+    per GPU of the 8-GPU node), each shard through pcp_raycast_fan, combined as the RCCL
+    all-reduce(MIN) combines them (dist.reduce_fan key vectors, elementwise min).  Blocked
+    counts and ray-hit tests of all 4096 poses and the best index against the oracle; first
+    hits of two sampled shards bit-exact."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    from pointcloud_processor_amd import dist as pd
+
+    T, _ = loaded
+    P, G = 4096, 8
+    poses, _ = bench._poses_for(gpu, bench._grid_bbox(scene.area), scene.zx120_pose5, P)
+    assert poses.shape == (P, 5)
+    fan = _abi.fan_params()
+    key = np.full(P, pd.INT64_MAX, np.int64)
+    units = np.zeros(P, np.uint64)
+    sampled = {0: None, 5: None}
+    for g in range(G):
+        lo, hi = pd.shard(P, G, g)
+        assert hi - lo == 512
+        b, u, fh, _ = gpu.raycast_fan(poses[lo:hi], fan, want_first_hit=g in sampled)
+        k, _ = pd.reduce_fan(b, lo, hi, P)          # this rank's contribution
+        key = np.minimum(key, k)                      # = all_reduce(MIN) over the ranks
+        units[lo:hi] = u
+        if g in sampled:
+            sampled[g] = fh
+    best = int(np.argmin(key))
+    oracle.set_threads(16)
+    try:
+        r_blocked, r_units, _ = oracle.raycast_fan(T, poses, 1024, 256, fan.el_min, fan.el_max,
+                                                   fan.max_distance, want_first_hit=False)
+        for g, fh in sampled.items():
+            lo, hi = pd.shard(P, G, g)
+            sel = np.arange(lo, hi, 16)                 # 32 poses of the shard
+            _, _, r_fh = oracle.raycast_fan(T, poses[sel], 1024, 256, fan.el_min, fan.el_max,
+                                            fan.max_distance)
+            bad = np.count_nonzero(fh[sel - lo] != r_fh)
+            assert bad == 0, f"shard {g}: {bad} first hits differ"
+    finally:
+        oracle.set_threads(1)
+    np.testing.assert_array_equal(key, r_blocked.astype(np.int64))
+    np.testing.assert_array_equal(units, r_units)
+    assert best == int(np.argmin(r_blocked))
+
+
+def test_terrain_replaced_after_block_copy(oracle, small_scene, scene):
+    """set_terrain(A), two fan queries (the second builds A's block-major copy), then
+    set_terrain(B) and a query: B's results must match the oracle on B (no stale copy or z
+    bands of A paired with B's grid)."""
+    ctx = _abi.Context(0)
+    try:
+        fan = _abi.fan_params(n_az=256, n_el=32)
+        poses = np.array([[1.0, 0.5, 1.5, -0.3, 0.4], [6.0, -2.0, 1.2, -0.4, 2.5]])
+        ctx.set_terrain(scene.terrain, point_step=32)
+        ctx.raycast_fan(poses, fan)
+        ctx.raycast_fan(poses, fan)
+        B = small_scene.terrain
+        ctx.set_terrain(B, point_step=32)
+        for _ in range(3):   # before and after B's own block copy
+            blocked, units, fh, _ = ctx.raycast_fan(poses, fan, want_first_hit=True)
+            r_b, r_u, r_fh = oracle.raycast_fan(oracle.Cloud(B), poses, 256, 32, fan.el_min,
+                                                fan.el_max, fan.max_distance)
+            np.testing.assert_array_equal(fh, r_fh)
+            np.testing.assert_array_equal(blocked, r_b)
+            np.testing.assert_array_equal(units, r_u)
+    finally:
+        ctx.close()
+
+
 def _rel_close(a, b, tol=1e-12):
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     return np.all(np.abs(a - b) <= tol * np.maximum(1.0, np.abs(b)))

@@ -25,7 +25,7 @@ if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
   step bench 600 python bench.py --steps 10 --warmup 3
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
-  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline
+  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --mode fan --steps 5 --warmup 2 --no-cpu-baseline
 fi
 if [ "$WHAT" = modes ]; then
   step bench_filter 300 python bench.py --mode filter --steps 10 --warmup 2
@@ -38,13 +38,13 @@ if [ "$WHAT" = pmc ] || [ "$WHAT" = modes ]; then
              "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
              "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
     i=$((i+1))
-    step pmc$i 300 rocprofv3 --pmc $set -d gpurun_out/pmc$i -o pmc --output-format csv -- python3 bench.py ${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}
+    step pmc$i 300 rocprofv3 --pmc $set -d gpurun_out/pmc$i -o pmc --output-format csv -- python3 bench.py ${BENCH_ARGS:---mode fan --steps 3 --warmup 1 --no-cpu-baseline}
   done
 fi
 if [ "$WHAT" = traffic ]; then
   # FETCH_SIZE and WRITE_SIZE in separate passes, for the fan kernel and the filter pipeline
-  step pmc_fan_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fan_fetch -o pmc --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
-  step pmc_fan_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_fan_write -o pmc --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+  step pmc_fan_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fan_fetch -o pmc --output-format csv -- python3 bench.py --mode fan --steps 3 --warmup 1 --no-cpu-baseline
+  step pmc_fan_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_fan_write -o pmc --output-format csv -- python3 bench.py --mode fan --steps 3 --warmup 1 --no-cpu-baseline
   export PCP_NO_GRAPHS=1   # every pipeline kernel its own dispatch: 1 + 3 + 3 = 7 pipeline runs
   step pmc_flt_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_flt_fetch -o pmc --output-format csv -- python3 bench.py --mode filter --steps 3 --warmup 1 --no-pcie
   step pmc_flt_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_flt_write -o pmc --output-format csv -- python3 bench.py --mode filter --steps 3 --warmup 1 --no-pcie

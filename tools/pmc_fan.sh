@@ -12,7 +12,7 @@ for set in "TA_TA_BUSY_sum GRBM_GUI_ACTIVE" "TA_ADDR_STALLED_BY_TC_CYCLES_sum" \
            "TD_TD_BUSY_sum" \
            "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --pmc $set -d gpurun_out/pmcf$i -o pmc --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcf$i.log 2>&1
+  timeout -k 10 120 rocprofv3 --pmc $set -d gpurun_out/pmcf$i -o pmc --output-format csv -- python3 bench.py --mode fan --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcf$i.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "pass $i rc=$rc"; tail -20 gpurun_out/pmcf$i.log; exit $rc; fi
 done
