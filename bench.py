@@ -171,15 +171,18 @@ def cpu_baseline_fan(terrain, poses, fan, budget_s: float, threads: int = 1):
     k = 0
     chunk = 1 if threads == 1 else max(1, threads // 16)
     t0 = time.perf_counter()
-    while k < len(poses) and time.perf_counter() - t0 < budget_s:
-        _, u, _ = pyoracle.raycast_fan(T, poses[k:k + chunk], fan.n_az, fan.n_el, fan.el_min,
-                                       fan.el_max, fan.max_distance, want_first_hit=False)
+    while time.perf_counter() - t0 < budget_s:   # cycles through the poses until the budget
+        j = k % len(poses)
+        sel = poses[j:j + chunk]
+        _, u, _ = pyoracle.raycast_fan(T, sel, fan.n_az, fan.n_el, fan.el_min, fan.el_max,
+                                       fan.max_distance, want_first_hit=False)
         units += int(u.sum())
-        k += min(chunk, len(poses) - k)
+        k += sel.shape[0]
     dt = time.perf_counter() - t0
     pyoracle.set_threads(1)
     return {"value": units / dt, "unit": "ray-hit tests/s", "cores": threads, "kind": "port",
-            "sample": f"{k} of {len(poses)} poses x full {fan.n_az}x{fan.n_el} fan, "
+            "sample": f"{k} pose fans (cycling the {len(poses)} poses) x full "
+                      f"{fan.n_az}x{fan.n_el}, "
                       f"{units} sample queries in {dt:.1f} s (oracle/pcp_oracle.c, "
                       f"{threads} thread{'s' if threads > 1 else ''})"}
 
@@ -197,8 +200,9 @@ def cpu_baseline_cells(terrain, aux, cells, poses, zx, budget_s: float, threads:
     pyoracle.set_threads(threads)
     k = 0
     t0 = time.perf_counter()
-    while k < len(poses) and time.perf_counter() - t0 < budget_s:
-        sel = poses[k:k + chunk]
+    while time.perf_counter() - t0 < budget_s:   # cycles through the poses until the budget
+        j = k % len(poses)
+        sel = poses[j:j + chunk]
         if threads == 1:
             pyoracle.score_poses(T, A, cells.xyz, cells.normals, sel, zx, prm, flags)
         else:
@@ -207,25 +211,30 @@ def cpu_baseline_cells(terrain, aux, cells, poses, zx, budget_s: float, threads:
     dt = time.perf_counter() - t0
     pyoracle.set_threads(1)
     return {"value": k / dt, "unit": "poses/s", "cores": threads, "kind": "port",
-            "sample": f"{k} of {len(poses)} poses x {cells.xyz.shape[0]} cells in {dt:.1f} s "
+            "sample": f"{k} pose evaluations (cycling the {len(poses)} poses) x "
+                      f"{cells.xyz.shape[0]} cells in {dt:.1f} s "
                       f"({'orc_score_poses' if threads == 1 else 'orc_score_totals, OpenMP'})"}
 
 
-def cpu_baseline_c3(clouds, box, leaf, tfs):
+def cpu_baseline_c3(clouds, box, leaf, tfs, budget_s: float = 4.0):
     """processCloudSimple (crop + VoxelGrid) per cloud, then processRobotCloud's transform +
     colour, on the CPU restatement: one whole C3 frame, one thread (PCL's path)."""
     pyoracle = _oracle()
     n_in = sum(c.shape[0] for c in clouds)
+    frames = 0
     t0 = time.perf_counter()
-    n_out = 0
-    for c, (t, q), rgb in zip(clouds, tfs, [(255, 0, 0), (0, 0, 255)]):
-        kept = pyoracle.crop_box(c, box)
-        vox, _, _, _ = pyoracle.voxel_grid(c[kept], leaf)
-        out = pyoracle.transform_rgb(vox, t, q, rgb)
-        n_out += out.shape[0]
-    dt = time.perf_counter() - t0
+    while frames == 0 or time.perf_counter() - t0 < budget_s:
+        n_out = 0
+        for c, (t, q), rgb in zip(clouds, tfs, [(255, 0, 0), (0, 0, 255)]):
+            kept = pyoracle.crop_box(c, box)
+            vox, _, _, _ = pyoracle.voxel_grid(c[kept], leaf)
+            out = pyoracle.transform_rgb(vox, t, q, rgb)
+            n_out += out.shape[0]
+        frames += 1
+    dt = (time.perf_counter() - t0) / frames
     return {"value": n_in / dt, "unit": "input points/s", "cores": 1, "kind": "port",
-            "sample": f"one whole frame: {n_in} input points -> {n_out} merged in {dt:.2f} s "
+            "sample": f"{frames} whole frames: {n_in} input points -> {n_out} merged, "
+                      f"{dt:.3f} s per frame "
                       "(oracle crop_box + voxel_grid + transform_rgb)"}
 
 
