@@ -295,6 +295,38 @@ int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
 int pcp_raycast_fan_stamps(pcp_ctx *ctx, const double *poses5, uint64_t n,
                            const pcp_fan_params *fan, uint64_t *stamps);
 
+/* ---- one process, n GPUs: the pose search sharded over devices ------ */
+/* pcp_multi_create(n_dev, devices, &m): one context per device (devices NULL: 0 .. n_dev-1)
+ * and ONE RCCL communicator over them (ncclCommInitAll).  Poses are partitioned contiguously
+ * (rank r takes [r*P/n, (r+1)*P/n), the first P % n ranks one more, the split of
+ * runOptimization's candidate loop, virtual_lidar.cpp:467-475); the terrain, zx120 cloud and
+ * cells are replicated; each query runs ONE collective:
+ *   pcp_multi_raycast_fan  ncclAllReduce(ncclUint64, ncclMin) over P keys (blocked << 32) | p
+ *                          -> blocked counts of every pose and the argmin (ties: lowest p)
+ *   pcp_multi_score_poses  ncclAllReduce(ncclUint64, ncclMax) over [P totals (IEEE bits of
+ *                          values >= +0) | P covered | 3 x n_cells newest-pose flag keys]
+ *                          -> the reference's strict-'>' argmax (:471-474) and the stale-flag
+ *                          colour statistics (:480-519), as pcp_score_poses.
+ * Results are identical to one context over all poses.  A device listed twice (a rehearsal
+ * on fewer GPUs) has no RCCL communicator: the key vectors are combined on that device by a
+ * kernel instead (pcp_multi_info reports uses_rccl = 0).  Not thread-safe, like pcp_ctx. */
+typedef struct pcp_multi pcp_multi;
+int pcp_multi_create(int n_dev, const int *devices, pcp_multi **out);
+void pcp_multi_destroy(pcp_multi *m);
+const char *pcp_multi_last_error(const pcp_multi *m);
+int pcp_multi_info(const pcp_multi *m, int *n_dev, int *uses_rccl);
+pcp_ctx *pcp_multi_ctx(pcp_multi *m, int rank);   /* a rank's context (per-rank calls) */
+int pcp_multi_set_terrain(pcp_multi *m, const pcp_cloud_view *terrain);
+int pcp_multi_set_aux_cloud(pcp_multi *m, const pcp_cloud_view *aux);
+int pcp_multi_set_cells(pcp_multi *m, const double *xyz, const float *normals, uint64_t n);
+int pcp_multi_raycast_fan(pcp_multi *m, const double *poses5, uint64_t n,
+                          const pcp_fan_params *fan, uint32_t *blocked, uint64_t *units,
+                          int64_t *best_idx);
+int pcp_multi_score_poses(pcp_multi *m, const double *poses5, uint64_t n,
+                          const double zx120_pose5[5], const pcp_vl_params *p,
+                          uint8_t *cell_flags, double *total_score, int32_t *covered,
+                          pcp_vl_report *rep);
+
 /* The march's sample distances: s_0 = 0.5, s_{k+1} = s_k + 0.3 (repeated double addition,
  * :765-796) while s_k < end.  Returns the count in *n (writes min(cap, n) values). */
 int pcp_step_table(double end, double *steps, uint64_t cap, uint64_t *n);

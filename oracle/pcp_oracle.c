@@ -29,10 +29,6 @@
 #endif
 
 /* virtual_lidar.cpp:100-114 */
-#define VL_MIN_DISTANCE 0.5
-#define VL_ZX120_OFFSET_X 0.4
-#define VL_RAY_STEP_SIZE 0.3
-#define VL_VISIBILITY_RADIUS 0.08
 #define VL_MIN_ELEVATION (-85.0 * M_PI / 180.0)
 #define VL_MAX_ELEVATION (85.0 * M_PI / 180.0)
 
@@ -186,6 +182,8 @@ void orc_transform_rgb(const float *pts, int64_t n, int64_t stride, const double
 /* Exact radius search (replaces KdTreeFLANN for the checker)                       */
 /* ================================================================================ */
 struct orc_cloud {
+    const orc_kdtree *kd;   /* non-NULL: radius queries answered by the restated KdTreeFLANN
+                               (pcp_flann.c) instead of the exact grid scan */
     int64_t n;              /* finite points kept */
     float *p;               /* 3 floats per point, sorted by cell */
     uint32_t *start;        /* ncell + 1 */
@@ -281,6 +279,7 @@ static inline void cell_range(const orc_cloud *c, double lo, double hi, double o
 
 static int any_within_r2(const orc_cloud *c, float qx, float qy, float qz, double radius, float r2)
 {
+    if (c->kd) return orc_kd_radius(c->kd, qx, qy, qz, r2, NULL, 0) > 0;
     if (c->n == 0) return 0;
     const double m = radius + 1e-3;
     int64_t x0, x1, y0, y1, z0, z1;
@@ -298,6 +297,29 @@ static int any_within_r2(const orc_cloud *c, float qx, float qy, float qz, doubl
     return 0;
 }
 
+void orc_cloud_use_kdtree(orc_cloud *c, const orc_kdtree *kd) { c->kd = kd; }
+
+/* exact grid count (never the attached tree: this is what the tree is checked against) */
+int64_t orc_cloud_count_within(const orc_cloud *c, float qx, float qy, float qz, double radius)
+{
+    if (c->n == 0) return 0;
+    const float r2 = (float)(radius * radius);
+    const double m = radius + 1e-3;
+    int64_t x0, x1, y0, y1, z0, z1, cnt = 0;
+    cell_range(c, (double)qx - m, (double)qx + m, c->ox, c->nx, &x0, &x1);
+    cell_range(c, (double)qy - m, (double)qy + m, c->oy, c->ny, &y0, &y1);
+    cell_range(c, (double)qz - m, (double)qz + m, c->oz, c->nz, &z0, &z1);
+    if (x0 > x1 || y0 > y1 || z0 > z1) return 0;
+    for (int64_t iz = z0; iz <= z1; ++iz)
+        for (int64_t iy = y0; iy <= y1; ++iy) {
+            const int64_t row = c->nx * (iy + c->ny * iz);
+            const uint32_t s = c->start[row + x0], e = c->start[row + x1 + 1];
+            for (uint32_t k = s; k < e; ++k)
+                cnt += flann_within(qx, qy, qz, c->p + 3 * (int64_t)k, r2);
+        }
+    return cnt;
+}
+
 int orc_cloud_any_within(const orc_cloud *c, float qx, float qy, float qz, double radius)
 {
     /* KdTreeFLANN::radiusSearch: static_cast<float>(radius * radius) */
@@ -311,6 +333,20 @@ double orc_ground_height(const orc_cloud *c, double x, double y)
     const float qx = (float)x, qy = (float)y, qz = 0.0f;   /* PointXYZRGB search_point */
     const double radius = 2.0;
     const float r2 = (float)(radius * radius);
+    if (c->kd) {   /* the tree's neighbour list (:611), then the 2-D filter (:613-620) */
+        const int64_t nn = orc_kd_radius(c->kd, qx, qy, qz, r2, NULL, 0);
+        if (nn == 0) return 0.0;
+        int64_t *idx = (int64_t *)malloc((size_t)nn * sizeof(int64_t));
+        orc_kd_radius(c->kd, qx, qy, qz, r2, idx, nn);
+        double max_z = -DBL_MAX;
+        for (int64_t k = 0; k < nn; ++k) {
+            const float *p = orc_kd_point(c->kd, idx[k]);
+            const double dx = (double)p[0] - x, dy = (double)p[1] - y;
+            if (sqrt(dx * dx + dy * dy) < 1.0 && (double)p[2] > max_z) max_z = (double)p[2];
+        }
+        free(idx);
+        return max_z != -DBL_MAX ? max_z : 0.0;
+    }
     if (c->n == 0) return 0.0;
     const double m = radius + 1e-3;
     int64_t x0, x1, y0, y1, z0, z1;

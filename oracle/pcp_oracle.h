@@ -51,12 +51,41 @@ void orc_transform_rgb(const float *pts, int64_t n, int64_t stride_floats,
                        const double t[3], const double q[4],
                        uint8_t r, uint8_t g, uint8_t b, float *out8);
 
+#define VL_MIN_DISTANCE 0.5
+#define VL_ZX120_OFFSET_X 0.4
+#define VL_RAY_STEP_SIZE 0.3
+#define VL_VISIBILITY_RADIUS 0.08
+
 /* ---- virtual_lidar.cpp ------------------------------------------------------------ */
 typedef struct orc_cloud orc_cloud;   /* exact radius-search structure (uniform grid) */
+typedef struct orc_kdtree orc_kdtree; /* restated KdTreeFLANN (pcp_flann.c) */
 orc_cloud *orc_cloud_build(const float *pts, int64_t n, int64_t stride_floats);
 void orc_cloud_free(orc_cloud *c);
 /* KdTreeFLANN::radiusSearch(q, radius) > 0  (FLANN L2_Simple, dist < float(r*r)) */
 int orc_cloud_any_within(const orc_cloud *c, float qx, float qy, float qz, double radius);
+/* the number of points with L2_Simple distance < float(r*r) (exact: every candidate cell) */
+int64_t orc_cloud_count_within(const orc_cloud *c, float qx, float qy, float qz, double radius);
+
+/* ---- pcp_flann.c: FLANN 1.9.1 KDTreeSingleIndex as PCL 1.12.1 KdTreeFLANN configures it
+ * (the second, independent checker of the radius predicate; see pcp_flann.c) -------------- */
+orc_kdtree *orc_kd_build(const float *pts, int64_t n, int64_t stride_floats, int leaf_max);
+void orc_kd_free(orc_kdtree *t);
+int64_t orc_kd_size(const orc_kdtree *t);
+const float *orc_kd_point(const orc_kdtree *t, int64_t cloud_idx);
+/* FLANN mode: every radius query of the oracle on c (ray march, relaxed check, ground
+ * height) goes through kd instead of the grid scan; NULL restores the grid */
+void orc_cloud_use_kdtree(orc_cloud *c, const orc_kdtree *kd);
+/* radiusSearch with r2 = float(r*r) already formed; idx (nullable) gets up to cap neighbours'
+ * indices in the caller's cloud (tree order, unsorted) */
+int64_t orc_kd_radius(const orc_kdtree *t, float qx, float qy, float qz, float r2,
+                      int64_t *idx, int64_t cap);
+int64_t orc_kd_radius_search(const orc_kdtree *t, float qx, float qy, float qz, double radius);
+void orc_kd_check_queries(const orc_kdtree *t, const orc_cloud *g, const float *q, int64_t nq,
+                          double radius, uint64_t stats[4]);
+void orc_kd_raycast_fan(const orc_kdtree *t, const orc_cloud *g, const double *poses5, int64_t P,
+                        int32_t n_az, int32_t n_el, double el_min, double el_max,
+                        double max_distance, int16_t *first_hit, uint32_t *blocked,
+                        uint64_t *units, uint64_t stats[4]);
 /* getGroundHeight (virtual_lidar.cpp:600-625) */
 double orc_ground_height(const orc_cloud *terrain, double x, double y);
 

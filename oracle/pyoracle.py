@@ -57,6 +57,16 @@ _SIGS = [
                                 C.POINTER(VlParams), _P, _P]),
     ("orc_raycast_fan", None, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                C.c_double, _P, _P, _P]),
+    ("orc_cloud_use_kdtree", None, [_P, _P]),
+    ("orc_cloud_count_within", C.c_int64, [_P, C.c_float, C.c_float, C.c_float, C.c_double]),
+    ("orc_kd_build", _P, [_P, C.c_int64, C.c_int64, C.c_int]),
+    ("orc_kd_free", None, [_P]),
+    ("orc_kd_size", C.c_int64, [_P]),
+    ("orc_kd_radius", C.c_int64, [_P, C.c_float, C.c_float, C.c_float, C.c_float, _P,
+                                  C.c_int64]),
+    ("orc_kd_check_queries", None, [_P, _P, _P, C.c_int64, C.c_double, _P]),
+    ("orc_kd_raycast_fan", None, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_double,
+                                  C.c_double, C.c_double, _P, _P, _P, _P]),
     ("orc_fan_tables", None, [C.c_int32, C.c_int32, C.c_double, C.c_double, _P, _P, _P, _P]),
     ("orc_area_normals", None, [_P, C.c_int64, C.c_int64, C.c_double, _P]),
     ("orc_terrain_height", C.c_double, [_P, C.c_int64, C.c_int64, C.c_double, C.c_double,
@@ -137,12 +147,20 @@ def transform_rgb(pts, t, q, rgb):
 
 
 class Cloud:
-    """Exact radius-search structure over a point array (replaces KdTreeFLANN)."""
+    """Exact radius-search structure over a point array (replaces KdTreeFLANN).
 
-    def __init__(self, pts):
+    flann=True: every radius query the oracle makes on this cloud (ray march, relaxed zx120
+    check, getGroundHeight) is answered by the restated KdTreeFLANN of pcp_flann.c instead of
+    the exact grid scan -- the reference's own search, float pruning included."""
+
+    def __init__(self, pts, flann=False):
         a = _f32(pts)
         self.n = a.shape[0]
         self.h = lib().orc_cloud_build(_p(a), a.shape[0], a.shape[1])
+        self.kd = None
+        if flann:
+            self.kd = KdTree(a)
+            lib().orc_cloud_use_kdtree(self.h, self.kd.h)
 
     def __del__(self):
         try:
@@ -157,6 +175,65 @@ class Cloud:
 
     def ground_height(self, x, y):
         return lib().orc_ground_height(self.h, x, y)
+
+    def count_within(self, q, radius):
+        return int(lib().orc_cloud_count_within(self.h, C.c_float(q[0]), C.c_float(q[1]),
+                                                C.c_float(q[2]), radius))
+
+
+class KdTree:
+    """FLANN 1.9.1 KDTreeSingleIndex as PCL 1.12.1 KdTreeFLANN builds and queries it
+    (oracle/pcp_flann.c): the reference's own radius search, float pruning included."""
+
+    def __init__(self, pts, leaf_max=15):
+        a = _f32(pts)
+        self.n = a.shape[0]
+        self.h = lib().orc_kd_build(_p(a), a.shape[0], a.shape[1], int(leaf_max))
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().orc_kd_free(self.h)
+        except Exception:
+            pass
+
+    def radius_search(self, q, radius, want_idx=False):
+        """-> neighbour count (and their cloud indices, sorted) with dist < float(r*r)."""
+        r2 = C.c_float(float(np.float32(radius * radius)))
+        q = [C.c_float(float(v)) for v in q[:3]]
+        n = lib().orc_kd_radius(self.h, *q, r2, None, 0)
+        if not want_idx:
+            return int(n)
+        idx = np.empty(max(n, 1), np.int64)
+        lib().orc_kd_radius(self.h, *q, r2, _p(idx), n)
+        return int(n), np.sort(idx[:n])
+
+    def check_queries(self, grid: "Cloud", queries, radius):
+        """Tree count vs the exact grid count for every query (float xyz rows) ->
+        {queries, count_mismatch, any_mismatch, neighbours}."""
+        q = np.ascontiguousarray(np.asarray(queries, np.float32)[:, :3])
+        st = np.zeros(4, np.uint64)
+        lib().orc_kd_check_queries(self.h, grid.h, _p(q), q.shape[0], float(radius), _p(st))
+        return dict(zip(("queries", "count_mismatch", "any_mismatch", "neighbours"),
+                        (int(x) for x in st)))
+
+
+def raycast_fan_kd(tree: KdTree, grid: "Cloud | None", poses5, n_az, n_el, el_min, el_max,
+                   max_distance, want_first_hit=True):
+    """The fan march with every sample answered by the restated KdTreeFLANN, each sample
+    cross-checked against the exact grid count -> (blocked, units, first_hit, stats)."""
+    poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+    P = poses.shape[0]
+    fh = np.empty((P, n_el, n_az), np.int16) if want_first_hit else None
+    blocked = np.zeros(max(P, 1), np.uint32)
+    units = np.zeros(max(P, 1), np.uint64)
+    st = np.zeros(4, np.uint64)
+    lib().orc_kd_raycast_fan(tree.h, grid.h if grid else None, _p(poses), P, n_az, n_el,
+                             el_min, el_max, max_distance, _p(fh), _p(blocked), _p(units),
+                             _p(st))
+    stats = dict(zip(("queries", "count_mismatch", "any_mismatch", "neighbours"),
+                     (int(x) for x in st)))
+    return blocked[:P].copy(), units[:P].copy(), fh, stats
 
 
 def vl_params(**kw):

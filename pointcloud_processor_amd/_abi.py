@@ -130,6 +130,18 @@ _SIGS = [
     ("pcp_raycast_fan_stamps", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P]),
     ("pcp_step_table", C.c_int, [C.c_double, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pcp_terrain_info", C.c_int, [_P, C.POINTER(IndexInfo)]),
+    ("pcp_multi_create", C.c_int, [C.c_int, _P, C.POINTER(_P)]),
+    ("pcp_multi_destroy", None, [_P]),
+    ("pcp_multi_last_error", C.c_char_p, [_P]),
+    ("pcp_multi_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("pcp_multi_ctx", _P, [_P, C.c_int]),
+    ("pcp_multi_set_terrain", C.c_int, [_P, C.POINTER(CloudView)]),
+    ("pcp_multi_set_aux_cloud", C.c_int, [_P, C.POINTER(CloudView)]),
+    ("pcp_multi_set_cells", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("pcp_multi_raycast_fan", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P, _P,
+                                        C.POINTER(C.c_int64)]),
+    ("pcp_multi_score_poses", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams), _P, _P,
+                                        _P, C.POINTER(VlReport)]),
 ]
 ABI_SYMBOLS = [s[0] for s in _SIGS]
 
@@ -512,6 +524,88 @@ class Context:
                                              _ptr(units), _ptr(fh), C.byref(best)),
                     "pcp_raycast_fan")
         return blocked[:P].copy(), units[:P].copy(), fh, best.value
+
+
+class Multi:
+    """pcp_multi: one process, n GPUs -- the pose search sharded over
+    contexts with ONE RCCL collective per query.  devices: one device id per rank (a device
+    listed twice rehearses n ranks on fewer GPUs: no RCCL, the keys combine on the device)."""
+
+    def __init__(self, devices, lib_path=None):
+        self.lib = load_library(lib_path)
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        rc = self.lib.pcp_multi_create(len(devices), devs, C.byref(h))
+        if rc != PCP_OK:
+            raise PcpError(rc, f"pcp_multi_create(devices={list(devices)}) failed")
+        self.h = h
+        n, rccl = C.c_int(), C.c_int()
+        self.lib.pcp_multi_info(self.h, C.byref(n), C.byref(rccl))
+        self.n, self.uses_rccl = n.value, bool(rccl.value)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pcp_multi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != PCP_OK:
+            msg = self.lib.pcp_multi_last_error(self.h)
+            raise PcpError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def set_terrain(self, cloud: np.ndarray, point_step=None, offs=(0, 4, 8)):
+        v = cloud_view(cloud, point_step, offs)
+        self._check(self.lib.pcp_multi_set_terrain(self.h, C.byref(v)), "pcp_multi_set_terrain")
+
+    def set_aux_cloud(self, cloud: np.ndarray, point_step=None, offs=(0, 4, 8)):
+        v = cloud_view(cloud, point_step, offs)
+        self._check(self.lib.pcp_multi_set_aux_cloud(self.h, C.byref(v)),
+                    "pcp_multi_set_aux_cloud")
+
+    def set_cells(self, xyz: np.ndarray, normals: np.ndarray):
+        xyz = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
+        nrm = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+        assert xyz.shape == nrm.shape
+        self._check(self.lib.pcp_multi_set_cells(self.h, _ptr(xyz), _ptr(nrm), xyz.shape[0]),
+                    "pcp_multi_set_cells")
+
+    def raycast_fan(self, poses5: np.ndarray, fan: FanParams):
+        poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+        P = poses.shape[0]
+        blocked = np.zeros(max(P, 1), np.uint32)
+        units = np.zeros(max(P, 1), np.uint64)
+        best = C.c_int64()
+        self._check(self.lib.pcp_multi_raycast_fan(self.h, _ptr(poses), P, C.byref(fan),
+                                                   _ptr(blocked), _ptr(units), C.byref(best)),
+                    "pcp_multi_raycast_fan")
+        return blocked[:P].copy(), units[:P].copy(), best.value
+
+    def score_poses(self, poses5: np.ndarray, zx120_pose5, params: VlParams,
+                    cell_flags: np.ndarray):
+        poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+        P = poses.shape[0]
+        zx = np.ascontiguousarray(zx120_pose5, np.float64)
+        assert cell_flags.dtype == np.uint8 and cell_flags.flags.c_contiguous
+        tot = np.empty(max(P, 1), np.float64)
+        cov = np.empty(max(P, 1), np.int32)
+        rep = VlReport()
+        self._check(self.lib.pcp_multi_score_poses(self.h, _ptr(poses), P, _ptr(zx),
+                                                   C.byref(params), _ptr(cell_flags), _ptr(tot),
+                                                   _ptr(cov), C.byref(rep)),
+                    "pcp_multi_score_poses")
+        return tot[:P].copy(), cov[:P].copy(), rep
 
 
 def _fan_stats(self, poses5, fan):

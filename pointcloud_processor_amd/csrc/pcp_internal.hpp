@@ -260,6 +260,45 @@ int terrain_blocks_before_query(pcp_ctx *ctx);
 size_t scan_tmp_bytes(uint64_t n);
 int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp);
 
+// fan query up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip): device results
+// in flight on return, the caller synchronizes.  n > 0.
+struct FanEnq {
+    uint32_t *blocked_d = nullptr;
+    unsigned long long *units_d = nullptr;
+    int16_t *fh_d = nullptr;
+    uint32_t rays = 0;
+    size_t stats_bytes = 0;
+    unsigned long long *stats_d = nullptr;
+};
+int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
+                bool want_fh, bool stats, bool stamps, FanEnq &o);
+
+// runOptimization's scoring up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip)
+struct ScoreEnq {
+    int P = 0, C = 0;
+    double *comb = nullptr;        // [P][C] mobile scores
+    uint8_t *mbits = nullptr;      // [P][C] result bits of the poses
+    uint8_t *zbits = nullptr;      // [C] result bits of the zx120 evaluation
+    uint8_t *flags_d = nullptr;    // [C] cell flag bytes (caller fills)
+    double *tot_d = nullptr;       // [P + 1] totals, row P = zx120
+    int32_t *cov_d = nullptr;      // [P + 1]
+    int32_t *stats = nullptr;      // 64 colour-statistics slots
+    size_t tc_bytes = 0, st_off = 0, fl_off = 0;   // pinned (res_host) layout
+};
+int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
+                  const pcp_vl_params *p, ScoreEnq &o);
+// key kernels of the pose-sharded search (pcp_vlidar.hip; used by pcp_multi.hip)
+void launch_fan_keys(hipStream_t st, const uint32_t *blocked_d, uint32_t lo, uint32_t cnt,
+                     uint32_t P, unsigned long long *keys);
+void launch_score_keys(hipStream_t st, const ScoreEnq &o, int lo, int P, unsigned long long *v);
+void launch_flags_from_keys(hipStream_t st, const unsigned long long *v, const uint8_t *zbits,
+                            int C, int P, uint8_t *flags, int32_t *stats);
+void launch_keys_combine(hipStream_t st, unsigned long long *a, const unsigned long long *b,
+                         size_t n, bool is_max);
+// the colour-statistics slots (k_cell_flags order) -> pcp_vl_report
+void fill_report(const int32_t *st_h, double zx_total, int64_t best_idx, double best,
+                 pcp_vl_report *rep);
+
 // validate a cloud view
 int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what);
 

@@ -506,6 +506,134 @@ k_cell_flags(const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbit
 }
 
 // ---------------------------------------------------------------------------------------
+// pose-sharded search across GPUs (pcp_multi.hip): per-rank key vectors, reduced by ONE
+// collective, then finalized on one rank
+// ---------------------------------------------------------------------------------------
+// fan: keys[i] = (blocked << 32) | i for this rank's poses [lo, lo + cnt), UINT64_MAX elsewhere;
+// all-reduce(MIN) leaves every pose's key on every rank and the minimum key is the reference
+// argmin with ties to the lowest index
+__global__ void __launch_bounds__(kT)
+k_fan_keys(const uint32_t *__restrict__ blocked, uint32_t lo, uint32_t cnt, uint32_t P,
+           unsigned long long *__restrict__ keys) {
+    const uint32_t i = blockIdx.x * kT + threadIdx.x;
+    if (i >= P) return;
+    keys[i] = (i >= lo && i - lo < cnt)
+                  ? (((unsigned long long)blocked[i - lo] << 32) | (unsigned long long)i)
+                  : ~0ull;
+}
+
+// reference mode: v = [P totals | P covered | C range | C fov | C vis], all-reduce(MAX).
+// Totals are >= +0.0 (sums of positive scores from +0.0), so their IEEE bits order like the
+// values; 0 = +0.0 marks other ranks' poses.  Per cell, the newest pose of this rank that
+// reached each stale-flag assignment (:662-687) as ((global index + 1) << 1) | bit, 0 = none:
+// the maximum over the ranks is the newest pose overall, which is what k_cell_flags resolves.
+__global__ void __launch_bounds__(kT)
+k_score_keys(const double *__restrict__ tot, const int32_t *__restrict__ cov,
+             const uint8_t *__restrict__ mbits, int C, int Pl, int lo, int P,
+             unsigned long long *__restrict__ v) {
+    const int i = blockIdx.x * kT + threadIdx.x;
+    if (i < P) {
+        const bool mine = i >= lo && i - lo < Pl;
+        v[i] = mine ? (unsigned long long)__double_as_longlong(tot[i - lo]) : 0ull;
+        v[P + i] = mine ? (unsigned long long)(uint32_t)cov[i - lo] : 0ull;
+    }
+    if (i < C) {
+        unsigned long long kr = 0, kf = 0, kv = 0;
+        if (Pl > 0) {
+            const uint32_t lb = mbits[(size_t)(Pl - 1) * C + i];
+            kr = ((unsigned long long)(lo + Pl) << 1) | (lb & 1u);
+            for (int q = Pl - 1; q >= 0 && (!kf || !kv); --q) {
+                const uint32_t b = mbits[(size_t)q * C + i];
+                const unsigned long long g1 = (unsigned long long)(lo + q + 1) << 1;
+                if (!kf && (b & 1u)) kf = g1 | ((b >> 1) & 1u);
+                if (!kv && (b & 3u) == 3u) kv = g1 | ((b >> 2) & 1u);
+            }
+        }
+        v[2 * (size_t)P + i] = kr;
+        v[2 * (size_t)P + C + i] = kf;
+        v[2 * (size_t)P + 2 * (size_t)C + i] = kv;
+    }
+}
+
+// colour statistics of one cell's final flags (evaluateZX120Only :377-397 and :487-501)
+__device__ __forceinline__ void count_flags(uint32_t f, int32_t *bst) {
+    const bool zr = f & PCP_F_RANGE_Z, zf = f & PCP_F_FOV_Z, zv = f & PCP_F_VIS_Z;
+    atomicAdd(&bst[S_TOTAL], 1);
+    if (zr) atomicAdd(&bst[S_ZR], 1);
+    if (zf) atomicAdd(&bst[S_ZF], 1);
+    if (zv) atomicAdd(&bst[S_ZV], 1);
+    if (!zr) atomicAdd(&bst[S_ZB], 1);
+    else if (!zf) atomicAdd(&bst[S_ZY], 1);
+    else if (!zv) atomicAdd(&bst[S_ZRED], 1);
+    else atomicAdd(&bst[S_ZG], 1);
+    const bool mr = f & PCP_F_RANGE_M, mf = f & PCP_F_FOV_M, mv = f & PCP_F_VIS_M;
+    if (!zr && !mr) atomicAdd(&bst[S_B], 1);
+    else if (!zf && !mf) atomicAdd(&bst[S_Y], 1);
+    else if (!zv && !mv) atomicAdd(&bst[S_RED], 1);
+    else atomicAdd(&bst[S_G], 1);
+}
+
+// the reduced keys -> cell flags + colour statistics (the k_cell_flags result)
+__global__ void __launch_bounds__(kT)
+k_flags_from_keys(const unsigned long long *__restrict__ v, const uint8_t *__restrict__ zbits,
+                  int C, int P, uint8_t *__restrict__ flags, int32_t *__restrict__ stats) {
+    const int c = blockIdx.x * kT + threadIdx.x;
+    __shared__ int32_t bst[S_N];
+    if (threadIdx.x < S_N) bst[threadIdx.x] = 0;
+    __syncthreads();
+    if (c < C) {
+        uint32_t f = flags[c];
+        const uint32_t z = zbits[c];
+        f = (z & 1u) ? (f | PCP_F_RANGE_Z) : (f & ~PCP_F_RANGE_Z);
+        if (z & 1u) f = (z & 2u) ? (f | PCP_F_FOV_Z) : (f & ~PCP_F_FOV_Z);
+        if ((z & 3u) == 3u) f = (z & 4u) ? (f | PCP_F_VIS_Z) : (f & ~PCP_F_VIS_Z);
+        const unsigned long long kr = v[2 * (size_t)P + c], kf = v[2 * (size_t)P + C + c],
+                                 kv = v[2 * (size_t)P + 2 * (size_t)C + c];
+        if (kr) f = (kr & 1ull) ? (f | PCP_F_RANGE_M) : (f & ~PCP_F_RANGE_M);
+        if (kf) f = (kf & 1ull) ? (f | PCP_F_FOV_M) : (f & ~PCP_F_FOV_M);
+        if (kv) f = (kv & 1ull) ? (f | PCP_F_VIS_M) : (f & ~PCP_F_VIS_M);
+        flags[c] = (uint8_t)f;
+        count_flags(f, bst);
+    }
+    __syncthreads();
+    if (threadIdx.x < S_N && bst[threadIdx.x]) atomicAdd(&stats[threadIdx.x], bst[threadIdx.x]);
+}
+
+// element-wise min / max of two key vectors (ranks sharing one device, no RCCL)
+__global__ void __launch_bounds__(kT)
+k_keys_combine(unsigned long long *__restrict__ a, const unsigned long long *__restrict__ b,
+               size_t n, int is_max) {
+    const size_t i = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    a[i] = is_max ? (a[i] > b[i] ? a[i] : b[i]) : (a[i] < b[i] ? a[i] : b[i]);
+}
+
+void launch_fan_keys(hipStream_t st, const uint32_t *blocked_d, uint32_t lo, uint32_t cnt,
+                     uint32_t P, unsigned long long *keys) {
+    hipLaunchKernelGGL(k_fan_keys, dim3((P + kT - 1) / kT), dim3(kT), 0, st, blocked_d, lo, cnt,
+                       P, keys);
+}
+void launch_score_keys(hipStream_t st, const ScoreEnq &o, int lo, int P,
+                       unsigned long long *v) {
+    const int n = std::max(P, o.C);
+    hipLaunchKernelGGL(k_score_keys, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, st,
+                       (const double *)o.tot_d, (const int32_t *)o.cov_d,
+                       (const uint8_t *)o.mbits, o.C, o.P, lo, P, v);
+}
+void launch_flags_from_keys(hipStream_t st, const unsigned long long *v, const uint8_t *zbits,
+                            int C, int P, uint8_t *flags, int32_t *stats) {
+    if (C)
+        hipLaunchKernelGGL(k_flags_from_keys, dim3((unsigned)((C + kT - 1) / kT)), dim3(kT), 0, st,
+                           v, zbits, C, P, flags, stats);
+}
+void launch_keys_combine(hipStream_t st, unsigned long long *a, const unsigned long long *b,
+                         size_t n, bool is_max) {
+    if (n)
+        hipLaunchKernelGGL(k_keys_combine, dim3((unsigned)((n + kT - 1) / kT)), dim3(kT), 0, st,
+                           a, b, n, is_max ? 1 : 0);
+}
+
+// ---------------------------------------------------------------------------------------
 // candidates (generateCandidatePositions :550-598, getGroundHeight :600-625)
 // ---------------------------------------------------------------------------------------
 struct CandArgs {
@@ -904,13 +1032,15 @@ static int ensure_steps(pcp_ctx *ctx, double end, int *K) {
     return PCP_OK;
 }
 
-int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
-                    const pcp_vl_params *p, uint8_t *cell_flags, double *total_score,
-                    int32_t *covered, pcp_vl_report *rep) {
-    if (!ctx) return PCP_E_INVALID;
-    if (!zx || !p || !rep || (n && !poses5) || (ctx->n_cells && !cell_flags))
-        return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: null argument");
-    if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: at most 65535 poses per call");
+}  // extern "C"
+
+namespace pcp {
+// runOptimization's scoring up to the per-pose sums, enqueued on ctx->stream: poses + the
+// zx120 pose uploaded through the pinned block, k_score_cells (rows 0..P-1 = poses, row P =
+// zx120), k_row_sum.  On return the device holds comb/mbits [P][C], zbits [C], tot_d/cov_d
+// [P+1] (row P = zx120); the caller synchronizes.  Validation is the caller's.
+int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
+                  const pcp_vl_params *p, ScoreEnq &o) {
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const int C = (int)ctx->n_cells, P = (int)n;
@@ -926,18 +1056,21 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     PCP_HIP(ctx, ctx->out_b.ensure(pc + (size_t)C * 2 + 64));
     PCP_HIP(ctx, ctx->out_c.ensure((size_t)(P + 1) * (sizeof(double) + sizeof(int32_t)) + 64));
     PCP_HIP(ctx, ctx->stats_d.ensure(64 * sizeof(int32_t)));
-    double *comb = ctx->out_a.as<double>();
-    double *score_z = comb + pc;
-    uint8_t *mbits = ctx->out_b.as<uint8_t>();
-    uint8_t *zbits = mbits + pc;
-    uint8_t *flags_d = zbits + C;
-    double *tot_d = ctx->out_c.as<double>();
-    int32_t *cov_d = reinterpret_cast<int32_t *>(tot_d + (P + 1));
-    int32_t *stats = ctx->stats_d.as<int32_t>();
+    o.P = P;
+    o.C = C;
+    o.comb = ctx->out_a.as<double>();
+    double *score_z = o.comb + pc;
+    o.mbits = ctx->out_b.as<uint8_t>();
+    o.zbits = o.mbits + pc;
+    o.flags_d = o.zbits + C;
+    o.tot_d = ctx->out_c.as<double>();
+    o.cov_d = reinterpret_cast<int32_t *>(o.tot_d + (P + 1));
+    o.stats = ctx->stats_d.as<int32_t>();
     // pinned staging: [totals f64 (P+1) | covered i32 (P+1)] [stats] [cell flags] [poses + zx120]
-    const size_t tc_bytes = (size_t)(P + 1) * (sizeof(double) + sizeof(int32_t));
-    const size_t st_off = (tc_bytes + 15) & ~(size_t)15, fl_off = st_off + 64 * sizeof(int32_t);
-    const size_t po_off = (fl_off + (size_t)C + 15) & ~(size_t)15;
+    o.tc_bytes = (size_t)(P + 1) * (sizeof(double) + sizeof(int32_t));
+    o.st_off = (o.tc_bytes + 15) & ~(size_t)15;
+    o.fl_off = o.st_off + 64 * sizeof(int32_t);
+    const size_t po_off = (o.fl_off + (size_t)C + 15) & ~(size_t)15;
     const size_t po_bytes = (size_t)(P + 1) * 5 * sizeof(double);
     PCP_HIP(ctx, ctx->res_host.ensure(po_off + po_bytes + 16));
     char *pin = ctx->res_host.as<char>();
@@ -945,11 +1078,6 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     if (P) std::memcpy(pin + po_off, poses5, (size_t)P * 5 * sizeof(double));
     std::memcpy(pin + po_off + (size_t)P * 5 * sizeof(double), zx, 5 * sizeof(double));
     PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pin + po_off, po_bytes, hipMemcpyHostToDevice, st));
-    if (C) {
-        std::memcpy(pin + fl_off, cell_flags, C);
-        PCP_HIP(ctx, hipMemcpyAsync(flags_d, pin + fl_off, C, hipMemcpyHostToDevice, st));
-    }
-    PCP_HIP(ctx, hipMemsetAsync(stats, 0, 64 * sizeof(int32_t), st));
     const unsigned cb = (unsigned)((C + kT - 1) / kT);
     if (C) {
         {
@@ -957,51 +1085,29 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
             hipLaunchKernelGGL(k_score_cells, dim3(cb, P + 1), dim3(kT), 0, st, E,
                                ctx->cells_xyz.as<const double>(), ctx->cells_nrm.as<const float>(),
                                C, ctx->poses_d.as<const double>(), P,
-                               ctx->poses_d.as<const double>() + 5 * (size_t)P, comb, mbits,
-                               score_z, zbits);
+                               ctx->poses_d.as<const double>() + 5 * (size_t)P, o.comb, o.mbits,
+                               score_z, o.zbits);
             PCP_CHECK_LAUNCH(ctx);
         }
         {
             ProfScope ps(ctx, PCP_K_POSE_SUM);
-            hipLaunchKernelGGL(k_row_sum, dim3(P + 1), dim3(64), 0, st, (const double *)comb,
-                               (const double *)score_z, C, P, tot_d, cov_d);
-            PCP_CHECK_LAUNCH(ctx);
-        }
-        {
-            ProfScope ps(ctx, PCP_K_CELL_FLAGS);
-            hipLaunchKernelGGL(k_cell_flags, dim3(cb), dim3(kT), 0, st, (const uint8_t *)zbits,
-                               (const uint8_t *)mbits, C, P, flags_d, stats);
+            hipLaunchKernelGGL(k_row_sum, dim3(P + 1), dim3(64), 0, st, (const double *)o.comb,
+                               (const double *)score_z, C, P, o.tot_d, o.cov_d);
             PCP_CHECK_LAUNCH(ctx);
         }
     } else {
-        PCP_HIP(ctx, hipMemsetAsync(tot_d, 0, (size_t)(P + 1) * sizeof(double), st));
-        PCP_HIP(ctx, hipMemsetAsync(cov_d, 0, (size_t)(P + 1) * sizeof(int32_t), st));
+        PCP_HIP(ctx, hipMemsetAsync(o.tot_d, 0, (size_t)(P + 1) * sizeof(double), st));
+        PCP_HIP(ctx, hipMemsetAsync(o.cov_d, 0, (size_t)(P + 1) * sizeof(int32_t), st));
     }
-    // totals and covered counts are adjacent on the device: one copy into the pinned block
-    const double *tot_h = reinterpret_cast<const double *>(pin);
-    const int32_t *cov_h = reinterpret_cast<const int32_t *>(tot_h + (P + 1));
-    const int32_t *st_h = reinterpret_cast<const int32_t *>(pin + st_off);
-    PCP_HIP(ctx, hipMemcpyAsync(pin, tot_d, tc_bytes, hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipMemcpyAsync(pin + st_off, stats, S_N * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    if (C) PCP_HIP(ctx, hipMemcpyAsync(pin + fl_off, flags_d, C, hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipStreamSynchronize(st));
-    if (C) std::memcpy(cell_flags, pin + fl_off, C);
-    prof_resolve(ctx);
-    // runOptimization candidate loop (:464-475): strict '>' keeps the first maximum
-    double best = -INFINITY;
-    int64_t best_idx = -1;
-    for (int k = 0; k < P; ++k) {
-        if (total_score) total_score[k] = tot_h[k];
-        if (covered) covered[k] = cov_h[k];
-        if (tot_h[k] > best) {
-            best = tot_h[k];
-            best_idx = k;
-        }
-    }
+    return PCP_OK;
+}
+
+void fill_report(const int32_t *st_h, double zx_total, int64_t best_idx, double best,
+                 pcp_vl_report *rep) {
     std::memset(rep, 0, sizeof(*rep));
     rep->best_idx = best_idx;
     rep->best_score = best;
-    rep->zx120_total_score = tot_h[P];
+    rep->zx120_total_score = zx_total;
     rep->total_cells = st_h[S_TOTAL];
     rep->zx120_range_ok = st_h[S_ZR];
     rep->zx120_fov_ok = st_h[S_ZF];
@@ -1014,22 +1120,73 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     rep->red = st_h[S_RED];
     rep->blue = st_h[S_B];
     rep->yellow = st_h[S_Y];
+}
+}  // namespace pcp
+
+extern "C" {
+
+int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
+                    const pcp_vl_params *p, uint8_t *cell_flags, double *total_score,
+                    int32_t *covered, pcp_vl_report *rep) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!zx || !p || !rep || (n && !poses5) || (ctx->n_cells && !cell_flags))
+        return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: null argument");
+    if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: at most 65535 poses per call");
+    ScoreEnq o;
+    if (int rc = score_enqueue(ctx, poses5, n, zx, p, o)) return rc;
+    hipStream_t st = ctx->stream;
+    const int C = o.C, P = o.P;
+    char *pin = ctx->res_host.as<char>();
+    if (C) {
+        std::memcpy(pin + o.fl_off, cell_flags, C);
+        PCP_HIP(ctx, hipMemcpyAsync(o.flags_d, pin + o.fl_off, C, hipMemcpyHostToDevice, st));
+    }
+    PCP_HIP(ctx, hipMemsetAsync(o.stats, 0, 64 * sizeof(int32_t), st));
+    if (C) {
+        ProfScope ps(ctx, PCP_K_CELL_FLAGS);
+        hipLaunchKernelGGL(k_cell_flags, dim3((unsigned)((C + kT - 1) / kT)), dim3(kT), 0, st,
+                           (const uint8_t *)o.zbits, (const uint8_t *)o.mbits, C, P, o.flags_d,
+                           o.stats);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    // totals and covered counts are adjacent on the device: one copy into the pinned block
+    const double *tot_h = reinterpret_cast<const double *>(pin);
+    const int32_t *cov_h = reinterpret_cast<const int32_t *>(tot_h + (P + 1));
+    const int32_t *st_h = reinterpret_cast<const int32_t *>(pin + o.st_off);
+    PCP_HIP(ctx, hipMemcpyAsync(pin, o.tot_d, o.tc_bytes, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipMemcpyAsync(pin + o.st_off, o.stats, S_N * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    if (C) PCP_HIP(ctx, hipMemcpyAsync(pin + o.fl_off, o.flags_d, C, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    if (C) std::memcpy(cell_flags, pin + o.fl_off, C);
+    prof_resolve(ctx);
+    // runOptimization candidate loop (:464-475): strict '>' keeps the first maximum
+    double best = -INFINITY;
+    int64_t best_idx = -1;
+    for (int k = 0; k < P; ++k) {
+        if (total_score) total_score[k] = tot_h[k];
+        if (covered) covered[k] = cov_h[k];
+        if (tot_h[k] > best) {
+            best = tot_h[k];
+            best_idx = k;
+        }
+    }
+    fill_report(st_h, tot_h[P], best_idx, best, rep);
     return PCP_OK;
 }
 
-static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
-                            const pcp_fan_params *fan, uint32_t *blocked, uint64_t *units,
-                            int16_t *first_hit, int64_t *best_idx, uint64_t *stats,
-                            uint64_t *stamps) {
-    if (!ctx) return PCP_E_INVALID;
-    if (!fan || (n && (!poses5 || !blocked)))
-        return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: null argument");
+}  // extern "C"
+
+namespace pcp {
+// Everything of a fan query up to the per-pose sums, enqueued on ctx->stream (no host sync
+// unless the fan tables or the step table change): poses uploaded through the pinned block,
+// the march, k_fan_reduce.  On return o.blocked_d / o.units_d (and o.fh_d when want_fh) are
+// device results in flight; the caller synchronizes.  n > 0.
+int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
+                bool want_fh, bool stats, bool stamps, FanEnq &o) {
     if (fan->n_az <= 0 || fan->n_el <= 0 || (int64_t)fan->n_az * fan->n_el > (1ll << 30))
         return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: bad fan size %d x %d", fan->n_az,
                        fan->n_el);
     if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: at most 65535 poses per call");
-    if (best_idx) *best_idx = -1;
-    if (n == 0) return PCP_OK;
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const int P = (int)n;
@@ -1081,7 +1238,7 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     unsigned long long *units_d = ctx->out_c.as<unsigned long long>();
     uint32_t *blocked_d = reinterpret_cast<uint32_t *>(units_d + P);
     int16_t *fh_d = nullptr;
-    if (first_hit) {
+    if (want_fh) {
         PCP_HIP(ctx, ctx->out_d.ensure((size_t)P * rays * sizeof(int16_t)));
         fh_d = ctx->out_d.as<int16_t>();
     }
@@ -1120,12 +1277,11 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
         hipLaunchKernelGGL(k_sum_u64, dim3(3), dim3(1024), 0, st,
                            (const unsigned long long *)a.stats, nw, a.stats + 3 * nw);
         PCP_CHECK_LAUNCH(ctx);
-        PCP_HIP(ctx, hipMemcpyAsync(stats, a.stats + 3 * nw, 3 * sizeof(uint64_t),
-                                    hipMemcpyDeviceToHost, st));
+        o.stats_d = a.stats + 3 * nw;
     } else if (stamps) {
         hipLaunchKernelGGL((k_raycast_fan<FAN_STAMPS>), grid1, dim3(64), 0, st, a, (uint32_t)P);
         PCP_CHECK_LAUNCH(ctx);
-        PCP_HIP(ctx, hipMemcpyAsync(stamps, a.stats, stats_bytes, hipMemcpyDeviceToHost, st));
+        o.stats_d = a.stats;
     } else {
         ProfScope ps(ctx, PCP_K_RAYCAST_FAN);
         // PCP_FAN_BATCH selects the A/B variants of DESIGN.md §6b
@@ -1141,12 +1297,50 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
                        (const uint2 *)a.wave_part, waves, (uint32_t)P, a.per_xcd, blocked_d,
                        units_d);
     PCP_CHECK_LAUNCH(ctx);
+    o.blocked_d = blocked_d;
+    o.units_d = units_d;
+    o.fh_d = fh_d;
+    o.rays = rays;
+    o.stats_bytes = stats_bytes;
+    return PCP_OK;
+}
+}  // namespace pcp
+
+extern "C" {
+
+static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                            const pcp_fan_params *fan, uint32_t *blocked, uint64_t *units,
+                            int16_t *first_hit, int64_t *best_idx, uint64_t *stats,
+                            uint64_t *stamps) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!fan || (n && (!poses5 || !blocked)))
+        return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: null argument");
+    if (best_idx) *best_idx = -1;
+    if (n == 0) {
+        if (fan->n_az <= 0 || fan->n_el <= 0 || (int64_t)fan->n_az * fan->n_el > (1ll << 30))
+            return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: bad fan size %d x %d",
+                           fan->n_az, fan->n_el);
+        return PCP_OK;
+    }
+    FanEnq o;
+    if (int rc = fan_enqueue(ctx, poses5, n, fan, first_hit != nullptr, stats != nullptr,
+                             stamps != nullptr, o))
+        return rc;
+    hipStream_t st = ctx->stream;
+    const int P = (int)n;
+    const uint32_t rays = o.rays;
+    if (stats)
+        PCP_HIP(ctx, hipMemcpyAsync(stats, o.stats_d, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                    st));
+    if (stamps)
+        PCP_HIP(ctx, hipMemcpyAsync(stamps, o.stats_d, o.stats_bytes, hipMemcpyDeviceToHost, st));
     // units and blocked are adjacent on the device: one copy into the pinned block
+    double *pose8 = ctx->fan_host.as<double>();
     uint64_t *u_h = reinterpret_cast<uint64_t *>(pose8 + 8 * (size_t)P);
     const uint32_t *b_h = reinterpret_cast<const uint32_t *>(u_h + P);
-    PCP_HIP(ctx, hipMemcpyAsync(u_h, units_d, (size_t)P * 12, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipMemcpyAsync(u_h, o.units_d, (size_t)P * 12, hipMemcpyDeviceToHost, st));
     if (first_hit)
-        PCP_HIP(ctx, hipMemcpyAsync(first_hit, fh_d, (size_t)P * rays * sizeof(int16_t),
+        PCP_HIP(ctx, hipMemcpyAsync(first_hit, o.fh_d, (size_t)P * rays * sizeof(int16_t),
                                     hipMemcpyDeviceToHost, st));
     PCP_HIP(ctx, hipStreamSynchronize(st));
     prof_resolve(ctx);

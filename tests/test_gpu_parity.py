@@ -803,3 +803,84 @@ def test_terrain_block_copy_dense_and_tiny(oracle, mode, monkeypatch):
                 np.testing.assert_array_equal(units, r_units)
         finally:
             ctx.close()
+
+
+# ---------------------------------------------------------------------------------- multi-GPU
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_multi_fan_matches_single_context(gpu, loaded, scene, devices):
+    """pcp_multi: the C2 poses sharded over the ranks, ONE all-reduce(MIN) over
+    the (blocked << 32) | pose keys -- RCCL over one device, or three ranks sharing device 0
+    (keys combined on the device) -- bit-identical to one context over all poses."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    poses, _ = bench._poses_for(gpu, bench._grid_bbox(scene.area), scene.zx120_pose5, 256)
+    fan = _abi.fan_params()
+    b1, u1, _, best1 = gpu.raycast_fan(poses, fan)
+    with _abi.Multi(devices) as m:
+        assert m.n == len(devices) and m.uses_rccl == (len(set(devices)) == len(devices))
+        m.set_terrain(scene.terrain, point_step=32)
+        for sel in (poses, poses[:5], poses[:1]):        # ranks with 0 poses too
+            b, u, best = m.raycast_fan(sel, fan)
+            n = sel.shape[0]
+            np.testing.assert_array_equal(b, b1[:n])
+            np.testing.assert_array_equal(u, u1[:n])
+            assert best == int(np.argmin(b1[:n]))
+        b, u, best = m.raycast_fan(poses[:0], fan)
+        assert b.size == 0 and best == -1
+    assert best1 == int(np.argmin(b1))
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_multi_score_matches_single_context(gpu, loaded, scene, cells, aux, devices):
+    """pcp_multi_score_poses: totals, covered counts, strict-'>' best index, stale flags and the
+    colour report over two ticks (the second starting from the first's flags), identical to
+    pcp_score_poses on one context."""
+    params = _abi.default_vl_params()
+    poses = gpu.generate_candidates(cells.grid_bbox, _abi.default_vl_params(num_candidates=400),
+                                    scene.zx120_pose5)
+    with _abi.Multi(devices) as m:
+        m.set_terrain(scene.terrain, point_step=32)
+        m.set_aux_cloud(aux, point_step=32)
+        m.set_cells(cells.xyz, cells.normals)
+        f1 = np.zeros(cells.xyz.shape[0], np.uint8)
+        fm = f1.copy()
+        for sel in (poses, poses[::7][:3], poses[:0]):
+            t1, c1, r1 = gpu.score_poses(sel, scene.zx120_pose5, params, f1)
+            tm, cm, rm = m.score_poses(sel, scene.zx120_pose5, params, fm)
+            np.testing.assert_array_equal(tm, t1)
+            np.testing.assert_array_equal(cm, c1)
+            np.testing.assert_array_equal(fm, f1)
+            assert rm.as_dict() == r1.as_dict()
+
+
+def test_gpu_matches_flann_restatement(gpu, oracle, loaded, scene):
+    """The GPU's first hits against the oracle in FLANN mode (oracle/pcp_flann.c: the
+    KdTreeFLANN search the reference runs, float pruning included) on 8 of the C2 poses,
+    every sample query also cross-checked against the exact grid count."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    poses, _ = bench._poses_for(gpu, bench._grid_bbox(scene.area), scene.zx120_pose5, 256)
+    sel = poses[::32]
+    fan = _abi.fan_params()
+    blocked, units, fh, _ = gpu.raycast_fan(sel, fan, want_first_hit=True)
+    T, _ = loaded
+    tree = oracle.KdTree(scene.terrain)
+    oracle.set_threads(16)
+    try:
+        rb, ru, rfh, st = oracle.raycast_fan_kd(tree, T, sel, 1024, 256, fan.el_min, fan.el_max,
+                                                fan.max_distance)
+    finally:
+        oracle.set_threads(1)
+    assert st["count_mismatch"] == 0 and st["any_mismatch"] == 0, st
+    assert st["queries"] == int(ru.sum())
+    np.testing.assert_array_equal(fh, rfh)
+    np.testing.assert_array_equal(blocked, rb)
+    np.testing.assert_array_equal(units, ru)
