@@ -64,7 +64,23 @@ Device::Device(int device) {
     if (rc != PCP_OK) throw std::runtime_error("pcp_create failed (no gfx950 device?)");
 }
 
-Device::~Device() { pcp_destroy(ctx_); }
+Device::~Device() {
+    if (owned_) pcp_destroy(ctx_);
+}
+
+MultiDevice::MultiDevice(const std::vector<int> &devices) {
+    const int rc = pcp_multi_create((int)devices.size(), devices.data(), &m_);
+    if (rc != PCP_OK) throw std::runtime_error("pcp_multi_create failed");
+    int rccl = 0;
+    pcp_multi_info(m_, &n_, &rccl);
+    rccl_ = rccl != 0;
+    r0_.reset(new Device(pcp_multi_ctx(m_, 0), Device::Borrow{}));
+}
+
+MultiDevice::~MultiDevice() {
+    r0_.reset();
+    pcp_multi_destroy(m_);
+}
 
 // ---- pointcloud_filter -----------------------------------------------------------------------
 PointCloud2 SimplifiedScanMatcher::processCloudSimple(const PointCloud2 &in,
@@ -148,13 +164,21 @@ void SimplifiedDualLidarOptimizer::terrainCallback(const PointCloud2 &msg) {
     pcp_cloud_view v{};
     if (!cloud_view(msg, v, &err_)) return;
     // empty cloud: the old tree stays (:184-191), ground heights see the empty cloud
-    if (pcp_set_terrain(dev_.ctx(), &v) != PCP_OK) err_ = dev_.error();
+    if (multi_) {
+        if (pcp_multi_set_terrain(multi_, &v) != PCP_OK) err_ = pcp_multi_last_error(multi_);
+    } else if (pcp_set_terrain(dev_.ctx(), &v) != PCP_OK) {
+        err_ = dev_.error();
+    }
 }
 
 void SimplifiedDualLidarOptimizer::zx120PointsCallback(const PointCloud2 &msg) {
     pcp_cloud_view v{};
     if (!cloud_view(msg, v, &err_)) return;
-    if (pcp_set_aux_cloud(dev_.ctx(), &v) != PCP_OK) err_ = dev_.error();
+    if (multi_) {
+        if (pcp_multi_set_aux_cloud(multi_, &v) != PCP_OK) err_ = pcp_multi_last_error(multi_);
+    } else if (pcp_set_aux_cloud(dev_.ctx(), &v) != PCP_OK) {
+        err_ = dev_.error();
+    }
 }
 
 void SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg) {
@@ -172,6 +196,16 @@ void SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg
         err_ = dev_.error();   // "Failed to process excavation area" (:175-177)
         return;
     }
+    if (multi_ && n) {   // rank 0 built the cells: replicate them on every rank
+        std::vector<double> xyz(3 * n);
+        std::vector<float> nrm(3 * n);
+        uint64_t got = 0;
+        if (pcp_get_cells(dev_.ctx(), xyz.data(), nrm.data(), n, &got) != PCP_OK ||
+            pcp_multi_set_cells(multi_, xyz.data(), nrm.data(), got) != PCP_OK) {
+            err_ = pcp_multi_last_error(multi_);
+            return;
+        }
+    }
     n_cells_ = n;
     flags_.assign(n_cells_, 0);   // excavation_grid_3d_ rebuilt from fresh GridCells (:259)
     std::memcpy(bbox_, bb, sizeof(bbox_));
@@ -183,8 +217,10 @@ void SimplifiedDualLidarOptimizer::setExcavationGrid(const std::vector<double> &
     n_cells_ = xyz.size() / 3;
     flags_.assign(n_cells_, 0);   // fresh GridCells (:259, ctor :34-43)
     std::memcpy(bbox_, grid_bbox, sizeof(bbox_));
-    if (pcp_set_cells(dev_.ctx(), xyz.data(), normals.data(), n_cells_) != PCP_OK) {
-        err_ = dev_.error();
+    const int rc = multi_ ? pcp_multi_set_cells(multi_, xyz.data(), normals.data(), n_cells_)
+                          : pcp_set_cells(dev_.ctx(), xyz.data(), normals.data(), n_cells_);
+    if (rc != PCP_OK) {
+        err_ = multi_ ? pcp_multi_last_error(multi_) : dev_.error();
         n_cells_ = 0;
     }
 }
@@ -223,9 +259,14 @@ SimplifiedDualLidarOptimizer::Result SimplifiedDualLidarOptimizer::runOptimizati
         return r;
     }
     std::vector<double> totals(n ? n : 1);
-    if (pcp_score_poses(dev_.ctx(), poses.data(), n, zx, &p, flags_.data(), totals.data(), nullptr,
-                        &r.report) != PCP_OK) {
-        err_ = dev_.error();
+    // the candidate loop (:467-475): on one device, or sharded over multi_'s devices with one
+    // collective (identical results)
+    const int rc = multi_ ? pcp_multi_score_poses(multi_, poses.data(), n, zx, &p, flags_.data(),
+                                                  totals.data(), nullptr, &r.report)
+                          : pcp_score_poses(dev_.ctx(), poses.data(), n, zx, &p, flags_.data(),
+                                            totals.data(), nullptr, &r.report);
+    if (rc != PCP_OK) {
+        err_ = multi_ ? pcp_multi_last_error(multi_) : dev_.error();
         return r;
     }
     r.ran = true;

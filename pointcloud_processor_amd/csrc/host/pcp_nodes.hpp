@@ -58,7 +58,33 @@ class Device {
     const char *error() const { return pcp_last_error(ctx_); }
 
    private:
+    friend class MultiDevice;
+    struct Borrow {};
+    Device(pcp_ctx *ctx, Borrow) : ctx_(ctx), owned_(false) {}   // a MultiDevice rank's context
     pcp_ctx *ctx_ = nullptr;
+    bool owned_ = true;
+};
+
+// n GPUs in this process (pcp_multi: one context per device + one RCCL communicator).  The
+// virtual-LiDAR node shards its candidate poses over them; rank 0's context serves every
+// other call (candidate generation, the excavation-area setup, the other nodes).
+class MultiDevice {
+   public:
+    explicit MultiDevice(const std::vector<int> &devices);
+    ~MultiDevice();
+    MultiDevice(const MultiDevice &) = delete;
+    MultiDevice &operator=(const MultiDevice &) = delete;
+    pcp_multi *get() const { return m_; }
+    int size() const { return n_; }
+    bool usesRccl() const { return rccl_; }
+    Device &rank0() { return *r0_; }
+    const char *error() const { return pcp_multi_last_error(m_); }
+
+   private:
+    pcp_multi *m_ = nullptr;
+    int n_ = 0;
+    bool rccl_ = false;
+    std::unique_ptr<Device> r0_;
 };
 
 // ---- pointcloud_filter.cpp (SimplifiedScanMatcher) -----------------------------------------
@@ -187,6 +213,10 @@ class SimplifiedDualLidarOptimizer {
     };
     explicit SimplifiedDualLidarOptimizer(Device &dev) : dev_(dev) {}
     SimplifiedDualLidarOptimizer(Device &dev, const Params &p) : dev_(dev), p_(p) {}
+    // the candidate loop sharded over the devices of md (one collective per tick)
+    explicit SimplifiedDualLidarOptimizer(MultiDevice &md) : dev_(md.rank0()), multi_(md.get()) {}
+    SimplifiedDualLidarOptimizer(MultiDevice &md, const Params &p)
+        : dev_(md.rank0()), multi_(md.get()), p_(p) {}
     Params &params() { return p_; }
     // excavationAreaCallback (:164-178): GPU normals + 3-D cell grid from /excavation_area;
     // an empty cloud keeps the previous grid (:168)
@@ -206,6 +236,7 @@ class SimplifiedDualLidarOptimizer {
 
    private:
     Device &dev_;
+    pcp_multi *multi_ = nullptr;   // non-null: poses sharded over its devices
     Params p_;
     bool terrain_cloud_ = false;   // terrain_cloud_ non-null (a message arrived)
     size_t n_cells_ = 0;

@@ -121,6 +121,19 @@ static int cmd_merge(Device &dev, char **a) {
     return 0;
 }
 
+// PCP_DEVICES=d0,d1,...: the virtual-LiDAR node shards its poses over these devices (pcp_multi)
+static std::unique_ptr<MultiDevice> multi_from_env() {
+    const char *e = std::getenv("PCP_DEVICES");
+    if (!e || !*e) return nullptr;
+    std::vector<int> d;
+    for (const char *p = e; *p;) {
+        d.push_back(std::atoi(p));
+        while (*p && *p != ',') ++p;
+        if (*p == ',') ++p;
+    }
+    return std::unique_ptr<MultiDevice>(new MultiDevice(d));
+}
+
 static int cmd_vlidar(Device &dev, char **a, int argc) {
     const auto t = read_file(a[0]), ax = read_file(a[2]), c = read_file(a[4]),
                nr = read_file(a[5]);
@@ -130,7 +143,10 @@ static int cmd_vlidar(Device &dev, char **a, int argc) {
     SimplifiedDualLidarOptimizer::Params p;
     p.num_candidates = std::atoi(a[9]);
     p.max_distance = std::strtod(a[10], nullptr);
-    SimplifiedDualLidarOptimizer node(dev, p);
+    std::unique_ptr<MultiDevice> md = multi_from_env();
+    std::unique_ptr<SimplifiedDualLidarOptimizer> nodep(
+        md ? new SimplifiedDualLidarOptimizer(*md, p) : new SimplifiedDualLidarOptimizer(dev, p));
+    SimplifiedDualLidarOptimizer &node = *nodep;
     Transform zx;
     zx.t[0] = zxt[0];
     zx.t[1] = zxt[1];
@@ -157,8 +173,10 @@ static int cmd_vlidar(Device &dev, char **a, int argc) {
     write_file(a[11], tot.data(), tot.size() * 8);
     write_file(a[12], node.cellFlags().data(), node.cellFlags().size());
     write_file(a[13], r.log.data(), r.log.size());
-    std::printf("{\"n_candidates\": %zu, \"best_idx\": %lld, \"best\": [%.17g, %.17g, %.17g]}\n",
-                r.candidates.size(), (long long)r.report.best_idx, r.best.x, r.best.y, r.best.z);
+    std::printf("{\"n_candidates\": %zu, \"best_idx\": %lld, \"best\": [%.17g, %.17g, %.17g], "
+                "\"devices\": %d, \"rccl\": %d}\n",
+                r.candidates.size(), (long long)r.report.best_idx, r.best.x, r.best.y, r.best.z,
+                md ? md->size() : 1, md && md->usesRccl() ? 1 : 0);
     return 0;
 }
 

@@ -15,10 +15,12 @@ GOLD = ROOT / "tests" / "golden"
 pytestmark = pytest.mark.gpu
 
 
-def _run(*args, timeout=300):
+def _run(*args, timeout=300, env=None):
+    import os
+
     assert CLI.exists(), "build first (__graft_entry__.build())"
     r = subprocess.run([str(CLI), *map(str, args)], capture_output=True, text=True,
-                       timeout=timeout)
+                       timeout=timeout, env=None if env is None else {**os.environ, **env})
     assert r.returncode == 0, (r.returncode, r.stderr)
     import json
 
@@ -62,7 +64,11 @@ def test_merger_node(tmp_path, oracle):
     np.testing.assert_array_equal(out[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
 
 
-def test_virtual_lidar_node(tmp_path):
+@pytest.mark.parametrize("devices", [None, "0", "0,0,0"])
+def test_virtual_lidar_node(tmp_path, devices):
+    """SimplifiedDualLidarOptimizer on one device, and with its candidate loop sharded over a
+    MultiDevice (pcp_multi: RCCL over device 0, or three ranks sharing device 0): the same
+    totals, stale flags, best pose and log tables."""
     d = np.load(GOLD / "score.npz")
     np.ascontiguousarray(d["terrain"]).tofile(tmp_path / "t.f32")
     np.ascontiguousarray(d["aux"]).tofile(tmp_path / "a.f32")
@@ -73,7 +79,11 @@ def test_virtual_lidar_node(tmp_path):
     res = _run("vlidar", tmp_path / "t.f32", d["terrain"].shape[0], tmp_path / "a.f32",
                d["aux"].shape[0], tmp_path / "c.f64", tmp_path / "n.f32", d["cells"].shape[0],
                _t(d["grid_bbox"]), _t(base), int(d["num_candidates"]), float(d["max_distance"]),
-               tmp_path / "tot.f64", tmp_path / "flags.u8", tmp_path / "log.txt")
+               tmp_path / "tot.f64", tmp_path / "flags.u8", tmp_path / "log.txt",
+               env=None if devices is None else {"PCP_DEVICES": devices})
+    if devices is not None:
+        assert res["devices"] == len(devices.split(","))
+        assert res["rccl"] == (1 if devices == "0" else 0)
     tot = np.fromfile(tmp_path / "tot.f64", np.float64)
     flags = np.fromfile(tmp_path / "flags.u8", np.uint8)
     np.testing.assert_allclose(tot, d["total"], rtol=1e-12, atol=0)
