@@ -271,16 +271,16 @@ def _timed(step, args, dist, on_gpu, dev):
 
 def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
     """Roofline of k_raycast_fan from the kernel's own request counts:
-    requested bytes = 2 B per z-band probe + 16 B per scanned block (8-B directory entry +
-    8-B step) + 16 B per point test + 16 B per ray (azimuth table) + 8 B per wave partial.
-    These are the bytes the kernel's loads and stores ask for (served by L1/L2/MALL: the 1M-pt
-    terrain's working set is cache-resident); the HBM-side bytes are the PMC `traffic`."""
+    requested bytes = 2 B per z-band probe + 8 B per candidate (its step) + 8 B per block
+    directory load + 12 B per point record loaded + 16 B per ray (azimuth table) + 8 B per wave
+    partial.  These are the bytes the kernel's loads and stores ask for (served by L1/L2/MALL:
+    the 1M-pt terrain's working set is cache-resident); the HBM-side bytes are the PMC
+    `traffic`."""
     st = ctx.raycast_fan_stats(poses, fan)
     rays = poses.shape[0] * fan.n_az * fan.n_el
     waves = poses.shape[0] * ((fan.n_az * fan.n_el + 63) // 64)
-    req = 2.0 * st["samples_visited"] + 16.0 * st["scanned_stencils"] + 16.0 * st["point_tests"] \
-        + 16.0 * rays \
-        + 8.0 * waves
+    req = 2.0 * st["samples_visited"] + 8.0 * st["scanned_stencils"] \
+        + 8.0 * st["directory_loads"] + 12.0 * st["point_tests"] + 16.0 * rays + 8.0 * waves
     ref_model = 64.0 * units_per_launch + 12.0 * st["point_tests"]
     traffic = _traffic_from_profiles("fan")
     achieved = _gbs(req, avg_kernel_s)
@@ -292,9 +292,9 @@ def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
         "traffic_frac": (_gbs(traffic, avg_kernel_s) or 0.0) / HBM_PEAK_GBS if traffic else None,
         "kernel": "k_raycast_fan<0, 64, true>", "avg_kernel_ms": avg_kernel_s * 1e3,
         "requested_bytes_per_launch": req,
-        "model": "requested bytes: 2 B/probe + 16 B/scan + 16 B/point test + 16 B/ray + "
-                 "8 B/wave (pcp_raycast_fan_stats counts); traffic = PMC FETCH(x2)+WRITE per "
-                 "launch (profiles/pmc_traffic.json)",
+        "model": "requested bytes: 2 B/probe + 8 B/candidate + 8 B/directory load + 12 B/point "
+                 "record + 16 B/ray + 8 B/wave (pcp_raycast_fan_stats counts); traffic = PMC "
+                 "FETCH(x2)+WRITE per launch (profiles/pmc_traffic.json)",
         "limiter": "vector-memory gather path (TA/TD busy, L1 tag lookups per instruction; "
                    "profiles/r02_fan_pmc*.txt), not HBM: the terrain lives in L2/MALL",
         "alg_reference_bytes_per_launch": ref_model,

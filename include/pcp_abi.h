@@ -284,10 +284,11 @@ int pcp_raycast_fan(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fa
                     uint32_t *blocked, uint64_t *units, int16_t *first_hit, int64_t *best_idx);
 
 /* Diagnostic build of the same march (not for timing): stats[0] = samples probed after the
- * exact clip, stats[1] = samples whose 2x2x2 stencil survives the z-band probe and is scanned
- * (directory reads), stats[2] = point tests.  Used to state the roofline's algorithmic bytes. */
+ * exact clip, stats[1] = samples whose 2x2x2 stencil survives the z-band probe and is scanned,
+ * stats[2] = point records loaded (12 B each), stats[3] = block directory entries loaded.
+ * Used to state the roofline's requested bytes. */
 int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
-                          const pcp_fan_params *fan, uint64_t stats[3]);
+                          const pcp_fan_params *fan, uint64_t stats[4]);
 
 /* Diagnostic build with s_memtime stamps (shader clock) per wave: stamps[(p*W + w)*4 + i],
  * W = ceil(n_az*n_el/64), i = 0 start, 1 after direction setup, 2 after the march, 3 end.

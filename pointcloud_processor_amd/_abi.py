@@ -610,11 +610,11 @@ class Multi:
 
 def _fan_stats(self, poses5, fan):
     poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
-    st = np.zeros(3, np.uint64)
+    st = np.zeros(4, np.uint64)
     self._check(self.lib.pcp_raycast_fan_stats(self.h, _ptr(poses), poses.shape[0], C.byref(fan),
                                                _ptr(st)), "pcp_raycast_fan_stats")
     return {"samples_visited": int(st[0]), "scanned_stencils": int(st[1]),
-            "point_tests": int(st[2])}
+            "point_tests": int(st[2]), "directory_loads": int(st[3])}
 
 
 Context.raycast_fan_stats = _fan_stats

@@ -824,11 +824,11 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
         a.wave_part[(size_t)(b & 7u) * a.per_xcd + (b >> 3)] =
             make_uint2((uint32_t)__popcll(bal), u);
     }
-    if (MODE == FAN_STATS) {   // per-wave slots [3][P * waves], summed by k_sum_u64
+    if (MODE == FAN_STATS) {   // per-wave slots [4][P * waves], summed by k_sum_u64
         const size_t nw = (size_t)gridDim.x * (BS / 64);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            unsigned long long v = cnt[q];
+        for (int q = 0; q < 4; ++q) {   // [3] directory loads: one per scan here
+            unsigned long long v = cnt[q < 3 ? q : 1];
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
             if ((threadIdx.x & 63) == 0 && wid < a.waves) a.stats[q * nw + wslot] = v;
@@ -1230,7 +1230,7 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
     PCP_HIP(ctx, ctx->out_b.ensure(((size_t)P * waves + 8) * sizeof(uint2)));
     // stamps: 4 per wave; stats: 3 per wave + the 3 sums
     const size_t stats_bytes = stamps  ? (size_t)P * waves * 4 * sizeof(uint64_t)
-                               : stats ? ((size_t)P * waves * 3 + 3) * sizeof(uint64_t)
+                               : stats ? ((size_t)P * waves * 4 + 4) * sizeof(uint64_t)
                                        : 64 * sizeof(uint64_t);
     PCP_HIP(ctx, ctx->stats_d.ensure(stats_bytes));
     PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pose8, (size_t)P * 8 * sizeof(double),
@@ -1274,10 +1274,10 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
         hipLaunchKernelGGL((k_raycast_fan<FAN_STATS>), grid1, dim3(64), 0, st, a, (uint32_t)P);
         PCP_CHECK_LAUNCH(ctx);
         const size_t nw = (size_t)P * waves;
-        hipLaunchKernelGGL(k_sum_u64, dim3(3), dim3(1024), 0, st,
-                           (const unsigned long long *)a.stats, nw, a.stats + 3 * nw);
+        hipLaunchKernelGGL(k_sum_u64, dim3(4), dim3(1024), 0, st,
+                           (const unsigned long long *)a.stats, nw, a.stats + 4 * nw);
         PCP_CHECK_LAUNCH(ctx);
-        o.stats_d = a.stats + 3 * nw;
+        o.stats_d = a.stats + 4 * nw;
     } else if (stamps) {
         hipLaunchKernelGGL((k_raycast_fan<FAN_STAMPS>), grid1, dim3(64), 0, st, a, (uint32_t)P);
         PCP_CHECK_LAUNCH(ctx);
@@ -1330,7 +1330,7 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     const int P = (int)n;
     const uint32_t rays = o.rays;
     if (stats)
-        PCP_HIP(ctx, hipMemcpyAsync(stats, o.stats_d, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+        PCP_HIP(ctx, hipMemcpyAsync(stats, o.stats_d, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost,
                                     st));
     if (stamps)
         PCP_HIP(ctx, hipMemcpyAsync(stamps, o.stats_d, o.stats_bytes, hipMemcpyDeviceToHost, st));
@@ -1363,10 +1363,10 @@ int pcp_raycast_fan(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fa
 }
 
 int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
-                          const pcp_fan_params *fan, uint64_t stats[3]) {
+                          const pcp_fan_params *fan, uint64_t stats[4]) {
     if (!ctx || !stats) return PCP_E_INVALID;
     std::vector<uint32_t> blocked(n ? n : 1);
-    stats[0] = stats[1] = stats[2] = 0;
+    stats[0] = stats[1] = stats[2] = stats[3] = 0;
     return raycast_fan_impl(ctx, poses5, n, fan, blocked.data(), nullptr, nullptr, nullptr, stats,
                             nullptr);
 }

@@ -43,4 +43,5 @@ for rnd in range(12):
 for v in variants:
     t = np.array(times[v])
     print(f"batch={v}: median {np.median(t):.4f} ms  min {t.min():.4f} ms")
-print("stats", ctxs[variants[0]].raycast_fan_stats(poses, fan))
+for v in variants:
+    print("stats", v, ctxs[v].raycast_fan_stats(poses, fan))
