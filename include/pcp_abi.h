@@ -74,6 +74,11 @@ int pcp_host_free(pcp_ctx *ctx, void *hptr);
 int pcp_host_register(pcp_ctx *ctx, void *hptr, uint64_t bytes);
 int pcp_host_unregister(pcp_ctx *ctx, void *hptr);
 
+/* process-wide counts of scratch (re)allocations by the library: device buffers, pinned
+ * staging buffers, bytes allocated.  Each device reallocation frees the old buffer (a device
+ * synchronization), so a streaming caller checks these settle after its first frames. */
+int pcp_alloc_stats(uint64_t *device_reallocs, uint64_t *pinned_reallocs, uint64_t *bytes);
+
 /* ---- in-library kernel timing (HIP events on the ctx stream) ------------------------ */
 enum pcp_kernel_id {
     PCP_K_RAYCAST_FAN = 0,   /* fan ray-march (BASELINE configs[1], the headline)   */

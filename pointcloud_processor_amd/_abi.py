@@ -83,6 +83,7 @@ _P = C.c_void_p
 _SIGS = [
     ("pcp_abi_version", C.c_int, []),
     ("pcp_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("pcp_alloc_stats", C.c_int, [_P, _P, _P]),
     ("pcp_create", C.c_int, [C.c_int, C.POINTER(_P)]),
     ("pcp_destroy", None, [_P]),
     ("pcp_last_error", C.c_char_p, [_P]),

@@ -207,6 +207,9 @@ static int cmd_replay(Device &dev, char **a) {
     // excavated_surface_generator, whose /excavated_terrain and /excavation_area feed
     // virtual_lidar every frame (terrain index, normals, cell grid rebuilt per frame)
     const bool chain = a[8] && std::atoi(a[8]) != 0;
+    // DUMP_DIR (optional): the inputs and every node's outputs of frames 0, 1, 2 and the last
+    // one, for the oracle check of the streamed chain (tests/test_nodes_cli.py)
+    const std::string dump = (a[8] && a[9]) ? a[9] : "";
     SimplifiedScanMatcher filt(dev);
     GnssGicpMatcher merger(dev);
     ExcavationTerrainGenerator gen(dev);
@@ -222,8 +225,12 @@ static int cmd_replay(Device &dev, char **a) {
     const Transform zx_tf{{0.55, 0.4, 3.5}, {0.0, 0.21633, 0.0, 0.97632}};
     const Transform zx_base{{0.0, 0.0, 0.0}, {0, 0, 0, 1}};
     std::vector<double> lat;
+    std::vector<double> lat_frame;   // in frame order (the sorted copy gives the percentiles)
     size_t merged_n = 0, best = 0, cells_n = cn;
+    uint64_t realloc_after_warmup = 0, ra0 = 0;
+    std::string dumped;
     for (int f = 0; f < frames + 2; ++f) {
+        if (f == 2) pcp_alloc_stats(&ra0, nullptr, nullptr);
         auto rs = synth_scan(npts, 2.0, rng), zs = synth_scan(npts, 3.5, rng);
         PointCloud2 rm = make_xyz_cloud(rs.data(), npts, "four_wheel_robot/velodyne_link");
         PointCloud2 zm = make_xyz_cloud(zs.data(), npts, "zx120/velodyne_link");
@@ -234,8 +241,9 @@ static int cmd_replay(Device &dev, char **a) {
         merger.robotCloudCallback(rf);
         merger.backhoeCloudCallback(zf);
         auto o = merger.processPointClouds(true, &robot_tf, &zx_tf);
+        ExcavationTerrainGenerator::Output e;
         if (chain) {
-            auto e = gen.matchedCloudCallback(o.merged, &zx_base);
+            e = gen.matchedCloudCallback(o.merged, &zx_base);
             if (!e.area_published) {
                 std::fprintf(stderr, "replay: carve failed: %s\n", gen.lastError().c_str());
                 return 1;
@@ -254,14 +262,58 @@ static int cmd_replay(Device &dev, char **a) {
         merged_n = o.merged.size();
         best = (size_t)r.report.best_idx;
         if (f >= 2) lat.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+        if (f >= 2) lat_frame.push_back(lat.back());
+        if (!dump.empty() && chain && (f < 3 || f == frames + 1)) {
+            const std::string pre = dump + "/f" + std::to_string(f) + "_";
+            write_file((pre + "rscan.f32").c_str(), rs.data(), rs.size() * 4);
+            write_file((pre + "zscan.f32").c_str(), zs.data(), zs.size() * 4);
+            write_file((pre + "rf.bin").c_str(), rf.data.data(), rf.data.size());
+            write_file((pre + "zf.bin").c_str(), zf.data.data(), zf.data.size());
+            write_file((pre + "merged.bin").c_str(), o.merged.data.data(), o.merged.data.size());
+            // the carve's outputs, as published (they are the node inputs of this frame)
+            write_file((pre + "terrain.bin").c_str(), e.excavated_terrain.data.data(),
+                       e.excavated_terrain.data.size());
+            write_file((pre + "area.bin").c_str(), e.excavation_area.data.data(),
+                       e.excavation_area.data.size());
+            uint64_t nc = 0;
+            pcp_get_cells(dev.ctx(), nullptr, nullptr, 0, &nc);
+            std::vector<double> cx(3 * nc);
+            std::vector<float> cnr(3 * nc);
+            if (nc) pcp_get_cells(dev.ctx(), cx.data(), cnr.data(), nc, &nc);
+            write_file((pre + "cells.f64").c_str(), cx.data(), cx.size() * 8);
+            write_file((pre + "cnrm.f32").c_str(), cnr.data(), cnr.size() * 4);
+            std::vector<double> ps, tot;
+            for (const auto &c : r.candidates) {
+                ps.insert(ps.end(), {c.x, c.y, c.z, c.pitch, c.yaw});
+                tot.push_back(c.total_score);
+            }
+            write_file((pre + "poses.f64").c_str(), ps.data(), ps.size() * 8);
+            write_file((pre + "tot.f64").c_str(), tot.data(), tot.size() * 8);
+            char buf[128];
+            std::snprintf(buf, sizeof(buf), "%s{\"frame\": %d, \"best_idx\": %lld}",
+                          dumped.empty() ? "" : ", ", f, (long long)r.report.best_idx);
+            dumped += buf;
+        }
+    }
+    {
+        uint64_t ra1 = 0;
+        pcp_alloc_stats(&ra1, nullptr, nullptr);
+        realloc_after_warmup = ra1 - ra0;
+    }
+    std::string lat_s;
+    for (size_t i = 0; i < lat_frame.size(); ++i) {
+        char b[32];
+        std::snprintf(b, sizeof(b), "%s%.4f", i ? ", " : "", lat_frame[i]);
+        lat_s += b;
     }
     std::sort(lat.begin(), lat.end());
     auto q = [&lat](double p) { return lat[std::min(lat.size() - 1, (size_t)(p * lat.size()))]; };
     std::printf("{\"frames\": %zu, \"points_per_scan\": %zu, \"chain\": %d, \"p50_ms\": %.4f, "
                 "\"p99_ms\": %.4f, \"max_ms\": %.4f, \"merged_points\": %zu, \"cells\": %zu, "
-                "\"best_idx\": %zu}\n",
+                "\"best_idx\": %zu, \"reallocs_after_warmup\": %llu, \"dumped\": [%s], "
+                "\"lat_ms\": [%s]}\n",
                 lat.size(), npts, chain ? 1 : 0, q(0.5), q(0.99), lat.back(), merged_n, cells_n,
-                best);
+                best, (unsigned long long)realloc_after_warmup, dumped.c_str(), lat_s.c_str());
     return 0;
 }
 

@@ -43,6 +43,15 @@ int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what) {
     return PCP_OK;
 }
 
+static std::atomic<uint64_t> g_reallocs{0}, g_pinned_reallocs{0}, g_alloc_bytes{0};
+void note_realloc(size_t bytes, bool pinned) {
+    (pinned ? g_pinned_reallocs : g_reallocs).fetch_add(1, std::memory_order_relaxed);
+    g_alloc_bytes.fetch_add(bytes, std::memory_order_relaxed);
+}
+uint64_t alloc_count(int which) {
+    return which == 0 ? g_reallocs.load() : which == 1 ? g_pinned_reallocs.load() : g_alloc_bytes.load();
+}
+
 int read_small(pcp_ctx *ctx, void *dst, const void *src_d, size_t bytes, hipStream_t st) {
     if (bytes > 4096) return set_err(ctx, PCP_E_INVALID, "read_small: %zu bytes", bytes);
     PCP_HIP(ctx, ctx->small_host.ensure(4096));
@@ -237,6 +246,13 @@ using namespace pcp;
 extern "C" {
 
 int pcp_abi_version(void) { return PCP_ABI_VERSION; }
+
+int pcp_alloc_stats(uint64_t *device_reallocs, uint64_t *pinned_reallocs, uint64_t *bytes) {
+    if (device_reallocs) *device_reallocs = alloc_count(0);
+    if (pinned_reallocs) *pinned_reallocs = alloc_count(1);
+    if (bytes) *bytes = alloc_count(2);
+    return PCP_OK;
+}
 
 int pcp_device_count(int *n) {
     if (!n) return PCP_E_INVALID;

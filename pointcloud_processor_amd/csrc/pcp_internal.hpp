@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -27,19 +29,28 @@ constexpr double kCellMargin = 4e-3;   // conservative margin of the stencil (se
 constexpr double kQueryMargin = 1e-3;
 
 // ---------------------------------------------------------------------------------------
-// device buffer (grow-only)
+// device buffer (grow-only).  A buffer that must grow is reallocated with 25 % headroom (and at
+// least 64 KiB): a hipFree synchronizes the whole device, so a per-frame chain whose sizes
+// wander (C5) must converge to few reallocations instead of one per new maximum.  Every
+// reallocation is counted process-wide (pcp_alloc_stats).
 // ---------------------------------------------------------------------------------------
+void note_realloc(size_t bytes, bool pinned);
+uint64_t alloc_count(int which);   // 0 device, 1 pinned reallocations, 2 bytes allocated
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
+        const bool grow = cap != 0;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
         size_t want = bytes < 256 ? 256 : bytes;
+        if (grow) want = std::max<size_t>(want + want / 4, 64u << 10);
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
+        note_realloc(want, false);
         return e;
     }
     void release() {
@@ -50,19 +61,22 @@ struct DevBuf {
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
-// pinned (page-locked) host staging buffer (grow-only): small per-call H2D / D2H transfers
-// from it skip the runtime's pageable staging copy
+// pinned (page-locked) host staging buffer (grow-only, same growth rule): small per-call H2D /
+// D2H transfers from it skip the runtime's pageable staging copy
 struct PinnedBuf {
     void *p = nullptr;
     size_t cap = 0;
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
+        const bool grow = cap != 0;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
         size_t want = bytes < 4096 ? 4096 : bytes;
+        if (grow) want = std::max<size_t>(want + want / 4, 64u << 10);
         hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
         if (e == hipSuccess) cap = want;
+        note_realloc(want, true);
         return e;
     }
     void release() {

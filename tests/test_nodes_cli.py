@@ -139,18 +139,77 @@ def test_excavation_area_node(tmp_path, oracle, small_scene):
     assert res["best_idx"] == rep.best_idx
 
 
-def test_streaming_replay_full_chain(tmp_path, scene, cells):
+def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells):
     """C5 with the launch file's whole chain per frame: filter x2 -> merge ->
     excavated_surface_generator (/excavated_terrain, /excavation_area) -> virtual_lidar
-    (terrain index, normals + cell grid, pose search)."""
+    (terrain index, normals + cell grid, pose search).  Frames 0, 1, 2 and the last one are
+    re-run through the oracle from their raw scans: filtered clouds, merged cloud, carved
+    terrain and excavation area bit-exact; cells exact, cell normals within 1e-4; candidate
+    poses exact (angles 1e-12); totals 1e-12 and the best pose exact (scored with the node's
+    own normals).  Scratch reallocations settle after the first frames."""
     np.ascontiguousarray(scene.terrain).tofile(tmp_path / "t.f32")
     np.ascontiguousarray(cells.xyz).tofile(tmp_path / "c.f64")
     np.ascontiguousarray(cells.normals).tofile(tmp_path / "n.f32")
+    frames = 8
     res = _run("replay", tmp_path / "t.f32", scene.terrain.shape[0], tmp_path / "c.f64",
-               tmp_path / "n.f32", cells.xyz.shape[0], _t(cells.grid_bbox), 6, 60032, 1)
-    assert res["frames"] == 6 and res["chain"] == 1
+               tmp_path / "n.f32", cells.xyz.shape[0], _t(cells.grid_bbox), frames, 60032, 1,
+               tmp_path)
+    assert res["frames"] == frames and res["chain"] == 1
     assert res["cells"] > 0 and res["merged_points"] > 0 and res["best_idx"] >= 0
     assert 0 < res["p50_ms"] <= res["p99_ms"]
+    assert len(res["lat_ms"]) == frames
+    assert [d["frame"] for d in res["dumped"]] == [0, 1, 2, frames + 1]
+    box = np.array([0.0, 15.0, -10.0, 10.0, -1.5, 10.0])     # pointcloud_filter.cpp:30-36
+    rt = ((8.0, -3.0, 2.0), (0.0, 0.0, 0.2588190451025208, 0.9659258262890683))
+    zt = ((0.55, 0.4, 3.5), (0.0, 0.21633, 0.0, 0.97632))
+    zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])   # getZX120Position on the origin
+
+    def ld(name, dt, cols):
+        return np.fromfile(tmp_path / name, dt).reshape(-1, cols)
+
+    for d in res["dumped"]:
+        pre = f"f{d['frame']}_"
+        filtered = []
+        for tag in ("rscan", "zscan"):
+            scan = ld(pre + tag + ".f32", np.float32, 4)
+            kept = oracle.crop_box(scan, box)
+            vox, _, _, _ = oracle.voxel_grid(scan[kept], 0.2)
+            got = ld(pre + tag[0] + "f.bin", np.float32, 4)
+            np.testing.assert_array_equal(got[:, :3], vox)
+            filtered.append(got)
+        ref = np.concatenate([oracle.transform_rgb(filtered[0], rt[0], rt[1], (255, 0, 0)),
+                              oracle.transform_rgb(filtered[1], zt[0], zt[1], (0, 0, 255))])
+        merged = ld(pre + "merged.bin", np.float32, 8)
+        np.testing.assert_array_equal(merged[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
+        keep, surf, area, _ = oracle.excavate(merged, (0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))
+        terr = ld(pre + "terrain.bin", np.float32, 8)
+        nk = int(keep.sum())
+        assert terr.shape[0] == nk + surf.shape[0]
+        np.testing.assert_array_equal(terr[:nk, [0, 1, 2, 4]].view(np.uint32),
+                                      merged[keep][:, [0, 1, 2, 4]].view(np.uint32))
+        np.testing.assert_array_equal(terr[nk:, [0, 1, 2, 4]].view(np.uint32), surf.view(np.uint32))
+        got_area = ld(pre + "area.bin", np.float32, 8)
+        np.testing.assert_array_equal(got_area[:, [0, 1, 2, 4]].view(np.uint32), area.view(np.uint32))
+        r_xyz, r_cn, bb, _ = oracle.excavation_grid(got_area, 0.1, 10,
+                                                    oracle.area_normals(got_area, 1.5))
+        cx, cn = ld(pre + "cells.f64", np.float64, 3), ld(pre + "cnrm.f32", np.float32, 3)
+        np.testing.assert_array_equal(cx, r_xyz)
+        np.testing.assert_allclose(cn, r_cn, rtol=0, atol=1e-4)
+        T = oracle.Cloud(terr)
+        poses = ld(pre + "poses.f64", np.float64, 5)
+        r_poses = oracle.generate_candidates(T, bb, oracle.vl_params(), zx)
+        assert poses.shape == r_poses.shape
+        np.testing.assert_array_equal(poses[:, :3], r_poses[:, :3])
+        np.testing.assert_allclose(poses[:, 3:], r_poses[:, 3:], rtol=0, atol=1e-12)
+        flags = np.zeros(cx.shape[0], np.uint8)
+        tot, _, rep = oracle.score_poses(T, oracle.Cloud(filtered[1]), cx, cn, poses, zx,
+                                         oracle.vl_params(), flags)
+        np.testing.assert_allclose(np.fromfile(tmp_path / (pre + "tot.f64"), np.float64), tot,
+                                   rtol=1e-12, atol=0)
+        assert d["best_idx"] == rep.best_idx
+    # scratch grows with 25 % headroom: a few reallocations while the sizes settle, not one
+    # per frame (each frees a buffer: a device synchronization in the frame)
+    assert res["reallocs_after_warmup"] <= 8, res["reallocs_after_warmup"]
 
 
 def test_drivable_area_node(tmp_path, oracle):
