@@ -277,9 +277,13 @@ def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
     the 1M-pt terrain's working set is cache-resident); the HBM-side bytes are the PMC
     `traffic`."""
     st = ctx.raycast_fan_stats(poses, fan)
+    layout = ctx.terrain_info()["scan_layout"]
+    # the fine-window layout's probe reads the 8-byte record (z band + run), the others a 2-byte
+    # z band and then one 8-byte directory entry per scan
+    probe_b = 8.0 if layout == "fine" else 2.0
     rays = poses.shape[0] * fan.n_az * fan.n_el
     waves = poses.shape[0] * ((fan.n_az * fan.n_el + 63) // 64)
-    req = 2.0 * st["samples_visited"] + 8.0 * st["scanned_stencils"] \
+    req = probe_b * st["samples_visited"] + 8.0 * st["scanned_stencils"] \
         + 8.0 * st["directory_loads"] + 12.0 * st["point_tests"] + 16.0 * rays + 8.0 * waves
     ref_model = 64.0 * units_per_launch + 12.0 * st["point_tests"]
     traffic = _traffic_from_profiles("fan")
@@ -290,11 +294,14 @@ def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
         "traffic": traffic,
         "traffic_gbs": _gbs(traffic, avg_kernel_s),
         "traffic_frac": (_gbs(traffic, avg_kernel_s) or 0.0) / HBM_PEAK_GBS if traffic else None,
-        "kernel": "k_raycast_fan<0, 64, true>", "avg_kernel_ms": avg_kernel_s * 1e3,
+        "kernel": ("k_raycast_fan<0, 64, true, 8, 1>" if layout == "fine"
+                   else "k_raycast_fan<0, 64, true, 7, 0>"),
+        "avg_kernel_ms": avg_kernel_s * 1e3, "scan_layout": layout,
         "requested_bytes_per_launch": req,
-        "model": "requested bytes: 2 B/probe + 8 B/candidate + 8 B/directory load + 12 B/point "
-                 "record + 16 B/ray + 8 B/wave (pcp_raycast_fan_stats counts); traffic = PMC "
-                 "FETCH(x2)+WRITE per launch (profiles/pmc_traffic.json)",
+        "model": f"requested bytes: {probe_b:.0f} B/probe + 8 B/candidate (its step) + 8 B/"
+                 "directory load + 12 B/point record + 16 B/ray + 8 B/wave "
+                 "(pcp_raycast_fan_stats counts); traffic = PMC FETCH(x2)+WRITE per launch "
+                 "(profiles/pmc_traffic.json)",
         "limiter": "vector-memory gather path (TA/TD busy, L1 tag lookups per instruction; "
                    "profiles/r02_fan_pmc*.txt), not HBM: the terrain lives in L2/MALL",
         "alg_reference_bytes_per_launch": ref_model,

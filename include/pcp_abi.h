@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PCP_ABI_VERSION 1
+#define PCP_ABI_VERSION 2   /* 2: pcp_index_info.scan_layout */
 
 enum pcp_status {
     PCP_OK = 0,
@@ -343,6 +343,9 @@ typedef struct pcp_index_info {
     double cell;
     int32_t nx, ny, nz;
     double bmin[3], bmax[3];
+    /* the layout the terrain scans walk: 0 per-cell runs, 1 2x2x2 block copy, 2 fine-window
+       copy (the copies are built at the second query after pcp_set_terrain) */
+    int32_t scan_layout;
 } pcp_index_info;
 int pcp_terrain_info(pcp_ctx *ctx, pcp_index_info *info);
 

@@ -274,6 +274,7 @@ int pcp_create(int device, pcp_ctx **out) {
     ctx->device = device;
     if (const char *fb = std::getenv("PCP_FAN_BATCH")) ctx->fan_batch = std::atoi(fb);
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
+    if (const char *tf = std::getenv("PCP_TERRAIN_FINE")) ctx->terrain_fine = std::atoi(tf);
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)

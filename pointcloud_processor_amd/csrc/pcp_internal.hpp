@@ -121,6 +121,14 @@ struct GridView {               // POD passed to kernels by value
     // early exit per scan instead of 4 + 8
     const uint32_t *bstart;
     const float4 *bpts;
+    // fine-window copy (null unless built): xy stencil corners at half the cell
+    // edge, each a window of 3 x 3 fine columns (0.18 m instead of 0.24 m square) whose points
+    // are one run in descending z, wpts.  One record per (fine corner x, y, coarse corner z),
+    // x-fastest, frx x fry x (nz - 1): {run start, z band | count << 16} of the window's points
+    // in coarse z cells iz, iz + 1 -- the march's probe and the scan's directory in one load.
+    const uint2 *frec;
+    const float4 *wpts;
+    uint32_t frx, fry;
 };
 constexpr float kZq = 2.0f / 250.0f;   // z band step, cells (2 cells = 250 steps)
 
@@ -131,11 +139,14 @@ struct GridIndex {
     double c = 0.0;
     int32_t nx = 0, ny = 0, nz = 0;
     double bmin[3] = {0, 0, 0}, bmax[3] = {0, 0, 0};
-    DevBuf pts, start, occ2, occz, bstart, bpts;
+    DevBuf pts, start, occ2, occz, bstart, bpts, frec, wpts;
     bool occz_ok = false;
     bool blk_ok = false;         // block-major copy built (bstart / bpts)
     bool blk_fail = false;       // copy unavailable for this index (size cap or allocation
                                  // failure): the scans keep the per-cell runs, no retry
+    bool fine_ok = false;        // fine-window copy built (frec / wpts)
+    bool fine_fail = false;      // fine copy past its caps / not allocated: no retry
+    uint32_t frx = 0, fry = 0;
     bool occ2_ok = false;        // occ2 built (only indices queried by stencil_any need it)
     GridView view() const;
     void release() {
@@ -145,9 +156,13 @@ struct GridIndex {
         occz.release();
         bstart.release();
         bpts.release();
+        frec.release();
+        wpts.release();
         occz_ok = false;
         blk_ok = false;
         blk_fail = false;
+        fine_ok = false;
+        fine_fail = false;
         occ2_ok = false;
         present = false;
         n_pts = 0;
@@ -214,6 +229,7 @@ struct pcp_ctx {
     int num_cus = 256;                       // multiprocessors of the device
     int fan_batch = 0;                       // fan kernel variant (PCP_FAN_BATCH), A/B only
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
+    int terrain_fine = 1;                    // fine-window layout of that copy (PCP_TERRAIN_FINE)
     int terrain_queries = 0;                 // queries since the last pcp_set_terrain
     // filter/merge scratch
     pcp::DevBuf f_in, f_misc;
@@ -264,6 +280,9 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
                 bool zsort = true, bool occ = true);
 // the block-major copy of a z-sorted index (GridView.bstart / bpts); no-op when built
 int build_blocks(pcp_ctx *ctx, GridIndex &g);
+// the fine-window copy of a z-sorted index (GridView.frec / wpts); no-op when built.  Marks
+// blk_fail (no retry) past its size caps or on an allocation failure.
+int build_fine(pcp_ctx *ctx, GridIndex &g);
 // before a terrain query: build the terrain's block copy per PCP_TERRAIN_BLOCKS (0 never,
 // 1 at the second query after pcp_set_terrain -- a terrain that is queried once, as in the
 // per-frame chain, does not pay for it --, 2 at the first)

@@ -82,6 +82,11 @@ __device__ __forceinline__ uint2 ld_u2o(const uint32_t *base, uint32_t i) {
         reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(base) + (i << 2));
     return make_uint2(p[0], p[1]);
 }
+// one 8-byte record (the fine-window directory: {start, band | count << 16}; build_fine caps
+// the directory below 2^29 records)
+__device__ __forceinline__ uint2 ld_rec(const uint2 *base, uint32_t i) {
+    return *reinterpret_cast<const uint2 *>(reinterpret_cast<const char *>(base) + (i << 3));
+}
 __device__ __forceinline__ uint32_t ld_u16o(const uint16_t *base, uint32_t i) {
     return *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(base) + (i << 1));
 }

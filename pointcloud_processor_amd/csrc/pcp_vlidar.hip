@@ -103,15 +103,14 @@ __device__ __forceinline__ bool scan_stencil(const GridView &g, uint32_t lin, fl
 #ifndef PCP_BLK_STEP
 #define PCP_BLK_STEP 1   // block-walk points per step (build knob)
 #endif
+// a z-descending run pts[k0 .. e): the walk of one block (or one fine window)
 template <bool STATS>
-__device__ __forceinline__ bool scan_block(const GridView &g, uint32_t lin, float qx, float qy,
-                                           float qz, float r2, uint32_t *cnt) {
-    const uint2 se = ld_u2o(g.bstart, lin);
-    const uint32_t e = se.y;
-    for (uint32_t k = se.x; k < e; k += PCP_BLK_STEP) {
+__device__ __forceinline__ bool scan_run(const float4 *pts, uint32_t k0, uint32_t e, float qx,
+                                         float qy, float qz, float r2, uint32_t *cnt) {
+    for (uint32_t k = k0; k < e; k += PCP_BLK_STEP) {
         P3 p[PCP_BLK_STEP];   // independent loads (the tail repeats the last entry)
 #pragma unroll
-        for (int i = 0; i < PCP_BLK_STEP; ++i) p[i] = ld_p3o(g.bpts, min(k + i, e - 1));
+        for (int i = 0; i < PCP_BLK_STEP; ++i) p[i] = ld_p3o(pts, min(k + i, e - 1));
 #pragma unroll
         for (int i = 0; i < PCP_BLK_STEP; ++i) {
             if (i > 0 && k + i >= e) return false;
@@ -122,6 +121,13 @@ __device__ __forceinline__ bool scan_block(const GridView &g, uint32_t lin, floa
         }
     }
     return false;
+}
+
+template <bool STATS>
+__device__ __forceinline__ bool scan_block(const GridView &g, uint32_t lin, float qx, float qy,
+                                           float qz, float r2, uint32_t *cnt) {
+    const uint2 se = ld_u2o(g.bstart, lin);
+    return scan_run<STATS>(g.bpts, se.x, se.y, qx, qy, qz, r2, cnt);
 }
 
 template <bool STATS>
@@ -189,11 +195,21 @@ __device__ __forceinline__ void clip_kf(const GridView &g, double px, double py,
 //    by the same repeated additions the reference performs) and scans the block of its exact
 //    corner, so every point test is the reference's test.
 // STATS counts probes, scanned stencils and point tests into cnt[0..2].
-template <bool STATS, bool ZB = true, int NB = 1>
+//  * FN (the fine-window copy, g.frec): the probe reads the record of the sample's fine corner
+//    -- its window's z band and run -- and a candidate walks that run with the exact q_k.  The
+//    approximate corner's window holds every point within r of q_k (the same margin argument as
+//    the block's), so no exact corner and no directory load are needed.  FN = 2 decides at run
+//    time (g.frec null or not).
+template <bool STATS, bool ZB = true, int NB = 1, int FN = 0>
 __device__ __forceinline__ int march(const GridView &g, double px, double py, double pz,
                                      double dx, double dy, double dz,
                                      const double *__restrict__ steps, int K, double end,
                                      float r2, uint32_t *cnt = nullptr) {
+    if (FN == 2) {
+        if (g.frec)
+            return march<STATS, ZB, NB, 1>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, cnt);
+        return march<STATS, ZB, NB, 0>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, cnt);
+    }
     int klo, khi;
     clip_kf(g, px, py, pz, dx, dy, dz, K, klo, khi);
     if (end < 1e299) {   // s_k < end: k <= (end - 0.5) / 0.3, with one sample of slack
@@ -208,6 +224,38 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
     const float Ay = ((float)py - g.flo_y) * g.finv_c + fdy * h;
     const float Az = ((float)pz - g.flo_z) * g.finv_c + fdz * h;
     const uint32_t nx = (uint32_t)g.nx, ny = (uint32_t)g.ny;
+    if (FN == 1) {
+        const uint32_t rx = g.frx, ry = g.fry;
+        for (int k = klo; k <= khi; ++k) {
+            const float kf = (float)k;
+            const float fx = __builtin_fmaf(Dx, kf, Ax);
+            const float fy = __builtin_fmaf(Dy, kf, Ay);
+            const float fz = __builtin_fmaf(Dz, kf, Az);
+            const bool ok = (fx >= 0.0f) & (fx < g.fnx1) & (fy >= 0.0f) & (fy < g.fny1) &
+                            (fz >= 0.0f) & (fz < g.fnz1);
+            const uint32_t izc = ok ? (uint32_t)fz : 0u;
+            // fine corner = floor(2 fx): 2 fx < 2 (nx - 1) = frx, exact doubling
+            const uint32_t rec =
+                ok ? (uint32_t)(2.0f * fx) + rx * ((uint32_t)(2.0f * fy) + ry * izc) : 0u;
+            const uint2 R = ld_rec(g.frec, rec);
+            const uint32_t zz = ok ? (R.y & 0xFFFFu) : 0x00FFu;
+            const uint32_t lo = zz & 255u, hi = zz >> 8;
+            const float u = fz - (float)izc + g.fzoff;
+            const bool cand = (lo <= hi) & ((hi == 255u) | (u - (float)hi * kZq < g.fzt)) &
+                              ((lo == 0u) | ((float)lo * kZq - u < g.fzt));
+            if (STATS) cnt[0] += 1;
+            if (cand) {
+                const double s = steps[k];
+                if (!(s < end)) return -1;
+                if (STATS) cnt[1] += 1;
+                const float qx = (float)(px + dx * s);
+                const float qy = (float)(py + dy * s);
+                const float qz = (float)(pz + dz * s);
+                if (scan_run<STATS>(g.wpts, R.x, R.x + (R.y >> 16), qx, qy, qz, r2, cnt)) return k;
+            }
+        }
+        return -1;
+    }
     if (NB > 1 && ZB) {
         // latency-bound callers (few rays in flight): NB probes per round as independent loads,
         // then taken in sample order -- the same samples, candidates and scans as below
@@ -332,8 +380,8 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
         visible = march<false, true, PCP_CELL_PROBES>(E.terrain, px, py, pz, ndx, ndy, ndz,
                                                       E.steps, E.K, end, 1e30f) < 0;
 #else
-        visible = march<false, true, PCP_CELL_PROBES>(E.terrain, px, py, pz, ndx, ndy, ndz,
-                                                      E.steps, E.K, end, E.r2_ray) < 0;
+        visible = march<false, true, PCP_CELL_PROBES, 2>(E.terrain, px, py, pz, ndx, ndy, ndz,
+                                                         E.steps, E.K, end, E.r2_ray) < 0;
 #endif
     }
     if (!visible) return 0.0;
@@ -782,7 +830,7 @@ enum { FAN_PLAIN = 0, FAN_STATS = 1, FAN_STAMPS = 2 };
 // termination on near-flat terrain).  Each wave writes its blocked-ray count and its
 // sample-query count to its own slot: the per-pose sums are formed by k_fan_reduce in a fixed
 // order (deterministic, no same-address atomics).
-template <int MODE, int BS, bool ZB = true>
+template <int MODE, int BS, bool ZB = true, int FN = 0>
 __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t rblock) {
     const uint32_t ray = rblock * BS + threadIdx.x;
     const uint32_t wid = ray >> 6;
@@ -807,8 +855,8 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
             asm volatile("" ::"v"(dx), "v"(dy));
             t1 = __builtin_amdgcn_s_memtime();
         }
-        hit = march<MODE == FAN_STATS, ZB>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps, a.K,
-                                           1e300, a.r2, cnt);
+        hit = march<MODE == FAN_STATS, ZB, 1, FN>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps,
+                                                  a.K, 1e300, a.r2, cnt);
     }
     if (MODE == FAN_STAMPS) {
         asm volatile("" ::"v"(hit));
@@ -827,8 +875,9 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
     if (MODE == FAN_STATS) {   // per-wave slots [4][P * waves], summed by k_sum_u64
         const size_t nw = (size_t)gridDim.x * (BS / 64);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {   // [3] directory loads: one per scan here
-            unsigned long long v = cnt[q < 3 ? q : 1];
+        for (int q = 0; q < 4; ++q) {   // [3] directory loads: one per scan (none: FN, the
+                                        // probe's record is the directory)
+            unsigned long long v = q < 3 ? cnt[q] : (FN ? 0u : cnt[1]);
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
             if ((threadIdx.x & 63) == 0 && wid < a.waves) a.stats[q * nw + wslot] = v;
@@ -848,10 +897,10 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
 // the rest of a workgroup), 1-D grid interleaving the poses (block b = ray block b / P of pose
 // b % P: the waves in flight at any time march the same ring of many poses), capped at 7 waves
 // per SIMD (94 SGPRs; the compiler's own choice, 106, admits only 6).
-template <int MODE, int BS = 64, bool ZB = true, int W = 7>
+template <int MODE, int BS = 64, bool ZB = true, int W = 7, int FN = 0>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(W, W)))
 k_raycast_fan(FanArgs a, uint32_t P) {
-    fan_body<MODE, BS, ZB>(a, blockIdx.x % P, blockIdx.x / P);
+    fan_body<MODE, BS, ZB, FN>(a, blockIdx.x % P, blockIdx.x / P);
 }
 
 // A/B: pose-major 2-D grid (blockIdx.y = pose), BS-thread workgroups
@@ -1271,7 +1320,11 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
     a.stats = ctx->stats_d.as<unsigned long long>();
     const dim3 grid1(waves * (uint32_t)P);           // 64-thread blocks, pose-interleaved
     if (stats) {
-        hipLaunchKernelGGL((k_raycast_fan<FAN_STATS>), grid1, dim3(64), 0, st, a, (uint32_t)P);
+        if (a.g.frec)
+            hipLaunchKernelGGL((k_raycast_fan<FAN_STATS, 64, true, 8, 1>), grid1, dim3(64), 0, st,
+                               a, (uint32_t)P);
+        else
+            hipLaunchKernelGGL((k_raycast_fan<FAN_STATS>), grid1, dim3(64), 0, st, a, (uint32_t)P);
         PCP_CHECK_LAUNCH(ctx);
         const size_t nw = (size_t)P * waves;
         hipLaunchKernelGGL(k_sum_u64, dim3(4), dim3(1024), 0, st,
@@ -1279,7 +1332,11 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
         PCP_CHECK_LAUNCH(ctx);
         o.stats_d = a.stats + 4 * nw;
     } else if (stamps) {
-        hipLaunchKernelGGL((k_raycast_fan<FAN_STAMPS>), grid1, dim3(64), 0, st, a, (uint32_t)P);
+        if (a.g.frec)
+            hipLaunchKernelGGL((k_raycast_fan<FAN_STAMPS, 64, true, 8, 1>), grid1, dim3(64), 0, st,
+                               a, (uint32_t)P);
+        else
+            hipLaunchKernelGGL((k_raycast_fan<FAN_STAMPS>), grid1, dim3(64), 0, st, a, (uint32_t)P);
         PCP_CHECK_LAUNCH(ctx);
         o.stats_d = a.stats;
     } else {
@@ -1289,7 +1346,22 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
         switch (ctx->fan_batch) {
         case 1: hipLaunchKernelGGL((k_raycast_fan_pm<128, true>), grid128, dim3(128), 0, st, a); break;
         case 2: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 64, false>), grid1, dim3(64), 0, st, a, (uint32_t)P); break;
-        default: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN>), grid1, dim3(64), 0, st, a, (uint32_t)P); break;
+        case 3:   // A/B: the fine-window kernel at 7 waves per SIMD
+            if (a.g.frec)
+                hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 64, true, 7, 1>), grid1, dim3(64), 0,
+                                   st, a, (uint32_t)P);
+            else
+                hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN>), grid1, dim3(64), 0, st, a,
+                                   (uint32_t)P);
+            break;
+        default:
+            if (a.g.frec)   // the fine-window copy: 33 VGPRs, 8 waves per SIMD
+                hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 64, true, 8, 1>), grid1, dim3(64), 0,
+                                   st, a, (uint32_t)P);
+            else
+                hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN>), grid1, dim3(64), 0, st, a,
+                                   (uint32_t)P);
+            break;
         }
         PCP_CHECK_LAUNCH(ctx);
     }

@@ -47,7 +47,7 @@ def test_binding_covers_the_header():
 
 def test_host_only_entry_points():
     lib = _abi.load_library()
-    assert lib.pcp_abi_version() == 1
+    assert lib.pcp_abi_version() == 2
     s = _abi.step_table(15.0 - 0.08)
     ref, x = [], 0.5
     while x < 14.92:

@@ -743,12 +743,17 @@ def test_drivable_area_matches_oracle(gpu, oracle, kw):
     assert {-1, 0, 100} <= set(np.unique(grid).tolist())
 
 
-@pytest.mark.parametrize("mode", ["0", "2"])
-def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, monkeypatch):
-    """PCP_TERRAIN_BLOCKS=0 scans the per-cell runs, =2 the block-major copy from the first
-    query on (the default, 1, switches at the second query): both bit-exact on the fan and the
-    reference-mode scoring."""
+# (PCP_TERRAIN_BLOCKS, PCP_TERRAIN_FINE) -> the layout the scans walk from the first query
+LAYOUTS = [("0", "1", "cells"), ("2", "0", "blocks"), ("2", "1", "fine")]
+
+
+@pytest.mark.parametrize("mode,fine,layout", LAYOUTS)
+def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, fine, layout, monkeypatch):
+    """PCP_TERRAIN_BLOCKS=0 scans the per-cell runs, =2 the block-major copy (PCP_TERRAIN_FINE=0:
+    2x2x2 blocks, 1: fine windows) from the first query on (the default, 1, switches at the
+    second query): all bit-exact on the fan and the reference-mode scoring."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", mode)
+    monkeypatch.setenv("PCP_TERRAIN_FINE", fine)
     ctx = _abi.Context(0)
     try:
         ctx.set_terrain(scene.terrain, point_step=32)
@@ -759,6 +764,7 @@ def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, monkeypatch):
         poses = ctx.generate_candidates(cells.grid_bbox, params, scene.zx120_pose5)
         fan = _abi.fan_params(n_az=128, n_el=48)
         _, _, fh, _ = ctx.raycast_fan(poses[:5], fan, want_first_hit=True)
+        assert ctx.terrain_info()["scan_layout"] == layout
         _, _, r_fh = oracle.raycast_fan(T, poses[:5], 128, 48, fan.el_min, fan.el_max,
                                         fan.max_distance)
         np.testing.assert_array_equal(fh, r_fh)
@@ -775,11 +781,12 @@ def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("mode", ["0", "2"])
-def test_terrain_block_copy_dense_and_tiny(oracle, mode, monkeypatch):
-    """Block-major copy on awkward terrains: 20 k points packed into a 0.3 m cube (blocks of
+@pytest.mark.parametrize("mode,fine,layout", LAYOUTS)
+def test_terrain_block_copy_dense_and_tiny(oracle, mode, fine, layout, monkeypatch):
+    """Block-major copies on awkward terrains: 20 k points packed into a 0.3 m cube (blocks of
     thousands of points, ties in z) next to a sparse plane, and a one-point terrain."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", mode)
+    monkeypatch.setenv("PCP_TERRAIN_FINE", fine)
     rng = np.random.default_rng(11)
     dense = np.column_stack([rng.uniform(2.0, 2.3, 20_000), rng.uniform(-0.15, 0.15, 20_000),
                              np.round(rng.uniform(0.0, 0.3, 20_000), 2)])
@@ -801,8 +808,33 @@ def test_terrain_block_copy_dense_and_tiny(oracle, mode, monkeypatch):
                 np.testing.assert_array_equal(fh, r_fh)
                 np.testing.assert_array_equal(blocked, r_blocked)
                 np.testing.assert_array_equal(units, r_units)
+                assert ctx.terrain_info()["scan_layout"] == layout
         finally:
             ctx.close()
+
+
+def test_fine_copy_count_overflow_falls_back(oracle, monkeypatch):
+    """A fine window holding more than 65,535 points (its record's 16-bit count) cannot use the
+    fine copy: the terrain falls back to the 2x2x2 block copy, still bit-exact."""
+    monkeypatch.setenv("PCP_TERRAIN_BLOCKS", "2")
+    rng = np.random.default_rng(5)
+    n = 70_000
+    cube = np.column_stack([rng.uniform(1.0, 1.05, n), rng.uniform(0.0, 0.05, n),
+                            rng.uniform(0.0, 0.05, n)])
+    cloud = np.zeros((n, 8), np.float32)
+    cloud[:, :3] = cube
+    poses = np.array([[0.0, 0.0, 0.3, -0.2, 0.0]])
+    fan = _abi.fan_params(n_az=64, n_el=8, el_min_deg=-30.0, el_max_deg=10.0, max_distance=3.0)
+    with _abi.Context(0) as ctx:
+        ctx.set_terrain(cloud, point_step=32)
+        blocked, units, fh, _ = ctx.raycast_fan(poses, fan, want_first_hit=True)
+        assert ctx.terrain_info()["scan_layout"] == "blocks"
+        r_blocked, r_units, r_fh = oracle.raycast_fan(oracle.Cloud(cloud), poses, 64, 8,
+                                                      fan.el_min, fan.el_max, 3.0)
+        np.testing.assert_array_equal(fh, r_fh)
+        np.testing.assert_array_equal(blocked, r_blocked)
+        np.testing.assert_array_equal(units, r_units)
+        assert blocked[0] > 0
 
 
 # ---------------------------------------------------------------------------------- multi-GPU
