@@ -63,7 +63,16 @@ GridView GridIndex::view() const {
     v.wpts = fine_ok ? wpts.as<const float4>() : nullptr;
     v.frx = fine_ok ? frx : 0u;
     v.fry = fine_ok ? fry : 0u;
+    v.frz = fine_ok ? frz : 0u;
+    v.fus_off = (float)(rm * v.inv_c / (double)kZq);
     return v;
+}
+
+float exit_dist(float r2) {
+    float d = std::sqrt(r2);
+    while (d * d < r2) d = std::nextafter(d, INFINITY);
+    for (float p = std::nextafter(d, 0.0f); p * p >= r2; p = std::nextafter(d, 0.0f)) d = p;
+    return d;
 }
 
 __device__ __forceinline__ float ld_f32(const unsigned char *base, uint32_t off) {
@@ -600,14 +609,14 @@ __device__ __forceinline__ int cell_z(const CellMap &m, float z) {
     return min(max(iz, 0), m.nz - 1);
 }
 
-// points per window (sum of its 9 fine columns)
+// entries per window: its 9 fine columns' points + one sentinel that ends every walk
 __global__ void __launch_bounds__(kThreads)
 k_fwin_size(const uint32_t *__restrict__ fstart, uint32_t fnx, uint32_t rx, uint32_t ry,
             uint32_t *__restrict__ wsize) {
     const uint32_t w = blockIdx.x * kThreads + threadIdx.x;
     if (w >= rx * ry) return;
     const uint32_t wx = w % rx, wy = w / rx;
-    uint32_t n = 0;
+    uint32_t n = 1;
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
         const uint32_t row = wx + fnx * (wy + b);
@@ -672,29 +681,37 @@ k_fwin_fill(const float4 *__restrict__ fp, uint64_t n, const uint32_t *__restric
 }
 
 // records of one window, one thread per window: for coarse z corner iz, the window's points in
-// coarse z cells iz, iz + 1 are the sub-run [first with cz <= iz + 1, first with cz < iz) of
-// the z-descending run (cz is non-increasing along it); z band as k_occz's.
+// coarse z cells iz, iz + 1 start at the first point with cz <= iz + 1 of the z-descending run
+// (cz is non-increasing along it).  No end is stored: the walk stops at the first point lying r
+// below q -- at the latest the first point below cell iz, which lies more than r + m below q
+// -- or at the window's sentinel (x, y NaN: never within r; z -inf: always r below).  The z band
+// is stored as probe thresholds in steps of kZq cells above the block floor: lo - T, hi + T with
+// T = ceil((r + 2 mm) / c / kZq) folded in (0 / 255 unbounded; empty: lo 255, hi 0), so the probe
+// is two compares.
 __global__ void __launch_bounds__(kThreads)
-k_frec(const float4 *__restrict__ wpts, const uint32_t *__restrict__ wstart, CellMap m, double c,
-       uint32_t rx, uint32_t ry, uint32_t rz, uint2 *__restrict__ frec,
-       uint32_t *__restrict__ overflow) {
+k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ wstart, CellMap m, double c,
+       uint32_t rx, uint32_t ry, uint32_t rz, uint32_t tsteps, uint2 *__restrict__ frec) {
     const uint32_t w = blockIdx.x * kThreads + threadIdx.x;
     if (w >= rx * ry) return;
-    const uint32_t s = wstart[w], e = wstart[w + 1];
+    const uint32_t s = wstart[w], e = wstart[w + 1] - 1;   // e: the sentinel
+    wpts[e] = make_float4(__int_as_float(0x7FC00000), __int_as_float(0x7FC00000), -INFINITY,
+                          __uint_as_float(0xFFFFFFFFu));
     const size_t plane = (size_t)rx * ry;
     uint32_t jt = s, jb = s;
-    bool big = false;
     for (int iz = (int)rz - 1; iz >= 0; --iz) {
         while (jt < e && cell_z(m, wpts[jt].z) > iz + 1) ++jt;
         if (jb < jt) jb = jt;
         while (jb < e && cell_z(m, wpts[jb].z) >= iz) ++jb;
-        const uint32_t n = jb - jt;
-        uint32_t band = 0x00FFu;
-        if (n) band = zband_code(wpts[jt].z, wpts[jb - 1].z, m.oz + (double)iz * c, c);
-        big |= n > 0xFFFFu;
-        frec[(size_t)iz * plane + w] = make_uint2(jt, band | (min(n, 0xFFFFu) << 16));
+        uint32_t band = 0x00FFu;   // empty
+        if (jb > jt) {
+            const uint32_t code = zband_code(wpts[jt].z, wpts[jb - 1].z, m.oz + (double)iz * c, c);
+            const uint32_t lo = code & 255u, hi = code >> 8;
+            const uint32_t lo2 = (lo == 0u || lo <= tsteps) ? 0u : lo - tsteps;
+            const uint32_t hi2 = (hi == 255u) ? 255u : min(hi + tsteps, 255u);
+            band = lo2 | (hi2 << 8);
+        }
+        frec[(size_t)iz * plane + w] = make_uint2(jt, band);
     }
-    if (big) atomicOr(overflow, 1u);
 }
 
 int build_fine(pcp_ctx *ctx, GridIndex &g) {
@@ -708,7 +725,8 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     const uint64_t fc = fnx * fny, nw = rx * ry;
     // the records are addressed with 32-bit byte offsets (ld_rec), the runs with 32-bit
     // indices; past either cap the scans keep the per-cell runs
-    if (rz == 0 || nw * rz >= (1ull << 29) || fc >= (1ull << 30)) {
+    if (rz == 0 || nw * rz >= (1ull << 29) || fc >= (1ull << 30) || rx >= (1ull << 24) ||
+        ry * rz >= (1ull << 24)) {   // (the probe's 24-bit multiplies)
         g.fine_fail = true;
         return PCP_OK;
     }
@@ -718,7 +736,7 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     // 1. fine columns: count -> prefix -> scatter -> descending z per column
     PCP_HIP(ctx, ctx->scratch[2].ensure(n * sizeof(uint32_t)));
     PCP_HIP(ctx, ctx->scratch[3].ensure((fc + 1) * sizeof(uint32_t)));
-    PCP_HIP(ctx, ctx->scratch[6].ensure((fc + 1 + 2 * nw + 1 + 64) * sizeof(uint32_t)));
+    PCP_HIP(ctx, ctx->scratch[6].ensure((fc + 1 + 2 * nw + 1) * sizeof(uint32_t)));
     PCP_HIP(ctx, ctx->scratch[4].ensure(scan_tmp_bytes(std::max(fc, nw)) +
                                         (std::max(fc, nw) + 1) * sizeof(uint32_t)));
     PCP_HIP(ctx, ctx->scratch[5].ensure(n * sizeof(float4)));
@@ -727,9 +745,7 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     uint32_t *fstart = ctx->scratch[6].as<uint32_t>();
     uint32_t *wsize = fstart + fc + 1;
     uint32_t *wstart = wsize + nw;
-    uint32_t *ovf = wstart + nw + 1;
     PCP_HIP(ctx, hipMemsetAsync(cnt, 0, (fc + 1) * sizeof(uint32_t), st));
-    PCP_HIP(ctx, hipMemsetAsync(ovf, 0, sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_cell_count, dim3(gridn), dim3(kThreads), 0, st, g.pts.as<const float4>(),
                        n, fm, ctx->scratch[2].as<uint32_t>(), cnt);
     PCP_CHECK_LAUNCH(ctx);
@@ -769,18 +785,16 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
                        (const uint32_t *)fstart, fm, (uint32_t)rx, (uint32_t)ry,
                        (const uint32_t *)wstart, g.wpts.as<float4>());
     PCP_CHECK_LAUNCH(ctx);
-    hipLaunchKernelGGL(k_frec, dim3(gridw), dim3(kThreads), 0, st, g.wpts.as<const float4>(),
+    // the probe's z band slack T in kZq steps: (r + 2 mm) / c, rounded up (the coarse probe's
+    // fzt)
+    const uint32_t tsteps = (uint32_t)std::ceil((g.r_q + 2e-3) / g.c / (double)kZq);
+    hipLaunchKernelGGL(k_frec, dim3(gridw), dim3(kThreads), 0, st, g.wpts.as<float4>(),
                        (const uint32_t *)wstart, m, g.c, (uint32_t)rx, (uint32_t)ry, (uint32_t)rz,
-                       g.frec.as<uint2>(), ovf);
+                       tsteps, g.frec.as<uint2>());
     PCP_CHECK_LAUNCH(ctx);
-    uint32_t big = 0;
-    if ((rc = read_small(ctx, &big, ovf, 4, st))) return rc;
-    if (big) {   // a record's count does not fit its 16 bits
-        g.fine_fail = true;
-        return PCP_OK;
-    }
     g.frx = (uint32_t)rx;
     g.fry = (uint32_t)ry;
+    g.frz = (uint32_t)rz;
     g.fine_ok = true;
     return PCP_OK;
 }

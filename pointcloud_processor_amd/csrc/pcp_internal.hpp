@@ -123,12 +123,15 @@ struct GridView {               // POD passed to kernels by value
     const float4 *bpts;
     // fine-window copy (null unless built): xy stencil corners at half the cell
     // edge, each a window of 3 x 3 fine columns (0.18 m instead of 0.24 m square) whose points
-    // are one run in descending z, wpts.  One record per (fine corner x, y, coarse corner z),
-    // x-fastest, frx x fry x (nz - 1): {run start, z band | count << 16} of the window's points
-    // in coarse z cells iz, iz + 1 -- the march's probe and the scan's directory in one load.
+    // are one run in descending z ended by a sentinel, wpts.  One record per (fine corner x, y,
+    // coarse corner z), x-fastest, frx x fry x frz (frz = nz - 1): {walk start, probe
+    // thresholds lo | hi << 8} for the window's points in coarse z cells iz, iz + 1 -- the
+    // march's probe and the scan's directory in one load.  fus_off = fzoff / kZq: the probe's
+    // sample height above the block floor in kZq steps is frac(fz) / kZq + fus_off.
     const uint2 *frec;
     const float4 *wpts;
-    uint32_t frx, fry;
+    uint32_t frx, fry, frz;
+    float fus_off;
 };
 constexpr float kZq = 2.0f / 250.0f;   // z band step, cells (2 cells = 250 steps)
 
@@ -146,7 +149,7 @@ struct GridIndex {
                                  // failure): the scans keep the per-cell runs, no retry
     bool fine_ok = false;        // fine-window copy built (frec / wpts)
     bool fine_fail = false;      // fine copy past its caps / not allocated: no retry
-    uint32_t frx = 0, fry = 0;
+    uint32_t frx = 0, fry = 0, frz = 0;
     bool occ2_ok = false;        // occ2 built (only indices queried by stencil_any need it)
     GridView view() const;
     void release() {
@@ -338,6 +341,11 @@ int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what);
 // a small (<= 4 KB) device -> host readback through pinned memory; synchronizes the stream
 // (a pageable destination costs a staging copy per call)
 int read_small(pcp_ctx *ctx, void *dst, const void *src_d, size_t bytes, hipStream_t st);
+
+// the smallest float d with fl(d * d) >= r2: a point with dz = qz - pz >= d fails FLANN's
+// float test (its sum is >= fl(dz^2) >= r2), and so does every lower point of a z-descending
+// run -- the walks' early exit as one compare
+float exit_dist(float r2);
 
 // fan tables (shared definition with the oracle's orc_fan_tables)
 void fan_tables(int32_t n_az, int32_t n_el, double el_min, double el_max, double *ca,

@@ -813,9 +813,9 @@ def test_terrain_block_copy_dense_and_tiny(oracle, mode, fine, layout, monkeypat
             ctx.close()
 
 
-def test_fine_copy_count_overflow_falls_back(oracle, monkeypatch):
-    """A fine window holding more than 65,535 points (its record's 16-bit count) cannot use the
-    fine copy: the terrain falls back to the 2x2x2 block copy, still bit-exact."""
+def test_fine_copy_dense_window(oracle, monkeypatch):
+    """70,000 points in a 5 cm cube: fine windows of 70 k points (the walks end at the first
+    point r below or at the window's sentinel, no stored count), bit-exact."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", "2")
     rng = np.random.default_rng(5)
     n = 70_000
@@ -828,7 +828,7 @@ def test_fine_copy_count_overflow_falls_back(oracle, monkeypatch):
     with _abi.Context(0) as ctx:
         ctx.set_terrain(cloud, point_step=32)
         blocked, units, fh, _ = ctx.raycast_fan(poses, fan, want_first_hit=True)
-        assert ctx.terrain_info()["scan_layout"] == "blocks"
+        assert ctx.terrain_info()["scan_layout"] == "fine"
         r_blocked, r_units, r_fh = oracle.raycast_fan(oracle.Cloud(cloud), poses, 64, 8,
                                                       fan.el_min, fan.el_max, 3.0)
         np.testing.assert_array_equal(fh, r_fh)
