@@ -295,6 +295,13 @@ int pcp_raycast_fan(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fa
 int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
                           const pcp_fan_params *fan, uint64_t stats[4]);
 
+/* Kernel timing for the roofline: the production fan kernel of this query, `reps` launches
+ * back-to-back between two stream events (after the query's own setup); *ms_per_launch = the
+ * interval / reps.  The queue does not idle inside the interval, so the figure agrees with a
+ * rocprofv3 kernel trace (a synchronous query's own events also hold the queue wake-up). */
+int pcp_raycast_fan_burst(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                          const pcp_fan_params *fan, int reps, double *ms_per_launch);
+
 /* Diagnostic build with s_memtime stamps (shader clock) per wave: stamps[(p*W + w)*4 + i],
  * W = ceil(n_az*n_el/64), i = 0 start, 1 after direction setup, 2 after the march, 3 end.
  * For locating where wave lifetime goes; never used for timing. */

@@ -132,6 +132,8 @@ _SIGS = [
                                   C.POINTER(C.c_int64)]),
     ("pcp_raycast_fan_stats", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P]),
     ("pcp_raycast_fan_stamps", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P]),
+    ("pcp_raycast_fan_burst", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), C.c_int,
+                                        C.POINTER(C.c_double)]),
     ("pcp_step_table", C.c_int, [C.c_double, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pcp_terrain_info", C.c_int, [_P, C.POINTER(IndexInfo)]),
     ("pcp_multi_create", C.c_int, [C.c_int, _P, C.POINTER(_P)]),
@@ -640,6 +642,18 @@ def _fan_stamps(self, poses5, fan):
 
 
 Context.raycast_fan_stamps = _fan_stamps
+
+
+def _fan_burst(self, poses5, fan, reps=20):
+    """Average launch time (ms) of the production fan kernel over `reps` back-to-back launches."""
+    poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+    ms = C.c_double()
+    self._check(self.lib.pcp_raycast_fan_burst(self.h, _ptr(poses), poses.shape[0], C.byref(fan),
+                                               reps, C.byref(ms)), "pcp_raycast_fan_burst")
+    return ms.value
+
+
+Context.raycast_fan_burst = _fan_burst
 
 
 def step_table(end: float) -> np.ndarray:

@@ -113,6 +113,17 @@ ProfScope::~ProfScope() {
     ctx->pending.push_back({kid, a, b});
 }
 
+KernelTimer::KernelTimer(pcp_ctx *c, int k) : ctx(c), kid(k) {
+    if (!ctx->prof || kid < 0 || ctx->capturing) return;
+    a = take_event(ctx);
+    b = take_event(ctx);
+    if (!a || !b) a = b = nullptr;
+}
+
+KernelTimer::~KernelTimer() {
+    if (a && b) ctx->pending.push_back({kid, a, b});
+}
+
 void prof_resolve(pcp_ctx *ctx) {
     for (auto &pe : ctx->pending) {
         float ms = 0.f;
@@ -275,6 +286,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *fb = std::getenv("PCP_FAN_BATCH")) ctx->fan_batch = std::atoi(fb);
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
     if (const char *tf = std::getenv("PCP_TERRAIN_FINE")) ctx->terrain_fine = std::atoi(tf);
+    if (const char *tt = std::getenv("PCP_FINE_TILE")) ctx->fine_tile = std::atoi(tt);
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
         cus > 0)

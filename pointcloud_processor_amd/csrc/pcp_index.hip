@@ -11,6 +11,7 @@
 #include <cstring>
 
 #include "pcp_internal.hpp"
+#include "pcp_grid.hpp"
 
 namespace pcp {
 
@@ -64,6 +65,8 @@ GridView GridIndex::view() const {
     v.frx = fine_ok ? frx : 0u;
     v.fry = fine_ok ? fry : 0u;
     v.frz = fine_ok ? frz : 0u;
+    v.ffine = fine_ok ? ffine : 0.0f;
+    v.ftile = fine_ok ? ftile : 0;
     v.fus_off = (float)(rm * v.inv_c / (double)kZq);
     return v;
 }
@@ -172,22 +175,6 @@ k_bbox_final(const float *__restrict__ part, const uint32_t *__restrict__ part_n
     *out_n = sc[0];
 }
 
-struct CellMap {
-    double ox, oy, oz, inv_c;
-    int32_t nx, ny, nz;
-};
-
-__device__ __forceinline__ uint32_t cell_of(const CellMap &m, float x, float y, float z) {
-    int ix = (int)floor(((double)x - m.ox) * m.inv_c);
-    int iy = (int)floor(((double)y - m.oy) * m.inv_c);
-    int iz = (int)floor(((double)z - m.oz) * m.inv_c);
-    // points lie in [1, n-2] by construction; clamp defensively
-    ix = min(max(ix, 0), m.nx - 1);
-    iy = min(max(iy, 0), m.ny - 1);
-    iz = min(max(iz, 0), m.nz - 1);
-    return (uint32_t)ix + (uint32_t)m.nx * ((uint32_t)iy + (uint32_t)m.ny * (uint32_t)iz);
-}
-
 // the active lanes of the wave holding the same 32-bit key as this lane.  Big cells (the 1.5 m
 // normal index is a 3 m grid) put many points of a wave into one cell, where per-lane atomics on
 // one counter serialize; one atomic per group of equal keys avoids that.
@@ -258,16 +245,6 @@ k_cell_rank_z(const float4 *__restrict__ in, uint64_t n, CellMap m,
         rank += (q.z > p.z || (q.z == p.z && __float_as_uint(q.w) < ok)) ? 1u : 0u;
     }
     out[s + rank] = p;
-}
-
-// u16 z band lo | hi << 8 of points with z in [zmin, zmax] above a block floor zb (cell edge c)
-__device__ __forceinline__ uint32_t zband_code(float zmax, float zmin, double zb, double c) {
-    const double step = (double)kZq * c;
-    const double h = ceil(((double)zmax - zb) / step) + 1.0;
-    const double l = floor(((double)zmin - zb) / step) - 1.0;
-    const uint32_t hi = h >= 255.0 ? 255u : (uint32_t)fmax(h, 1.0);
-    const uint32_t lo = l <= 0.0 ? 0u : (uint32_t)fmin(l, 254.0);
-    return lo | (hi << 8);
 }
 
 // z band per stencil corner (z-sorted cells: a cell's first point is its highest, its last
@@ -592,210 +569,6 @@ int build_blocks(pcp_ctx *ctx, GridIndex &g) {
                        g.bstart.as<const uint32_t>(), g.bpts.as<float4>());
     PCP_CHECK_LAUNCH(ctx);
     g.blk_ok = true;
-    return PCP_OK;
-}
-
-// ---------------------------------------------------------------------------------------
-// fine-window copy: fine columns at half the cell edge c_f = c / 2 >= r + m in
-// x and y (all z); the window of fine corner (wx, wy) = fine columns wx .. wx + 2, wy .. wy + 2
-// (3 c_f = 0.18 m for the ray radius, against the 2 c = 0.24 m of the 2x2x2 block: 56 % of the
-// area, so 56 % of the points a scan walks on a surface).  q - r - m in fine column wx puts
-// [q - r, q + r] inside the window with m of slack below and 2 c_f - 2 r - m above.
-// ---------------------------------------------------------------------------------------
-
-// a point's coarse z cell (cell_of's z)
-__device__ __forceinline__ int cell_z(const CellMap &m, float z) {
-    const int iz = (int)floor(((double)z - m.oz) * m.inv_c);
-    return min(max(iz, 0), m.nz - 1);
-}
-
-// entries per window: its 9 fine columns' points + one sentinel that ends every walk
-__global__ void __launch_bounds__(kThreads)
-k_fwin_size(const uint32_t *__restrict__ fstart, uint32_t fnx, uint32_t rx, uint32_t ry,
-            uint32_t *__restrict__ wsize) {
-    const uint32_t w = blockIdx.x * kThreads + threadIdx.x;
-    if (w >= rx * ry) return;
-    const uint32_t wx = w % rx, wy = w / rx;
-    uint32_t n = 1;
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-        const uint32_t row = wx + fnx * (wy + b);
-        n += fstart[row + 3] - fstart[row];   // 3 adjacent columns are one range
-    }
-    wsize[w] = n;
-}
-
-// points of fine column run [s, e) (descending z, ties by index) ahead of p
-__device__ __forceinline__ uint32_t rank_in_run(const float4 *__restrict__ fp, uint32_t s,
-                                                uint32_t e, float pz, uint32_t pi) {
-    uint32_t lo = s, hi = e;   // first j with !zbefore(fp[j], p)
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const float4 q = fp[mid];
-        if (zbefore(q.z, __float_as_uint(q.w), pz, pi)) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo - s;
-}
-
-// window fill, one thread per point p of fine column C (columns z-sorted): p's place in window
-// W = sum over W's 9 columns of its rank there; the 25 columns around C cover the 9 windows
-// holding C.
-__global__ void __launch_bounds__(kThreads)
-k_fwin_fill(const float4 *__restrict__ fp, uint64_t n, const uint32_t *__restrict__ fstart,
-            CellMap fm, uint32_t rx, uint32_t ry, const uint32_t *__restrict__ wstart,
-            float4 *__restrict__ wpts) {
-    const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (k >= n) return;
-    const float4 p = fp[k];
-    const uint32_t pi = __float_as_uint(p.w);
-    const uint32_t c = cell_of(fm, p.x, p.y, p.z);   // fm.nz == 1: the fine column
-    const int fnx = fm.nx, fny = fm.ny;
-    const int fx = (int)(c % (uint32_t)fnx), fy = (int)(c / (uint32_t)fnx);
-    uint32_t rk[25];   // rank in column (fx + dx, fy + dy), index (dy + 2) * 5 + (dx + 2)
-#pragma unroll
-    for (int t = 0; t < 25; ++t) {
-        const int dx = t % 5 - 2, dy = t / 5 - 2;
-        uint32_t r = 0;
-        if (dx == 0 && dy == 0) {
-            r = (uint32_t)k - fstart[c];
-        } else if (fx + dx >= 0 && fx + dx < fnx && fy + dy >= 0 && fy + dy < fny) {
-            const uint32_t d = (uint32_t)(fx + dx + fnx * (fy + dy));
-            r = rank_in_run(fp, fstart[d], fstart[d + 1], p.z, pi);
-        }
-        rk[t] = r;
-    }
-#pragma unroll
-    for (int a = 0; a < 9; ++a) {   // window (fx - ax, fy - ay)
-        const int ax = a % 3, ay = a / 3;
-        const int wx = fx - ax, wy = fy - ay;
-        if (wx < 0 || wy < 0 || wx >= (int)rx || wy >= (int)ry) continue;
-        uint32_t pos = 0;
-#pragma unroll
-        for (int b = 0; b < 9; ++b) {   // the window's columns (wx + bx, wy + by) = C + (b - a)
-            const int dx = b % 3 - ax, dy = b / 3 - ay;
-            pos += rk[(dy + 2) * 5 + (dx + 2)];
-        }
-        wpts[wstart[(uint32_t)wx + rx * (uint32_t)wy] + pos] = p;
-    }
-}
-
-// records of one window, one thread per window: for coarse z corner iz, the window's points in
-// coarse z cells iz, iz + 1 start at the first point with cz <= iz + 1 of the z-descending run
-// (cz is non-increasing along it).  No end is stored: the walk stops at the first point lying r
-// below q -- at the latest the first point below cell iz, which lies more than r + m below q
-// -- or at the window's sentinel (x, y NaN: never within r; z -inf: always r below).  The z band
-// is stored as probe thresholds in steps of kZq cells above the block floor: lo - T, hi + T with
-// T = ceil((r + 2 mm) / c / kZq) folded in (0 / 255 unbounded; empty: lo 255, hi 0), so the probe
-// is two compares.
-__global__ void __launch_bounds__(kThreads)
-k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ wstart, CellMap m, double c,
-       uint32_t rx, uint32_t ry, uint32_t rz, uint32_t tsteps, uint2 *__restrict__ frec) {
-    const uint32_t w = blockIdx.x * kThreads + threadIdx.x;
-    if (w >= rx * ry) return;
-    const uint32_t s = wstart[w], e = wstart[w + 1] - 1;   // e: the sentinel
-    wpts[e] = make_float4(__int_as_float(0x7FC00000), __int_as_float(0x7FC00000), -INFINITY,
-                          __uint_as_float(0xFFFFFFFFu));
-    const size_t plane = (size_t)rx * ry;
-    uint32_t jt = s, jb = s;
-    for (int iz = (int)rz - 1; iz >= 0; --iz) {
-        while (jt < e && cell_z(m, wpts[jt].z) > iz + 1) ++jt;
-        if (jb < jt) jb = jt;
-        while (jb < e && cell_z(m, wpts[jb].z) >= iz) ++jb;
-        uint32_t band = 0x00FFu;   // empty
-        if (jb > jt) {
-            const uint32_t code = zband_code(wpts[jt].z, wpts[jb - 1].z, m.oz + (double)iz * c, c);
-            const uint32_t lo = code & 255u, hi = code >> 8;
-            const uint32_t lo2 = (lo == 0u || lo <= tsteps) ? 0u : lo - tsteps;
-            const uint32_t hi2 = (hi == 255u) ? 255u : min(hi + tsteps, 255u);
-            band = lo2 | (hi2 << 8);
-        }
-        frec[(size_t)iz * plane + w] = make_uint2(jt, band);
-    }
-}
-
-int build_fine(pcp_ctx *ctx, GridIndex &g) {
-    if (g.fine_ok || g.fine_fail || !g.present || !g.occz_ok || g.n_pts == 0) return PCP_OK;
-    hipStream_t st = ctx->stream;
-    ProfScope prof(ctx, PCP_K_INDEX_BUILD);
-    const GridView gv = g.view();
-    const CellMap m{gv.ox, gv.oy, gv.oz, gv.inv_c, g.nx, g.ny, g.nz};
-    const uint64_t fnx = 2 * (uint64_t)g.nx, fny = 2 * (uint64_t)g.ny;
-    const uint64_t rx = fnx - 2, ry = fny - 2, rz = (uint64_t)(g.nz > 1 ? g.nz - 1 : 0);
-    const uint64_t fc = fnx * fny, nw = rx * ry;
-    // the records are addressed with 32-bit byte offsets (ld_rec), the runs with 32-bit
-    // indices; past either cap the scans keep the per-cell runs
-    if (rz == 0 || nw * rz >= (1ull << 29) || fc >= (1ull << 30) || rx >= (1ull << 24) ||
-        ry * rz >= (1ull << 24)) {   // (the probe's 24-bit multiplies)
-        g.fine_fail = true;
-        return PCP_OK;
-    }
-    const CellMap fm{gv.ox, gv.oy, gv.oz, 2.0 * gv.inv_c, (int32_t)fnx, (int32_t)fny, 1};
-    const uint64_t n = g.n_pts;
-    const unsigned gridn = (unsigned)((n + kThreads - 1) / kThreads);
-    // 1. fine columns: count -> prefix -> scatter -> descending z per column
-    PCP_HIP(ctx, ctx->scratch[2].ensure(n * sizeof(uint32_t)));
-    PCP_HIP(ctx, ctx->scratch[3].ensure((fc + 1) * sizeof(uint32_t)));
-    PCP_HIP(ctx, ctx->scratch[6].ensure((fc + 1 + 2 * nw + 1) * sizeof(uint32_t)));
-    PCP_HIP(ctx, ctx->scratch[4].ensure(scan_tmp_bytes(std::max(fc, nw)) +
-                                        (std::max(fc, nw) + 1) * sizeof(uint32_t)));
-    PCP_HIP(ctx, ctx->scratch[5].ensure(n * sizeof(float4)));
-    PCP_HIP(ctx, ctx->scratch[7].ensure(n * sizeof(float4)));
-    uint32_t *cnt = ctx->scratch[3].as<uint32_t>();
-    uint32_t *fstart = ctx->scratch[6].as<uint32_t>();
-    uint32_t *wsize = fstart + fc + 1;
-    uint32_t *wstart = wsize + nw;
-    PCP_HIP(ctx, hipMemsetAsync(cnt, 0, (fc + 1) * sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_cell_count, dim3(gridn), dim3(kThreads), 0, st, g.pts.as<const float4>(),
-                       n, fm, ctx->scratch[2].as<uint32_t>(), cnt);
-    PCP_CHECK_LAUNCH(ctx);
-    int rc = exclusive_scan_u32(ctx, cnt, fstart, fc, ctx->scratch[4].p);
-    if (rc) return rc;
-    PCP_HIP(ctx, hipMemcpyAsync(cnt, fstart, fc * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-    float4 *scat = ctx->scratch[5].as<float4>(), *fp = ctx->scratch[7].as<float4>();
-    hipLaunchKernelGGL(k_cell_scatter, dim3(gridn), dim3(kThreads), 0, st, g.pts.as<const float4>(),
-                       n, ctx->scratch[2].as<const uint32_t>(), cnt, scat);
-    PCP_CHECK_LAUNCH(ctx);
-    hipLaunchKernelGGL(k_cell_rank_z, dim3(gridn), dim3(kThreads), 0, st, (const float4 *)scat, n,
-                       fm, (const uint32_t *)fstart, fp);
-    PCP_CHECK_LAUNCH(ctx);
-    // 2. windows: sizes -> prefix
-    const unsigned gridw = (unsigned)((nw + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(k_fwin_size, dim3(gridw), dim3(kThreads), 0, st, (const uint32_t *)fstart,
-                       (uint32_t)fnx, (uint32_t)rx, (uint32_t)ry, wsize);
-    PCP_CHECK_LAUNCH(ctx);
-    if ((rc = exclusive_scan_u32(ctx, wsize, wstart, nw, ctx->scratch[4].p))) return rc;
-    uint32_t tot = 0;
-    if ((rc = read_small(ctx, &tot, wstart + nw, 4, st))) return rc;
-    if (tot == 0 || tot >= (1u << 28)) {
-        g.fine_fail = true;
-        return PCP_OK;
-    }
-    // the copy is an optional speed-up: an allocation failure keeps the per-cell runs
-    if (g.wpts.ensure((size_t)tot * sizeof(float4)) != hipSuccess ||
-        g.frec.ensure((size_t)nw * rz * sizeof(uint2)) != hipSuccess) {
-        (void)hipGetLastError();
-        g.wpts.release();
-        g.frec.release();
-        g.fine_fail = true;
-        return PCP_OK;
-    }
-    // 3. fill, records
-    hipLaunchKernelGGL(k_fwin_fill, dim3(gridn), dim3(kThreads), 0, st, (const float4 *)fp, n,
-                       (const uint32_t *)fstart, fm, (uint32_t)rx, (uint32_t)ry,
-                       (const uint32_t *)wstart, g.wpts.as<float4>());
-    PCP_CHECK_LAUNCH(ctx);
-    // the probe's z band slack T in kZq steps: (r + 2 mm) / c, rounded up (the coarse probe's
-    // fzt)
-    const uint32_t tsteps = (uint32_t)std::ceil((g.r_q + 2e-3) / g.c / (double)kZq);
-    hipLaunchKernelGGL(k_frec, dim3(gridw), dim3(kThreads), 0, st, g.wpts.as<float4>(),
-                       (const uint32_t *)wstart, m, g.c, (uint32_t)rx, (uint32_t)ry, (uint32_t)rz,
-                       tsteps, g.frec.as<uint2>());
-    PCP_CHECK_LAUNCH(ctx);
-    g.frx = (uint32_t)rx;
-    g.fry = (uint32_t)ry;
-    g.frz = (uint32_t)rz;
-    g.fine_ok = true;
     return PCP_OK;
 }
 

@@ -121,17 +121,18 @@ struct GridView {               // POD passed to kernels by value
     // early exit per scan instead of 4 + 8
     const uint32_t *bstart;
     const float4 *bpts;
-    // fine-window copy (null unless built): xy stencil corners at half the cell
-    // edge, each a window of 3 x 3 fine columns (0.18 m instead of 0.24 m square) whose points
-    // are one run in descending z ended by a sentinel, wpts.  One record per (fine corner x, y,
-    // coarse corner z), x-fastest, frx x fry x frz (frz = nz - 1): {walk start, probe
+    // fine-window copy (null unless built, pcp_fine.hip): fine cells of c / F
+    // in x, y (F = ffine); the window of fine cell W = the points within r + m (xy) of W's
+    // rectangle, one run in descending z ended by a sentinel, wpts.  One record per (fine cell
+    // x, y, coarse corner z), x-fastest, frx x fry x frz (frz = nz - 1): {walk start, probe
     // thresholds lo | hi << 8} for the window's points in coarse z cells iz, iz + 1 -- the
     // march's probe and the scan's directory in one load.  fus_off = fzoff / kZq: the probe's
     // sample height above the block floor in kZq steps is frac(fz) / kZq + fus_off.
     const uint2 *frec;
     const float4 *wpts;
     uint32_t frx, fry, frz;
-    float fus_off;
+    float fus_off, ffine;
+    int32_t ftile;              // records in 4 x 4 xy tiles (PCP_FINE_TILE)
 };
 constexpr float kZq = 2.0f / 250.0f;   // z band step, cells (2 cells = 250 steps)
 
@@ -150,6 +151,8 @@ struct GridIndex {
     bool fine_ok = false;        // fine-window copy built (frec / wpts)
     bool fine_fail = false;      // fine copy past its caps / not allocated: no retry
     uint32_t frx = 0, fry = 0, frz = 0;
+    float ffine = 0.0f;
+    int32_t ftile = 0;
     bool occ2_ok = false;        // occ2 built (only indices queried by stencil_any need it)
     GridView view() const;
     void release() {
@@ -232,7 +235,9 @@ struct pcp_ctx {
     int num_cus = 256;                       // multiprocessors of the device
     int fan_batch = 0;                       // fan kernel variant (PCP_FAN_BATCH), A/B only
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
-    int terrain_fine = 1;                    // fine-window layout of that copy (PCP_TERRAIN_FINE)
+    int fine_tile = 1;                       // fine records in 4 x 4 tiles (PCP_FINE_TILE)
+    int terrain_fine = 2;                    // fine-window layout of that copy, cells of c / F
+                                             // (PCP_TERRAIN_FINE = F; 0: the 2x2x2 blocks)
     int terrain_queries = 0;                 // queries since the last pcp_set_terrain
     // filter/merge scratch
     pcp::DevBuf f_in, f_misc;
@@ -275,6 +280,17 @@ struct ProfScope {
 };
 void prof_resolve(pcp_ctx *ctx);   // after a stream sync
 
+// profiling of ONE kernel through the events hipExtLaunchKernelGGL records around its own
+// execution: unlike stream-ordered events on an idle queue, the interval excludes the host's
+// submission gap before the launch (pass .a / .b to the launch; null when not profiling)
+struct KernelTimer {
+    pcp_ctx *ctx;
+    int kid;
+    hipEvent_t a = nullptr, b = nullptr;
+    KernelTimer(pcp_ctx *c, int k);
+    ~KernelTimer();
+};
+
 // index ----------------------------------------------------------------------------------
 // zsort: points of each cell in descending z (needed by scan_stencil's early exit: the
 // terrain and aux indices); the other indices' queries are order-free
@@ -306,8 +322,11 @@ struct FanEnq {
     size_t stats_bytes = 0;
     unsigned long long *stats_d = nullptr;
 };
+// burst > 0: the plain kernel `burst` times back-to-back between two events, the average
+// launch time to *burst_ms (pcp_raycast_fan_burst)
 int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
-                bool want_fh, bool stats, bool stamps, FanEnq &o);
+                bool want_fh, bool stats, bool stamps, FanEnq &o, int burst = 0,
+                double *burst_ms = nullptr);
 
 // runOptimization's scoring up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip)
 struct ScoreEnq {

@@ -12,6 +12,8 @@
 #include <cstring>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "pcp_internal.hpp"
 #include "pcp_stencil.hpp"
 
@@ -229,6 +231,9 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
                                      const double *__restrict__ steps, int K, double end,
                                      float r2, float rexit, uint32_t *cnt = nullptr) {
     if (FN == 2) {
+        if (g.frec && g.ftile)
+            return march<STATS, ZB, NB, 4>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, rexit,
+                                           cnt);
         if (g.frec)
             return march<STATS, ZB, NB, 1>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, rexit,
                                            cnt);
@@ -248,12 +253,16 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
     const float Ay = ((float)py - g.flo_y) * g.finv_c + fdy * h;
     const float Az = ((float)pz - g.flo_z) * g.finv_c + fdz * h;
     const uint32_t nx = (uint32_t)g.nx, ny = (uint32_t)g.ny;
-    if (FN == 1) {
-        // fine units for x, y (the fine corner is floor(2 f)), coarse for z; out-of-range
-        // corners are clamped: a sample outside the grid has no point within r, and a clamped
-        // record can only cost a walk whose exact tests all fail
-        const float D2x = 2.0f * Dx, D2y = 2.0f * Dy, A2x = 2.0f * Ax, A2y = 2.0f * Ay;
-        const uint32_t rx = g.frx, ry = g.fry, mx = g.frx - 1, my = g.fry - 1, mz = g.frz - 1;
+    if (FN == 1 || FN == 4) {
+        // fine units for x, y (the fine cell of the sample, (q - o) / c_f = F (f + fzoff)),
+        // coarse stencil-corner units for z; out-of-range cells are clamped: a sample outside
+        // the grid has no point within r, and a clamped record can only cost a walk whose exact
+        // tests all fail.  The float cell is within ~1e-5 m of the exact one, inside the margin
+        // m of the window's radius r + m (pcp_fine.hip).
+        const float F = g.ffine;
+        const float D2x = F * Dx, D2y = F * Dy, A2x = F * (Ax + g.fzoff), A2y = F * (Ay + g.fzoff);
+        const uint32_t mx = g.frx - 1, my = g.fry - 1, mz = g.frz - 1;
+        const uint32_t rx = FN == 4 ? (g.frx + 3) >> 2 : g.frx, ry = FN == 4 ? (g.fry + 3) >> 2 : g.fry;
         for (int k = klo; k <= khi; ++k) {
             const float kf = (float)k;
             const float fx = __builtin_fmaf(D2x, kf, A2x);
@@ -262,8 +271,13 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
             const uint32_t ix = min((uint32_t)fmaxf(fx, 0.0f), mx);
             const uint32_t iy = min((uint32_t)fmaxf(fy, 0.0f), my);
             const uint32_t iz = min((uint32_t)fmaxf(fz, 0.0f), mz);
-            // 24-bit multiply-adds (full rate): build_fine caps frx, fry * frz below 2^24
-            const uint2 R = ld_rec(g.frec, mad_u24(rx, mad_u24(ry, iz, iy), ix));
+            // 24-bit multiply-adds (full rate): build_fine caps frx, fry * frz below 2^24.
+            // FN 4: records in 4 x 4 xy tiles, one 128-byte line each (a wave's arc of probes
+            // touches fewer lines whatever its direction); rx, ry are then the tile counts.
+            const uint32_t ri = FN == 4 ? (mad_u24(rx, mad_u24(ry, iz, iy >> 2), ix >> 2) << 4) |
+                                              ((iy & 3u) << 2) | (ix & 3u)
+                                        : mad_u24(rx, mad_u24(ry, iz, iy), ix);
+            const uint2 R = ld_rec(g.frec, ri);
             // height above the block floor in kZq steps against the record's thresholds
             const float us = __builtin_fmaf(fz - (float)iz, 1.0f / kZq, g.fus_off);
             const bool cand = (us < (float)((R.y >> 8) & 255u)) & (us > (float)(R.y & 255u));
@@ -1281,7 +1295,7 @@ namespace pcp {
 // the march, k_fan_reduce.  On return o.blocked_d / o.units_d (and o.fh_d when want_fh) are
 // device results in flight; the caller synchronizes.  n > 0.
 int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
-                bool want_fh, bool stats, bool stamps, FanEnq &o) {
+                bool want_fh, bool stats, bool stamps, FanEnq &o, int burst, double *burst_ms) {
     if (fan->n_az <= 0 || fan->n_el <= 0 || (int64_t)fan->n_az * fan->n_el > (1ll << 30))
         return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: bad fan size %d x %d", fan->n_az,
                        fan->n_el);
@@ -1372,10 +1386,16 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
     const dim3 grid1(waves * (uint32_t)P);           // 64-thread blocks, pose-interleaved
     // the fine-window kernels (28 VGPRs, 8 waves per SIMD), the ring index a
     // scalar when n_az % 64 == 0 (UE); the coarse layouts' kernel otherwise
-    const bool fine = a.g.frec != nullptr, ue = a.uniform_el != 0;
+    const bool fine = a.g.frec != nullptr, ue = a.uniform_el != 0, tile = a.g.ftile != 0;
 #define PCP_FAN_LAUNCH(MODE)                                                                   \
     do {                                                                                       \
-        if (fine && ue)                                                                        \
+        if (fine && tile && ue)                                                                \
+            hipLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 4, true>), grid1, dim3(64), 0, \
+                               st, a, (uint32_t)P);                                            \
+        else if (fine && tile)                                                                 \
+            hipLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 4, false>), grid1, dim3(64), 0,\
+                               st, a, (uint32_t)P);                                            \
+        else if (fine && ue)                                                                   \
             hipLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 1, true>), grid1, dim3(64), 0, \
                                st, a, (uint32_t)P);                                            \
         else if (fine)                                                                         \
@@ -1383,6 +1403,24 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
                                st, a, (uint32_t)P);                                            \
         else                                                                                   \
             hipLaunchKernelGGL((k_raycast_fan<MODE>), grid1, dim3(64), 0, st, a, (uint32_t)P); \
+    } while (0)
+#define PCP_FAN_LAUNCH_T(MODE)                                                                 \
+    do {                                                                                       \
+        if (fine && tile && ue)                                                                \
+            hipExtLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 4, true>), grid1, dim3(64), \
+                                  0, st, kt.a, kt.b, 0, a, (uint32_t)P);                       \
+        else if (fine && tile)                                                                 \
+            hipExtLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 4, false>), grid1, dim3(64),\
+                                  0, st, kt.a, kt.b, 0, a, (uint32_t)P);                       \
+        else if (fine && ue)                                                                   \
+            hipExtLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 1, true>), grid1, dim3(64), \
+                                  0, st, kt.a, kt.b, 0, a, (uint32_t)P);                       \
+        else if (fine)                                                                         \
+            hipExtLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 1, false>), grid1, dim3(64),\
+                                  0, st, kt.a, kt.b, 0, a, (uint32_t)P);                       \
+        else                                                                                   \
+            hipExtLaunchKernelGGL((k_raycast_fan<MODE>), grid1, dim3(64), 0, st, kt.a, kt.b, 0, \
+                                  a, (uint32_t)P);                                             \
     } while (0)
     if (stats) {
         PCP_FAN_LAUNCH(FAN_STATS);
@@ -1396,27 +1434,57 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
         PCP_FAN_LAUNCH(FAN_STAMPS);
         PCP_CHECK_LAUNCH(ctx);
         o.stats_d = a.stats;
-    } else {
-        ProfScope ps(ctx, PCP_K_RAYCAST_FAN);
-        // PCP_FAN_BATCH selects the A/B variants of DESIGN.md §6b
-        const dim3 grid128((rays + 127) / 128, P);
-        switch (ctx->fan_batch) {
-        case 1: hipLaunchKernelGGL((k_raycast_fan_pm<128, true>), grid128, dim3(128), 0, st, a); break;
-        case 2: hipLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 64, false>), grid1, dim3(64), 0, st, a, (uint32_t)P); break;
-        case 4: PCP_FAN_LAUNCH(FAN_PLAIN); break;   // A/B: plain pose interleaving
-        default:
-            // XCD-chunked placement (each XCD's L2 serves neighbouring poses' overlapping fans):
-            // 0.61 vs 0.63 ms on C2 (DESIGN.md §6b)
-            if (fine && ue && P % 8 == 0)
+    } else if (burst > 0) {
+        // the production kernel `burst` times back-to-back between two events: the queue never
+        // idles between the events, so the interval is the launches themselves (the per-call
+        // events of a synchronous query also hold the queue's wake-up before the kernel)
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        PCP_HIP(ctx, hipEventCreate(&e0));
+        PCP_HIP(ctx, hipEventCreate(&e1));
+        PCP_HIP(ctx, hipEventRecord(e0, st));
+        for (int r = 0; r < burst; ++r) {
+            if (fine && tile && ue && P % 8 == 0)
+                hipLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN, 64, true, 8, 4>), grid1, dim3(64),
+                                   0, st, a, (uint32_t)P);
+            else if (fine && ue && P % 8 == 0)
                 hipLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN>), grid1, dim3(64), 0, st, a,
                                    (uint32_t)P);
             else
                 PCP_FAN_LAUNCH(FAN_PLAIN);
+        }
+        PCP_CHECK_LAUNCH(ctx);
+        PCP_HIP(ctx, hipEventRecord(e1, st));
+        PCP_HIP(ctx, hipEventSynchronize(e1));
+        float ms = 0.0f;
+        PCP_HIP(ctx, hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (burst_ms) *burst_ms = (double)ms / burst;
+    } else {
+        KernelTimer kt(ctx, PCP_K_RAYCAST_FAN);   // events around the kernel itself
+        // PCP_FAN_BATCH selects the A/B variants of DESIGN.md §6b
+        const dim3 grid128((rays + 127) / 128, P);
+        switch (ctx->fan_batch) {
+        case 1: hipExtLaunchKernelGGL((k_raycast_fan_pm<128, true>), grid128, dim3(128), 0, st, kt.a, kt.b, 0, a); break;
+        case 2: hipExtLaunchKernelGGL((k_raycast_fan<FAN_PLAIN, 64, false>), grid1, dim3(64), 0, st, kt.a, kt.b, 0, a, (uint32_t)P); break;
+        case 4: PCP_FAN_LAUNCH_T(FAN_PLAIN); break;   // A/B: plain pose interleaving
+        default:
+            // XCD-chunked placement (each XCD's L2 serves neighbouring poses' overlapping fans):
+            // 0.61 vs 0.63 ms on C2 (DESIGN.md §6b)
+            if (fine && tile && ue && P % 8 == 0)
+                hipExtLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN, 64, true, 8, 4>), grid1,
+                                      dim3(64), 0, st, kt.a, kt.b, 0, a, (uint32_t)P);
+            else if (fine && ue && P % 8 == 0)
+                hipExtLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN>), grid1, dim3(64), 0, st, kt.a,
+                                      kt.b, 0, a, (uint32_t)P);
+            else
+                PCP_FAN_LAUNCH_T(FAN_PLAIN);
             break;
         }
         PCP_CHECK_LAUNCH(ctx);
     }
 #undef PCP_FAN_LAUNCH
+#undef PCP_FAN_LAUNCH_T
     hipLaunchKernelGGL(k_fan_reduce, dim3(P), dim3(kT), 0, st,
                        (const uint2 *)a.wave_part, waves, (uint32_t)P, a.per_xcd, blocked_d,
                        units_d);
@@ -1435,7 +1503,7 @@ extern "C" {
 static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
                             const pcp_fan_params *fan, uint32_t *blocked, uint64_t *units,
                             int16_t *first_hit, int64_t *best_idx, uint64_t *stats,
-                            uint64_t *stamps) {
+                            uint64_t *stamps, int burst = 0, double *burst_ms = nullptr) {
     if (!ctx) return PCP_E_INVALID;
     if (!fan || (n && (!poses5 || !blocked)))
         return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: null argument");
@@ -1448,7 +1516,7 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     }
     FanEnq o;
     if (int rc = fan_enqueue(ctx, poses5, n, fan, first_hit != nullptr, stats != nullptr,
-                             stamps != nullptr, o))
+                             stamps != nullptr, o, burst, burst_ms))
         return rc;
     hipStream_t st = ctx->stream;
     const int P = (int)n;
@@ -1493,6 +1561,15 @@ int pcp_raycast_fan_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
     stats[0] = stats[1] = stats[2] = stats[3] = 0;
     return raycast_fan_impl(ctx, poses5, n, fan, blocked.data(), nullptr, nullptr, nullptr, stats,
                             nullptr);
+}
+
+int pcp_raycast_fan_burst(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                          const pcp_fan_params *fan, int reps, double *ms_per_launch) {
+    if (!ctx || !ms_per_launch || reps <= 0) return PCP_E_INVALID;
+    std::vector<uint32_t> blocked(n ? n : 1);
+    *ms_per_launch = 0.0;
+    return raycast_fan_impl(ctx, poses5, n, fan, blocked.data(), nullptr, nullptr, nullptr,
+                            nullptr, nullptr, reps, ms_per_launch);
 }
 
 int pcp_raycast_fan_stamps(pcp_ctx *ctx, const double *poses5, uint64_t n,

@@ -744,14 +744,14 @@ def test_drivable_area_matches_oracle(gpu, oracle, kw):
 
 
 # (PCP_TERRAIN_BLOCKS, PCP_TERRAIN_FINE) -> the layout the scans walk from the first query
-LAYOUTS = [("0", "1", "cells"), ("2", "0", "blocks"), ("2", "1", "fine")]
+LAYOUTS = [("0", "3", "cells"), ("2", "0", "blocks"), ("2", "2", "fine"), ("2", "3", "fine")]
 
 
 @pytest.mark.parametrize("mode,fine,layout", LAYOUTS)
 def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, fine, layout, monkeypatch):
     """PCP_TERRAIN_BLOCKS=0 scans the per-cell runs, =2 the block-major copy (PCP_TERRAIN_FINE=0:
-    2x2x2 blocks, 1: fine windows) from the first query on (the default, 1, switches at the
-    second query): all bit-exact on the fan and the reference-mode scoring."""
+    2x2x2 blocks, F > 0: windows of fine cells c / F) from the first query on (the default, 1,
+    switches at the second query): all bit-exact on the fan and the reference-mode scoring."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", mode)
     monkeypatch.setenv("PCP_TERRAIN_FINE", fine)
     ctx = _abi.Context(0)
