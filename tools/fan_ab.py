@@ -63,6 +63,15 @@ for rnd in range(12):
             ref = (b, u)
         if not v.startswith("x"):
             assert np.array_equal(b, ref[0]) and np.array_equal(u, ref[1]), v
+# across processes (tools/ab_proc.sh): the first run of a box leaves its outputs, every later
+# variant must reproduce them
+reff = ROOT / "gpurun_out" / "fan_ab_ref.npz"
+if reff.exists():
+    z = np.load(reff)
+    assert np.array_equal(z["b"], ref[0]) and np.array_equal(z["u"], ref[1]), "differs from " + str(reff)
+else:
+    reff.parent.mkdir(exist_ok=True)
+    np.savez(reff, b=ref[0], u=ref[1])
 for v in names:
     t = np.array(times[v])
     print(f"{v}: median {np.median(t):.4f} ms  min {t.min():.4f} ms")
