@@ -67,10 +67,10 @@ k_zkeys(const float4 *__restrict__ pts, uint32_t n, unsigned long long *__restri
     val[i] = i;
 }
 
-// windows holding each point (in z order): count per point and per window
+// windows holding each point (in z order): count per point
 __global__ void __launch_bounds__(kThreads)
 k_win_count(const float4 *__restrict__ pts, const uint32_t *__restrict__ zord, uint32_t n,
-            FineGeo f, uint32_t *__restrict__ pcount, uint32_t *__restrict__ wcount) {
+            FineGeo f, uint32_t *__restrict__ pcount) {
     const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= n) return;
     const float4 p = pts[zord[i]];
@@ -79,10 +79,7 @@ k_win_count(const float4 *__restrict__ pts, const uint32_t *__restrict__ zord, u
     uint32_t c = 0;
     for (int wy = max(cy - f.reach, 0); wy <= min(cy + f.reach, f.fny - 1); ++wy)
         for (int wx = max(cx - f.reach, 0); wx <= min(cx + f.reach, f.fnx - 1); ++wx)
-            if (in_window(f, (double)p.x, (double)p.y, wx, wy)) {
-                atomicAdd(&wcount[(uint32_t)wx + (uint32_t)f.fnx * (uint32_t)wy], 1u);
-                ++c;
-            }
+            if (in_window(f, (double)p.x, (double)p.y, wx, wy)) ++c;
     pcount[i] = c;
 }
 
@@ -105,6 +102,21 @@ k_win_emit(const float4 *__restrict__ pts, const uint32_t *__restrict__ zord, ui
             }
 }
 
+// cstart[w] = first sorted pair of window w (lower bound in the sorted window keys), w <= nw
+__global__ void __launch_bounds__(kThreads)
+k_win_bounds(const uint32_t *__restrict__ wkey, uint32_t np, uint32_t nw,
+             uint32_t *__restrict__ cstart) {
+    const uint32_t w = blockIdx.x * kThreads + threadIdx.x;
+    if (w > nw) return;
+    uint32_t lo = 0, hi = np;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (wkey[mid] < w) lo = mid + 1;
+        else hi = mid;
+    }
+    cstart[w] = lo;
+}
+
 // sorted pair k of window W lands at k + W (one sentinel ends each earlier window)
 __global__ void __launch_bounds__(kThreads)
 k_win_place(const float4 *__restrict__ pts, const uint32_t *__restrict__ zord,
@@ -120,31 +132,55 @@ k_win_place(const float4 *__restrict__ pts, const uint32_t *__restrict__ zord,
 // (cz is non-increasing along it); no end is stored (see the header).  The z band is stored as
 // probe thresholds in steps of kZq cells above the block floor: lo - T, hi + T with
 // T = ceil((r + 2 mm) / c / kZq) folded in (0 / 255 unbounded; empty: lo 255, hi 0), so the
-// probe is two compares.
+// probe is two compares.  (One thread per record with two binary searches each
+// measured 1.7x slower: 17 levels re-search the same short run.)
 __global__ void __launch_bounds__(kThreads)
 k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ cstart, CellMap m, double c,
        uint32_t fnx, uint32_t fny, uint32_t rz, uint32_t tsteps, int tile,
        uint2 *__restrict__ frec) {
     const uint32_t nw = fnx * fny, w = blockIdx.x * kThreads + threadIdx.x;
+    const uint32_t tx = (fnx + 3) >> 2, ty = (fny + 3) >> 2;
+    const size_t plane = tile ? (size_t)tx * ty * 16 : (size_t)nw;
+    if (tile && w < tx * ty * 16u) {   // padding records of the tiles (never windows)
+        const uint32_t t = w >> 4, sub = w & 15u;
+        const uint32_t px = (t % tx) * 4u + (sub & 3u), py = (t / tx) * 4u + (sub >> 2);
+        if (px >= fnx || py >= fny)
+            for (uint32_t iz = 0; iz < rz; ++iz) frec[(size_t)iz * plane + w] = make_uint2(0u, 0x00FFu);
+    }
     if (w >= nw) return;
     // record index of (w, iz): x-fastest, or 4 x 4 xy tiles of 16 records (one 128-byte line)
     const uint32_t wx = w % fnx, wy = w / fnx;
-    const uint32_t tx = (fnx + 3) >> 2, ty = (fny + 3) >> 2;
-    const size_t plane = tile ? (size_t)tx * ty * 16 : (size_t)nw;
     const size_t base = tile ? ((size_t)((wy >> 2) * tx + (wx >> 2)) << 4) | ((wy & 3u) << 2) |
                                    (wx & 3u)
                              : (size_t)w;
     const uint32_t s = cstart[w] + w, e = cstart[w + 1] + w;   // e: the sentinel
     wpts[e] = make_float4(__int_as_float(0x7FC00000), __int_as_float(0x7FC00000), -INFINITY,
                           __uint_as_float(0xFFFFFFFFu));
+    // one pass down the run: jt / jb advance monotonically, each entry's z and coarse z cell
+    // loaded once per pointer (the walk of every level reuses them)
     uint32_t jt = s, jb = s;
+    float zt = wpts[s].z, zb = zt, zlast = zt;
+    int ct = s < e ? cell_z(m, zt) : -1, cb = ct;
     for (int iz = (int)rz - 1; iz >= 0; --iz) {
-        while (jt < e && cell_z(m, wpts[jt].z) > iz + 1) ++jt;
-        if (jb < jt) jb = jt;
-        while (jb < e && cell_z(m, wpts[jb].z) >= iz) ++jb;
+        while (jt < e && ct > iz + 1) {
+            ++jt;
+            zt = wpts[jt].z;
+            ct = jt < e ? cell_z(m, zt) : -1;
+        }
+        if (jb < jt) {
+            jb = jt;
+            zb = zt;
+            cb = ct;
+        }
+        while (jb < e && cb >= iz) {
+            zlast = zb;
+            ++jb;
+            zb = wpts[jb].z;
+            cb = jb < e ? cell_z(m, zb) : -1;
+        }
         uint32_t band = 0x00FFu;   // empty
         if (jb > jt) {
-            const uint32_t code = zband_code(wpts[jt].z, wpts[jb - 1].z, m.oz + (double)iz * c, c);
+            const uint32_t code = zband_code(zt, zlast, m.oz + (double)iz * c, c);
             const uint32_t lo = code & 255u, hi = code >> 8;
             const uint32_t lo2 = (lo == 0u || lo <= tsteps) ? 0u : lo - tsteps;
             const uint32_t hi2 = (hi == 255u) ? 255u : min(hi + tsteps, 255u);
@@ -195,10 +231,10 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     uint32_t *v0 = reinterpret_cast<uint32_t *>(k1 + n), *zord = v0 + n;
     hipLaunchKernelGGL(k_zkeys, dim3(gridn), dim3(kThreads), 0, st, pts, n, k0, v0);
     PCP_CHECK_LAUNCH(ctx);
-    // 2. windows per point (pcount), points per window (wcount)
-    PCP_HIP(ctx, ctx->scratch[3].ensure((size_t)(n + 1) * 8 + (nw + 1) * 8 + 64));
+    // 2. windows per point (pcount); points per window come from the sorted pairs (step 4)
+    PCP_HIP(ctx, ctx->scratch[3].ensure((size_t)(n + 1) * 8 + (nw + 1) * 4 + 64));
     uint32_t *pcount = ctx->scratch[3].as<uint32_t>(), *poff = pcount + (n + 1);
-    uint32_t *wcount = poff + (n + 1), *cstart = wcount + (nw + 1);
+    uint32_t *cstart = poff + (n + 1);
     // 3. scans
     const size_t tscan = scan_tmp_bytes(std::max<uint64_t>(n, nw)) +
                          (std::max<uint64_t>(n, nw) + 1) * sizeof(uint32_t);
@@ -206,13 +242,10 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     if (hipcub::DeviceRadixSort::SortPairs(ctx->scratch[4].p, t1, k0, k1, v0, zord, (int)n, 0, 64,
                                            st) != hipSuccess)
         return set_err(ctx, PCP_E_HIP, "build_fine: z sort failed");
-    PCP_HIP(ctx, hipMemsetAsync(wcount, 0, (nw + 1) * sizeof(uint32_t), st));
-    hipLaunchKernelGGL(k_win_count, dim3(gridn), dim3(kThreads), 0, st, pts, zord, n, f, pcount,
-                       wcount);
+    hipLaunchKernelGGL(k_win_count, dim3(gridn), dim3(kThreads), 0, st, pts, zord, n, f, pcount);
     PCP_CHECK_LAUNCH(ctx);
     int rc = exclusive_scan_u32(ctx, pcount, poff, n, ctx->scratch[4].p);
     if (rc) return rc;
-    if ((rc = exclusive_scan_u32(ctx, wcount, cstart, nw, ctx->scratch[4].p))) return rc;
     uint32_t np = 0;
     if ((rc = read_small(ctx, &np, poff + n, 4, st))) return rc;
     // entries = pairs + one sentinel per window, addressed with 32-bit indices (<< 4 bytes)
@@ -236,6 +269,9 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     if (hipcub::DeviceRadixSort::SortPairs(ctx->scratch[6].p, t2, wk0, wk1, rk0, rk1, (int)np, 0,
                                            wbits, st) != hipSuccess)
         return set_err(ctx, PCP_E_HIP, "build_fine: window sort failed");
+    hipLaunchKernelGGL(k_win_bounds, dim3((unsigned)((nw + kThreads) / kThreads)), dim3(kThreads),
+                       0, st, (const uint32_t *)wk1, np, (uint32_t)nw, cstart);
+    PCP_CHECK_LAUNCH(ctx);
     // the copy is an optional speed-up: an allocation failure keeps the other layouts
     const size_t nent = (size_t)np + nw;
     if (g.wpts.ensure(nent * sizeof(float4)) != hipSuccess ||
@@ -252,7 +288,8 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     PCP_CHECK_LAUNCH(ctx);
     // 5. records (and the sentinels)
     const uint32_t tsteps = (uint32_t)std::ceil((g.r_q + 2e-3) / g.c / (double)kZq);
-    hipLaunchKernelGGL(k_frec, dim3((unsigned)((nw + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+    const uint64_t nthr = std::max<uint64_t>(nw, tile ? nrec / rz : 0);
+    hipLaunchKernelGGL(k_frec, dim3((unsigned)((nthr + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                        st, g.wpts.as<float4>(), (const uint32_t *)cstart, m, g.c, (uint32_t)fnx,
                        (uint32_t)fny, (uint32_t)rz, tsteps, tile, g.frec.as<uint2>());
     PCP_CHECK_LAUNCH(ctx);
