@@ -626,9 +626,12 @@ __global__ void __launch_bounds__(kST) k_seg_count(const JobBatch jobs) {
 // voxel s = the s-th head in sorted order: CentroidPoint<PointXYZ> = float sums of its points
 // in (stable) input order, / (float)n.  The tile's sorted points are staged in LDS; run ends
 // come from the tile's head list and the next tile holding a head.  The last tile writes the
-// voxel count (res[slot]).
+// voxel count (res[slot]).  emit != null (pcp_filter_merge when every cloud is voxelised): the
+// centroid goes straight through the cloud's transform + colour into the concatenated output
+// at the cloud's offset (the voxel counts of the earlier clouds, from their k_seg_count), as
+// k_emit_rgb would write it -- one launch and the out4 round trip fewer.
 __global__ void __launch_bounds__(kST)
-k_seg_centroid(const JobBatch jobs, uint32_t *__restrict__ res) {
+k_seg_centroid(const JobBatch jobs, uint32_t *__restrict__ res, float4 *__restrict__ emit) {
     const CloudJob &J = jobs.j[blockIdx.y];
     if (J.passes == 0) return;
     const uint32_t *keys = (J.passes & 1) ? J.keys1 : J.keys0;
@@ -646,6 +649,12 @@ k_seg_centroid(const JobBatch jobs, uint32_t *__restrict__ res) {
     __shared__ uint32_t hpos[kSortTile + 1];
     __shared__ float4 lp[kSortTile];   // the tile's sorted points
     __shared__ uint32_t wo[kSortItems][kSW];
+    uint32_t ebase = 0;   // the cloud's first output record (emit)
+    if (emit && nact > blockIdx.x)
+        for (int y = 0; y < (int)blockIdx.y; ++y) {
+            const CloudJob &K = jobs.j[y];
+            ebase += block_prefix_sum<kST>(K.tcount, sort_tiles(*K.vp), lds);
+        }
     for (uint32_t t = blockIdx.x; t < nact; t += gridDim.x) {
     const uint64_t base = (uint64_t)t * kSortTile;
     FLT_STAMP(1, t, 0);
@@ -736,9 +745,13 @@ k_seg_centroid(const JobBatch jobs, uint32_t *__restrict__ res) {
         if (!((head >> j) & 1u)) continue;
         const float cnt = (float)n_[j];
         const uint32_t s = pre + loc[j];
-        out[s] = make_float4(sx[j] / cnt, sy[j] / cnt, sz[j] / cnt, 1.0f);
-        out_idx[s] = hkey[j];
-        out_cnt[s] = n_[j];
+        if (emit) {
+            xform_store(J.rig, sx[j] / cnt, sy[j] / cnt, sz[j] / cnt, emit + 2 * ((size_t)ebase + s));
+        } else {
+            out[s] = make_float4(sx[j] / cnt, sy[j] / cnt, sz[j] / cnt, 1.0f);
+            out_idx[s] = hkey[j];
+            out_cnt[s] = n_[j];
+        }
     }
     }   // tot != 0
     __syncthreads();
@@ -896,7 +909,8 @@ static std::vector<Batch> batches_of(const std::vector<CloudJob> &jobs) {
 }
 
 // crop [-> voxel] of every cloud of one batch, on stream st
-static int enqueue_chain(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream_t st) {
+static int enqueue_chain(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream_t st,
+                         float4 *emit = nullptr) {
     const unsigned k = (unsigned)bt.k;
     {
         ProfScope ps(ctx, PCP_K_CROP, st);
@@ -926,7 +940,7 @@ static int enqueue_chain(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream
         }
         hipLaunchKernelGGL(k_seg_count, dim3(gx, k), dim3(kST), 0, st, bt.jb);
         PCP_CHECK_LAUNCH(ctx);
-        hipLaunchKernelGGL(k_seg_centroid, dim3(gx, k), dim3(kST), 0, st, bt.jb, res);
+        hipLaunchKernelGGL(k_seg_centroid, dim3(gx, k), dim3(kST), 0, st, bt.jb, res, emit);
         PCP_CHECK_LAUNCH(ctx);
     }
     return PCP_OK;
@@ -943,8 +957,32 @@ static int enqueue_emit(pcp_ctx *ctx, const Batch &bt, const uint32_t *res, floa
     return PCP_OK;
 }
 
+// every cloud of a one-batch call certainly voxelised: a non-empty input and a finite crop box
+// whose voxel keys fit 31 bits (then PCL's int32 guard cannot fire on the cropped points'
+// smaller bbox) -- the centroid kernel can emit the merged records itself
+static bool emit_in_centroid(const std::vector<Batch> &bts) {
+    if (bts.size() != 1) return false;
+    const Batch &bt = bts[0];
+    for (int i = 0; i < bt.k; ++i) {
+        const CloudJob &J = bt.jb.j[i];
+        if (J.in.n == 0 || !(J.leaf > 0.0f) || J.passes <= 0 ||
+            J.passes * kDigitBits > 31 + kDigitBits - 1)
+            return false;
+        const Box &b = J.box;
+        const double lo[3] = {b.x0, b.y0, b.z0}, hi[3] = {b.x1, b.y1, b.z1};
+        double nv = 1.0;
+        for (int a = 0; a < 3; ++a) {
+            if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) return false;
+            nv *= std::floor((hi[a] - lo[a]) / (double)J.leaf) + 3.0;
+        }
+        if (!(nv < 2147483647.0)) return false;
+    }
+    return true;
+}
+
 static int enqueue_all(pcp_ctx *ctx, const std::vector<Batch> &bts, uint32_t *res,
                        float4 *emit_out, hipStream_t st) {
+    if (emit_out && emit_in_centroid(bts)) return enqueue_chain(ctx, bts[0], res, st, emit_out);
     for (const Batch &bt : bts) {
         int rc = enqueue_chain(ctx, bt, res, st);
         if (rc) return rc;
