@@ -332,16 +332,24 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
 struct ScoreEnq {
     int P = 0, C = 0;
     double *comb = nullptr;        // [P][C] mobile scores
+    double *score_z = nullptr;     // [C] zx120 scores
     uint8_t *mbits = nullptr;      // [P][C] result bits of the poses
     uint8_t *zbits = nullptr;      // [C] result bits of the zx120 evaluation
     uint8_t *flags_d = nullptr;    // [C] cell flag bytes (caller fills)
     double *tot_d = nullptr;       // [P + 1] totals, row P = zx120
     int32_t *cov_d = nullptr;      // [P + 1]
     int32_t *stats = nullptr;      // 64 colour-statistics slots
-    size_t tc_bytes = 0, st_off = 0, fl_off = 0;   // pinned (res_host) layout
+    // the query's block (poses_d on the device, res_host pinned, same offsets): poses at 0,
+    // cell flags at fl_off, totals + covered (tc_bytes) ending at most at st_off, stats at
+    // st_off, blk_bytes in all
+    size_t tc_bytes = 0, st_off = 0, fl_off = 0, blk_bytes = 0;
 };
+// cell_flags (C bytes) travel with the poses when given (pcp_score_poses); k_score_cells zeroes
+// the statistics
+// fuse_tail: the row sums are left to the caller's k_sum_flags launch (pcp_score_poses)
 int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
-                  const pcp_vl_params *p, ScoreEnq &o);
+                  const pcp_vl_params *p, ScoreEnq &o, const uint8_t *cell_flags = nullptr,
+                  bool fuse_tail = false);
 // key kernels of the pose-sharded search (pcp_vlidar.hip; used by pcp_multi.hip)
 void launch_fan_keys(hipStream_t st, const uint32_t *blocked_d, uint32_t lo, uint32_t cnt,
                      uint32_t P, unsigned long long *keys);

@@ -443,9 +443,12 @@ __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(PCP_SCO
 k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict__ cn, int C,
               const double *__restrict__ poses5, int P, const double *__restrict__ zx5,
               double *__restrict__ sm_out, uint8_t *__restrict__ mbits,
-              double *__restrict__ score_z, uint8_t *__restrict__ zbits) {
+              double *__restrict__ score_z, uint8_t *__restrict__ zbits,
+              int32_t *__restrict__ stats) {
     const int c = blockIdx.x * kT + threadIdx.x;
     const int p = blockIdx.y;
+    // the colour-statistics slots k_cell_flags accumulates into (it runs after this kernel)
+    if (stats && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) stats[threadIdx.x] = 0;
     if (c >= C) return;
     const bool zrow = p == P;
     const double *Q = zrow ? zx5 : poses5 + 5 * (size_t)p;
@@ -474,11 +477,11 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-__global__ void __launch_bounds__(64)
-k_row_sum(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
-          double *__restrict__ total, int32_t *__restrict__ covered) {
-    const int r = blockIdx.x;
-    const int lane = threadIdx.x;
+__device__ __forceinline__ void row_sum_body(const double *__restrict__ sm,
+                                             const double *__restrict__ score_z, int C, int P,
+                                             double *__restrict__ total,
+                                             int32_t *__restrict__ covered, int r) {
+    const int lane = threadIdx.x & 63;
     const double *row = sm + (size_t)r * C;
     constexpr int kPer = kSumChunk / 64;
     double v[kPer], wz[kPer], wm[kPer];
@@ -532,6 +535,12 @@ k_row_sum(const double *__restrict__ sm, const double *__restrict__ score_z, int
     }
 }
 
+__global__ void __launch_bounds__(64)
+k_row_sum(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
+          double *__restrict__ total, int32_t *__restrict__ covered) {
+    row_sum_body(sm, score_z, C, P, total, covered, blockIdx.x);
+}
+
 // stats slots
 enum {
     S_TOTAL = 0, S_ZR, S_ZF, S_ZV, S_ZG, S_ZRED, S_ZB, S_ZY, S_G, S_RED, S_B, S_Y, S_N
@@ -539,10 +548,11 @@ enum {
 
 // stale-flag resolution (virtual_lidar.cpp:487-501 read flags written by the LAST
 // evaluation that reached each assignment, :662-687) + colour statistics
-__global__ void __launch_bounds__(kT)
-k_cell_flags(const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbits, int C, int P,
-             uint8_t *__restrict__ flags, int32_t *__restrict__ stats) {
-    const int c = blockIdx.x * kT + threadIdx.x;
+__device__ __forceinline__ void cell_flags_body(const uint8_t *__restrict__ zbits,
+                                                const uint8_t *__restrict__ mbits, int C, int P,
+                                                uint8_t *__restrict__ flags,
+                                                int32_t *__restrict__ stats, int blk) {
+    const int c = blk * kT + threadIdx.x;
     __shared__ int32_t bst[S_N];
     if (threadIdx.x < S_N) bst[threadIdx.x] = 0;
     __syncthreads();
@@ -591,6 +601,27 @@ k_cell_flags(const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbit
     }
     __syncthreads();
     if (threadIdx.x < S_N && bst[threadIdx.x]) atomicAdd(&stats[threadIdx.x], bst[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(kT)
+k_cell_flags(const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbits, int C, int P,
+             uint8_t *__restrict__ flags, int32_t *__restrict__ stats) {
+    cell_flags_body(zbits, mbits, C, P, flags, stats, blockIdx.x);
+}
+
+// the two independent tails of a score query in ONE launch: blocks 0 .. P are the ordered row
+// sums (wave 0 of each; a 3,704-add chain, ~30 us), the blocks after them the stale-flag
+// resolution (~7 us), which so runs beside the chains instead of after them
+__global__ void __launch_bounds__(kT)
+k_sum_flags(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
+            double *__restrict__ total, int32_t *__restrict__ covered,
+            const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbits,
+            uint8_t *__restrict__ flags, int32_t *__restrict__ stats) {
+    if ((int)blockIdx.x <= P) {
+        if (threadIdx.x < 64) row_sum_body(sm, score_z, C, P, total, covered, blockIdx.x);
+        return;
+    }
+    cell_flags_body(zbits, mbits, C, P, flags, stats, (int)blockIdx.x - (P + 1));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1153,7 +1184,8 @@ namespace pcp {
 // zx120), k_row_sum.  On return the device holds comb/mbits [P][C], zbits [C], tot_d/cov_d
 // [P+1] (row P = zx120); the caller synchronizes.  Validation is the caller's.
 int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
-                  const pcp_vl_params *p, ScoreEnq &o) {
+                  const pcp_vl_params *p, ScoreEnq &o, const uint8_t *cell_flags,
+                  bool fuse_tail) {
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const int C = (int)ctx->n_cells, P = (int)n;
@@ -1162,35 +1194,42 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
     if (rc) return rc;
     if ((rc = terrain_blocks_before_query(ctx))) return rc;
     VisEnv E = make_env(ctx, p, ctx->steps_d.as<const double>(), K);
-    // buffers
+    // buffers.  One device block mirrors the pinned one, so a query is ONE upload and ONE
+    // download: [poses + zx120 (P + 1) x 5 f64 | cell flags C | totals f64 (P + 1) | covered
+    // i32 (P + 1) | stats 64 i32] -- upload [poses .. flags], download [flags .. stats]
     const size_t pc = (size_t)P * (size_t)C;
-    PCP_HIP(ctx, ctx->poses_d.ensure((size_t)(P + 1) * 5 * sizeof(double) + 16));
+    auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    o.fl_off = a16((size_t)(P + 1) * 5 * sizeof(double));
+    const size_t to_off = a16(o.fl_off + (size_t)C);
+    o.tc_bytes = (size_t)(P + 1) * (sizeof(double) + sizeof(int32_t));
+    o.st_off = a16(to_off + o.tc_bytes);
+    o.blk_bytes = o.st_off + 64 * sizeof(int32_t);
+    PCP_HIP(ctx, ctx->poses_d.ensure(o.blk_bytes + 64));
     PCP_HIP(ctx, ctx->out_a.ensure(pc * sizeof(double) + (size_t)C * sizeof(double) + 64));
     PCP_HIP(ctx, ctx->out_b.ensure(pc + (size_t)C * 2 + 64));
-    PCP_HIP(ctx, ctx->out_c.ensure((size_t)(P + 1) * (sizeof(double) + sizeof(int32_t)) + 64));
-    PCP_HIP(ctx, ctx->stats_d.ensure(64 * sizeof(int32_t)));
+    char *blk = ctx->poses_d.as<char>();
     o.P = P;
     o.C = C;
     o.comb = ctx->out_a.as<double>();
     double *score_z = o.comb + pc;
     o.mbits = ctx->out_b.as<uint8_t>();
     o.zbits = o.mbits + pc;
-    o.flags_d = o.zbits + C;
-    o.tot_d = ctx->out_c.as<double>();
+    o.flags_d = reinterpret_cast<uint8_t *>(blk + o.fl_off);
+    o.tot_d = reinterpret_cast<double *>(blk + to_off);
     o.cov_d = reinterpret_cast<int32_t *>(o.tot_d + (P + 1));
-    o.stats = ctx->stats_d.as<int32_t>();
-    // pinned staging: [totals f64 (P+1) | covered i32 (P+1)] [stats] [cell flags] [poses + zx120]
-    o.tc_bytes = (size_t)(P + 1) * (sizeof(double) + sizeof(int32_t));
-    o.st_off = (o.tc_bytes + 15) & ~(size_t)15;
-    o.fl_off = o.st_off + 64 * sizeof(int32_t);
-    const size_t po_off = (o.fl_off + (size_t)C + 15) & ~(size_t)15;
-    const size_t po_bytes = (size_t)(P + 1) * 5 * sizeof(double);
-    PCP_HIP(ctx, ctx->res_host.ensure(po_off + po_bytes + 16));
+    o.stats = reinterpret_cast<int32_t *>(blk + o.st_off);
+    PCP_HIP(ctx, ctx->res_host.ensure(o.blk_bytes + 64));
     char *pin = ctx->res_host.as<char>();
-    // the candidates, then the zx120 pose behind them (row P of k_score_cells): one upload
-    if (P) std::memcpy(pin + po_off, poses5, (size_t)P * 5 * sizeof(double));
-    std::memcpy(pin + po_off + (size_t)P * 5 * sizeof(double), zx, 5 * sizeof(double));
-    PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pin + po_off, po_bytes, hipMemcpyHostToDevice, st));
+    // the candidates, then the zx120 pose behind them (row P of k_score_cells), then the
+    // caller's cell flags: one upload
+    if (P) std::memcpy(pin, poses5, (size_t)P * 5 * sizeof(double));
+    std::memcpy(pin + (size_t)P * 5 * sizeof(double), zx, 5 * sizeof(double));
+    size_t up = (size_t)(P + 1) * 5 * sizeof(double);
+    if (cell_flags && C) {
+        std::memcpy(pin + o.fl_off, cell_flags, C);
+        up = o.fl_off + C;
+    }
+    PCP_HIP(ctx, hipMemcpyAsync(blk, pin, up, hipMemcpyHostToDevice, st));
     const unsigned cb = (unsigned)((C + kT - 1) / kT);
     if (C) {
         {
@@ -1199,10 +1238,11 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
                                ctx->cells_xyz.as<const double>(), ctx->cells_nrm.as<const float>(),
                                C, ctx->poses_d.as<const double>(), P,
                                ctx->poses_d.as<const double>() + 5 * (size_t)P, o.comb, o.mbits,
-                               score_z, o.zbits);
+                               score_z, o.zbits, o.stats);
             PCP_CHECK_LAUNCH(ctx);
         }
-        {
+        o.score_z = score_z;
+        if (!fuse_tail) {   // (fused: k_sum_flags, launched by the caller)
             ProfScope ps(ctx, PCP_K_POSE_SUM);
             hipLaunchKernelGGL(k_row_sum, dim3(P + 1), dim3(64), 0, st, (const double *)o.comb,
                                (const double *)score_z, C, P, o.tot_d, o.cov_d);
@@ -1211,6 +1251,7 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
     } else {
         PCP_HIP(ctx, hipMemsetAsync(o.tot_d, 0, (size_t)(P + 1) * sizeof(double), st));
         PCP_HIP(ctx, hipMemsetAsync(o.cov_d, 0, (size_t)(P + 1) * sizeof(int32_t), st));
+        PCP_HIP(ctx, hipMemsetAsync(o.stats, 0, 64 * sizeof(int32_t), st));
     }
     return PCP_OK;
 }
@@ -1246,30 +1287,26 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
         return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: null argument");
     if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: at most 65535 poses per call");
     ScoreEnq o;
-    if (int rc = score_enqueue(ctx, poses5, n, zx, p, o)) return rc;
+    if (int rc = score_enqueue(ctx, poses5, n, zx, p, o, cell_flags, true)) return rc;
     hipStream_t st = ctx->stream;
     const int C = o.C, P = o.P;
     char *pin = ctx->res_host.as<char>();
-    if (C) {
-        std::memcpy(pin + o.fl_off, cell_flags, C);
-        PCP_HIP(ctx, hipMemcpyAsync(o.flags_d, pin + o.fl_off, C, hipMemcpyHostToDevice, st));
-    }
-    PCP_HIP(ctx, hipMemsetAsync(o.stats, 0, 64 * sizeof(int32_t), st));
-    if (C) {
-        ProfScope ps(ctx, PCP_K_CELL_FLAGS);
-        hipLaunchKernelGGL(k_cell_flags, dim3((unsigned)((C + kT - 1) / kT)), dim3(kT), 0, st,
-                           (const uint8_t *)o.zbits, (const uint8_t *)o.mbits, C, P, o.flags_d,
+    if (C) {   // the ordered row sums and the stale-flag resolution side by side
+        ProfScope ps(ctx, PCP_K_POSE_SUM);
+        hipLaunchKernelGGL(k_sum_flags, dim3((unsigned)(P + 1 + (C + kT - 1) / kT)), dim3(kT), 0,
+                           st, (const double *)o.comb, (const double *)o.score_z, C, P, o.tot_d,
+                           o.cov_d, (const uint8_t *)o.zbits, (const uint8_t *)o.mbits, o.flags_d,
                            o.stats);
         PCP_CHECK_LAUNCH(ctx);
     }
-    // totals and covered counts are adjacent on the device: one copy into the pinned block
-    const double *tot_h = reinterpret_cast<const double *>(pin);
+    // flags, totals, covered counts and statistics are one span of the block: one download
+    PCP_HIP(ctx, hipMemcpyAsync(pin + o.fl_off, reinterpret_cast<const char *>(o.flags_d),
+                                o.blk_bytes - o.fl_off, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    const double *tot_h = reinterpret_cast<const double *>(
+        pin + (reinterpret_cast<const char *>(o.tot_d) - ctx->poses_d.as<const char>()));
     const int32_t *cov_h = reinterpret_cast<const int32_t *>(tot_h + (P + 1));
     const int32_t *st_h = reinterpret_cast<const int32_t *>(pin + o.st_off);
-    PCP_HIP(ctx, hipMemcpyAsync(pin, o.tot_d, o.tc_bytes, hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipMemcpyAsync(pin + o.st_off, o.stats, S_N * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    if (C) PCP_HIP(ctx, hipMemcpyAsync(pin + o.fl_off, o.flags_d, C, hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipStreamSynchronize(st));
     if (C) std::memcpy(cell_flags, pin + o.fl_off, C);
     prof_resolve(ctx);
     // runOptimization candidate loop (:464-475): strict '>' keeps the first maximum

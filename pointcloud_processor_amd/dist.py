@@ -53,8 +53,11 @@ def reduce_scores(total_local: np.ndarray, lo: int, hi: int, total: int, dist_mo
     vec = np.full(total, -np.inf, np.float64)
     vec[lo:hi] = np.asarray(total_local, np.float64)
     vec = _reduce(vec, "max", dist_mod, device)
-    best, best_idx = -np.inf, -1
-    for k in range(total):          # runOptimization :471-474, first maximum wins
-        if vec[k] > best:
-            best, best_idx = vec[k], k
-    return vec, best_idx, best
+    # runOptimization :471-474: `if (total > best)` from best = -inf, so the first maximum wins
+    # and no NaN or -inf total is ever taken -- np.argmax over the NaN-free values gives the
+    # first occurrence of the maximum
+    finite = np.where(np.isnan(vec), -np.inf, vec)
+    if total == 0 or not (finite.max() > -np.inf):
+        return vec, -1, -np.inf
+    best_idx = int(np.argmax(finite))
+    return vec, best_idx, float(finite[best_idx])
