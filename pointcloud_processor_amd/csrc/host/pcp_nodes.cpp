@@ -85,6 +85,7 @@ MultiDevice::~MultiDevice() {
 // ---- pointcloud_filter -----------------------------------------------------------------------
 PointCloud2 SimplifiedScanMatcher::processCloudSimple(const PointCloud2 &in,
                                                       const std::string &vehicle_type) {
+    err_.clear();
     // cropFrontArea parameter selection (:93-101)
     double front, side, height;
     if (vehicle_type == "robot") {
@@ -118,6 +119,7 @@ PointCloud2 SimplifiedScanMatcher::processCloudSimple(const PointCloud2 &in,
 GnssGicpMatcher::Output GnssGicpMatcher::processPointClouds(bool origin_set,
                                                            const Transform *robot_tf,
                                                            const Transform *zx120_tf) {
+    err_.clear();
     Output o;
     o.merged = make_xyzrgb_cloud(nullptr, 0, "map");
     o.robot_colored = o.merged;
@@ -160,6 +162,7 @@ GnssGicpMatcher::Output GnssGicpMatcher::processPointClouds(bool origin_set,
 
 // ---- virtual_lidar ---------------------------------------------------------------------------
 void SimplifiedDualLidarOptimizer::terrainCallback(const PointCloud2 &msg) {
+    err_.clear();
     terrain_cloud_ = true;
     pcp_cloud_view v{};
     if (!cloud_view(msg, v, &err_)) return;
@@ -172,6 +175,7 @@ void SimplifiedDualLidarOptimizer::terrainCallback(const PointCloud2 &msg) {
 }
 
 void SimplifiedDualLidarOptimizer::zx120PointsCallback(const PointCloud2 &msg) {
+    err_.clear();
     pcp_cloud_view v{};
     if (!cloud_view(msg, v, &err_)) return;
     if (multi_) {
@@ -182,6 +186,7 @@ void SimplifiedDualLidarOptimizer::zx120PointsCallback(const PointCloud2 &msg) {
 }
 
 void SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg) {
+    err_.clear();
     pcp_cloud_view v;
     std::string why;
     if (!cloud_view(msg, v, &why)) {   // fromROSMsg would throw: logged, nothing rebuilt
@@ -214,6 +219,7 @@ void SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg
 void SimplifiedDualLidarOptimizer::setExcavationGrid(const std::vector<double> &xyz,
                                                      const std::vector<float> &normals,
                                                      const double grid_bbox[6]) {
+    err_.clear();
     n_cells_ = xyz.size() / 3;
     flags_.assign(n_cells_, 0);   // fresh GridCells (:259, ctor :34-43)
     std::memcpy(bbox_, grid_bbox, sizeof(bbox_));
@@ -239,6 +245,7 @@ static void appendf(std::string &s, const char *fmt, ...) {
 SimplifiedDualLidarOptimizer::Result SimplifiedDualLidarOptimizer::runOptimization(
     const Transform *zx120_base) {
     Result r;
+    err_.clear();
     // :455 -- no grid, no terrain message, or getZX120Position failed
     if (n_cells_ == 0 || !terrain_cloud_ || !zx120_base) return r;
     // getZX120Position (:342-358)

@@ -98,6 +98,7 @@ class SimplifiedScanMatcher {
     explicit SimplifiedScanMatcher(Device &dev) : dev_(dev) {}
     SimplifiedScanMatcher(Device &dev, const Params &p) : dev_(dev), p_(p) {}
     Params &params() { return p_; }
+    const Params &params() const { return p_; }
     // callbacks (:52-62): the returned message is what the node publishes
     PointCloud2 robotCloudCallback(const PointCloud2 &msg) { return processCloudSimple(msg, "robot"); }
     PointCloud2 backhoeCloudCallback(const PointCloud2 &msg) { return processCloudSimple(msg, "backhoe"); }
@@ -151,6 +152,7 @@ class ExcavationTerrainGenerator {
     explicit ExcavationTerrainGenerator(Device &dev) : dev_(dev) {}
     ExcavationTerrainGenerator(Device &dev, const Params &p) : dev_(dev), p_(p) {}
     Params &params() { return p_; }
+    const Params &params() const { return p_; }
     // matchedCloudCallback (:259-326); zx120_base = TF map -> zx120/base_link, nullptr = the
     // lookup threw: the input is republished unchanged (as when disabled, :260-263, :276-279)
     Output matchedCloudCallback(const PointCloud2 &msg, const Transform *zx120_base);
@@ -218,6 +220,7 @@ class SimplifiedDualLidarOptimizer {
     SimplifiedDualLidarOptimizer(MultiDevice &md, const Params &p)
         : dev_(md.rank0()), multi_(md.get()), p_(p) {}
     Params &params() { return p_; }
+    const Params &params() const { return p_; }
     // excavationAreaCallback (:164-178): GPU normals + 3-D cell grid from /excavation_area;
     // an empty cloud keeps the previous grid (:168)
     void excavationAreaCallback(const PointCloud2 &msg);

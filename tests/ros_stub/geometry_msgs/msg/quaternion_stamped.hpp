@@ -1,0 +1,2 @@
+#pragma once
+#include "ros_stub_all.hpp"
