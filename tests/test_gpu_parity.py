@@ -196,6 +196,36 @@ def test_filter_merge_full_c3_frame(gpu, oracle):
     np.testing.assert_array_equal(out[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
 
 
+@pytest.mark.parametrize("second", ["direct", "unbounded", "empty"])
+def test_filter_merge_sparse_survivors(gpu, oracle, second):
+    """A certainly-voxelised cloud whose ~3,000 survivors are spread over ~1,500 crop tiles
+    (one sort tile spans more crop tiles than the first sort pass stages in LDS), batched with a
+    second cloud that is voxelised the same way, through the compaction-kernel path (unbounded
+    box) or is empty; three calls in a row (the crop's block tickets reset)."""
+    rng = np.random.default_rng(77)
+    n = 6_000_000
+    a = rng.uniform(20.0, 40.0, (n, 4)).astype(np.float32)          # outside BOX
+    idx = rng.choice(n, 3000, replace=False)
+    a[idx, :3] = rng.uniform([0.5, -5.0, 0.0], [10.0, 5.0, 5.0], (3000, 3)).astype(np.float32)
+    b = synth.lidar_cloud(150_000, seed=3) if second != "empty" else np.zeros((0, 4), np.float32)
+    box_b = BOX if second != "unbounded" else np.array([-np.inf, np.inf] * 3)
+    tfs = _tfs()
+    rgbs = [(255, 0, 0), (0, 0, 255)]
+    parts = []
+    for c, box, tf, rgb in zip([a, b], [BOX, box_b], tfs, rgbs):
+        if c.shape[0] == 0:
+            continue
+        k = oracle.crop_box(c, box)
+        v, _, _, pt = oracle.voxel_grid(c[k], 0.05)
+        assert not pt
+        parts.append(oracle.transform_rgb(v, *tf, rgb))
+    ref = np.concatenate(parts)
+    for _ in range(3):
+        out, per = gpu.filter_merge([a, b], [BOX, box_b], 0.05, tfs, rgbs)
+        assert list(per)[:len(parts)] == [p.shape[0] for p in parts]
+        np.testing.assert_array_equal(out[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
+
+
 def test_filter_merge_device_graph_replay(gpu, oracle):
     """Device-resident inputs: the pipeline is captured into a hipGraph and replayed; every
     replay must equal the eager host-path result and the oracle."""
