@@ -269,10 +269,21 @@ def _timed(step, args, dist, on_gpu, dev):
     return float(t.item()), float(uu.item()), res
 
 
+def _fan_npw(n_poses):
+    """Poses per wave of the production fan kernel: the library's rule (pcp_vlidar.hip
+    raycast_fan_impl) -- PCP_FAN_NPW (default 8), halved until it divides the XCD pose chunk."""
+    npw = int(os.environ.get("PCP_FAN_NPW", "8"))
+    npw = npw if npw in (1, 2, 4, 8, 16, 32) else 1
+    while npw > 1 and n_poses % (8 * npw):
+        npw //= 2
+    return npw
+
+
 def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
     """Roofline of k_raycast_fan from the kernel's own request counts:
-    requested bytes = 2 B per z-band probe + 8 B per candidate (its step) + 8 B per block
-    directory load + 12 B per point record loaded + 16 B per ray (azimuth table) + 8 B per wave
+    requested bytes = 2 B per z-band probe (8 B per fine-window record) + 8 B per candidate
+    (its step) + 8 B per block directory load + 12 B per point record loaded + 16 B per ray and
+    wave-pose group (azimuth table, loaded once for the wave's NPW poses) + 8 B per wave
     partial.  These are the bytes the kernel's loads and stores ask for (served by L1/L2/MALL:
     the 1M-pt terrain's working set is cache-resident); the HBM-side bytes are the PMC
     `traffic`."""
@@ -283,8 +294,10 @@ def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
     probe_b = 8.0 if layout == "fine" else 2.0
     rays = poses.shape[0] * fan.n_az * fan.n_el
     waves = poses.shape[0] * ((fan.n_az * fan.n_el + 63) // 64)
+    npw = _fan_npw(poses.shape[0]) if layout == "fine" else 1
     req = probe_b * st["samples_visited"] + 8.0 * st["scanned_stencils"] \
-        + 8.0 * st["directory_loads"] + 12.0 * st["point_tests"] + 16.0 * rays + 8.0 * waves
+        + 8.0 * st["directory_loads"] + 12.0 * st["point_tests"] + 16.0 * rays / npw \
+        + 8.0 * waves
     ref_model = 64.0 * units_per_launch + 12.0 * st["point_tests"]
     traffic = _traffic_from_profiles("fan")
     achieved = _gbs(req, avg_kernel_s)
@@ -294,12 +307,13 @@ def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
         "traffic": traffic,
         "traffic_gbs": _gbs(traffic, avg_kernel_s),
         "traffic_frac": (_gbs(traffic, avg_kernel_s) or 0.0) / HBM_PEAK_GBS if traffic else None,
-        "kernel": ("k_raycast_fan<0, 64, true, 8, 1>" if layout == "fine"
+        "kernel": (f"k_raycast_fan_xcd<0, 64, true, 8, 4, true, {npw}>" if layout == "fine"
                    else "k_raycast_fan<0, 64, true, 7, 0>"),
+        "poses_per_wave": npw,
         "avg_kernel_ms": avg_kernel_s * 1e3, "scan_layout": layout,
         "requested_bytes_per_launch": req,
         "model": f"requested bytes: {probe_b:.0f} B/probe + 8 B/candidate (its step) + 8 B/"
-                 "directory load + 12 B/point record + 16 B/ray + 8 B/wave "
+                 "directory load + 12 B/point record + 16 B/ray/NPW + 8 B/wave "
                  "(pcp_raycast_fan_stats counts); traffic = PMC FETCH(x2)+WRITE per launch "
                  "(profiles/pmc_traffic.json)",
         "limiter": "vector-memory gather path (TA/TD busy, L1 tag lookups per instruction; "

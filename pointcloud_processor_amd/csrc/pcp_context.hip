@@ -284,6 +284,10 @@ int pcp_create(int device, pcp_ctx **out) {
     if (!ctx) return PCP_E_NOMEM;
     ctx->device = device;
     if (const char *fb = std::getenv("PCP_FAN_BATCH")) ctx->fan_batch = std::atoi(fb);
+    if (const char *fw = std::getenv("PCP_FAN_NPW")) {
+        const int v = std::atoi(fw);
+        ctx->fan_npw = (v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 1;
+    }
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
     if (const char *tf = std::getenv("PCP_TERRAIN_FINE")) ctx->terrain_fine = std::atoi(tf);
     if (const char *tt = std::getenv("PCP_FINE_TILE")) ctx->fine_tile = std::atoi(tt);

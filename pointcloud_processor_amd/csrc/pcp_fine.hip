@@ -223,7 +223,7 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     const float4 *pts = g.pts.as<const float4>();
     // 1. global z order
     size_t t1 = 0, t2 = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, t1, (unsigned long long *)nullptr,
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, (unsigned long long *)nullptr,
                                        (unsigned long long *)nullptr, (uint32_t *)nullptr,
                                        (uint32_t *)nullptr, (int)n, 0, 64, st);
     PCP_HIP(ctx, ctx->scratch[2].ensure((size_t)n * 24 + 64));   // keys x2, vals x2
@@ -256,7 +256,7 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     // 4. pairs (window, z rank), stable sort by window
     int wbits = 1;
     while ((1ull << wbits) < nw) ++wbits;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, t2, (uint32_t *)nullptr, (uint32_t *)nullptr,
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t2, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                        (uint32_t *)nullptr, (uint32_t *)nullptr, (int)np, 0, wbits,
                                        st);
     PCP_HIP(ctx, ctx->scratch[5].ensure((size_t)np * 16 + 64));

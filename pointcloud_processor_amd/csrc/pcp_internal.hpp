@@ -234,6 +234,7 @@ struct pcp_ctx {
     int steps_K = 0;
     int num_cus = 256;                       // multiprocessors of the device
     int fan_batch = 0;                       // fan kernel variant (PCP_FAN_BATCH), A/B only
+    int fan_npw = 8;                         // poses per wave of the fan kernel (PCP_FAN_NPW)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
     int fine_tile = 1;                       // fine records in 4 x 4 tiles (PCP_FINE_TILE)
     int terrain_fine = 2;                    // fine-window layout of that copy, cells of c / F

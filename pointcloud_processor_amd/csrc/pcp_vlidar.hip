@@ -914,24 +914,35 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // termination on near-flat terrain).  Each wave writes its blocked-ray count and its
 // sample-query count to its own slot: the per-pose sums are formed by k_fan_reduce in a fixed
 // order (deterministic, no same-address atomics).
-template <int MODE, int BS, bool ZB = true, int FN = 0, bool UE = false>
-__device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t rblock) {
+template <int MODE, int BS, bool ZB = true, int FN = 0, bool UE = false, int NPW = 1>
+__device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p0, uint32_t rblock) {
     const uint32_t ray = rblock * BS + threadIdx.x;
     const uint32_t wid = ray >> 6;
     const bool active = ray < a.rays;
+    // the ray's direction in the pose frame, loaded once for the wave's NPW poses (poses
+    // p0 .. p0 + NPW - 1 share the fan: the table loads are a quarter of the launch's
+    // vector-memory bytes at NPW 1)
+    double lx = 0.0, ly = 0.0, lz = 0.0;
+    if (active && a.present) {
+        // UE (n_az % 64 == 0): the wave's ring is uniform, a scalar division of its first ray
+        const uint32_t j = UE ? (rblock * BS + (threadIdx.x & ~63u)) / (uint32_t)a.n_az
+                              : ray / (uint32_t)a.n_az;
+        const uint32_t i = ray - j * (uint32_t)a.n_az;
+        const double cej = a.ce[j];
+        lx = cej * a.ca[i];
+        ly = cej * a.sa[i];
+        lz = a.se[j];
+    }
+#pragma unroll 1
+    for (int q = 0; q < NPW; ++q) {
+    const uint32_t p = p0 + (uint32_t)q;
     const uint32_t wslot = p * a.waves + wid;
     unsigned long long t0 = 0, t1 = 0, t2 = 0;
     if (MODE == FAN_STAMPS) t0 = __builtin_amdgcn_s_memtime();
     int hit = -1;
     uint32_t cnt[3] = {0, 0, 0};
     if (active && a.present) {
-        // UE (n_az % 64 == 0): the wave's ring is uniform, a scalar division of its first ray
-        const uint32_t j = UE ? (rblock * BS + (threadIdx.x & ~63u)) / (uint32_t)a.n_az
-                              : ray / (uint32_t)a.n_az;
-        const uint32_t i = ray - j * (uint32_t)a.n_az;
         const double *P = a.pose + 8 * (size_t)p;
-        const double cej = a.ce[j];
-        const double lx = cej * a.ca[i], ly = cej * a.sa[i], lz = a.se[j];
         const double cy = P[5], sy = P[6];
         const double dx = cy * lx - sy * ly;
         const double dy = sy * lx + cy * ly;
@@ -957,14 +968,14 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
             make_uint2((uint32_t)__popcll(bal), u);
     }
     if (MODE == FAN_STATS) {   // per-wave slots [4][P * waves], summed by k_sum_u64
-        const size_t nw = (size_t)gridDim.x * (BS / 64);
+        const size_t nw = (size_t)a.P * a.waves;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {   // [3] directory loads: one per scan (none: FN, the
+        for (int c = 0; c < 4; ++c) {   // [3] directory loads: one per scan (none: FN, the
                                         // probe's record is the directory)
-            unsigned long long v = q < 3 ? cnt[q] : (FN ? 0u : cnt[1]);
+            unsigned long long v = c < 3 ? cnt[c] : (FN ? 0u : cnt[1]);
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if ((threadIdx.x & 63) == 0 && wid < a.waves) a.stats[q * nw + wslot] = v;
+            if ((threadIdx.x & 63) == 0 && wid < a.waves) a.stats[c * nw + wslot] = v;
         }
     }
     if (MODE == FAN_STAMPS && (threadIdx.x & 63) == 0 && wid < a.waves) {
@@ -975,6 +986,7 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p, uint32_t 
         o[2] = t2;
         o[3] = t3;
     }
+    }   // poses of the wave
 }
 
 // The fan kernel: one wave per workgroup (a finished wave's slot refills without waiting for
@@ -990,11 +1002,13 @@ k_raycast_fan(FanArgs a, uint32_t P) {
 // A/B: XCD-chunked placement (P % 8 == 0): workgroup b runs on XCD b % 8, which takes the
 // contiguous pose chunk [x P/8, (x + 1) P/8) -- neighbouring candidate poses, overlapping fans
 // -- interleaved inside the XCD as above
-template <int MODE, int BS = 64, bool ZB = true, int W = 8, int FN = 1, bool UE = true>
+// NPW > 1: each wave marches its rays for NPW consecutive poses of the chunk (one direction-
+// table load for all of them); P % (8 NPW) == 0, grid = waves * P / NPW
+template <int MODE, int BS = 64, bool ZB = true, int W = 8, int FN = 1, bool UE = true, int NPW = 1>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(W, W)))
 k_raycast_fan_xcd(FanArgs a, uint32_t P) {
-    const uint32_t pc = P >> 3, j = blockIdx.x >> 3;
-    fan_body<MODE, BS, ZB, FN, UE>(a, (blockIdx.x & 7u) * pc + j % pc, j / pc);
+    const uint32_t pc = P >> 3, gpc = pc / NPW, j = blockIdx.x >> 3;
+    fan_body<MODE, BS, ZB, FN, UE, NPW>(a, (blockIdx.x & 7u) * pc + (j % gpc) * NPW, j / gpc);
 }
 
 // A/B: pose-major 2-D grid (blockIdx.y = pose), BS-thread workgroups
@@ -1052,6 +1066,25 @@ k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves, uint32_t P, uint32_
         blocked[p] = sb[0] + sb[1] + sb[2] + sb[3];
         units[p] = su[0] + su[1] + su[2] + su[3];
     }
+}
+
+// the production fan kernel (fine tiled windows, uniform rings, XCD pose chunks) with NPW poses
+// per wave; ev0/ev1 non-null: hipExtLaunchKernelGGL's start/stop events
+static void launch_xcd(int npw, const FanArgs &a, uint32_t P, uint32_t waves, hipStream_t st,
+                       hipEvent_t ev0, hipEvent_t ev1) {
+    const dim3 g(waves * P / (uint32_t)npw);
+#define PCP_XCD(N)                                                                          \
+    hipExtLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN, 64, true, 8, 4, true, N>), g, dim3(64), \
+                          0, st, ev0, ev1, 0, a, P)
+    switch (npw) {
+    case 2: PCP_XCD(2); break;
+    case 4: PCP_XCD(4); break;
+    case 8: PCP_XCD(8); break;
+    case 16: PCP_XCD(16); break;
+    case 32: PCP_XCD(32); break;
+    default: PCP_XCD(1); break;
+    }
+#undef PCP_XCD
 }
 
 static VisEnv make_env(pcp_ctx *ctx, const pcp_vl_params *p, const double *steps_d, int K) {
@@ -1424,6 +1457,9 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
     // the fine-window kernels (28 VGPRs, 8 waves per SIMD), the ring index a
     // scalar when n_az % 64 == 0 (UE); the coarse layouts' kernel otherwise
     const bool fine = a.g.frec != nullptr, ue = a.uniform_el != 0, tile = a.g.ftile != 0;
+    // poses per wave: the largest of ctx->fan_npw, ..., 2, 1 that divides the XCD pose chunk
+    int npw = ctx->fan_npw;
+    while (npw > 1 && P % (8 * npw) != 0) npw >>= 1;
 #define PCP_FAN_LAUNCH(MODE)                                                                   \
     do {                                                                                       \
         if (fine && tile && ue)                                                                \
@@ -1480,9 +1516,8 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
         PCP_HIP(ctx, hipEventCreate(&e1));
         PCP_HIP(ctx, hipEventRecord(e0, st));
         for (int r = 0; r < burst; ++r) {
-            if (fine && tile && ue && P % 8 == 0)
-                hipLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN, 64, true, 8, 4>), grid1, dim3(64),
-                                   0, st, a, (uint32_t)P);
+            if (fine && tile && ue && P % (8 * npw) == 0)
+                launch_xcd(npw, a, (uint32_t)P, waves, st, nullptr, nullptr);
             else if (fine && ue && P % 8 == 0)
                 hipLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN>), grid1, dim3(64), 0, st, a,
                                    (uint32_t)P);
@@ -1508,9 +1543,8 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
         default:
             // XCD-chunked placement (each XCD's L2 serves neighbouring poses' overlapping fans):
             // 0.61 vs 0.63 ms on C2
-            if (fine && tile && ue && P % 8 == 0)
-                hipExtLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN, 64, true, 8, 4>), grid1,
-                                      dim3(64), 0, st, kt.a, kt.b, 0, a, (uint32_t)P);
+            if (fine && tile && ue && P % (8 * npw) == 0)
+                launch_xcd(npw, a, (uint32_t)P, waves, st, kt.a, kt.b);
             else if (fine && ue && P % 8 == 0)
                 hipExtLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN>), grid1, dim3(64), 0, st, kt.a,
                                       kt.b, 0, a, (uint32_t)P);
