@@ -137,21 +137,32 @@ k_win_place(const float4 *__restrict__ pts, const uint32_t *__restrict__ zord,
 __global__ void __launch_bounds__(kThreads)
 k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ cstart, CellMap m, double c,
        uint32_t fnx, uint32_t fny, uint32_t rz, uint32_t tsteps, int tile,
-       uint2 *__restrict__ frec) {
+       uint2 *__restrict__ frec, uint16_t *__restrict__ fband, uint32_t *__restrict__ fstart) {
     const uint32_t nw = fnx * fny, w = blockIdx.x * kThreads + threadIdx.x;
-    const uint32_t tx = (fnx + 3) >> 2, ty = (fny + 3) >> 2;
-    const size_t plane = tile ? (size_t)tx * ty * 16 : (size_t)nw;
-    if (tile && w < tx * ty * 16u) {   // padding records of the tiles (never windows)
-        const uint32_t t = w >> 4, sub = w & 15u;
-        const uint32_t px = (t % tx) * 4u + (sub & 3u), py = (t / tx) * 4u + (sub >> 2);
+    // tiles of T x T records: 4 x 4 8-byte records (tile 1) or 8 x 8 split records (tile 2),
+    // 128 bytes of probe data each
+    const uint32_t sh = tile == 2 ? 3u : 2u, T = 1u << sh, TS = T * T;
+    const uint32_t tx = (fnx + T - 1) >> sh, ty = (fny + T - 1) >> sh;
+    const size_t plane = tile ? (size_t)tx * ty * TS : (size_t)nw;
+    auto put = [&](size_t r, uint32_t start, uint32_t band) {
+        if (tile == 2) {
+            fband[r] = (uint16_t)band;
+            fstart[r] = start;
+        } else {
+            frec[r] = make_uint2(start, band);
+        }
+    };
+    if (tile && w < tx * ty * TS) {   // padding records of the tiles (never windows)
+        const uint32_t t = w >> (2 * sh), sub = w & (TS - 1);
+        const uint32_t px = (t % tx) * T + (sub & (T - 1)), py = (t / tx) * T + (sub >> sh);
         if (px >= fnx || py >= fny)
-            for (uint32_t iz = 0; iz < rz; ++iz) frec[(size_t)iz * plane + w] = make_uint2(0u, 0x00FFu);
+            for (uint32_t iz = 0; iz < rz; ++iz) put((size_t)iz * plane + w, 0u, 0x00FFu);
     }
     if (w >= nw) return;
-    // record index of (w, iz): x-fastest, or 4 x 4 xy tiles of 16 records (one 128-byte line)
+    // record index of (w, iz): x-fastest, or T x T xy tiles
     const uint32_t wx = w % fnx, wy = w / fnx;
-    const size_t base = tile ? ((size_t)((wy >> 2) * tx + (wx >> 2)) << 4) | ((wy & 3u) << 2) |
-                                   (wx & 3u)
+    const size_t base = tile ? ((size_t)((wy >> sh) * tx + (wx >> sh)) << (2 * sh)) |
+                                   ((wy & (T - 1)) << sh) | (wx & (T - 1))
                              : (size_t)w;
     const uint32_t s = cstart[w] + w, e = cstart[w + 1] + w;   // e: the sentinel
     wpts[e] = make_float4(__int_as_float(0x7FC00000), __int_as_float(0x7FC00000), -INFINITY,
@@ -186,7 +197,7 @@ k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ cstart, CellMap m
             const uint32_t hi2 = (hi == 255u) ? 255u : min(hi + tsteps, 255u);
             band = lo2 | (hi2 << 8);
         }
-        frec[(size_t)iz * plane + base] = make_uint2(jt, band);
+        put((size_t)iz * plane + base, jt, band);
     }
 }
 
@@ -202,8 +213,11 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     const uint64_t fnx = (uint64_t)F * g.nx, fny = (uint64_t)F * g.ny;
     const uint64_t rz = (uint64_t)(g.nz > 1 ? g.nz - 1 : 0), nw = fnx * fny;
     // caps: 32-bit record byte offsets (< 2^29 records), 24-bit probe multiplies, window keys
-    const int tile = ctx->fine_tile ? 1 : 0;
-    const uint64_t nrec = tile ? ((fnx + 3) / 4) * ((fny + 3) / 4) * 16 * rz : nw * rz;
+    const int tile = ctx->fine_tile == 2 ? 2 : ctx->fine_tile ? 1 : 0;
+    const uint64_t T = tile == 2 ? 8 : 4;
+    const uint64_t nrec = tile ? ((fnx + T - 1) / T) * ((fny + T - 1) / T) * T * T * rz : nw * rz;
+    const size_t band_bytes = ((size_t)nrec * 2 + 255) & ~(size_t)255;
+    const size_t rec_bytes = tile == 2 ? band_bytes + (size_t)nrec * 4 : (size_t)nrec * sizeof(uint2);
     if (rz == 0 || nrec >= (1ull << 29) || fnx >= (1ull << 24) || fny * rz >= (1ull << 24)) {
         g.fine_fail = true;
         return PCP_OK;
@@ -275,7 +289,7 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     // the copy is an optional speed-up: an allocation failure keeps the other layouts
     const size_t nent = (size_t)np + nw;
     if (g.wpts.ensure(nent * sizeof(float4)) != hipSuccess ||
-        g.frec.ensure((size_t)nrec * sizeof(uint2)) != hipSuccess) {
+        g.frec.ensure(rec_bytes) != hipSuccess) {
         (void)hipGetLastError();
         g.wpts.release();
         g.frec.release();
@@ -291,13 +305,16 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     const uint64_t nthr = std::max<uint64_t>(nw, tile ? nrec / rz : 0);
     hipLaunchKernelGGL(k_frec, dim3((unsigned)((nthr + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                        st, g.wpts.as<float4>(), (const uint32_t *)cstart, m, g.c, (uint32_t)fnx,
-                       (uint32_t)fny, (uint32_t)rz, tsteps, tile, g.frec.as<uint2>());
+                       (uint32_t)fny, (uint32_t)rz, tsteps, tile, g.frec.as<uint2>(),
+                       g.frec.as<uint16_t>(),
+                       reinterpret_cast<uint32_t *>(g.frec.as<char>() + band_bytes));
     PCP_CHECK_LAUNCH(ctx);
     g.frx = (uint32_t)fnx;
     g.fry = (uint32_t)fny;
     g.frz = (uint32_t)rz;
     g.ffine = (float)F;
     g.ftile = tile;
+    g.fstart_off = tile == 2 ? band_bytes : 0;
     g.fine_ok = true;
     return PCP_OK;
 }

@@ -67,6 +67,10 @@ GridView GridIndex::view() const {
     v.frz = fine_ok ? frz : 0u;
     v.ffine = fine_ok ? ffine : 0.0f;
     v.ftile = fine_ok ? ftile : 0;
+    v.fband = (fine_ok && ftile == 2) ? frec.as<const uint16_t>() : nullptr;
+    v.fstart = (fine_ok && ftile == 2)
+                   ? reinterpret_cast<const uint32_t *>(frec.as<const char>() + fstart_off)
+                   : nullptr;
     v.fus_off = (float)(rm * v.inv_c / (double)kZq);
     return v;
 }

@@ -132,7 +132,11 @@ struct GridView {               // POD passed to kernels by value
     const float4 *wpts;
     uint32_t frx, fry, frz;
     float fus_off, ffine;
-    int32_t ftile;              // records in 4 x 4 xy tiles (PCP_FINE_TILE)
+    int32_t ftile;              // records in 4 x 4 xy tiles (1) or split (2), PCP_FINE_TILE
+    // ftile 2: the record split in two arrays of 8 x 8 xy tiles -- the probe's 2-byte
+    // thresholds (one 128-byte line per tile) and the 4-byte walk start, read by candidates only
+    const uint16_t *fband;
+    const uint32_t *fstart;
 };
 constexpr float kZq = 2.0f / 250.0f;   // z band step, cells (2 cells = 250 steps)
 
@@ -153,6 +157,7 @@ struct GridIndex {
     uint32_t frx = 0, fry = 0, frz = 0;
     float ffine = 0.0f;
     int32_t ftile = 0;
+    size_t fstart_off = 0;       // ftile 2: byte offset of the start array inside frec
     bool occ2_ok = false;        // occ2 built (only indices queried by stencil_any need it)
     GridView view() const;
     void release() {
@@ -236,7 +241,8 @@ struct pcp_ctx {
     int fan_batch = 0;                       // fan kernel variant (PCP_FAN_BATCH), A/B only
     int fan_npw = 8;                         // poses per wave of the fan kernel (PCP_FAN_NPW)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
-    int fine_tile = 1;                       // fine records in 4 x 4 tiles (PCP_FINE_TILE)
+    int fine_tile = 2;                       // fine records: 0 x-fastest, 1 4 x 4 tiles, 2 split
+                                             // in 8 x 8 tiles (PCP_FINE_TILE)
     int terrain_fine = 2;                    // fine-window layout of that copy, cells of c / F
                                              // (PCP_TERRAIN_FINE = F; 0: the 2x2x2 blocks)
     int terrain_queries = 0;                 // queries since the last pcp_set_terrain

@@ -231,6 +231,9 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
                                      const double *__restrict__ steps, int K, double end,
                                      float r2, float rexit, uint32_t *cnt = nullptr) {
     if (FN == 2) {
+        if (g.frec && g.ftile == 2)
+            return march<STATS, ZB, NB, 8>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, rexit,
+                                           cnt);
         if (g.frec && g.ftile)
             return march<STATS, ZB, NB, 4>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, rexit,
                                            cnt);
@@ -253,7 +256,7 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
     const float Ay = ((float)py - g.flo_y) * g.finv_c + fdy * h;
     const float Az = ((float)pz - g.flo_z) * g.finv_c + fdz * h;
     const uint32_t nx = (uint32_t)g.nx, ny = (uint32_t)g.ny;
-    if (FN == 1 || FN == 4) {
+    if (FN == 1 || FN == 4 || FN == 8) {
         // fine units for x, y (the fine cell of the sample, (q - o) / c_f = F (f + fzoff)),
         // coarse stencil-corner units for z; out-of-range cells are clamped: a sample outside
         // the grid has no point within r, and a clamped record can only cost a walk whose exact
@@ -262,7 +265,8 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
         const float F = g.ffine;
         const float D2x = F * Dx, D2y = F * Dy, A2x = F * (Ax + g.fzoff), A2y = F * (Ay + g.fzoff);
         const uint32_t mx = g.frx - 1, my = g.fry - 1, mz = g.frz - 1;
-        const uint32_t rx = FN == 4 ? (g.frx + 3) >> 2 : g.frx, ry = FN == 4 ? (g.fry + 3) >> 2 : g.fry;
+        const uint32_t rx = FN == 4 ? (g.frx + 3) >> 2 : FN == 8 ? (g.frx + 7) >> 3 : g.frx;
+        const uint32_t ry = FN == 4 ? (g.fry + 3) >> 2 : FN == 8 ? (g.fry + 7) >> 3 : g.fry;
         for (int k = klo; k <= khi; ++k) {
             const float kf = (float)k;
             const float fx = __builtin_fmaf(D2x, kf, A2x);
@@ -274,10 +278,17 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
             // 24-bit multiply-adds (full rate): build_fine caps frx, fry * frz below 2^24.
             // FN 4: records in 4 x 4 xy tiles, one 128-byte line each (a wave's arc of probes
             // touches fewer lines whatever its direction); rx, ry are then the tile counts.
-            const uint32_t ri = FN == 4 ? (mad_u24(rx, mad_u24(ry, iz, iy >> 2), ix >> 2) << 4) |
+            // FN 8: the split records in 8 x 8 tiles, the probe reads only the 2-byte thresholds
+            // (64 per 128-byte line: a quarter of FN 4's bytes through the texture path) and a
+            // candidate then its 4-byte walk start
+            const uint32_t ri = FN == 8 ? (mad_u24(rx, mad_u24(ry, iz, iy >> 3), ix >> 3) << 6) |
+                                              ((iy & 7u) << 3) | (ix & 7u)
+                              : FN == 4 ? (mad_u24(rx, mad_u24(ry, iz, iy >> 2), ix >> 2) << 4) |
                                               ((iy & 3u) << 2) | (ix & 3u)
                                         : mad_u24(rx, mad_u24(ry, iz, iy), ix);
-            const uint2 R = ld_rec(g.frec, ri);
+            uint2 R;
+            if (FN == 8) R.y = ld_u16o(g.fband, ri);
+            else R = ld_rec(g.frec, ri);
             // height above the block floor in kZq steps against the record's thresholds
             const float us = __builtin_fmaf(fz - (float)iz, 1.0f / kZq, g.fus_off);
             const bool cand = (us < (float)((R.y >> 8) & 255u)) & (us > (float)(R.y & 255u));
@@ -289,7 +300,8 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
                 const float qx = (float)(px + dx * s);
                 const float qy = (float)(py + dy * s);
                 const float qz = (float)(pz + dz * s);
-                if (scan_window<STATS>(g.wpts, R.x, qx, qy, qz, r2, rexit, cnt)) return k;
+                const uint32_t w0 = FN == 8 ? ld_u32o(g.fstart, ri) : R.x;
+                if (scan_window<STATS>(g.wpts, w0, qx, qy, qz, r2, rexit, cnt)) return k;
             }
         }
         return -1;
@@ -896,6 +908,7 @@ struct FanArgs {
 };
 
 enum { FAN_PLAIN = 0, FAN_STATS = 1, FAN_STAMPS = 2 };
+constexpr int kStepLds = 256;   // step tables up to this long are read from LDS by the fan
 
 // sum over the 64 lanes (all active): rotate-adds inside each 16-lane row (DPP row_ror 8, 4,
 // 2, 1), then the four row sums by readlane -- no LDS crossbar round trips
@@ -914,7 +927,8 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 // termination on near-flat terrain).  Each wave writes its blocked-ray count and its
 // sample-query count to its own slot: the per-pose sums are formed by k_fan_reduce in a fixed
 // order (deterministic, no same-address atomics).
-template <int MODE, int BS, bool ZB = true, int FN = 0, bool UE = false, int NPW = 1>
+template <int MODE, int BS, bool ZB = true, int FN = 0, bool UE = false, int NPW = 1,
+          bool SL = false>
 __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p0, uint32_t rblock) {
     const uint32_t ray = rblock * BS + threadIdx.x;
     const uint32_t wid = ray >> 6;
@@ -923,6 +937,15 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p0, uint32_t
     // p0 .. p0 + NPW - 1 share the fan: the table loads are a quarter of the launch's
     // vector-memory bytes at NPW 1)
     double lx = 0.0, ly = 0.0, lz = 0.0;
+    // SL: the step table in LDS (the launcher guarantees K <= kStepLds): one load per 64
+    // entries per workgroup, then a candidate's step is an LDS read instead of a gather through
+    // the texture path
+    __shared__ double s_steps[SL ? kStepLds : 1];
+    if (SL) {
+        for (int q = threadIdx.x; q < a.K; q += BS) s_steps[q] = a.steps[q];
+        __syncthreads();
+    }
+    const double *steps = SL ? s_steps : a.steps;
     if (active && a.present) {
         // UE (n_az % 64 == 0): the wave's ring is uniform, a scalar division of its first ray
         const uint32_t j = UE ? (rblock * BS + (threadIdx.x & ~63u)) / (uint32_t)a.n_az
@@ -951,7 +974,7 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p0, uint32_t
             asm volatile("" ::"v"(dx), "v"(dy));
             t1 = __builtin_amdgcn_s_memtime();
         }
-        hit = march<MODE == FAN_STATS, ZB, 1, FN>(a.g, P[0], P[1], P[2], dx, dy, dz, a.steps,
+        hit = march<MODE == FAN_STATS, ZB, 1, FN>(a.g, P[0], P[1], P[2], dx, dy, dz, steps,
                                                   a.K, 1e300, a.r2, a.rexit, cnt);
     }
     if (MODE == FAN_STAMPS) {
@@ -1008,7 +1031,8 @@ template <int MODE, int BS = 64, bool ZB = true, int W = 8, int FN = 1, bool UE 
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(W, W)))
 k_raycast_fan_xcd(FanArgs a, uint32_t P) {
     const uint32_t pc = P >> 3, gpc = pc / NPW, j = blockIdx.x >> 3;
-    fan_body<MODE, BS, ZB, FN, UE, NPW>(a, (blockIdx.x & 7u) * pc + (j % gpc) * NPW, j / gpc);
+    fan_body<MODE, BS, ZB, FN, UE, NPW, true>(a, (blockIdx.x & 7u) * pc + (j % gpc) * NPW,
+                                             j / gpc);
 }
 
 // A/B: pose-major 2-D grid (blockIdx.y = pose), BS-thread workgroups
@@ -1073,9 +1097,15 @@ k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves, uint32_t P, uint32_
 static void launch_xcd(int npw, const FanArgs &a, uint32_t P, uint32_t waves, hipStream_t st,
                        hipEvent_t ev0, hipEvent_t ev1) {
     const dim3 g(waves * P / (uint32_t)npw);
-#define PCP_XCD(N)                                                                          \
-    hipExtLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN, 64, true, 8, 4, true, N>), g, dim3(64), \
-                          0, st, ev0, ev1, 0, a, P)
+#define PCP_XCD(N)                                                                             \
+    do {                                                                                       \
+        if (a.g.ftile == 2)                                                                    \
+            hipExtLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN, 64, true, 8, 8, true, N>), g,   \
+                                  dim3(64), 0, st, ev0, ev1, 0, a, P);                         \
+        else                                                                                   \
+            hipExtLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN, 64, true, 8, 4, true, N>), g,   \
+                                  dim3(64), 0, st, ev0, ev1, 0, a, P);                         \
+    } while (0)
     switch (npw) {
     case 2: PCP_XCD(2); break;
     case 4: PCP_XCD(4); break;
@@ -1457,12 +1487,19 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
     // the fine-window kernels (28 VGPRs, 8 waves per SIMD), the ring index a
     // scalar when n_az % 64 == 0 (UE); the coarse layouts' kernel otherwise
     const bool fine = a.g.frec != nullptr, ue = a.uniform_el != 0, tile = a.g.ftile != 0;
+    const bool split = a.g.ftile == 2;
     // poses per wave: the largest of ctx->fan_npw, ..., 2, 1 that divides the XCD pose chunk
     int npw = ctx->fan_npw;
     while (npw > 1 && P % (8 * npw) != 0) npw >>= 1;
 #define PCP_FAN_LAUNCH(MODE)                                                                   \
     do {                                                                                       \
-        if (fine && tile && ue)                                                                \
+        if (fine && split && ue)                                                               \
+            hipLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 8, true>), grid1, dim3(64), 0, \
+                               st, a, (uint32_t)P);                                            \
+        else if (fine && split)                                                                \
+            hipLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 8, false>), grid1, dim3(64), 0,\
+                               st, a, (uint32_t)P);                                            \
+        else if (fine && tile && ue)                                                           \
             hipLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 4, true>), grid1, dim3(64), 0, \
                                st, a, (uint32_t)P);                                            \
         else if (fine && tile)                                                                 \
@@ -1479,7 +1516,13 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
     } while (0)
 #define PCP_FAN_LAUNCH_T(MODE)                                                                 \
     do {                                                                                       \
-        if (fine && tile && ue)                                                                \
+        if (fine && split && ue)                                                               \
+            hipExtLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 8, true>), grid1, dim3(64), \
+                                  0, st, kt.a, kt.b, 0, a, (uint32_t)P);                       \
+        else if (fine && split)                                                                \
+            hipExtLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 8, false>), grid1, dim3(64),\
+                                  0, st, kt.a, kt.b, 0, a, (uint32_t)P);                       \
+        else if (fine && tile && ue)                                                           \
             hipExtLaunchKernelGGL((k_raycast_fan<MODE, 64, true, 8, 4, true>), grid1, dim3(64), \
                                   0, st, kt.a, kt.b, 0, a, (uint32_t)P);                       \
         else if (fine && tile)                                                                 \
@@ -1516,9 +1559,9 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
         PCP_HIP(ctx, hipEventCreate(&e1));
         PCP_HIP(ctx, hipEventRecord(e0, st));
         for (int r = 0; r < burst; ++r) {
-            if (fine && tile && ue && P % (8 * npw) == 0)
+            if (fine && tile && ue && P % (8 * npw) == 0 && K <= kStepLds)
                 launch_xcd(npw, a, (uint32_t)P, waves, st, nullptr, nullptr);
-            else if (fine && ue && P % 8 == 0)
+            else if (fine && ue && P % 8 == 0 && K <= kStepLds)
                 hipLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN>), grid1, dim3(64), 0, st, a,
                                    (uint32_t)P);
             else
@@ -1543,9 +1586,9 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
         default:
             // XCD-chunked placement (each XCD's L2 serves neighbouring poses' overlapping fans):
             // 0.61 vs 0.63 ms on C2
-            if (fine && tile && ue && P % (8 * npw) == 0)
+            if (fine && tile && ue && P % (8 * npw) == 0 && K <= kStepLds)
                 launch_xcd(npw, a, (uint32_t)P, waves, st, kt.a, kt.b);
-            else if (fine && ue && P % 8 == 0)
+            else if (fine && ue && P % 8 == 0 && K <= kStepLds)
                 hipExtLaunchKernelGGL((k_raycast_fan_xcd<FAN_PLAIN>), grid1, dim3(64), 0, st, kt.a,
                                       kt.b, 0, a, (uint32_t)P);
             else

@@ -774,16 +774,23 @@ def test_drivable_area_matches_oracle(gpu, oracle, kw):
 
 
 # (PCP_TERRAIN_BLOCKS, PCP_TERRAIN_FINE) -> the layout the scans walk from the first query
-LAYOUTS = [("0", "3", "cells"), ("2", "0", "blocks"), ("2", "2", "fine"), ("2", "3", "fine")]
+# (PCP_TERRAIN_BLOCKS, PCP_TERRAIN_FINE, PCP_FINE_TILE, expected scan layout); fine tile 0:
+# x-fastest 8-byte records, 1: 4 x 4 tiles of them, 2: split records (2-byte thresholds +
+# 4-byte starts) in 8 x 8 tiles
+LAYOUTS = [("0", "3", "1", "cells"), ("2", "0", "1", "blocks"), ("2", "2", "1", "fine"),
+           ("2", "3", "1", "fine"), ("2", "2", "0", "fine"), ("2", "2", "2", "fine"),
+           ("2", "3", "2", "fine")]
 
 
-@pytest.mark.parametrize("mode,fine,layout", LAYOUTS)
-def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, fine, layout, monkeypatch):
+@pytest.mark.parametrize("mode,fine,tile,layout", LAYOUTS)
+def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, fine, tile, layout,
+                                  monkeypatch):
     """PCP_TERRAIN_BLOCKS=0 scans the per-cell runs, =2 the block-major copy (PCP_TERRAIN_FINE=0:
     2x2x2 blocks, F > 0: windows of fine cells c / F) from the first query on (the default, 1,
     switches at the second query): all bit-exact on the fan and the reference-mode scoring."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", mode)
     monkeypatch.setenv("PCP_TERRAIN_FINE", fine)
+    monkeypatch.setenv("PCP_FINE_TILE", tile)
     ctx = _abi.Context(0)
     try:
         ctx.set_terrain(scene.terrain, point_step=32)
@@ -811,12 +818,13 @@ def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, fine, layout,
         ctx.close()
 
 
-@pytest.mark.parametrize("mode,fine,layout", LAYOUTS)
-def test_terrain_block_copy_dense_and_tiny(oracle, mode, fine, layout, monkeypatch):
+@pytest.mark.parametrize("mode,fine,tile,layout", LAYOUTS)
+def test_terrain_block_copy_dense_and_tiny(oracle, mode, fine, tile, layout, monkeypatch):
     """Block-major copies on awkward terrains: 20 k points packed into a 0.3 m cube (blocks of
     thousands of points, ties in z) next to a sparse plane, and a one-point terrain."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", mode)
     monkeypatch.setenv("PCP_TERRAIN_FINE", fine)
+    monkeypatch.setenv("PCP_FINE_TILE", tile)
     rng = np.random.default_rng(11)
     dense = np.column_stack([rng.uniform(2.0, 2.3, 20_000), rng.uniform(-0.15, 0.15, 20_000),
                              np.round(rng.uniform(0.0, 0.3, 20_000), 2)])
