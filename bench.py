@@ -269,6 +269,21 @@ def _timed(step, args, dist, on_gpu, dev):
     return float(t.item()), float(uu.item()), res
 
 
+def _profiled(ctx, step, reps, names):
+    """Per-launch event times of `names` over `reps` extra steps run AFTER the timed loop: the
+    library's event instrumentation (ctx.profile) stays out of the timed region."""
+    ctx.profile(True)
+    ctx.profile_reset()
+    for _ in range(reps):
+        step()
+    ctx.profile(False)
+    out = {}
+    for k in names:
+        ms, n = ctx.profile_get(k)
+        out[k] = ms / max(n, 1)
+    return out
+
+
 def _fan_npw(n_poses):
     """Poses per wave of the production fan kernel: the library's rule (pcp_vlidar.hip
     raycast_fan_impl) -- PCP_FAN_NPW (default 8), halved until it divides the XCD pose chunk."""
@@ -289,13 +304,16 @@ def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
     `traffic`."""
     st = ctx.raycast_fan_stats(poses, fan)
     layout = ctx.terrain_info()["scan_layout"]
-    # the fine-window layout's probe reads the 8-byte record (z band + run), the others a 2-byte
-    # z band and then one 8-byte directory entry per scan
-    probe_b = 8.0 if layout == "fine" else 2.0
+    # the fine-window layout's probe reads the 8-byte record (z band + run; split records: the
+    # 2-byte band, then 4 bytes of walk start per candidate), the others a 2-byte z band and then
+    # one 8-byte directory entry per scan; the XCD-chunk kernels read the step from LDS
+    split = layout == "fine" and ctx.terrain_info().get("fine_tile") == 2
+    probe_b = 8.0 if layout == "fine" and not split else 2.0
+    cand_b = 4.0 if split else 8.0
     rays = poses.shape[0] * fan.n_az * fan.n_el
     waves = poses.shape[0] * ((fan.n_az * fan.n_el + 63) // 64)
     npw = _fan_npw(poses.shape[0]) if layout == "fine" else 1
-    req = probe_b * st["samples_visited"] + 8.0 * st["scanned_stencils"] \
+    req = probe_b * st["samples_visited"] + cand_b * st["scanned_stencils"] \
         + 8.0 * st["directory_loads"] + 12.0 * st["point_tests"] + 16.0 * rays / npw \
         + 8.0 * waves
     ref_model = 64.0 * units_per_launch + 12.0 * st["point_tests"]
@@ -307,12 +325,14 @@ def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
         "traffic": traffic,
         "traffic_gbs": _gbs(traffic, avg_kernel_s),
         "traffic_frac": (_gbs(traffic, avg_kernel_s) or 0.0) / HBM_PEAK_GBS if traffic else None,
-        "kernel": (f"k_raycast_fan_xcd<0, 64, true, 8, 4, true, {npw}>" if layout == "fine"
+        "kernel": (f"k_raycast_fan_xcd<0, 64, true, 8, {8 if split else 4}, true, {npw}>"
+                   if layout == "fine"
                    else "k_raycast_fan<0, 64, true, 7, 0>"),
         "poses_per_wave": npw,
         "avg_kernel_ms": avg_kernel_s * 1e3, "scan_layout": layout,
         "requested_bytes_per_launch": req,
-        "model": f"requested bytes: {probe_b:.0f} B/probe + 8 B/candidate (its step) + 8 B/"
+        "model": f"requested bytes: {probe_b:.0f} B/probe + {cand_b:.0f} B/candidate (its "
+                 "walk start for split records, else its step) + 8 B/"
                  "directory load + 12 B/point record + 16 B/ray/NPW + 8 B/wave "
                  "(pcp_raycast_fan_stats counts); traffic = PMC FETCH(x2)+WRITE per launch "
                  "(profiles/pmc_traffic.json)",
@@ -357,11 +377,8 @@ def run_all(args, torch, dist, world, rank, local, backend):
         best["fan"] = b
         return int(units.sum()), keys
 
-    ctx.profile(True)
-    ctx.profile_reset()
     dt, units_all, _ = _timed(fan_step, args, dist, on_gpu, dev)
-    ctx.profile(False)
-    k_ms, k_n = ctx.profile_get("raycast_fan")
+    k_avg = _profiled(ctx, fan_step, max(args.steps, 3), ["raycast_fan"])["raycast_fan"]
     # the kernel's launch time: the same launch 20 times back-to-back between two events on the
     # library's stream (the per-step events of the synchronous loop also hold the idle queue's
     # wake-up before each launch; kept below as event_avg_ms_in_loop)
@@ -394,7 +411,7 @@ def run_all(args, torch, dist, world, rank, local, backend):
     }
     out["roofline"]["kernel_time_source"] = ("HIP events around 20 back-to-back launches "
                                              "(pcp_raycast_fan_burst)")
-    out["roofline"]["event_avg_ms_in_loop"] = k_ms / max(k_n, 1)
+    out["roofline"]["event_avg_ms_in_loop"] = k_avg
     if dist is not None and backend == "gloo" and on_gpu:
         out["rehearsal"] = (f"{world} ranks on {torch.cuda.device_count()} GPU(s): collective "
                             "over gloo, ranks share devices")
@@ -424,12 +441,9 @@ def run_all(args, torch, dist, world, rank, local, backend):
             best["cells"] = b
             return cposes.shape[0], tot
 
-        ctx.profile(True)
-        ctx.profile_reset()
         cdt, cunits, _ = _timed(cells_step, args, dist, on_gpu, dev)
-        ctx.profile(False)
-        kern = {k: ctx.profile_get(k)[0] / max(ctx.profile_get(k)[1], 1)
-                for k in ("score_cells", "pose_sum", "cell_flags")}
+        kern = _profiled(ctx, cells_step, max(args.steps, 3),
+                         ("score_cells", "pose_sum", "cell_flags"))
         out["poses_per_s_reference_mode"] = cunits / cdt
         out["reference_mode"] = {
             "workload": f"runOptimization: {P_total} candidate poses x {cells.xyz.shape[0]} "
@@ -528,12 +542,8 @@ def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=Fal
         last["n_out"], last["per"] = n_out, per
         return n_in, n_out
 
-    ctx.profile(True)
-    ctx.profile_reset()
     dt, units_all, _ = _timed(step, args, dist, on_gpu, dev)
-    ctx.profile(False)
-    g_ms, g_n = ctx.profile_get("filter_merge")
-    step_dev_ms = g_ms / max(g_n, 1)
+    step_dev_ms = _profiled(ctx, step, max(args.steps, 3), ["filter_merge"])["filter_merge"]
     n_out = last["n_out"]
     stages = None
     pcie = None

@@ -353,6 +353,10 @@ typedef struct pcp_index_info {
     /* the layout the terrain scans walk: 0 per-cell runs, 1 2x2x2 block copy, 2 fine-window
        copy (the copies are built at the second query after pcp_set_terrain) */
     int32_t scan_layout;
+    /* fine-window record layout (scan_layout 2): 0 x-fastest 8-byte records, 1 4 x 4 tiles of
+       them, 2 split records -- 2-byte probe thresholds + 4-byte walk starts, 8 x 8 tiles (this
+       field sits in what was the struct's tail padding: the size is unchanged) */
+    int32_t fine_tile;
 } pcp_index_info;
 int pcp_terrain_info(pcp_ctx *ctx, pcp_index_info *info);
 

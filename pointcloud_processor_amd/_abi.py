@@ -78,7 +78,7 @@ ABI_VERSION = 2   # PCP_ABI_VERSION of include/pcp_abi.h
 class IndexInfo(C.Structure):
     _fields_ = [("n_points", C.c_uint64), ("cell", C.c_double), ("nx", C.c_int32),
                 ("ny", C.c_int32), ("nz", C.c_int32), ("bmin", C.c_double * 3),
-                ("bmax", C.c_double * 3), ("scan_layout", C.c_int32)]
+                ("bmax", C.c_double * 3), ("scan_layout", C.c_int32), ("fine_tile", C.c_int32)]
 
 
 # (name, restype, argtypes) for every entry point of include/pcp_abi.h
@@ -494,7 +494,8 @@ class Context:
         return {"n_points": info.n_points, "cell": info.cell,
                 "dims": (info.nx, info.ny, info.nz),
                 "bmin": tuple(info.bmin), "bmax": tuple(info.bmax),
-                "scan_layout": ("cells", "blocks", "fine")[info.scan_layout]}
+                "scan_layout": ("cells", "blocks", "fine")[info.scan_layout],
+                "fine_tile": int(info.fine_tile)}
 
     def generate_candidates(self, grid_bbox, params: VlParams, zx120_pose5, cap=None):
         bb = np.ascontiguousarray(grid_bbox, np.float64)

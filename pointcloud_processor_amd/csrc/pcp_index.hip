@@ -634,6 +634,7 @@ int pcp_terrain_info(pcp_ctx *ctx, pcp_index_info *info) {
         info->bmax[a] = g.bmax[a];
     }
     info->scan_layout = g.fine_ok ? 2 : g.blk_ok ? 1 : 0;
+    info->fine_tile = g.fine_ok ? g.ftile : 0;
     return PCP_OK;
 }
 
