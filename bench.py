@@ -284,6 +284,17 @@ def _profiled(ctx, step, reps, names):
     return out
 
 
+def _gather_path():
+    """The fan kernel's texture-path counters (profiles/pmc_fan_gather.json, from
+    tools/pmc_fan.sh): what actually bounds it -- TD busy, L1 tag lookups per instruction."""
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_fan_gather.json")
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
 def _fan_npw(n_poses):
     """Poses per wave of the production fan kernel: the library's rule (pcp_vlidar.hip
     raycast_fan_impl) -- PCP_FAN_NPW (default 8), halved until it divides the XCD pose chunk."""
@@ -345,6 +356,7 @@ def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
                                "test; > 1 because the kernel skips ~95 % of the sample "
                                "queries exactly (DESIGN.md §5)",
         "diag": st,
+        "gather_path": _gather_path(),
     }
 
 
