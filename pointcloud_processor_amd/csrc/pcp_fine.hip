@@ -169,8 +169,8 @@ k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ cstart, CellMap m
                           __uint_as_float(0xFFFFFFFFu));
     // one pass down the run: jt / jb advance monotonically, each entry's z and coarse z cell
     // loaded once per pointer (the walk of every level reuses them)
-    uint32_t jt = s, jb = s;
-    float zt = wpts[s].z, zb = zt, zlast = zt;
+    uint32_t jt = s, jb = s, j2 = s;
+    float zt = wpts[s].z, zb = zt, zlast = zt, z2 = zt;
     int ct = s < e ? cell_z(m, zt) : -1, cb = ct;
     for (int iz = (int)rz - 1; iz >= 0; --iz) {
         while (jt < e && ct > iz + 1) {
@@ -197,7 +197,19 @@ k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ cstart, CellMap m
             const uint32_t hi2 = (hi == 255u) ? 255u : min(hi + tsteps, 255u);
             band = lo2 | (hi2 << 8);
         }
-        put((size_t)iz * plane + base, jt, band);
+        // split records: the entries from jt that lie at or above oz + (iz + 1.5) c (at most
+        // 15 of them) can be skipped by a query more than r below that height (march, FN 8)
+        uint32_t skip = 0;
+        if (tile == 2) {
+            if (j2 < jt) {
+                j2 = jt;
+                z2 = zt;
+            }
+            const double h2 = m.oz + ((double)iz + 1.5) * c;
+            while (j2 < e && (double)z2 >= h2) z2 = wpts[++j2].z;
+            skip = min(j2 - jt, 15u);
+        }
+        put((size_t)iz * plane + base, jt | (skip << 28), band);
     }
 }
 

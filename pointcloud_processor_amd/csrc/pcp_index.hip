@@ -68,6 +68,8 @@ GridView GridIndex::view() const {
     v.ffine = fine_ok ? ffine : 0.0f;
     v.ftile = fine_ok ? ftile : 0;
     v.fband = (fine_ok && ftile == 2) ? frec.as<const uint16_t>() : nullptr;
+    v.fzc = (float)c;
+    v.fzo = (float)v.oz;
     v.fstart = (fine_ok && ftile == 2)
                    ? reinterpret_cast<const uint32_t *>(frec.as<const char>() + fstart_off)
                    : nullptr;

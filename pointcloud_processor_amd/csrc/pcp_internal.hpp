@@ -136,7 +136,10 @@ struct GridView {               // POD passed to kernels by value
     // ftile 2: the record split in two arrays of 8 x 8 xy tiles -- the probe's 2-byte
     // thresholds (one 128-byte line per tile) and the 4-byte walk start, read by candidates only
     const uint16_t *fband;
-    const uint32_t *fstart;
+    const uint32_t *fstart;     // walk start (28 bits) | skip (4 bits, << 28): entries of the
+                                // run at or above oz + (iz + 1.5) c, skipped by a candidate
+                                // whose q lies more than r below that height
+    float fzc, fzo;             // c and oz in float (the skip test)
 };
 constexpr float kZq = 2.0f / 250.0f;   // z band step, cells (2 cells = 250 steps)
 

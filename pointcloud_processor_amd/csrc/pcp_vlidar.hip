@@ -300,7 +300,12 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
                 const float qx = (float)(px + dx * s);
                 const float qy = (float)(py + dy * s);
                 const float qz = (float)(pz + dz * s);
-                const uint32_t w0 = FN == 8 ? ld_u32o(g.fstart, ri) : R.x;
+                uint32_t w0 = R.x;
+                if (FN == 8) {   // skip the run's entries > r above q (pcp_fine.hip, k_frec)
+                    const uint32_t ws = ld_u32o(g.fstart, ri);
+                    const float h2 = __builtin_fmaf((float)iz + 1.5f, g.fzc, g.fzo);
+                    w0 = (ws & 0x0FFFFFFFu) + (qz + (rexit + 1e-4f) < h2 ? ws >> 28 : 0u);
+                }
                 if (scan_window<STATS>(g.wpts, w0, qx, qy, qz, r2, rexit, cnt)) return k;
             }
         }
