@@ -20,6 +20,7 @@
 namespace pcp {
 
 constexpr int kT = 256;
+constexpr int kStepLds = 256;   // step tables up to this long are read from LDS (fan, cells)
 #ifndef PCP_CELL_PROBES
 // z-band probes issued per round in the cell-scoring march (build knob; 4 measured 130 vs 132
 // us per 256-pose k_score_cells: that march is not probe-latency bound)
@@ -409,7 +410,7 @@ struct VisEnv {
 __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double py, double pz,
                                             double pitch, double cx, double cy, double cz,
                                             float nx, float ny, float nz, bool is_zx120,
-                                            uint32_t &bits) {
+                                            uint32_t &bits, const double *steps) {
     const double dx = cx - px, dy = cy - py, dz = cz - pz;
     const double L = sqrt(dx * dx + dy * dy + dz * dz);
     bits = 0;
@@ -434,10 +435,10 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
         visible = end > 1e300;
 #elif defined(PCP_CELL_EXP) && PCP_CELL_EXP == 2  // A/B timing only: probes, a candidate = hit
         visible = march<false, true, PCP_CELL_PROBES>(E.terrain, px, py, pz, ndx, ndy, ndz,
-                                                      E.steps, E.K, end, 1e30f, 1e15f) < 0;
+                                                      steps, E.K, end, 1e30f, 1e15f) < 0;
 #else
         visible = march<false, true, PCP_CELL_PROBES, 2>(E.terrain, px, py, pz, ndx, ndy, ndz,
-                                                         E.steps, E.K, end, E.r2_ray,
+                                                         steps, E.K, end, E.r2_ray,
                                                          E.rexit_ray) < 0;
 #endif
     }
@@ -456,6 +457,10 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
 #ifndef PCP_SCORE_WAVES
 #define PCP_SCORE_WAVES 6   // waves per SIMD of k_score_cells (build knob)
 #endif
+// SL: the step table in LDS (K <= kStepLds, checked by the launcher).  (Several rows per
+// thread, the cell loaded once, spilled ~120 dwords: the loop hoists both GridViews' kernel
+// arguments into registers.)
+template <bool SL>
 __global__ void __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(PCP_SCORE_WAVES, 8)))
 k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict__ cn, int C,
               const double *__restrict__ poses5, int P, const double *__restrict__ zx5,
@@ -463,15 +468,22 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
               double *__restrict__ score_z, uint8_t *__restrict__ zbits,
               int32_t *__restrict__ stats) {
     const int c = blockIdx.x * kT + threadIdx.x;
-    const int p = blockIdx.y;
     // the colour-statistics slots k_cell_flags accumulates into (it runs after this kernel)
     if (stats && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) stats[threadIdx.x] = 0;
+    __shared__ double s_steps[SL ? kStepLds : 1];
+    if (SL) {
+        for (int q = threadIdx.x; q < E.K; q += kT) s_steps[q] = E.steps[q];
+        __syncthreads();
+    }
+    const double *steps = SL ? s_steps : E.steps;
     if (c >= C) return;
+    const int p = blockIdx.y;
     const bool zrow = p == P;
     const double *Q = zrow ? zx5 : poses5 + 5 * (size_t)p;
     uint32_t bits;
     const double s = eval_cell(E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1],
-                               cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], zrow, bits);
+                               cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], zrow, bits,
+                               steps);
     if (zrow) {
         score_z[c] = s;
         zbits[c] = (uint8_t)bits;
@@ -913,7 +925,6 @@ struct FanArgs {
 };
 
 enum { FAN_PLAIN = 0, FAN_STATS = 1, FAN_STAMPS = 2 };
-constexpr int kStepLds = 256;   // step tables up to this long are read from LDS by the fan
 
 // sum over the 64 lanes (all active): rotate-adds inside each 16-lane row (DPP row_ror 8, 4,
 // 2, 1), then the four row sums by readlane -- no LDS crossbar round trips
@@ -1302,11 +1313,21 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
     if (C) {
         {
             ProfScope ps(ctx, PCP_K_SCORE_CELLS);
-            hipLaunchKernelGGL(k_score_cells, dim3(cb, P + 1), dim3(kT), 0, st, E,
-                               ctx->cells_xyz.as<const double>(), ctx->cells_nrm.as<const float>(),
-                               C, ctx->poses_d.as<const double>(), P,
-                               ctx->poses_d.as<const double>() + 5 * (size_t)P, o.comb, o.mbits,
-                               score_z, o.zbits, o.stats);
+            const dim3 g(cb, (unsigned)(P + 1));
+            if (E.K <= kStepLds)
+                hipLaunchKernelGGL(k_score_cells<true>, g, dim3(kT), 0, st, E,
+                                   ctx->cells_xyz.as<const double>(),
+                                   ctx->cells_nrm.as<const float>(), C,
+                                   ctx->poses_d.as<const double>(), P,
+                                   ctx->poses_d.as<const double>() + 5 * (size_t)P, o.comb,
+                                   o.mbits, score_z, o.zbits, o.stats);
+            else
+                hipLaunchKernelGGL(k_score_cells<false>, g, dim3(kT), 0, st, E,
+                                   ctx->cells_xyz.as<const double>(),
+                                   ctx->cells_nrm.as<const float>(), C,
+                                   ctx->poses_d.as<const double>(), P,
+                                   ctx->poses_d.as<const double>() + 5 * (size_t)P, o.comb,
+                                   o.mbits, score_z, o.zbits, o.stats);
             PCP_CHECK_LAUNCH(ctx);
         }
         o.score_z = score_z;
