@@ -380,6 +380,36 @@ def test_raycast_fan_random_poses(gpu, oracle, loaded, scene):
         np.testing.assert_array_equal(units, r_units)
 
 
+@pytest.mark.parametrize("npw,tile", [("1", "2"), ("2", "2"), ("8", "2"), ("8", "1")])
+def test_raycast_fan_poses_per_wave(oracle, loaded, scene, cells, npw, tile, monkeypatch):
+    """64 poses (P % 64 == 0: the XCD-chunk kernel with NPW poses per wave, its step table in
+    LDS) on split and 8-byte fine records: blocked counts, units and first hits exact."""
+    T, _ = loaded
+    monkeypatch.setenv("PCP_FAN_NPW", npw)
+    monkeypatch.setenv("PCP_FINE_TILE", tile)
+    monkeypatch.setenv("PCP_TERRAIN_BLOCKS", "2")
+    ctx = _abi.Context(0)
+    try:
+        ctx.set_terrain(scene.terrain, point_step=32)
+        p = _abi.default_vl_params(num_candidates=100)
+        poses = ctx.generate_candidates(cells.grid_bbox, p, scene.zx120_pose5)
+        poses = np.ascontiguousarray(np.resize(poses, (64, 5)))
+        fan = _abi.fan_params(n_az=256, n_el=32)
+        blocked, units, fh, best = ctx.raycast_fan(poses, fan, want_first_hit=True)
+        info = ctx.terrain_info()
+        assert info["scan_layout"] == "fine" and info["fine_tile"] == int(tile)
+    finally:
+        ctx.close()
+    oracle.set_threads(8)
+    r_blocked, r_units, r_fh = oracle.raycast_fan(T, poses, 256, 32, fan.el_min, fan.el_max,
+                                                  fan.max_distance)
+    oracle.set_threads(1)
+    np.testing.assert_array_equal(fh, r_fh)
+    np.testing.assert_array_equal(blocked, r_blocked)
+    np.testing.assert_array_equal(units, r_units)
+    assert best == int(np.argmin(r_blocked))
+
+
 def test_raycast_fan_full_size_two_poses(gpu, oracle, loaded, scene, cells):
     """BASELINE configs[1] fan (1024 x 256) on two poses, bit-exact against the oracle."""
     T, _ = loaded
