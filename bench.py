@@ -383,11 +383,14 @@ def run_all(args, torch, dist, world, rank, local, backend):
     # ---- C2 / C4: the fan (the headline) -------------------------------------------------
     best = {}
 
+    blocked_h = np.zeros(max(poses.shape[0], 1), np.uint32)
+    units_h = np.zeros(max(poses.shape[0], 1), np.uint64)
+
     def fan_step():
-        blocked, units, _, _ = ctx.raycast_fan(poses, fan)
-        keys, b = pd.reduce_fan(blocked, lo, hi, P_total, dist, dev)   # the one collective
-        best["fan"] = b
-        return int(units.sum()), keys
+        ctx.raycast_fan_into(poses, fan, blocked_h, units_h)
+        keys, b = pd.reduce_fan(blocked_h[:poses.shape[0]], lo, hi, P_total, dist, dev)
+        best["fan"] = b   # ^ the one collective
+        return int(units_h[:poses.shape[0]].sum()), keys
 
     dt, units_all, _ = _timed(fan_step, args, dist, on_gpu, dev)
     k_avg = _profiled(ctx, fan_step, max(args.steps, 3), ["raycast_fan"])["raycast_fan"]
@@ -447,9 +450,14 @@ def run_all(args, torch, dist, world, rank, local, backend):
         params = _abi.default_vl_params()
         flags = np.zeros(cells.xyz.shape[0], np.uint8)
 
+        tot = np.zeros(max(cposes.shape[0], 1), np.float64)
+        cov = np.zeros(max(cposes.shape[0], 1), np.int32)
+        rep = _abi.VlReport()
+        zx5 = np.ascontiguousarray(scene.zx120_pose5, np.float64)
+
         def cells_step():
-            tot, cov, rep = ctx.score_poses(cposes, scene.zx120_pose5, params, flags)
-            _, b, _ = pd.reduce_scores(tot, lo, hi, P_total, dist, dev)   # the one collective
+            ctx.score_poses_into(cposes, zx5, params, flags, tot, cov, rep)
+            _, b, _ = pd.reduce_scores(tot[:cposes.shape[0]], lo, hi, P_total, dist, dev)
             best["cells"] = b
             return cposes.shape[0], tot
 

@@ -524,6 +524,40 @@ class Context:
                                              C.byref(rep)), "pcp_score_poses")
         return tot[:P].copy(), cov[:P].copy(), rep
 
+    def score_poses_into(self, poses5: np.ndarray, zx120_pose5: np.ndarray, params: VlParams,
+                         cell_flags: np.ndarray, tot: np.ndarray, cov: np.ndarray,
+                         rep: "VlReport"):
+        """score_poses into caller-owned arrays (steady-state query, no allocation): poses5
+        C-contiguous float64 [P, 5], zx120_pose5 float64 [5], tot float64 [>=P], cov int32
+        [>=P]; cell_flags updated in place."""
+        P = poses5.shape[0]
+        if (poses5.dtype != np.float64 or not poses5.flags.c_contiguous or poses5.ndim != 2
+                or zx120_pose5.dtype != np.float64 or not zx120_pose5.flags.c_contiguous
+                or cell_flags.dtype != np.uint8 or not cell_flags.flags.c_contiguous
+                or tot.dtype != np.float64 or cov.dtype != np.int32
+                or tot.shape[0] < P or cov.shape[0] < P):
+            raise ValueError("score_poses_into: bad array types or sizes")
+        self._check(self.lib.pcp_score_poses(self.h, poses5.ctypes.data, P,
+                                             zx120_pose5.ctypes.data, C.byref(params),
+                                             cell_flags.ctypes.data, tot.ctypes.data,
+                                             cov.ctypes.data, C.byref(rep)), "pcp_score_poses")
+
+    def raycast_fan_into(self, poses5: np.ndarray, fan: FanParams, blocked: np.ndarray,
+                         units: np.ndarray) -> int:
+        """raycast_fan into caller-owned arrays (no allocation per call: the benchmark's and a
+        node's steady-state query); poses5 C-contiguous float64 [P, 5], blocked uint32 [P],
+        units uint64 [P].  Returns the best (fewest blocked, lowest) pose index."""
+        P = poses5.shape[0]
+        if (poses5.dtype != np.float64 or not poses5.flags.c_contiguous or poses5.ndim != 2
+                or poses5.shape[1] != 5 or blocked.dtype != np.uint32 or units.dtype != np.uint64
+                or blocked.shape[0] < P or units.shape[0] < P):
+            raise ValueError("raycast_fan_into: poses float64 [P,5], blocked u32 [>=P], units u64 [>=P]")
+        best = C.c_int64()
+        self._check(self.lib.pcp_raycast_fan(self.h, poses5.ctypes.data, P, C.byref(fan),
+                                             blocked.ctypes.data, units.ctypes.data, None,
+                                             C.byref(best)), "pcp_raycast_fan")
+        return best.value
+
     def raycast_fan(self, poses5: np.ndarray, fan: FanParams, want_first_hit=False):
         poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
         P = poses.shape[0]

@@ -380,6 +380,31 @@ def test_raycast_fan_random_poses(gpu, oracle, loaded, scene):
         np.testing.assert_array_equal(units, r_units)
 
 
+def test_into_wrappers_match(gpu, loaded, scene, cells):
+    """The allocation-free steady-state calls give the allocating calls' results."""
+    p = _abi.default_vl_params(num_candidates=100)
+    poses = np.ascontiguousarray(gpu.generate_candidates(cells.grid_bbox, p, scene.zx120_pose5))
+    fan = _abi.fan_params(n_az=128, n_el=16)
+    blocked, units, _, best = gpu.raycast_fan(poses, fan)
+    b2 = np.zeros(poses.shape[0], np.uint32)
+    u2 = np.zeros(poses.shape[0], np.uint64)
+    assert gpu.raycast_fan_into(poses, fan, b2, u2) == best
+    np.testing.assert_array_equal(b2, blocked)
+    np.testing.assert_array_equal(u2, units)
+    f1 = np.zeros(cells.xyz.shape[0], np.uint8)
+    f2 = f1.copy()
+    tot, cov, rep = gpu.score_poses(poses, scene.zx120_pose5, p, f1)
+    t2 = np.zeros(poses.shape[0], np.float64)
+    c2 = np.zeros(poses.shape[0], np.int32)
+    r2 = _abi.VlReport()
+    gpu.score_poses_into(poses, np.ascontiguousarray(scene.zx120_pose5, np.float64), p, f2, t2, c2,
+                         r2)
+    np.testing.assert_array_equal(t2, tot)
+    np.testing.assert_array_equal(c2, cov)
+    np.testing.assert_array_equal(f2, f1)
+    assert r2.best_idx == rep.best_idx and r2.green == rep.green
+
+
 @pytest.mark.parametrize("npw,tile", [("1", "2"), ("2", "2"), ("8", "2"), ("8", "1")])
 def test_raycast_fan_poses_per_wave(oracle, loaded, scene, cells, npw, tile, monkeypatch):
     """64 poses (P % 64 == 0: the XCD-chunk kernel with NPW poses per wave, its step table in
