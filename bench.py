@@ -556,9 +556,11 @@ def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=Fal
     n_in = sum(c.shape[0] for c in clouds)
     last = {}
 
-    def step():
-        n_out, per = ctx.filter_merge_device(views, [box, box], 0.05, tfs,
+    frame = ctx.filter_merge_device_prepared(views, [box, box], 0.05, tfs,
                                              [(255, 0, 0), (0, 0, 255)], out_d, cap)
+
+    def step():
+        n_out, per = frame()
         last["n_out"], last["per"] = n_out, per
         return n_in, n_out
 

@@ -394,6 +394,32 @@ class Context:
                     "pcp_filter_merge")
         return n.value, per[:k].copy()
 
+    def filter_merge_device_prepared(self, views, boxes, leaf, tfs, rgbs, out_dev: int,
+                                     cap: int):
+        """filter_merge_device with its ctypes arguments built once: returns a call that runs
+        one frame and returns (n_out, per_cloud) -- the steady-state frame of a node whose
+        clouds land in the same device buffers every time (the library replays its graph)."""
+        k = len(views)
+        varr = (CloudView * max(k, 1))(*views)
+        rgb = np.ascontiguousarray(np.asarray(rgbs, np.uint8).reshape(-1))
+        bx = np.ascontiguousarray(np.asarray(boxes, np.float64).reshape(-1))
+        rig = self._rigids(tfs)
+        n = C.c_uint64()
+        per = np.zeros(max(k, 1), np.uint64)
+        keep = (varr, rgb, bx, rig, n, per)
+        fn, h, lf, nref = self.lib.pcp_filter_merge, self.h, C.c_float(leaf), C.byref(n)
+        bxp, rgbp, perp = bx.ctypes.data, rgb.ctypes.data, per.ctypes.data
+        flags = PCP_MEM_DEVICE_IN | PCP_MEM_DEVICE_OUT
+
+        def run():
+            rc = fn(h, k, varr, bxp, lf, rig, rgbp, out_dev, cap, nref, perp, flags)
+            if rc != PCP_OK:
+                self._check(rc, "pcp_filter_merge")
+            return n.value, per[:k]
+
+        run.keep = keep
+        return run
+
     # -- virtual_lidar ------------------------------------------------------------------------
     def set_terrain(self, cloud: np.ndarray, point_step=None, offs=(0, 4, 8)):
         v = cloud_view(cloud, point_step, offs)

@@ -247,6 +247,14 @@ def test_filter_merge_device_graph_replay(gpu, oracle):
             got = np.empty((n, 8), np.float32)
             gpu.d2h(got, out_d)
             np.testing.assert_array_equal(got[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
+        # the prepared steady-state call replays the same graph
+        frame = gpu.filter_merge_device_prepared(views, [BOX, BOX], 0.05, tfs, rgbs, out_d, cap)
+        for _ in range(2):
+            n3, per3 = frame()
+            assert n3 == ref.shape[0] and list(per3) == list(per_ref)
+            got = np.empty((n3, 8), np.float32)
+            gpu.d2h(got, out_d)
+            np.testing.assert_array_equal(got[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
         # a different box invalidates the captured graph
         box2 = BOX.copy()
         box2[1] = 8.0
