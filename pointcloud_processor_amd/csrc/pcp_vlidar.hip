@@ -287,7 +287,7 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
                               : FN == 4 ? (mad_u24(rx, mad_u24(ry, iz, iy >> 2), ix >> 2) << 4) |
                                               ((iy & 3u) << 2) | (ix & 3u)
                                         : mad_u24(rx, mad_u24(ry, iz, iy), ix);
-            uint2 R;
+            uint2 R = make_uint2(0u, 0u);   // FN 8: only the thresholds (.y) come with the probe
             if (FN == 8) R.y = ld_u16o(g.fband, ri);
             else R = ld_rec(g.frec, ri);
             // height above the block floor in kZq steps against the record's thresholds
