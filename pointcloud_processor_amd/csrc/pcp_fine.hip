@@ -213,6 +213,17 @@ k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ cstart, CellMap m
     }
 }
 
+// the fine-window entries packed to 12 bytes (x, y, z): a quarter less working set for the walks
+__global__ void __launch_bounds__(kThreads)
+k_pack3(const float4 *__restrict__ src, uint32_t n, float *__restrict__ dst) {
+    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = src[i];
+    dst[3 * (size_t)i] = p.x;
+    dst[3 * (size_t)i + 1] = p.y;
+    dst[3 * (size_t)i + 2] = p.z;
+}
+
 }  // namespace
 
 int build_fine(pcp_ctx *ctx, GridIndex &g) {
@@ -300,7 +311,10 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     PCP_CHECK_LAUNCH(ctx);
     // the copy is an optional speed-up: an allocation failure keeps the other layouts
     const size_t nent = (size_t)np + nw;
-    if (g.wpts.ensure(nent * sizeof(float4)) != hipSuccess ||
+    const bool pack = ctx->fine_pack != 0;
+    // packed: the float4 entries are built in scratch, then packed into wpts
+    if ((pack && ctx->scratch[7].ensure(nent * sizeof(float4)) != hipSuccess) ||
+        g.wpts.ensure(pack ? nent * 12 + 16 : nent * sizeof(float4)) != hipSuccess ||
         g.frec.ensure(rec_bytes) != hipSuccess) {
         (void)hipGetLastError();
         g.wpts.release();
@@ -308,19 +322,27 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
         g.fine_fail = true;
         return PCP_OK;
     }
+    float4 *went = pack ? ctx->scratch[7].as<float4>() : g.wpts.as<float4>();
     hipLaunchKernelGGL(k_win_place, dim3((np + kThreads - 1) / kThreads), dim3(kThreads), 0, st,
                        pts, (const uint32_t *)zord, (const uint32_t *)wk1, (const uint32_t *)rk1,
-                       np, g.wpts.as<float4>());
+                       np, went);
     PCP_CHECK_LAUNCH(ctx);
     // 5. records (and the sentinels)
     const uint32_t tsteps = (uint32_t)std::ceil((g.r_q + 2e-3) / g.c / (double)kZq);
     const uint64_t nthr = std::max<uint64_t>(nw, tile ? nrec / rz : 0);
     hipLaunchKernelGGL(k_frec, dim3((unsigned)((nthr + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                       st, g.wpts.as<float4>(), (const uint32_t *)cstart, m, g.c, (uint32_t)fnx,
+                       st, went, (const uint32_t *)cstart, m, g.c, (uint32_t)fnx,
                        (uint32_t)fny, (uint32_t)rz, tsteps, tile, g.frec.as<uint2>(),
                        g.frec.as<uint16_t>(),
                        reinterpret_cast<uint32_t *>(g.frec.as<char>() + band_bytes));
     PCP_CHECK_LAUNCH(ctx);
+    if (pack) {
+        hipLaunchKernelGGL(k_pack3, dim3((unsigned)((nent + kThreads - 1) / kThreads)),
+                           dim3(kThreads), 0, st, (const float4 *)went, (uint32_t)nent,
+                           g.wpts.as<float>());
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    g.wpack = pack ? 1 : 0;
     g.frx = (uint32_t)fnx;
     g.fry = (uint32_t)fny;
     g.frz = (uint32_t)rz;

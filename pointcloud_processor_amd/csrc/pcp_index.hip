@@ -69,6 +69,7 @@ GridView GridIndex::view() const {
     v.ftile = fine_ok ? ftile : 0;
     v.fband = (fine_ok && ftile == 2) ? frec.as<const uint16_t>() : nullptr;
     v.fzc = (float)c;
+    v.wpack = fine_ok ? wpack : 0;
     v.fzo = (float)v.oz;
     v.fstart = (fine_ok && ftile == 2)
                    ? reinterpret_cast<const uint32_t *>(frec.as<const char>() + fstart_off)

@@ -140,6 +140,7 @@ struct GridView {               // POD passed to kernels by value
                                 // run at or above oz + (iz + 1.5) c, skipped by a candidate
                                 // whose q lies more than r below that height
     float fzc, fzo;             // c and oz in float (the skip test)
+    int32_t wpack;              // wpts entries packed to 12 bytes (x, y, z), PCP_FINE_PACK
 };
 constexpr float kZq = 2.0f / 250.0f;   // z band step, cells (2 cells = 250 steps)
 
@@ -158,6 +159,7 @@ struct GridIndex {
     bool fine_ok = false;        // fine-window copy built (frec / wpts)
     bool fine_fail = false;      // fine copy past its caps / not allocated: no retry
     uint32_t frx = 0, fry = 0, frz = 0;
+    int32_t wpack = 0;           // wpts as 12-byte (x, y, z) entries
     float ffine = 0.0f;
     int32_t ftile = 0;
     size_t fstart_off = 0;       // ftile 2: byte offset of the start array inside frec
@@ -244,6 +246,7 @@ struct pcp_ctx {
     int fan_batch = 0;                       // fan kernel variant (PCP_FAN_BATCH), A/B only
     int fan_npw = 8;                         // poses per wave of the fan kernel (PCP_FAN_NPW)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
+    int fine_pack = 1;                       // fine-window entries as 12 bytes (PCP_FINE_PACK)
     int fine_tile = 2;                       // fine records: 0 x-fastest, 1 4 x 4 tiles, 2 split
                                              // in 8 x 8 tiles (PCP_FINE_TILE)
     int terrain_fine = 2;                    // fine-window layout of that copy, cells of c / F

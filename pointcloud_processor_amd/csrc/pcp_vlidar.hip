@@ -134,6 +134,23 @@ __device__ __forceinline__ bool scan_run(const float4 *pts, uint32_t k0, uint32_
     return false;
 }
 
+// the packed (12-byte) entries' walk: the same test on x, y, z at k * 12
+template <bool STATS>
+__device__ __forceinline__ bool scan_window3(const float *pts, uint32_t k, float qx, float qy,
+                                             float qz, float r2, float rexit, uint32_t *cnt) {
+    bool within, stop;
+    do {
+        const float *f = reinterpret_cast<const float *>(reinterpret_cast<const char *>(pts) +
+                                                         ((k << 3) + (k << 2)));
+        const P3 p = P3{f[0], f[1], f[2]};
+        ++k;
+        if (STATS) cnt[2] += 1;
+        within = flann_within(qx, qy, qz, p, r2);
+        stop = within | (qz - p.z >= rexit);
+    } while (!stop);
+    return within;
+}
+
 // a fine window's walk from k: z-descending, ended by the window's sentinel (never within r,
 // always r below), so no end index; dz >= rexit is FLANN's "fl(dz^2) >= r2" as one compare
 template <bool STATS>
@@ -307,7 +324,10 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
                     const float h2 = __builtin_fmaf((float)iz + 1.5f, g.fzc, g.fzo);
                     w0 = (ws & 0x0FFFFFFFu) + (qz + (rexit + 1e-4f) < h2 ? ws >> 28 : 0u);
                 }
-                if (scan_window<STATS>(g.wpts, w0, qx, qy, qz, r2, rexit, cnt)) return k;
+                if (g.wpack ? scan_window3<STATS>(reinterpret_cast<const float *>(g.wpts), w0, qx,
+                                                  qy, qz, r2, rexit, cnt)
+                            : scan_window<STATS>(g.wpts, w0, qx, qy, qz, r2, rexit, cnt))
+                    return k;
             }
         }
         return -1;

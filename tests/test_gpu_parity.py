@@ -419,7 +419,8 @@ def test_raycast_fan_poses_per_wave(oracle, loaded, scene, cells, npw, tile, mon
     LDS) on split and 8-byte fine records: blocked counts, units and first hits exact."""
     T, _ = loaded
     monkeypatch.setenv("PCP_FAN_NPW", npw)
-    monkeypatch.setenv("PCP_FINE_TILE", tile)
+    monkeypatch.setenv("PCP_FINE_TILE", tile.rstrip("u"))
+    monkeypatch.setenv("PCP_FINE_PACK", "0" if tile.endswith("u") else "1")
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", "2")
     ctx = _abi.Context(0)
     try:
@@ -840,9 +841,10 @@ def test_drivable_area_matches_oracle(gpu, oracle, kw):
 # (PCP_TERRAIN_BLOCKS, PCP_TERRAIN_FINE, PCP_FINE_TILE, expected scan layout); fine tile 0:
 # x-fastest 8-byte records, 1: 4 x 4 tiles of them, 2: split records (2-byte thresholds +
 # 4-byte starts) in 8 x 8 tiles
+# (the fine-window entries are 12-byte packed unless the tile field carries "u": PCP_FINE_PACK=0)
 LAYOUTS = [("0", "3", "1", "cells"), ("2", "0", "1", "blocks"), ("2", "2", "1", "fine"),
            ("2", "3", "1", "fine"), ("2", "2", "0", "fine"), ("2", "2", "2", "fine"),
-           ("2", "3", "2", "fine")]
+           ("2", "3", "2", "fine"), ("2", "2", "2u", "fine")]
 
 
 @pytest.mark.parametrize("mode,fine,tile,layout", LAYOUTS)
@@ -853,7 +855,8 @@ def test_terrain_block_copy_paths(oracle, scene, cells, aux, mode, fine, tile, l
     switches at the second query): all bit-exact on the fan and the reference-mode scoring."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", mode)
     monkeypatch.setenv("PCP_TERRAIN_FINE", fine)
-    monkeypatch.setenv("PCP_FINE_TILE", tile)
+    monkeypatch.setenv("PCP_FINE_TILE", tile.rstrip("u"))
+    monkeypatch.setenv("PCP_FINE_PACK", "0" if tile.endswith("u") else "1")
     ctx = _abi.Context(0)
     try:
         ctx.set_terrain(scene.terrain, point_step=32)
@@ -887,7 +890,8 @@ def test_terrain_block_copy_dense_and_tiny(oracle, mode, fine, tile, layout, mon
     thousands of points, ties in z) next to a sparse plane, and a one-point terrain."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", mode)
     monkeypatch.setenv("PCP_TERRAIN_FINE", fine)
-    monkeypatch.setenv("PCP_FINE_TILE", tile)
+    monkeypatch.setenv("PCP_FINE_TILE", tile.rstrip("u"))
+    monkeypatch.setenv("PCP_FINE_PACK", "0" if tile.endswith("u") else "1")
     rng = np.random.default_rng(11)
     dense = np.column_stack([rng.uniform(2.0, 2.3, 20_000), rng.uniform(-0.15, 0.15, 20_000),
                              np.round(rng.uniform(0.0, 0.3, 20_000), 2)])
