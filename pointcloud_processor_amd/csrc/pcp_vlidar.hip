@@ -584,10 +584,169 @@ __device__ __forceinline__ void row_sum_body(const double *__restrict__ sm,
     }
 }
 
+// The same sums, one ROW PER LANE: a block of kT threads owns kSumRows rows.  Waves 1..3 load
+// chunks of kSumCh cells of those rows (coalesced, one row per pass, kSumLpt cells per thread),
+// form the values (the max with score_z, x > 0 ? x : +0.0, the covered counts) and stage them
+// in LDS [row][cell]; lane r of wave 0 then walks row r of the chunk in cell order -- its
+// chain is the dependent v_add_f64s alone (~6 clocks each on gfx950, tools/mb/chain.hip), the
+// LDS reads of the next two groups of 32 values in flight under the adds of the current group,
+// with no readlane traffic in front of each add (the one-wave-per-row chain above: 2 readlanes
+// per add, ~19 clocks).  Three LDS buffers: the loaders fill chunk k + 2 while the chain walks
+// chunk k, one barrier per chunk; their global loads run two chunks further ahead.
+// k_sum_flags at 256 poses x 3,704 cells (tools/ab_libs.sh): 29.6 us one wave per row; lane
+// per row with 16 / 8 / 4 / 2 rows per block 33 / 27 / 25.5 / 25.5 us (a block's loads are
+// latency x concurrency bound on its CU, so few rows per block), the ring walk 20.5 us.
+#ifndef PCP_SUM_ROWS
+#define PCP_SUM_ROWS 4   // rows per block: few, so the loads of the rows spread over many CUs
+#endif
+#ifndef PCP_SUM_LPT
+#define PCP_SUM_LPT 2    // cells per loader thread per chunk (chunk = 192 x this)
+#endif
+#ifndef PCP_SUM_BATCH
+#define PCP_SUM_BATCH 16 // ds_read_b128 per group of the walk
+#endif
+constexpr int kSumRows = PCP_SUM_ROWS, kSumLpt = PCP_SUM_LPT, kSumCh = (kT - 64) * kSumLpt;
+constexpr int kSumLd = kSumCh + 2;   // +2: b128 reads of lanes r, r + 1 four banks apart
+__device__ __forceinline__ void row_group_body(const double *__restrict__ sm,
+                                               const double *__restrict__ score_z, int C, int P,
+                                               double *__restrict__ total,
+                                               int32_t *__restrict__ covered, int g) {
+    __shared__ double s_v[3][kSumRows][kSumLd];
+    __shared__ int32_t s_cov[kSumRows];
+    const int tid = threadIdx.x, r0 = g * kSumRows;
+    const int nch = (C + kSumCh - 1) / kSumCh;
+    if (tid < kSumRows) s_cov[tid] = 0;
+    const int lt = tid - 64;   // loader thread (waves 1..3): cells lt + (kT - 64) i of a chunk
+    int32_t cov[kSumRows];
+#pragma unroll
+    for (int q = 0; q < kSumRows; ++q) cov[q] = 0;
+    // raw loads into registers, unconditional (row and cell clamped into the buffer; the
+    // formation masks them), in two register sets for chunks of even / odd index: the loads
+    // of chunk k + 4 go out while chunk k + 2 is formed, two chain chunks ahead of their use
+    double mA[kSumLpt][kSumRows], szA[kSumLpt], mB[kSumLpt][kSumRows], szB[kSumLpt];
+    auto load = [&](int k, double (&m)[kSumLpt][kSumRows], double (&sz)[kSumLpt]) {
+#pragma unroll
+        for (int i = 0; i < kSumLpt; ++i) {
+            const int c = min(k * kSumCh + lt + (kT - 64) * i, C - 1);
+            sz[i] = score_z[c];
+#pragma unroll
+            for (int q = 0; q < kSumRows; ++q)
+                m[i][q] = sm[(size_t)max(min(r0 + q, P - 1), 0) * C + c];
+        }
+    };
+    auto form = [&](int k, const double (&m)[kSumLpt][kSumRows], const double (&sz)[kSumLpt]) {
+        double(*dst)[kSumLd] = s_v[k % 3];
+#pragma unroll
+        for (int i = 0; i < kSumLpt; ++i) {
+            const int cl = lt + (kT - 64) * i;
+            const bool in = k * kSumCh + cl < C;
+#pragma unroll
+            for (int q = 0; q < kSumRows; ++q) {
+                const double x = r0 + q < P ? ((sz[i] < m[i][q]) ? m[i][q] : sz[i]) : sz[i];
+                const bool pos = in && x > 0;   // (cells past C add +0.0)
+                cov[q] += pos ? 1 : 0;
+                dst[q][cl] = pos ? x : 0.0;
+            }
+        }
+    };
+    double acc = 0.0;
+    auto walk = [&](int k) {
+        // software-pipelined walk over a ring of three groups of kG b128 reads: the adds of
+        // group i run while groups i + 1 and i + 2 are in flight.  lgkmcnt counts at most 15
+        // outstanding LDS operations, so a wait for group i also waits for the head of group
+        // i + 1 -- issued a whole group of adds earlier, so already in -- but never for group
+        // i + 2, issued just before.  The scheduling barriers keep each group's reads ahead of
+        // the adds before it (the scheduler otherwise sinks them next to their use, exposing
+        // the LDS latency).  tools/ab_libs.sh: two batches of 4 / 6 / 16 reads 24.1 / 23.2 /
+        // 21.0 us per k_sum_flags, the ring of 8 / 16 21.1 / 20.5 us.
+        const double2 *v = reinterpret_cast<const double2 *>(s_v[k % 3][tid]);
+        constexpr int kG = PCP_SUM_BATCH, kN = kSumCh / 2;
+        static_assert(kN % (3 * kG) == 0, "whole group triples per chunk");
+        double2 g0[kG], g1[kG], g2[kG];
+        auto rd = [&](double2 *g, int j) {
+#pragma unroll
+            for (int i = 0; i < kG; ++i) g[i] = v[j + i];
+        };
+        auto add = [&](const double2 *g) {
+#pragma unroll
+            for (int i = 0; i < kG; ++i) {
+                acc += g[i].x;
+                acc += g[i].y;
+            }
+        };
+        rd(g0, 0);
+        rd(g1, kG);
+#pragma unroll
+        for (int j = 0; j < kN; j += 3 * kG) {
+            if (j + 2 * kG < kN) rd(g2, j + 2 * kG);
+            __builtin_amdgcn_sched_barrier(0);
+            add(g0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (j + 3 * kG < kN) rd(g0, j + 3 * kG);
+            __builtin_amdgcn_sched_barrier(0);
+            add(g1);
+            __builtin_amdgcn_sched_barrier(0);
+            if (j + 4 * kG < kN) rd(g1, j + 4 * kG);
+            __builtin_amdgcn_sched_barrier(0);
+            add(g2);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    // one chunk: the loaders form chunk k + 2 (and load k + 4) while the chain walks chunk k
+    auto step = [&](int k, double (&m)[kSumLpt][kSumRows], double (&sz)[kSumLpt]) {
+        if (tid >= 64) {
+            if (k + 2 < nch) {
+                form(k + 2, m, sz);
+                if (k + 4 < nch) load(k + 4, m, sz);
+            }
+        } else if (tid < kSumRows) {
+            walk(k);
+        }
+        __syncthreads();
+    };
+    if (tid >= 64) {
+        load(0, mA, szA);
+        if (nch > 1) load(1, mB, szB);
+        form(0, mA, szA);
+        if (nch > 2) load(2, mA, szA);
+        if (nch > 1) form(1, mB, szB);
+        if (nch > 3) load(3, mB, szB);
+    }
+    __syncthreads();
+    for (int k = 0; k < nch; k += 2) {
+        step(k, mA, szA);
+        if (k + 1 < nch) step(k + 1, mB, szB);
+    }
+    if (tid >= 64) {
+#pragma unroll
+        for (int q = 0; q < kSumRows; ++q) {
+            int32_t x = cov[q];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+            if ((tid & 63) == 0) atomicAdd(&s_cov[q], x);
+        }
+    }
+    __syncthreads();
+    if (tid < kSumRows && r0 + tid <= P) {
+        total[r0 + tid] = acc;
+        covered[r0 + tid] = s_cov[tid];
+    }
+}
+__host__ __device__ constexpr int sum_groups(int P) { return (P + 1 + kSumRows - 1) / kSumRows; }
+
+#ifndef PCP_ROW_SUM_LANES
+#define PCP_ROW_SUM_LANES 1   // 0: the readlane chain (one wave per row) above
+#endif
+
 __global__ void __launch_bounds__(64)
 k_row_sum(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
           double *__restrict__ total, int32_t *__restrict__ covered) {
     row_sum_body(sm, score_z, C, P, total, covered, blockIdx.x);
+}
+__global__ void __launch_bounds__(kT)
+k_row_sum_lanes(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
+                double *__restrict__ total, int32_t *__restrict__ covered) {
+    row_group_body(sm, score_z, C, P, total, covered, blockIdx.x);
 }
 
 // stats slots
@@ -658,19 +817,32 @@ k_cell_flags(const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbit
     cell_flags_body(zbits, mbits, C, P, flags, stats, blockIdx.x);
 }
 
-// the two independent tails of a score query in ONE launch: blocks 0 .. P are the ordered row
-// sums (wave 0 of each; a 3,704-add chain, ~30 us), the blocks after them the stale-flag
-// resolution (~7 us), which so runs beside the chains instead of after them
+// the two independent tails of a score query in ONE launch: the first blocks are the ordered
+// row sums (row_group_body, kSumRows rows per block; a 3,704-add chain per row, ~20 us), the
+// blocks after them the stale-flag resolution (~7 us), which so runs beside the chains
+// instead of after them
 __global__ void __launch_bounds__(kT)
 k_sum_flags(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
             double *__restrict__ total, int32_t *__restrict__ covered,
             const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbits,
             uint8_t *__restrict__ flags, int32_t *__restrict__ stats) {
-    if ((int)blockIdx.x <= P) {
+#if PCP_ROW_SUM_LANES
+    const int nr = sum_groups(P);
+    if ((int)blockIdx.x < nr) {
+        row_group_body(sm, score_z, C, P, total, covered, blockIdx.x);
+        return;
+    }
+#else
+    const int nr = P + 1;
+    if ((int)blockIdx.x < nr) {
         if (threadIdx.x < 64) row_sum_body(sm, score_z, C, P, total, covered, blockIdx.x);
         return;
     }
-    cell_flags_body(zbits, mbits, C, P, flags, stats, (int)blockIdx.x - (P + 1));
+#endif
+    cell_flags_body(zbits, mbits, C, P, flags, stats, (int)blockIdx.x - nr);
+}
+__host__ __device__ constexpr int sum_flag_row_blocks(int P) {
+    return PCP_ROW_SUM_LANES ? sum_groups(P) : P + 1;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1353,8 +1525,13 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
         o.score_z = score_z;
         if (!fuse_tail) {   // (fused: k_sum_flags, launched by the caller)
             ProfScope ps(ctx, PCP_K_POSE_SUM);
-            hipLaunchKernelGGL(k_row_sum, dim3(P + 1), dim3(64), 0, st, (const double *)o.comb,
-                               (const double *)score_z, C, P, o.tot_d, o.cov_d);
+            if (PCP_ROW_SUM_LANES)
+                hipLaunchKernelGGL(k_row_sum_lanes, dim3((unsigned)sum_groups(P)), dim3(kT), 0, st,
+                                   (const double *)o.comb, (const double *)score_z, C, P, o.tot_d,
+                                   o.cov_d);
+            else
+                hipLaunchKernelGGL(k_row_sum, dim3(P + 1), dim3(64), 0, st, (const double *)o.comb,
+                                   (const double *)score_z, C, P, o.tot_d, o.cov_d);
             PCP_CHECK_LAUNCH(ctx);
         }
     } else {
@@ -1402,7 +1579,9 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     char *pin = ctx->res_host.as<char>();
     if (C) {   // the ordered row sums and the stale-flag resolution side by side
         ProfScope ps(ctx, PCP_K_POSE_SUM);
-        hipLaunchKernelGGL(k_sum_flags, dim3((unsigned)(P + 1 + (C + kT - 1) / kT)), dim3(kT), 0,
+        hipLaunchKernelGGL(k_sum_flags,
+                           dim3((unsigned)(sum_flag_row_blocks(P) + (C + kT - 1) / kT)), dim3(kT),
+                           0,
                            st, (const double *)o.comb, (const double *)o.score_z, C, P, o.tot_d,
                            o.cov_d, (const uint8_t *)o.zbits, (const uint8_t *)o.mbits, o.flags_d,
                            o.stats);
