@@ -437,10 +437,18 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
     const bool in_range = (L >= kMinDistance && L <= E.max_distance);
     if (!in_range) return 0.0;
     bits |= 1u;
-    const double elevation = atan2(dz, sqrt(dx * dx + dy * dy));
-    const double elevation_diff = elevation - pitch;
     const double fov_local = 180.0 * kPi / 180.0;
-    if (!(fabs(elevation_diff) <= fov_local / 2.0)) return 0.0;
+    // the FOV decision, exactly the reference's double one: a float atan2 (error < 1e-6 rad
+    // including the rounding of its arguments) decides every case farther than 1e-5 rad from
+    // the boundary; the double atan2 only the rest
+    const double h2 = dx * dx + dy * dy;
+    const double dfast = (double)atan2f((float)dz, sqrtf((float)h2)) - pitch;
+    if (fabs(dfast) > fov_local / 2.0 + 1e-5) return 0.0;
+    if (!(fabs(dfast) < fov_local / 2.0 - 1e-5)) {
+        const double elevation = atan2(dz, sqrt(h2));
+        const double elevation_diff = elevation - pitch;
+        if (!(fabs(elevation_diff) <= fov_local / 2.0)) return 0.0;
+    }
     bits |= 2u;
     bool visible;
     const double ndx = dx / L, ndy = dy / L, ndz = dz / L;
