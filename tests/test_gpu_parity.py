@@ -657,6 +657,43 @@ def test_score_poses_matches_reference_loop(gpu, oracle, loaded, scene, cells):
     assert rep2.best_idx == r_rep2.best_idx
 
 
+def test_score_fov_boundary(oracle):
+    """The FOV decision (virtual_lidar.cpp:665-672, |elevation - pitch| <= fov / 2) at and around
+    its boundary: cells straight below and above a pose (elevation exactly -pi/2, +pi/2) and a
+    hair off the vertical, pitches 0, +-1e-7, +-3e-6 (inside the band the kernel settles with
+    the double atan2) and +-2e-5, +-1e-3 (settled by its float atan2).  No terrain: every cell
+    in range and in view is visible, so the flags carry the FOV bits.  Flags, covered counts
+    and totals against the oracle."""
+    xyz = np.array([[0.0, 0.0, 0.0], [0.0, 0.0, 4.0], [1e-6, 0.0, 0.0], [0.0, -1e-4, 0.0],
+                    [0.01, 0.0, 0.0], [0.0, 0.0, 0.5], [3.0, 0.0, 2.0], [0.0, 1e-7, 4.0],
+                    [-2.0, 1.0, -3.0]])
+    nrm = np.tile(np.array([[0.0, 0.0, 1.0]], np.float32), (xyz.shape[0], 1))
+    pitches = [0.0, 1e-7, -1e-7, 3e-6, -3e-6, 2e-5, -2e-5, 1e-3, -1e-3]
+    poses = np.array([[0.0, 0.0, 2.0, pt, 0.4] for pt in pitches])
+    zx = np.array([0.0, 0.0, 2.0, 1e-7, 0.0])
+    params = _abi.default_vl_params()
+    with _abi.Context(0) as ctx:
+        ctx.set_cells(xyz, nrm)
+        fg = np.zeros(xyz.shape[0], np.uint8)
+        fr = fg.copy()
+        for tick in range(2):   # each pose alone: the flags show every pose's own bits
+            for k in range(len(pitches)):
+                tot, cov, rep = ctx.score_poses(poses[k:k + 1].copy(), zx, params, fg)
+                r_tot, r_cov, r_rep = oracle.score_poses(None, None, xyz, nrm, poses[k:k + 1],
+                                                         zx, oracle.vl_params(), fr)
+                np.testing.assert_array_equal(fg, fr)
+                np.testing.assert_array_equal(cov, r_cov)
+                assert _rel_close(tot, r_tot)
+                assert rep.green == r_rep.green and rep.yellow == r_rep.yellow
+    # both sides of the boundary occur (the same double expression, in numpy)
+    d = xyz[None, :, :] - poses[:, None, :3]
+    L = np.linalg.norm(d, axis=2)
+    ediff = np.arctan2(d[..., 2], np.hypot(d[..., 0], d[..., 1])) - poses[:, 3:4]
+    fov = np.abs(ediff) <= (180.0 * np.pi / 180.0) / 2.0
+    inr = (L >= 0.5) & (L <= params.max_distance)
+    assert (inr & fov).any() and (inr & ~fov).any()
+
+
 def test_score_poses_clutter(oracle):
     """Reference-mode scoring against the volumetric cloud: visibility marches that end at the
     cell (s_k < L - 0.08), cells inside the clutter, behind the wall and in the open."""
