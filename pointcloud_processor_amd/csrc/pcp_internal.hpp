@@ -245,6 +245,8 @@ struct pcp_ctx {
     int num_cus = 256;                       // multiprocessors of the device
     int fan_batch = 0;                       // fan kernel variant (PCP_FAN_BATCH), A/B only
     int fan_npw = 8;                         // poses per wave of the fan kernel (PCP_FAN_NPW)
+    bool fan_host_out = true;                // k_fan_reduce stores into the pinned landing
+                                             // block, no D2H copy (PCP_FAN_HOST_OUT)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
     int fine_pack = 1;                       // fine-window entries as 12 bytes (PCP_FINE_PACK)
     int fine_tile = 2;                       // fine records: 0 x-fastest, 1 4 x 4 tiles, 2 split
@@ -336,10 +338,12 @@ struct FanEnq {
     unsigned long long *stats_d = nullptr;
 };
 // burst > 0: the plain kernel `burst` times back-to-back between two events, the average
-// launch time to *burst_ms (pcp_raycast_fan_burst)
+// launch time to *burst_ms (pcp_raycast_fan_burst).  host_out: k_fan_reduce stores the
+// per-pose {units u64[n], blocked u32[n]} straight into the pinned landing block
+// (ctx->fan_host past the staged poses) instead of device memory; o.*_d stay null.
 int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
                 bool want_fh, bool stats, bool stamps, FanEnq &o, int burst = 0,
-                double *burst_ms = nullptr);
+                double *burst_ms = nullptr, bool host_out = false);
 
 // runOptimization's scoring up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip)
 struct ScoreEnq {

@@ -1305,6 +1305,7 @@ k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves, uint32_t P, uint32_
     if (threadIdx.x == 0) {
         blocked[p] = sb[0] + sb[1] + sb[2] + sb[3];
         units[p] = su[0] + su[1] + su[2] + su[3];
+        __threadfence_system();   // the outputs may be pinned host memory (fan_host_out)
     }
 }
 
@@ -1628,7 +1629,8 @@ namespace pcp {
 // the march, k_fan_reduce.  On return o.blocked_d / o.units_d (and o.fh_d when want_fh) are
 // device results in flight; the caller synchronizes.  n > 0.
 int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_params *fan,
-                bool want_fh, bool stats, bool stamps, FanEnq &o, int burst, double *burst_ms) {
+                bool want_fh, bool stats, bool stamps, FanEnq &o, int burst, double *burst_ms,
+                bool host_out) {
     if (fan->n_az <= 0 || fan->n_el <= 0 || (int64_t)fan->n_az * fan->n_el > (1ll << 30))
         return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan: bad fan size %d x %d", fan->n_az,
                        fan->n_el);
@@ -1681,7 +1683,11 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
     PCP_HIP(ctx, ctx->stats_d.ensure(stats_bytes));
     PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pose8, (size_t)P * 8 * sizeof(double),
                                 hipMemcpyHostToDevice, st));
-    unsigned long long *units_d = ctx->out_c.as<unsigned long long>();
+    // results land in device memory, or (host_out) straight in the pinned block behind the
+    // staged poses: one copy and its dispatch fewer per query
+    unsigned long long *units_d =
+        host_out ? reinterpret_cast<unsigned long long *>(pose8 + 8 * (size_t)P)
+                 : ctx->out_c.as<unsigned long long>();
     uint32_t *blocked_d = reinterpret_cast<uint32_t *>(units_d + P);
     int16_t *fh_d = nullptr;
     if (want_fh) {
@@ -1836,8 +1842,8 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
                        (const uint2 *)a.wave_part, waves, (uint32_t)P, a.per_xcd, blocked_d,
                        units_d);
     PCP_CHECK_LAUNCH(ctx);
-    o.blocked_d = blocked_d;
-    o.units_d = units_d;
+    o.blocked_d = host_out ? nullptr : blocked_d;
+    o.units_d = host_out ? nullptr : units_d;
     o.fh_d = fh_d;
     o.rays = rays;
     o.stats_bytes = stats_bytes;
@@ -1862,8 +1868,9 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
         return PCP_OK;
     }
     FanEnq o;
+    const bool host_out = ctx->fan_host_out;
     if (int rc = fan_enqueue(ctx, poses5, n, fan, first_hit != nullptr, stats != nullptr,
-                             stamps != nullptr, o, burst, burst_ms))
+                             stamps != nullptr, o, burst, burst_ms, host_out))
         return rc;
     hipStream_t st = ctx->stream;
     const int P = (int)n;
@@ -1877,7 +1884,8 @@ static int raycast_fan_impl(pcp_ctx *ctx, const double *poses5, uint64_t n,
     double *pose8 = ctx->fan_host.as<double>();
     uint64_t *u_h = reinterpret_cast<uint64_t *>(pose8 + 8 * (size_t)P);
     const uint32_t *b_h = reinterpret_cast<const uint32_t *>(u_h + P);
-    PCP_HIP(ctx, hipMemcpyAsync(u_h, o.units_d, (size_t)P * 12, hipMemcpyDeviceToHost, st));
+    if (!host_out)   // else k_fan_reduce stored them into u_h / b_h itself
+        PCP_HIP(ctx, hipMemcpyAsync(u_h, o.units_d, (size_t)P * 12, hipMemcpyDeviceToHost, st));
     if (first_hit)
         PCP_HIP(ctx, hipMemcpyAsync(first_hit, o.fh_d, (size_t)P * rays * sizeof(int16_t),
                                     hipMemcpyDeviceToHost, st));
