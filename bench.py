@@ -23,6 +23,7 @@ all three on rank 0 at N = 1.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -160,13 +161,17 @@ def _oracle():
     return pyoracle
 
 
-def cpu_baseline_fan(terrain, poses, fan, budget_s: float, threads: int = 1):
+def cpu_baseline_fan(terrain, poses, fan, budget_s: float, threads: int = 1,
+                     kdtree: bool = False):
     """The oracle (CPU restatement) on a bounded sample: the first k poses of this workload,
     whole fans, until ~budget_s elapsed.  threads = 1 is the reference's single-threaded
-    executor; threads > 1 is the OpenMP variant SURVEY 8d asks for beside it."""
+    executor; threads > 1 is the OpenMP variant SURVEY 8d asks for beside it.  kdtree: every
+    sample query answered by the restated KdTreeFLANN radiusSearch (oracle/pcp_flann.c) --
+    the reference's own search structure (virtual_lidar.cpp:782) -- instead of the exact
+    grid scan."""
     pyoracle = _oracle()
     pyoracle.set_threads(threads)
-    T = pyoracle.Cloud(terrain)
+    T = pyoracle.Cloud(terrain, flann=kdtree)
     units = 0
     k = 0
     chunk = 1 if threads == 1 else max(1, threads // 16)
@@ -183,17 +188,21 @@ def cpu_baseline_fan(terrain, poses, fan, budget_s: float, threads: int = 1):
     return {"value": units / dt, "unit": "ray-hit tests/s", "cores": threads, "kind": "port",
             "sample": f"{k} pose fans (cycling the {len(poses)} poses) x full "
                       f"{fan.n_az}x{fan.n_el}, "
-                      f"{units} sample queries in {dt:.1f} s (oracle/pcp_oracle.c, "
-                      f"{threads} thread{'s' if threads > 1 else ''})"}
+                      f"{units} sample queries in {dt:.1f} s ("
+                      + ("KdTreeFLANN restatement, oracle/pcp_flann.c, " if kdtree else
+                         "oracle/pcp_oracle.c, ")
+                      + f"{threads} thread{'s' if threads > 1 else ''})"}
 
 
-def cpu_baseline_cells(terrain, aux, cells, poses, zx, budget_s: float, threads: int = 1):
+def cpu_baseline_cells(terrain, aux, cells, poses, zx, budget_s: float, threads: int = 1,
+                       kdtree: bool = False):
     """runOptimization's candidate loop on the CPU: 1 thread = the reference's own loop
-    (orc_score_poses, flags and all); threads > 1 = per-pose totals over OpenMP."""
+    (orc_score_poses, flags and all); threads > 1 = per-pose totals over OpenMP.  kdtree:
+    the radius searches on the restated KdTreeFLANN (oracle/pcp_flann.c), as the reference."""
     pyoracle = _oracle()
     import numpy as np
 
-    T, A = pyoracle.Cloud(terrain), pyoracle.Cloud(aux)
+    T, A = pyoracle.Cloud(terrain, flann=kdtree), pyoracle.Cloud(aux, flann=kdtree)
     prm = pyoracle.vl_params()
     flags = np.zeros(cells.xyz.shape[0], np.uint8)
     chunk = 1 if threads == 1 else threads
@@ -213,7 +222,8 @@ def cpu_baseline_cells(terrain, aux, cells, poses, zx, budget_s: float, threads:
     return {"value": k / dt, "unit": "poses/s", "cores": threads, "kind": "port",
             "sample": f"{k} pose evaluations (cycling the {len(poses)} poses) x "
                       f"{cells.xyz.shape[0]} cells in {dt:.1f} s "
-                      f"({'orc_score_poses' if threads == 1 else 'orc_score_totals, OpenMP'})"}
+                      f"({'orc_score_poses' if threads == 1 else 'orc_score_totals, OpenMP'}"
+                      + (", KdTreeFLANN restatement oracle/pcp_flann.c)" if kdtree else ")")}
 
 
 def cpu_baseline_c3(clouds, box, leaf, tfs, budget_s: float = 4.0):
@@ -251,15 +261,22 @@ def _timed(step, args, dist, on_gpu, dev):
 
     for _ in range(args.warmup):
         step()
-    barrier_sync()
-    t0 = time.perf_counter()
-    units = 0.0
-    res = None
-    for _ in range(args.steps):
-        u, res = step()
-        units += u
-    barrier_sync()
-    dt = time.perf_counter() - t0
+    gc_was = gc.isenabled()
+    gc.collect()
+    gc.disable()   # no collector pause inside the K timed steps (host-side jitter only)
+    try:
+        barrier_sync()
+        t0 = time.perf_counter()
+        units = 0.0
+        res = None
+        for _ in range(args.steps):
+            u, res = step()
+            units += u
+        barrier_sync()
+        dt = time.perf_counter() - t0
+    finally:
+        if gc_was:
+            gc.enable()
     t = torch.tensor([dt], dtype=torch.float64)
     uu = torch.tensor([units], dtype=torch.float64)
     if dist is not None:
@@ -438,6 +455,10 @@ def run_all(args, torch, dist, world, rank, local, backend):
                                                   args.cpu_seconds / 2,
                                                   threads=host["threads_used"])
         out["cpu_baseline_mt"]["host"] = host
+        # the reference's own search structure on one core: the march of virtual_lidar.cpp:
+        # 765-797 with radiusSearch on the restated KdTreeFLANN (FLANN 1.9.1 as PCL configures it)
+        out["cpu_baseline_kdtree"] = cpu_baseline_fan(scene.terrain, poses, fan,
+                                                      args.cpu_seconds / 2, kdtree=True)
 
     # ---- reference mode: runOptimization over the excavation cells (poses/s) -----------
     if not args.fan_only:
@@ -478,6 +499,9 @@ def run_all(args, torch, dist, world, rank, local, backend):
             out["reference_mode"]["cpu_baseline_mt"] = cpu_baseline_cells(
                 scene.terrain, aux, cells, cposes, scene.zx120_pose5, args.cpu_seconds / 2,
                 threads=host["threads_used"])
+            out["reference_mode"]["cpu_baseline_kdtree"] = cpu_baseline_cells(
+                scene.terrain, aux, cells, cposes, scene.zx120_pose5, args.cpu_seconds / 2,
+                kdtree=True)
         out["c3"] = run_filter(args, torch, dist, world, rank, local, backend, embedded=True,
                                cpu=cpu)
     ctx.close()
@@ -631,7 +655,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--mode", choices=["all", "fan", "filter", "cells", "launch-check"],
                     default="all",
                     help="all (default): the fan line with reference-mode scoring and C3 as "

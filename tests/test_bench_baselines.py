@@ -1,0 +1,32 @@
+"""bench.py's CPU baselines (the oracle timed on the host): the grid-scan and the KdTreeFLANN
+restatements march the same fans to the same sample-query counts, so their rates are rates of
+the same work (bench.py cpu_baseline / cpu_baseline_kdtree)."""
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+import bench  # noqa: E402
+import pyoracle  # noqa: E402
+from pointcloud_processor_amd import _abi, synth  # noqa: E402
+
+
+def test_fan_baseline_grid_and_kdtree_count_the_same_work():
+    sc = synth.terrain_scene(n_side=120, x0=-2.0, y0=-4.0)
+    poses = np.array([[8.0, -3.0, 1.1, -0.5, 2.6], [1.0, 3.0, 1.1, -0.4, -1.2]])
+    fan = _abi.fan_params(n_az=64, n_el=16)
+    grid = pyoracle.Cloud(sc.terrain)
+    tree = pyoracle.Cloud(sc.terrain, flann=True)
+    args = (poses, fan.n_az, fan.n_el, fan.el_min, fan.el_max, fan.max_distance)
+    bg, ug, fg = pyoracle.raycast_fan(grid, *args, want_first_hit=True)
+    bt, ut, ft = pyoracle.raycast_fan(tree, *args, want_first_hit=True)
+    assert np.array_equal(bg, bt) and np.array_equal(ug, ut) and np.array_equal(fg, ft)
+    # the baselines report sample queries per second over whole fans, labelled by structure
+    for kd in (False, True):
+        r = bench.cpu_baseline_fan(sc.terrain, poses, fan, 0.05, kdtree=kd)
+        assert r["value"] > 0 and r["cores"] == 1 and r["kind"] == "port"
+        assert ("KdTreeFLANN" in r["sample"]) == kd

@@ -22,7 +22,7 @@ if [ "$WHAT" = all ] || [ "$WHAT" = test ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
-  step bench 600 python bench.py --steps 10 --warmup 3
+  step bench 600 python bench.py
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --mode fan --steps 5 --warmup 2 --no-cpu-baseline
