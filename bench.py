@@ -404,8 +404,11 @@ def run_all(args, torch, dist, world, rank, local, backend):
     units_h = np.zeros(max(poses.shape[0], 1), np.uint64)
 
     def fan_step():
-        ctx.raycast_fan_into(poses, fan, blocked_h, units_h)
-        keys, b = pd.reduce_fan(blocked_h[:poses.shape[0]], lo, hi, P_total, dist, dev)
+        b = ctx.raycast_fan_into(poses, fan, blocked_h, units_h)   # argmin of its poses (C)
+        if dist is None:   # one rank: the library's argmin is the node's answer
+            keys = blocked_h
+        else:
+            keys, b = pd.reduce_fan(blocked_h[:poses.shape[0]], lo, hi, P_total, dist, dev)
         best["fan"] = b   # ^ the one collective
         return int(units_h[:poses.shape[0]].sum()), keys
 
@@ -478,7 +481,10 @@ def run_all(args, torch, dist, world, rank, local, backend):
 
         def cells_step():
             ctx.score_poses_into(cposes, zx5, params, flags, tot, cov, rep)
-            _, b, _ = pd.reduce_scores(tot[:cposes.shape[0]], lo, hi, P_total, dist, dev)
+            if dist is None:   # one rank: the library's strict-'>' argmax (rep.best_idx)
+                b = rep.best_idx
+            else:
+                _, b, _ = pd.reduce_scores(tot[:cposes.shape[0]], lo, hi, P_total, dist, dev)
             best["cells"] = b
             return cposes.shape[0], tot
 

@@ -1115,11 +1115,12 @@ struct FanArgs {
     float r2, rexit;
     int present;
     int16_t *first_hit;
-    // per-wave partials {blocked, units}, one 8-byte store per wave (no atomics).  Wave w of
-    // pose p is launch item b = w * P + p; its slot groups the items by XCD (item b runs on XCD
-    // b % 8), so each XCD's L2 fills whole lines before they leave: slot = (b % 8) * per + b / 8
+    // per-wave partials {blocked, units}, one 8-byte store per wave (no atomics), pose-major:
+    // slot = p * waves + w.  Every wave of a pose runs on one XCD (the XCD-chunk kernels: XCD
+    // p / (P / 8); the interleaved ones: XCD p % 8), so that XCD's L2 fills the pose's lines,
+    // and k_fan_reduce reads each pose's partials as one contiguous run
     uint2 *wave_part;
-    uint32_t P, per_xcd;
+    uint32_t P;
     unsigned long long *stats;     // MODE 1: probes, scanned stencils, point tests
                                    // MODE 2: per-wave s_memtime stamps [P*waves][4]
 };
@@ -1202,9 +1203,7 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p0, uint32_t
     uint32_t u = active ? (hit >= 0 ? (uint32_t)hit + 1u : (uint32_t)a.K) : 0u;
     u = wave_sum_u32(u);
     if ((threadIdx.x & 63) == 0 && wid < a.waves) {
-        const uint32_t b = wid * a.P + p;
-        a.wave_part[(size_t)(b & 7u) * a.per_xcd + (b >> 3)] =
-            make_uint2((uint32_t)__popcll(bal), u);
+        a.wave_part[(size_t)p * a.waves + wid] = make_uint2((uint32_t)__popcll(bal), u);
     }
     if (MODE == FAN_STATS) {   // per-wave slots [4][P * waves], summed by k_sum_u64
         const size_t nw = (size_t)a.P * a.waves;
@@ -1279,14 +1278,14 @@ k_sum_u64(const unsigned long long *__restrict__ in, size_t n, unsigned long lon
 // per-pose sums of the per-wave partials: one block per pose, fixed order (integer sums:
 // exact and deterministic)
 __global__ void __launch_bounds__(kT)
-k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves, uint32_t P, uint32_t per_xcd,
+k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves,
              uint32_t *__restrict__ blocked, unsigned long long *__restrict__ units) {
     const uint32_t p = blockIdx.x;
+    const uint2 *row = part + (size_t)p * waves;   // the pose's partials, contiguous
     uint32_t b = 0;
     unsigned long long u = 0;
     for (uint32_t w = threadIdx.x; w < waves; w += kT) {
-        const uint32_t it = w * P + p;
-        const uint2 v = part[(size_t)(it & 7u) * per_xcd + (it >> 3)];
+        const uint2 v = row[w];
         b += v.x;
         u += v.y;
     }
@@ -1305,7 +1304,9 @@ k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves, uint32_t P, uint32_
     if (threadIdx.x == 0) {
         blocked[p] = sb[0] + sb[1] + sb[2] + sb[3];
         units[p] = su[0] + su[1] + su[2] + su[3];
+#ifndef PCP_NO_HOSTOUT_FENCE
         __threadfence_system();   // the outputs may be pinned host memory (fan_host_out)
+#endif
     }
 }
 
@@ -1719,7 +1720,6 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
     a.r2 = (float)(kRayRadius * kRayRadius);
     a.rexit = exit_dist(a.r2);
     a.first_hit = fh_d;
-    a.per_xcd = (uint32_t)(((uint64_t)waves * P + 7) / 8);
     a.wave_part = ctx->out_b.as<uint2>();
     a.stats = ctx->stats_d.as<unsigned long long>();
     const dim3 grid1(waves * (uint32_t)P);           // 64-thread blocks, pose-interleaved
@@ -1839,7 +1839,7 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
 #undef PCP_FAN_LAUNCH
 #undef PCP_FAN_LAUNCH_T
     hipLaunchKernelGGL(k_fan_reduce, dim3(P), dim3(kT), 0, st,
-                       (const uint2 *)a.wave_part, waves, (uint32_t)P, a.per_xcd, blocked_d,
+                       (const uint2 *)a.wave_part, waves, blocked_d,
                        units_d);
     PCP_CHECK_LAUNCH(ctx);
     o.blocked_d = host_out ? nullptr : blocked_d;
