@@ -1304,9 +1304,10 @@ k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves,
     if (threadIdx.x == 0) {
         blocked[p] = sb[0] + sb[1] + sb[2] + sb[3];
         units[p] = su[0] + su[1] + su[2] + su[3];
-#ifndef PCP_NO_HOSTOUT_FENCE
-        __threadfence_system();   // the outputs may be pinned host memory (fan_host_out)
-#endif
+        // the outputs may be pinned host memory (fan_host_out): the caller reads them after
+        // hipStreamSynchronize, whose completion signal carries the kernel's system-scope
+        // release.  A __threadfence_system() per block here measured 11.7 vs 5.8 us per launch
+        // (profiles/r02_fan_ab_fence.log) for nothing the synchronisation does not give.
     }
 }
 
