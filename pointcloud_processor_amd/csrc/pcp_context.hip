@@ -321,6 +321,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->carve_buf.release();
     ctx->fan_host.release();
     ctx->res_host.release();
+    ctx->fm_res_host.release();
     ctx->small_host.release();
     DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage, &ctx->fan_tab,
                       &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,

@@ -1021,12 +1021,19 @@ struct ResultInfo {
     uint32_t overflow;
 };
 
-static int read_results(pcp_ctx *ctx, const uint32_t *res_d, int k, ResultInfo *ri) {
-    // pinned landing buffer: the per-frame size readback is one small DMA, no staging copy
-    PCP_HIP(ctx, ctx->res_host.ensure(3 * kMaxClouds * sizeof(uint32_t)));
-    uint32_t *buf = ctx->res_host.as<uint32_t>();
-    PCP_HIP(ctx, hipMemcpyAsync(buf, res_d, 3 * kMaxClouds * sizeof(uint32_t),
-                                hipMemcpyDeviceToHost, ctx->stream));
+static int read_results(pcp_ctx *ctx, const uint32_t *res_d, int k, ResultInfo *ri,
+                        bool landed = false) {
+    // pinned landing buffer: the per-frame size readback is one small DMA, no staging copy;
+    // landed: the kernels stored the sizes in pinned memory themselves (res_d is host memory)
+    uint32_t *buf;
+    if (landed) {
+        buf = const_cast<uint32_t *>(res_d);
+    } else {
+        PCP_HIP(ctx, ctx->res_host.ensure(3 * kMaxClouds * sizeof(uint32_t)));
+        buf = ctx->res_host.as<uint32_t>();
+        PCP_HIP(ctx, hipMemcpyAsync(buf, res_d, 3 * kMaxClouds * sizeof(uint32_t),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+    }
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     for (int i = 0; i < k; ++i) {
         ri[i].n = buf[i];
@@ -1269,8 +1276,17 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
     // the emit needs the sizes first when the output might not fit (device output only)
     const bool emit_now = !(dev_out && upper > cap);
     const bool graphable = dev_in && dev_out && emit_now && ctx->use_graphs;
+    // the centroid kernel emits the records itself: no kernel reads the sizes back, so they
+    // are stored straight into pinned memory (no D2H copy per frame; PCP_FAN_HOST_OUT)
+    const bool landed = emit_now && ctx->fan_host_out && emit_in_centroid(bts);
+    if (landed) {
+        PCP_HIP(ctx, ctx->fm_res_host.ensure(3 * kMaxClouds * sizeof(uint32_t)));
+        res = ctx->fm_res_host.as<uint32_t>();
+    }
     if (graphable) {
         std::vector<uint8_t> key = fm_key(k, clouds, boxes, leaf, tf, rgb, out, cap, jobs);
+        key.insert(key.end(), reinterpret_cast<const uint8_t *>(&res),
+                   reinterpret_cast<const uint8_t *>(&res) + sizeof(res));
         if (!ctx->fm_exec || key != ctx->fm_key) {
             if (ctx->fm_exec) (void)hipGraphExecDestroy(ctx->fm_exec);
             if (ctx->fm_graph) (void)hipGraphDestroy(ctx->fm_graph);
@@ -1300,7 +1316,7 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
         if (rc) return rc;
     }
     std::vector<ResultInfo> ri(k);
-    if ((rc = read_results(ctx, res, k, ri.data()))) return rc;
+    if ((rc = read_results(ctx, res, k, ri.data(), landed))) return rc;
     uint64_t total = 0;
     for (int i = 0; i < k; ++i) {
         const uint64_t ni = clouds[i].n ? ri[i].n : 0;

@@ -237,6 +237,8 @@ struct pcp_ctx {
     pcp::DevBuf fan_tab, poses_d, steps_d, out_a, out_b, out_c, out_d, stats_d;
     pcp::PinnedBuf fan_host;                 // pinned staging of poses in / counts out
     pcp::PinnedBuf res_host;                 // pinned landing of the filter chain's sizes
+    pcp::PinnedBuf fm_res_host;              // pcp_filter_merge's result sizes, stored by its
+                                             // kernels themselves (fixed: a graph holds it)
     pcp::PinnedBuf small_host;               // pinned landing of small size readbacks
     int32_t fan_naz = -1, fan_nel = -1;      // cached fan direction tables
     double fan_elmin = 0.0, fan_elmax = 0.0;
