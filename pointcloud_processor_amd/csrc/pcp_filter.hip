@@ -233,7 +233,13 @@ struct JobBatch {
 
 // ---- crop: one read of the input; stable compaction of each tile into its own slot of a
 //      sparse buffer (kept count + bbox partial per tile); k_compact_keys closes the gaps ----
-__global__ void __launch_bounds__(kCT) k_crop_tile(const JobBatch jobs) {
+// PCP_CROP_WAVES (build knob, A/B): the crop's waves-per-SIMD floor (84 VGPRs -> 5 by default)
+#ifdef PCP_CROP_WAVES
+#define PCP_CROP_ATTR __attribute__((amdgpu_waves_per_eu(PCP_CROP_WAVES, PCP_CROP_WAVES)))
+#else
+#define PCP_CROP_ATTR
+#endif
+__global__ void __launch_bounds__(kCT) PCP_CROP_ATTR k_crop_tile(const JobBatch jobs) {
     const CloudJob &J = jobs.j[blockIdx.y];
     if (blockIdx.x >= J.nb) return;
     const CloudIn c = J.in;
