@@ -185,10 +185,12 @@ k_scan_tile_sums(const uint32_t *__restrict__ in, uint64_t n, uint32_t *__restri
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
-// scans each tile locally (thread owns kScanItems consecutive items), adds tile offset
+// scans each tile locally (thread owns kScanItems consecutive items), adds tile offset;
+// out2 (may be null, may be `in` itself: every thread reads its own items before it writes
+// them) receives a second copy of out[0 .. n)
 __global__ void __launch_bounds__(kScanThreads)
-k_scan_tiles(const uint32_t *__restrict__ in, uint64_t n, const uint32_t *__restrict__ offs,
-             uint32_t *__restrict__ out) {
+k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
+             uint32_t *__restrict__ out, uint32_t *out2) {
     __shared__ uint32_t lds4[4];
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
     uint32_t v[kScanItems];
@@ -204,7 +206,10 @@ k_scan_tiles(const uint32_t *__restrict__ in, uint64_t n, const uint32_t *__rest
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
         const uint64_t k = base + i;
-        if (k < n) out[k] = run;
+        if (k < n) {
+            out[k] = run;
+            if (out2) out2[k] = run;
+        }
         run += v[i];
     }
     // out[n] written by the last tile's last thread
@@ -221,7 +226,8 @@ size_t scan_tmp_bytes(uint64_t n) {
     return bytes + 256;
 }
 
-int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp) {
+int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp,
+                       uint32_t *out2) {
     if (n == 0) {
         PCP_HIP(ctx, hipMemsetAsync(out, 0, sizeof(uint32_t), ctx->stream));
         return PCP_OK;
@@ -229,7 +235,7 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
     const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
     if (tiles == 1) {
         hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, ctx->stream, in, n,
-                           (const uint32_t *)nullptr, out);
+                           (const uint32_t *)nullptr, out, out2);
         PCP_CHECK_LAUNCH(ctx);
         return PCP_OK;
     }
@@ -242,7 +248,7 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
     int rc = exclusive_scan_u32(ctx, sums, sums_scan, tiles, next);
     if (rc) return rc;
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(kScanThreads), 0, ctx->stream, in,
-                       n, (const uint32_t *)sums_scan, out);
+                       n, (const uint32_t *)sums_scan, out, out2);
     PCP_CHECK_LAUNCH(ctx);
     return PCP_OK;
 }

@@ -490,12 +490,11 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     // 5. prefix -> start
     PCP_HIP(ctx, g.start.ensure((ncell + 1) * sizeof(uint32_t)));
     PCP_HIP(ctx, ctx->scratch[4].ensure(scan_tmp_bytes(ncell) + (ncell + 1) * sizeof(uint32_t)));
+    // 6. scatter cursors = a copy of start, written by the scan over the counts in place (no
+    //    device-to-device copy)
     int rc = exclusive_scan_u32(ctx, ctx->scratch[3].as<const uint32_t>(), g.start.as<uint32_t>(),
-                                ncell, ctx->scratch[4].p);
+                                ncell, ctx->scratch[4].p, ctx->scratch[3].as<uint32_t>());
     if (rc) return rc;
-    // 6. scatter (cursor = copy of start)
-    PCP_HIP(ctx, hipMemcpyAsync(ctx->scratch[3].p, g.start.p, ncell * sizeof(uint32_t),
-                                hipMemcpyDeviceToDevice, st));
     PCP_HIP(ctx, g.pts.ensure((size_t)nfin * sizeof(float4)));
     // (with zsort the scatter lands in a temporary and the rank pass writes g.pts)
     if (zsort) PCP_HIP(ctx, ctx->scratch[5].ensure((size_t)nfin * sizeof(float4)));

@@ -327,7 +327,9 @@ int terrain_blocks_before_query(pcp_ctx *ctx);
 // scan: exclusive prefix sum of n uint32 values into out (n + 1 entries, out[n] = total).
 // tmp must hold scan_tmp_bytes(n).
 size_t scan_tmp_bytes(uint64_t n);
-int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp);
+// out2 (optional, may alias in): a second copy of out[0 .. n), e.g. a scatter's cursors
+int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp,
+                       uint32_t *out2 = nullptr);
 
 // fan query up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip): device results
 // in flight on return, the caller synchronizes.  n > 0.

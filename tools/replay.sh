@@ -18,7 +18,7 @@ open("gpurun_out/replay/args", "w").write(
     f"{sc.terrain.shape[0]} {cells.xyz.shape[0]} " + ",".join(repr(float(v)) for v in cells.grid_bbox) + "\n")
 PY
 read TN CN BB < gpurun_out/replay/args
-CLI=pointcloud_processor_amd/_lib/pcp_nodes_cli
+CLI=${CLI:-pointcloud_processor_amd/_lib/pcp_nodes_cli}
 for chain in 0 1; do
   timeout -k 10 300 $CLI replay gpurun_out/replay/t.f32 $TN gpurun_out/replay/c.f64 gpurun_out/replay/n.f32 $CN $BB ${FRAMES:-50} 60032 $chain
 done
