@@ -25,10 +25,13 @@ from __future__ import annotations
 import argparse
 import gc
 import json
+import math
 import os
 import sys
 import time
 from pathlib import Path
+
+import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -55,12 +58,19 @@ def _self_launch(n: int) -> int:
                                       sys.argv[1:], env=env))
     rc = 0
     try:
-        for p in procs:
-            rc = max(rc, p.wait())
-            if rc:
-                break
+        # any rank may die first: poll them all, and a non-zero exit ends the others (they
+        # would wait in a collective for the dead rank until the backend's timeout)
+        live = list(procs)
+        while live and not rc:
+            for p in list(live):
+                code = p.poll()
+                if code is not None:
+                    live.remove(p)
+                    rc = max(rc, code if code >= 0 else 128 - code)
+            if live and not rc:
+                time.sleep(0.05)
     finally:
-        for p in procs:   # a failed rank leaves the others stuck in a collective
+        for p in procs:
             if p.poll() is None:
                 p.kill()
                 p.wait()
@@ -111,17 +121,24 @@ def _grid_bbox(area, res=0.1):
                      p[:, 1].max() + res, p[:, 2].min() - res, p[:, 2].max() + res])
 
 
+TRAFFIC_FILES = ("r03_pmc_traffic.json", "pmc_traffic.json")   # newest round first
+
+
 def _traffic_from_profiles(workload_key: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py), or
-    None when no measurement for this workload is committed."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
-    if not f.exists():
-        return None
-    try:
-        d = json.loads(f.read_text()).get(workload_key)
-        return None if d is None else float(d["bytes_per_launch"])
-    except Exception:
-        return None
+    """HBM-side bytes per launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    (tools/pmc_traffic.py, the MI355X guide's gfx950 correction applied) -> (bytes, source
+    file), or (None, None) when no measurement of this workload is committed."""
+    for name in TRAFFIC_FILES:
+        f = ROOT / "profiles" / name
+        if not f.exists():
+            continue
+        try:
+            d = json.loads(f.read_text()).get(workload_key)
+        except ValueError:
+            continue
+        if d is not None:
+            return float(d["bytes_per_launch"]), f"profiles/{name}"
+    return None, None
 
 
 def _gbs(nbytes, seconds):
@@ -226,26 +243,36 @@ def cpu_baseline_cells(terrain, aux, cells, poses, zx, budget_s: float, threads:
                       + (", KdTreeFLANN restatement oracle/pcp_flann.c)" if kdtree else ")")}
 
 
-def cpu_baseline_c3(clouds, box, leaf, tfs, budget_s: float = 4.0):
+def cpu_baseline_c3(clouds, box, leaf, tfs, budget_s: float = 4.0, threads: int = 1):
     """processCloudSimple (crop + VoxelGrid) per cloud, then processRobotCloud's transform +
-    colour, on the CPU restatement: one whole C3 frame, one thread (PCL's path)."""
+    colour, on the CPU restatement: one whole C3 frame.  threads = 1: the reference's own
+    single-threaded path (orc_crop_box + orc_voxel_grid + orc_transform_rgb); threads > 1: the
+    same bytes from the OpenMP frame (oracle/pcp_oracle_mt.c: chunked crop, parallel stable
+    radix sort of the voxel keys, per-voxel in-order sums, parallel transform)."""
     pyoracle = _oracle()
     n_in = sum(c.shape[0] for c in clouds)
+    rgbs = [(255, 0, 0), (0, 0, 255)]
     frames = 0
     t0 = time.perf_counter()
     while frames == 0 or time.perf_counter() - t0 < budget_s:
-        n_out = 0
-        for c, (t, q), rgb in zip(clouds, tfs, [(255, 0, 0), (0, 0, 255)]):
-            kept = pyoracle.crop_box(c, box)
-            vox, _, _, _ = pyoracle.voxel_grid(c[kept], leaf)
-            out = pyoracle.transform_rgb(vox, t, q, rgb)
-            n_out += out.shape[0]
+        if threads == 1:
+            n_out = 0
+            for c, (t, q), rgb in zip(clouds, tfs, rgbs):
+                kept = pyoracle.crop_box(c, box)
+                vox, _, _, _ = pyoracle.voxel_grid(c[kept], leaf)
+                out = pyoracle.transform_rgb(vox, t, q, rgb)
+                n_out += out.shape[0]
+        else:
+            out, _ = pyoracle.filter_frame_mt(clouds, [box] * len(clouds), leaf, tfs, rgbs,
+                                              threads)
+            n_out = out.shape[0]
         frames += 1
     dt = (time.perf_counter() - t0) / frames
-    return {"value": n_in / dt, "unit": "input points/s", "cores": 1, "kind": "port",
+    how = ("oracle crop_box + voxel_grid + transform_rgb, 1 thread" if threads == 1 else
+           f"oracle filter_frame_mt, OpenMP, {threads} threads")
+    return {"value": n_in / dt, "unit": "input points/s", "cores": threads, "kind": "port",
             "sample": f"{frames} whole frames: {n_in} input points -> {n_out} merged, "
-                      f"{dt:.3f} s per frame "
-                      "(oracle crop_box + voxel_grid + transform_rgb)"}
+                      f"{dt:.3f} s per frame ({how})"}
 
 
 def _timed(step, args, dist, on_gpu, dev):
@@ -322,50 +349,60 @@ def _fan_npw(n_poses):
     return npw
 
 
+GATHER_PEAK = 256 * 2.4e9   # lane-loads/s: 256 CUs x 2.4 GHz peak clock x 1 divergent
+                            # lane-load per cycle per CU through the texture path (TA/TD)
+
+
 def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
-    """Roofline of k_raycast_fan from the kernel's own request counts:
-    requested bytes = 2 B per z-band probe (8 B per fine-window record) + 8 B per candidate
-    (its step) + 8 B per block directory load + 12 B per point record loaded + 16 B per ray and
-    wave-pose group (azimuth table, loaded once for the wave's NPW poses) + 8 B per wave
-    partial.  These are the bytes the kernel's loads and stores ask for (served by L1/L2/MALL:
-    the 1M-pt terrain's working set is cache-resident); the HBM-side bytes are the PMC
-    `traffic`."""
+    """Roofline of k_raycast_fan.  The kernel's bound is the texture path of its
+    gathers, not HBM: each lane of a probe, walk-start or point-record load hits its own cache
+    line, and the TA/TD units retire about one such lane-load per cycle per CU (TD 95 % busy,
+    profiles/r0*_fan_pmc_pack.txt).  So `achieved` = the gather lane-loads of one launch
+    (pcp_raycast_fan_stats: z-band probes + candidate walk starts + point records + directory
+    loads) / the launch time, against 256 CUs x 2.4 GHz x 1; the coalesced table loads and the
+    stores are left out (a wave's 64 lanes share their lines).  HBM is reported beside it from
+    the PMC bytes (hbm_frac), and the bytes the loads request (served by L1/L2/MALL: the
+    terrain copy is cache-resident) as requested_*."""
     st = ctx.raycast_fan_stats(poses, fan)
     layout = ctx.terrain_info()["scan_layout"]
-    # the fine-window layout's probe reads the 8-byte record (z band + run; split records: the
-    # 2-byte band, then 4 bytes of walk start per candidate), the others a 2-byte z band and then
-    # one 8-byte directory entry per scan; the XCD-chunk kernels read the step from LDS
     split = layout == "fine" and ctx.terrain_info().get("fine_tile") == 2
     probe_b = 8.0 if layout == "fine" and not split else 2.0
     cand_b = 4.0 if split else 8.0
     rays = poses.shape[0] * fan.n_az * fan.n_el
     waves = poses.shape[0] * ((fan.n_az * fan.n_el + 63) // 64)
     npw = _fan_npw(poses.shape[0]) if layout == "fine" else 1
+    gathers = (st["samples_visited"] + st["scanned_stencils"] + st["point_tests"]
+               + st["directory_loads"])
     req = probe_b * st["samples_visited"] + cand_b * st["scanned_stencils"] \
         + 8.0 * st["directory_loads"] + 12.0 * st["point_tests"] + 16.0 * rays / npw \
         + 8.0 * waves
     ref_model = 64.0 * units_per_launch + 12.0 * st["point_tests"]
-    traffic = _traffic_from_profiles("fan")
-    achieved = _gbs(req, avg_kernel_s)
+    traffic, tsrc = _traffic_from_profiles("fan")
+    achieved = gathers / avg_kernel_s if avg_kernel_s else None
+    hbm_gbs = _gbs(traffic, avg_kernel_s)
     return {
-        "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBS if achieved else None,
+        "bound": "gather (TA/TD)",
+        "achieved": achieved / 1e9 if achieved else None, "peak": GATHER_PEAK / 1e9,
+        "unit": "G lane-loads/s",
+        "frac": achieved / GATHER_PEAK if achieved else None,
         "traffic": traffic,
-        "traffic_gbs": _gbs(traffic, avg_kernel_s),
-        "traffic_frac": (_gbs(traffic, avg_kernel_s) or 0.0) / HBM_PEAK_GBS if traffic else None,
+        "traffic_source": tsrc,
+        "hbm_gbs": hbm_gbs,
+        "hbm_frac": hbm_gbs / HBM_PEAK_GBS if hbm_gbs else None,
+        "gather_lane_loads_per_launch": gathers,
+        "model": "frac = (probes + walk starts + point records + directory loads per launch, "
+                 "pcp_raycast_fan_stats) / avg_kernel_ms / (256 CUs x 2.4 GHz x 1 lane-load per "
+                 "cycle); hbm_frac = traffic (PMC FETCH_SIZE x2 + WRITE_SIZE per launch) / "
+                 "avg_kernel_ms / 8 TB/s",
         "kernel": (f"k_raycast_fan_xcd<0, 64, true, 8, {8 if split else 4}, true, {npw}>"
                    if layout == "fine"
                    else "k_raycast_fan<0, 64, true, 7, 0>"),
         "poses_per_wave": npw,
         "avg_kernel_ms": avg_kernel_s * 1e3, "scan_layout": layout,
         "requested_bytes_per_launch": req,
-        "model": f"requested bytes: {probe_b:.0f} B/probe + {cand_b:.0f} B/candidate (its "
-                 "walk start for split records, else its step) + 8 B/"
-                 "directory load + 12 B/point record + 16 B/ray/NPW + 8 B/wave "
-                 "(pcp_raycast_fan_stats counts); traffic = PMC FETCH(x2)+WRITE per launch "
-                 "(profiles/pmc_traffic.json)",
-        "limiter": "vector-memory gather path (TA/TD busy, L1 tag lookups per instruction; "
-                   "profiles/r02_fan_pmc*.txt), not HBM: the terrain lives in L2/MALL",
+        "requested_gbs": _gbs(req, avg_kernel_s),
+        "requested_model": f"{probe_b:.0f} B/probe + {cand_b:.0f} B/candidate + 8 B/directory "
+                           "load + 12 B/point record + 16 B/ray/NPW + 8 B/wave partial",
         "alg_reference_bytes_per_launch": ref_model,
         "alg_reference_bytes_frac": (ref_model / avg_kernel_s / 1e9 / HBM_PEAK_GBS)
         if avg_kernel_s else None,
@@ -402,17 +439,59 @@ def run_all(args, torch, dist, world, rank, local, backend):
 
     blocked_h = np.zeros(max(poses.shape[0], 1), np.uint32)
     units_h = np.zeros(max(poses.shape[0], 1), np.uint64)
+    # N > 1 over RCCL: the per-pose keys never leave the device before the collective --
+    # pcp_raycast_fan_keys writes (blocked << 32) | pose into a torch int64 vector (INT64_MAX
+    # in the other ranks' slots) on the library's stream, torch's stream waits on it, one
+    # all_reduce(MIN) in place, and only the reduced vector comes back D2H.  The gloo
+    # rehearsal (ranks sharing one GPU) keeps the host-side vector of dist.reduce_fan.
+    dev_keys = dist is not None and on_gpu and backend == "nccl"
+    if dev_keys:
+        keys_t = torch.empty(P_total, dtype=torch.int64, device=dev)
+        units_t = torch.zeros(max(poses.shape[0], 1), dtype=torch.int64, device=dev)
+        stream_ptr = torch.cuda.current_stream(dev).cuda_stream
+        units_step = {}
 
-    def fan_step():
-        b = ctx.raycast_fan_into(poses, fan, blocked_h, units_h)   # argmin of its poses (C)
-        if dist is None:   # one rank: the library's argmin is the node's answer
-            keys = blocked_h
-        else:
-            keys, b = pd.reduce_fan(blocked_h[:poses.shape[0]], lo, hi, P_total, dist, dev)
-        best["fan"] = b   # ^ the one collective
-        return int(units_h[:poses.shape[0]].sum()), keys
+        def fan_step():
+            ctx.raycast_fan_keys(poses, fan, lo, P_total, keys_t.data_ptr(), units_t.data_ptr(),
+                                 stream_ptr)
+            dist.all_reduce(keys_t, op=dist.ReduceOp.MIN)   # the one collective
+            kh = keys_t.cpu().numpy()                        # the reduced vector, D2H once
+            best["fan"] = int(kh.min()) & 0xFFFFFFFF
+            if "u" not in units_step:   # constant per pose set; re-read after the timed loop
+                units_step["u"] = int(units_t[:poses.shape[0]].sum().item())
+            return units_step["u"], kh
+    else:
+        def fan_step():
+            b = ctx.raycast_fan_into(poses, fan, blocked_h, units_h)   # argmin of its poses
+            if dist is None:   # one rank: the library's argmin is the node's answer
+                keys = blocked_h
+            else:
+                keys, b = pd.reduce_fan(blocked_h[:poses.shape[0]], lo, hi, P_total, dist, dev)
+            best["fan"] = b   # ^ the one collective
+            return int(units_h[:poses.shape[0]].sum()), keys
 
     dt, units_all, _ = _timed(fan_step, args, dist, on_gpu, dev)
+    collective = None
+    if dev_keys:
+        # the count the timed steps used is the kernel's (same poses, same work every step)
+        if int(units_t[:poses.shape[0]].sum().item()) != units_step["u"]:
+            raise SystemExit("bench.py: ray-hit tests changed between steps")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ms = []
+        for _ in range(max(args.steps, 3)):   # after the timed loop: events around the collective
+            ctx.raycast_fan_keys(poses, fan, lo, P_total, keys_t.data_ptr(), units_t.data_ptr(),
+                                 stream_ptr)
+            e0.record()
+            dist.all_reduce(keys_t, op=dist.ReduceOp.MIN)
+            e1.record()
+            e1.synchronize()
+            ms.append(e0.elapsed_time(e1))
+        collective = {"op": "all_reduce(MIN) int64", "backend": backend,
+                      "bytes": 8 * P_total, "collective_ms": float(np.median(ms)),
+                      "path": "device keys (pcp_raycast_fan_keys), reduced vector D2H once"}
+    elif dist is not None:
+        collective = {"op": "all_reduce(MIN) int64", "backend": backend, "bytes": 8 * P_total,
+                      "path": "host vector (gloo rehearsal: ranks share devices)"}
     k_avg = _profiled(ctx, fan_step, max(args.steps, 3), ["raycast_fan"])["raycast_fan"]
     # the kernel's launch time: the same launch 20 times back-to-back between two events on the
     # library's stream (the per-step events of the synchronous loop also hold the idle queue's
@@ -440,6 +519,7 @@ def run_all(args, torch, dist, world, rank, local, backend):
                    "poses_total": P_total, "fan": [args.n_az, args.n_el],
                    "num_candidates_lattice": nc, "parallelism": f"pose-shard x{world}",
                    "collective": None if dist is None else f"all_reduce(MIN) over {backend}"},
+        "collective": collective,
         "poses_per_s": P_total * args.steps / dt,
         "best_pose": best["fan"],
         "roofline": _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch),
@@ -510,6 +590,8 @@ def run_all(args, torch, dist, world, rank, local, backend):
                 kdtree=True)
         out["c3"] = run_filter(args, torch, dist, world, rank, local, backend, embedded=True,
                                cpu=cpu)
+        if rank == 0 and world == 1:
+            out["c1"] = run_c1(args, local, cpu)
     ctx.close()
     return out
 
@@ -613,7 +695,8 @@ def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=Fal
         ectx.close()
         pcie = None if args.no_pcie else _pcie_inclusive(ctx, clouds, box, tfs, n_in, cap)
     alg = 12.0 * n_in + 16.0 * n_out
-    traffic = _traffic_from_profiles("filter")
+    traffic, tsrc = _traffic_from_profiles("filter")
+    hbm_gbs = _gbs(traffic, step_dev_ms * 1e-3)
     res = {
         "metric": "crop+voxel+transform points/s (C3)", "value": units_all / dt,
         "unit": "input points/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -625,12 +708,16 @@ def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=Fal
         "roofline": {"bound": "hbm", "achieved": alg / (step_dev_ms * 1e-3) / 1e9,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": alg / (step_dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": traffic,
-                     "traffic_gbs": _gbs(traffic, step_dev_ms * 1e-3),
+                     "traffic": traffic, "traffic_source": tsrc,
+                     "hbm_gbs": hbm_gbs,
+                     "hbm_frac": hbm_gbs / HBM_PEAK_GBS if hbm_gbs else None,
+                     "traffic_over_alg": traffic / alg if traffic else None,
                      "limiter": "crop streams at ~4.8 TB/s; the voxel stage (sort of the ~1 M "
                                 "cropped points) is launch- and latency-bound",
                      "kernel": "filter_merge graph (all stages)", "avg_kernel_ms": step_dev_ms,
-                     "model": "12 B/input point + 16 B/output point (SURVEY 8d)"},
+                     "model": "achieved = 12 B/input point + 16 B/output point (SURVEY 8d) / "
+                              "device time of the frame; hbm_frac = traffic (PMC FETCH_SIZE x2 "
+                              "+ WRITE_SIZE per frame) / device time / 8 TB/s"},
     }
     if stages is not None:
         res["roofline"]["eager_stage_ms"] = stages
@@ -638,10 +725,119 @@ def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=Fal
         res["pcie_inclusive"] = pcie
     if cpu or (not embedded and rank == 0 and world == 1 and not args.no_cpu_baseline):
         res["cpu_baseline"] = cpu_baseline_c3(clouds, np.array(box), 0.05, tfs)
+        host = _host_cpu()
+        res["cpu_baseline_mt"] = cpu_baseline_c3(clouds, np.array(box), 0.05, tfs, budget_s=2.0,
+                                                 threads=host["threads_used"])
+        res["cpu_baseline_mt"]["host"] = host
     for p in dptr + [out_d]:
         ctx.dev_free(p)
     ctx.close()
     return res
+
+
+C1_BOX = [0.0, 15.0, -10.0, 10.0, -1.5, 10.0]   # pointcloud_filter.cpp:30-36 defaults
+C1_LEAF = 0.2                                    # voxel_leaf_size (:39)
+C1_TFS = [((8.0, -3.0, 2.0), (0.0, 0.0, 0.2588190451025208, 0.9659258262890683)),   # robot
+          ((0.55, 0.4, 3.5), (0.0, 0.21633, 0.0, 0.97632))]   # tf_zx120.launch.xml extrinsic
+C1_ZX_BASE = ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))        # map -> zx120/base_link
+
+
+def _c1_scans(points=60_032, seed=101):
+    """One rosbag frame of BASELINE configs[0]: an HDL-64-like scan per sensor (64 rings,
+    -24.9..+2 deg, ranges clipped at the ground; sensor heights 2.0 / 3.5 m)."""
+    from pointcloud_processor_amd import synth
+
+    return [synth.lidar_cloud(points, sensor_height=2.0, seed=seed),
+            synth.lidar_cloud(points, sensor_height=3.5, seed=seed + 1)]
+
+
+def c1_frame_gpu(ctx, scans, nc_lattice=1):
+    """The launch file's per-frame chain on one GPU through the C ABI, host buffers in and out
+    (a rosbag message is a host buffer): pointcloud_filter x2 (crop + VoxelGrid 0.2) ->
+    pointcloud_merger (transform + colour + concat) -> excavated_surface_generator (carve) ->
+    virtual_lidar (normals + cell grid, terrain index, zx120 cloud, runOptimization with ONE
+    candidate pose).  -> (n_candidates, best_idx, totals)."""
+    from pointcloud_processor_amd import _abi
+
+    filtered = [ctx.crop_voxel(sc, C1_BOX, C1_LEAF)[0] for sc in scans]
+    merged = ctx.transform_concat(filtered, C1_TFS, [(255, 0, 0), (0, 0, 255)])
+    terr, area, _ = ctx.excavate(merged, C1_ZX_BASE)
+    bbox, nc = ctx.set_excavation_area(area, 0.1, 10)
+    ctx.set_terrain(terr, point_step=32)
+    ctx.set_aux_cloud(filtered[1])
+    zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])   # getZX120Position on zx120/base_link
+    params = _abi.default_vl_params(num_candidates=nc_lattice)
+    cand = ctx.generate_candidates(bbox, params, zx)[:1]   # ONE candidate pose is scored
+    tot, _, rep = ctx.score_poses(cand, zx, params, np.zeros(nc, np.uint8))
+    return cand.shape[0], int(rep.best_idx), tot
+
+
+def c1_frame_oracle(pyoracle, scans, nc_lattice=1):
+    """The same frame on the CPU restatement, one thread (the reference's executor)."""
+    filtered = []
+    for sc in scans:
+        kept = pyoracle.crop_box(sc, np.array(C1_BOX))
+        filtered.append(pyoracle.voxel_grid(sc[kept], C1_LEAF)[0])
+    merged = np.concatenate([pyoracle.transform_rgb(f, t, q, rgb) for f, (t, q), rgb in
+                             zip(filtered, C1_TFS, [(255, 0, 0), (0, 0, 255)])])
+    keep, surf, area, _ = pyoracle.excavate(merged, *C1_ZX_BASE)
+    terr = np.concatenate([merged[keep][:, [0, 1, 2, 4]], surf])
+    xyz, cn, bbox, _ = pyoracle.excavation_grid(area, 0.1, 10, pyoracle.area_normals(area, 1.5))
+    T = pyoracle.Cloud(terr)
+    zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])
+    params = pyoracle.vl_params(num_candidates=nc_lattice)
+    cand = pyoracle.generate_candidates(T, bbox, params, zx)[:1]
+    flt = np.zeros((filtered[1].shape[0], 4), np.float32)
+    flt[:, :3] = filtered[1]
+    tot, _, rep = pyoracle.score_poses(T, pyoracle.Cloud(flt), xyz, cn, cand, zx, params,
+                                       np.zeros(xyz.shape[0], np.uint8))
+    return cand.shape[0], int(rep.best_idx), tot
+
+
+def run_c1(args, local, cpu: bool):
+    """BASELINE configs[0]: rosbag replay, 2 x 60,032-pt scans per frame, 1 candidate pose.
+    ms per frame of the GPU chain (K frames after W warm-up frames, host buffers, PCIe and
+    every host round trip included) and of the oracle chain on one thread, same frame."""
+    from pointcloud_processor_amd import _abi
+
+    ctx = _abi.Context(local)
+    scans = _c1_scans()
+    # the smallest candidate lattice (num_candidates = 1, 4, 9, ...) in which a pose survives
+    # generateCandidatePositions' filters (:550-598) on this frame; its first pose is scored
+    nc_lattice = 1
+    while c1_frame_gpu(ctx, scans, nc_lattice)[0] == 0 and nc_lattice < 400:
+        nc_lattice = (int(math.isqrt(nc_lattice)) + 1) ** 2
+    for _ in range(max(args.warmup, 1)):
+        res = c1_frame_gpu(ctx, scans, nc_lattice)
+    lat = []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        res = c1_frame_gpu(ctx, scans, nc_lattice)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    ctx.close()
+    out = {"workload": "C1: 2 x 60,032-pt HDL-64-like scans -> filter (crop + voxel 0.2) x2 -> "
+                       "merge -> carve -> normals + cell grid -> 1-candidate pose search",
+           "unit": "ms/frame", "higher_is_better": False,
+           "value": float(np.median(lat)), "p99_ms": float(np.percentile(lat, 99)),
+           "frames": args.steps, "candidates": res[0], "best_idx": res[1],
+           "num_candidates_lattice": nc_lattice,
+           "data": "synthetic scans (bench._c1_scans), host buffers"}
+    if cpu:
+        pyoracle = _oracle()
+        pyoracle.set_threads(1)
+        t0 = time.perf_counter()
+        frames = 0
+        while frames == 0 or (time.perf_counter() - t0 < 4.0 and frames < 3):
+            ref = c1_frame_oracle(pyoracle, scans, nc_lattice)
+            frames += 1
+        dt = (time.perf_counter() - t0) / frames
+        out["cpu_baseline"] = {"value": dt * 1e3, "unit": "ms/frame", "cores": 1, "kind": "port",
+                               "sample": f"{frames} frames of the same scans through the oracle "
+                                         "chain (crop_box, voxel_grid, transform_rgb, excavate, "
+                                         "area_normals + excavation_grid, score_poses), 1 thread"}
+        out["matches_oracle"] = bool(ref[0] == res[0] and ref[1] == res[1] and
+                                     np.allclose(ref[2], res[2], rtol=1e-12, atol=0))
+    return out
 
 
 def run_cells(args, torch, dist, world, rank, local, backend=None):
@@ -662,7 +858,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--mode", choices=["all", "fan", "filter", "cells", "launch-check"],
+    ap.add_argument("--mode", choices=["all", "fan", "filter", "cells", "c1", "launch-check"],
                     default="all",
                     help="all (default): the fan line with reference-mode scoring and C3 as "
                          "extra keys; fan: the fan alone (profiling); filter: C3 with PCIe and "
@@ -689,6 +885,8 @@ def main():
         out = run_filter(args, torch, dist, world, rank, local, backend)
     elif args.mode == "cells":
         out = run_cells(args, torch, dist, world, rank, local, backend)
+    elif args.mode == "c1":
+        out = run_c1(args, local, cpu=not args.no_cpu_baseline)
     else:
         out = run_all(args, torch, dist, world, rank, local, backend)
     if rank == 0:

@@ -308,6 +308,20 @@ int pcp_raycast_fan_burst(pcp_ctx *ctx, const double *poses5, uint64_t n,
 int pcp_raycast_fan_stamps(pcp_ctx *ctx, const double *poses5, uint64_t n,
                            const pcp_fan_params *fan, uint64_t *stamps);
 
+/* One rank's shard of a pose-sharded fan query whose collective the CALLER runs (one process
+ * per GPU: bench.py --gpus N over torch.distributed / RCCL).  The fans of poses5[0 .. n) --
+ * global poses [lo, lo + n) of p_total -- are cast as pcp_raycast_fan does, and their keys
+ * (blocked << 32) | global pose index are written into the caller's DEVICE buffer
+ * keys_dev[p_total] (int64; INT64_MAX in the other ranks' slots), so one all-reduce(MIN) over
+ * int64 gives every rank the blocked count of every pose and the argmin (ties: lowest index;
+ * virtual_lidar.cpp:467-475).  units_dev (device, nullable, n entries): ray-hit tests per pose.
+ * wait_stream (a hipStream_t of the same device, nullable): that stream is made to wait for
+ * the keys (hipStreamWaitEvent) and the call returns without a host synchronisation; NULL:
+ * the call returns once the keys are written.  No host copy of the results is made. */
+int pcp_raycast_fan_keys(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                         const pcp_fan_params *fan, uint64_t lo, uint64_t p_total,
+                         int64_t *keys_dev, uint64_t *units_dev, void *wait_stream);
+
 /* ---- one process, n GPUs: the pose search sharded over devices ------ */
 /* pcp_multi_create(n_dev, devices, &m): one context per device (devices NULL: 0 .. n_dev-1)
  * and ONE RCCL communicator over them (ncclCommInitAll).  Poses are partitioned contiguously
@@ -320,9 +334,11 @@ int pcp_raycast_fan_stamps(pcp_ctx *ctx, const double *poses5, uint64_t n,
  *                          values >= +0) | P covered | 3 x n_cells newest-pose flag keys]
  *                          -> the reference's strict-'>' argmax (:471-474) and the stale-flag
  *                          colour statistics (:480-519), as pcp_score_poses.
- * Results are identical to one context over all poses.  A device listed twice (a rehearsal
- * on fewer GPUs) has no RCCL communicator: the key vectors are combined on that device by a
- * kernel instead (pcp_multi_info reports uses_rccl = 0).  Not thread-safe, like pcp_ctx. */
+ * Results are identical to one context over all poses.  The devices must be either all
+ * distinct (RCCL) or all the same device (a rehearsal on one GPU: no communicator, the key
+ * vectors are combined on that device by a kernel, pcp_multi_info reports uses_rccl = 0); a
+ * mixed list such as {0, 0, 1} is refused with PCP_E_INVALID.  The per-device index builds
+ * of pcp_multi_set_* run on one host thread per device.  Not thread-safe, like pcp_ctx. */
 typedef struct pcp_multi pcp_multi;
 int pcp_multi_create(int n_dev, const int *devices, pcp_multi **out);
 void pcp_multi_destroy(pcp_multi *m);

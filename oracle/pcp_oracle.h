@@ -51,6 +51,16 @@ void orc_transform_rgb(const float *pts, int64_t n, int64_t stride_floats,
                        const double t[3], const double q[4],
                        uint8_t r, uint8_t g, uint8_t b, float *out8);
 
+/* the whole C3 frame on `threads` OpenMP threads (pcp_oracle_mt.c; bench.py's MT CPU
+ * baseline): per cloud crop -> VoxelGrid(leaf > 0) -> transform + colour, concatenated in
+ * cloud order into out8 (PointXYZRGB records); the bytes of the sequential composition.
+ * t3q4: per cloud t[3] then q[4] (x, y, z, w).  Returns the record count, -1 on overflow of
+ * cap or leaf <= 0. */
+int64_t orc_filter_frame_mt(int k, const float *const *pts, const int64_t *n,
+                            const int64_t *stride, const double *boxes, float leaf,
+                            const double *t3q4, const uint8_t *rgb, float *out8, int64_t cap,
+                            int64_t *n_per, int threads);
+
 #define VL_MIN_DISTANCE 0.5
 #define VL_ZX120_OFFSET_X 0.4
 #define VL_RAY_STEP_SIZE 0.3

@@ -78,6 +78,8 @@ _SIGS = [
                             C.c_int64, _P, _P]),
     ("orc_excavation_grid", C.c_int64, [_P, C.c_int64, C.c_int64, C.c_double, C.c_int32, _P, _P,
                                         _P, C.c_int64, _P, _P]),
+    ("orc_filter_frame_mt", C.c_int64, [C.c_int, _P, _P, _P, _P, C.c_float, _P, _P, _P,
+                                        C.c_int64, _P, C.c_int]),
 ]
 
 _lib = None
@@ -144,6 +146,27 @@ def transform_rgb(pts, t, q, rgb):
     lib().orc_transform_rgb(_p(a), a.shape[0], a.shape[1], _p(t), _p(q), int(rgb[0]),
                             int(rgb[1]), int(rgb[2]), _p(out))
     return out[: a.shape[0]].copy()
+
+
+def filter_frame_mt(clouds, boxes, leaf, tfs, rgbs, threads):
+    """The C3 frame on `threads` OpenMP threads (pcp_oracle_mt.c): per cloud crop ->
+    VoxelGrid -> transform + colour, concatenated -> (N, 8) float32 records, per-cloud counts."""
+    arrs = [_f32(c) for c in clouds]
+    k = len(arrs)
+    ptrs = (C.c_void_p * k)(*[a.ctypes.data for a in arrs])
+    n = np.array([a.shape[0] for a in arrs], np.int64)
+    stride = np.array([a.shape[1] for a in arrs], np.int64)
+    bx = np.ascontiguousarray(np.asarray(boxes, np.float64).reshape(k, 6))
+    tq = np.ascontiguousarray([list(t) + list(q) for t, q in tfs], np.float64)
+    rgb = np.ascontiguousarray(np.asarray(rgbs, np.uint8).reshape(k, 3))
+    cap = int(n.sum())
+    out = np.empty((max(cap, 1), 8), np.float32)
+    per = np.zeros(k, np.int64)
+    m = lib().orc_filter_frame_mt(k, ptrs, _p(n), _p(stride), _p(bx), C.c_float(leaf), _p(tq),
+                                  _p(rgb), _p(out), cap, _p(per), int(threads))
+    if m < 0:
+        raise ValueError("orc_filter_frame_mt failed")
+    return out[:m].copy(), per
 
 
 class Cloud:

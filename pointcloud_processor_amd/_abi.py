@@ -134,6 +134,8 @@ _SIGS = [
     ("pcp_raycast_fan_stamps", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P]),
     ("pcp_raycast_fan_burst", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), C.c_int,
                                         C.POINTER(C.c_double)]),
+    ("pcp_raycast_fan_keys", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), C.c_uint64,
+                                       C.c_uint64, _P, _P, _P]),
     ("pcp_step_table", C.c_int, [C.c_double, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pcp_terrain_info", C.c_int, [_P, C.POINTER(IndexInfo)]),
     ("pcp_multi_create", C.c_int, [C.c_int, _P, C.POINTER(_P)]),
@@ -175,6 +177,13 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
     if path is None:
         _lib = lib
     return lib
+
+
+def device_count() -> int:
+    """Visible gfx950 devices (pcp_device_count)."""
+    n = C.c_int(0)
+    rc = load_library().pcp_device_count(C.byref(n))
+    return n.value if rc == PCP_OK else 0
 
 
 def _ptr(a: np.ndarray | None):
@@ -584,6 +593,21 @@ class Context:
                                              C.byref(best)), "pcp_raycast_fan")
         return best.value
 
+    def raycast_fan_keys(self, poses5: np.ndarray, fan: FanParams, lo: int, p_total: int,
+                         keys_dev_ptr: int, units_dev_ptr: int | None = None,
+                         wait_stream: int | None = None):
+        """pcp_raycast_fan_keys: this rank's poses [lo, lo + P) of p_total as int64 keys
+        (blocked << 32) | pose in the DEVICE buffer at keys_dev_ptr (p_total entries, INT64_MAX
+        in other ranks' slots), e.g. a torch int64 tensor's data_ptr(); wait_stream: a
+        hipStream_t (torch.cuda.current_stream().cuda_stream) made to wait for the keys."""
+        P = poses5.shape[0]
+        if (poses5.dtype != np.float64 or not poses5.flags.c_contiguous or poses5.ndim != 2
+                or poses5.shape[1] != 5):
+            raise ValueError("raycast_fan_keys: poses float64 [P, 5]")
+        self._check(self.lib.pcp_raycast_fan_keys(self.h, poses5.ctypes.data, P, C.byref(fan),
+                                                  lo, p_total, keys_dev_ptr, units_dev_ptr,
+                                                  wait_stream), "pcp_raycast_fan_keys")
+
     def raycast_fan(self, poses5: np.ndarray, fan: FanParams, want_first_hit=False):
         poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
         P = poses.shape[0]
@@ -599,8 +623,9 @@ class Context:
 
 class Multi:
     """pcp_multi: one process, n GPUs -- the pose search sharded over
-    contexts with ONE RCCL collective per query.  devices: one device id per rank (a device
-    listed twice rehearses n ranks on fewer GPUs: no RCCL, the keys combine on the device)."""
+    contexts with ONE RCCL collective per query.  devices: one device id per rank, all
+    distinct (RCCL) or all the same (a rehearsal of n ranks on one GPU: no RCCL, the keys
+    combine on the device); a mixed list is refused."""
 
     def __init__(self, devices, lib_path=None):
         self.lib = load_library(lib_path)

@@ -178,6 +178,7 @@ void SimplifiedDualLidarOptimizer::zx120PointsCallback(const PointCloud2 &msg) {
     err_.clear();
     pcp_cloud_view v{};
     if (!cloud_view(msg, v, &err_)) return;
+    zx120_size_ = v.n;   // zx120_cloud_ is replaced by every message, empty ones too (:195-196)
     if (multi_) {
         if (pcp_multi_set_aux_cloud(multi_, &v) != PCP_OK) err_ = pcp_multi_last_error(multi_);
     } else if (pcp_set_aux_cloud(dev_.ctx(), &v) != PCP_OK) {
@@ -185,21 +186,21 @@ void SimplifiedDualLidarOptimizer::zx120PointsCallback(const PointCloud2 &msg) {
     }
 }
 
-void SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg) {
+bool SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg) {
     err_.clear();
     pcp_cloud_view v;
     std::string why;
     if (!cloud_view(msg, v, &why)) {   // fromROSMsg would throw: logged, nothing rebuilt
         err_ = "excavation area: " + why;
-        return;
+        return false;
     }
-    if (msg.empty()) return;   // :168
+    if (msg.empty()) return false;   // :168
     double bb[6];
     uint64_t n = 0;
     if (pcp_set_excavation_area(dev_.ctx(), &v, p_.grid_resolution, p_.vertical_layers, bb, &n) !=
         PCP_OK) {
         err_ = dev_.error();   // "Failed to process excavation area" (:175-177)
-        return;
+        return false;
     }
     if (multi_ && n) {   // rank 0 built the cells: replicate them on every rank
         std::vector<double> xyz(3 * n);
@@ -208,12 +209,13 @@ void SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg
         if (pcp_get_cells(dev_.ctx(), xyz.data(), nrm.data(), n, &got) != PCP_OK ||
             pcp_multi_set_cells(multi_, xyz.data(), nrm.data(), got) != PCP_OK) {
             err_ = pcp_multi_last_error(multi_);
-            return;
+            return false;
         }
     }
     n_cells_ = n;
     flags_.assign(n_cells_, 0);   // excavation_grid_3d_ rebuilt from fresh GridCells (:259)
     std::memcpy(bbox_, bb, sizeof(bbox_));
+    return true;
 }
 
 void SimplifiedDualLidarOptimizer::setExcavationGrid(const std::vector<double> &xyz,
@@ -289,31 +291,58 @@ SimplifiedDualLidarOptimizer::Result SimplifiedDualLidarOptimizer::runOptimizati
     }
     r.best_score = r.report.best_score;
     if (r.report.best_idx >= 0) r.best = r.candidates[r.report.best_idx];   // else default (:465)
-    // the two RCLCPP_INFO tables
+    // the two RCLCPP_INFO tables, line for line: evaluateZX120Only (:419-451) and the dual
+    // configuration (:522-543)
     const pcp_vl_report &q = r.report;
     const int tc = q.total_cells;
     auto pct = [tc](int v) { return tc > 0 ? (double)v / tc * 100.0 : 0.0; };
+    auto ratio = [](int red, int green) {
+        return green > 0 ? (double)red / green
+                         : (red > 0 ? std::numeric_limits<double>::infinity() : 0.0);
+    };
+    const char *rule = "========================================";
+    const char *thin = "----------------------------------------";
+    appendf(r.log, "%s", rule);
+    appendf(r.log, "ZX120 LiDAR Only Evaluation");
+    appendf(r.log, "%s", rule);
     appendf(r.log, "ZX120 Position: (%.2f, %.2f, %.2f)", r.zx120.x, r.zx120.y, r.zx120.z);
     appendf(r.log, "Total Score (ZX120 only): %.2f", q.zx120_total_score);
+    appendf(r.log, "%s", thin);
+    appendf(r.log, "Debug Info:");
     appendf(r.log, "  Cells in range: %d (%.1f%%)", q.zx120_range_ok, pct(q.zx120_range_ok));
     appendf(r.log, "  Cells in FOV: %d (%.1f%%)", q.zx120_fov_ok, pct(q.zx120_fov_ok));
     appendf(r.log, "  Cells visible: %d (%.1f%%)", q.zx120_visible_ok, pct(q.zx120_visible_ok));
+    appendf(r.log, "  ZX120 point cloud size: %zu", zx120_size_);
+    appendf(r.log, "%s", thin);
+    appendf(r.log, "Color-based Area Analysis (ZX120 only):");
+    appendf(r.log, "  Total cells: %d", tc);
     appendf(r.log, "  Green (Observable): %d cells (%.1f%%)", q.zx120_green, pct(q.zx120_green));
     appendf(r.log, "  Red (Occluded): %d cells (%.1f%%)", q.zx120_red, pct(q.zx120_red));
     appendf(r.log, "  Blue (Out of range): %d cells (%.1f%%)", q.zx120_blue, pct(q.zx120_blue));
     appendf(r.log, "  Yellow (Out of FOV): %d cells (%.1f%%)", q.zx120_yellow, pct(q.zx120_yellow));
+    appendf(r.log, "  ---");
+    appendf(r.log, "  Red/Green Ratio: %.3f", ratio(q.zx120_red, q.zx120_green));
+    const int unobs_z = q.zx120_red + q.zx120_blue + q.zx120_yellow;
+    appendf(r.log, "  Total Unobservable: %d cells (%.1f%%)", unobs_z, pct(unobs_z));
+    appendf(r.log, "%s", rule);
+    appendf(r.log, "%s", "");
+    appendf(r.log, "%s", rule);
+    appendf(r.log, "Dual LiDAR Configuration (ZX120 + Mobile)");
+    appendf(r.log, "%s", rule);
     appendf(r.log, "Best Mobile LiDAR Position: (%.2f, %.2f, %.2f)", r.best.x, r.best.y, r.best.z);
     appendf(r.log, "Total Score: %.2f", r.best_score);
+    appendf(r.log, "%s", rule);
+    appendf(r.log, "Color-based Area Analysis:");
     appendf(r.log, "  Total cells: %d", tc);
     appendf(r.log, "  Green (Observable): %d cells (%.1f%%)", q.green, pct(q.green));
     appendf(r.log, "  Red (Occluded): %d cells (%.1f%%)", q.red, pct(q.red));
     appendf(r.log, "  Blue (Out of range): %d cells (%.1f%%)", q.blue, pct(q.blue));
     appendf(r.log, "  Yellow (Out of FOV): %d cells (%.1f%%)", q.yellow, pct(q.yellow));
-    const double rg = q.green > 0 ? (double)q.red / q.green
-                                  : (q.red > 0 ? std::numeric_limits<double>::infinity() : 0.0);
-    appendf(r.log, "  Red/Green Ratio: %.3f", rg);
+    appendf(r.log, "  ---");
+    appendf(r.log, "  Red/Green Ratio: %.3f", ratio(q.red, q.green));
     const int unobs = q.red + q.blue + q.yellow;
     appendf(r.log, "  Total Unobservable: %d cells (%.1f%%)", unobs, pct(unobs));
+    appendf(r.log, "%s", rule);
     return r;
 }
 

@@ -222,8 +222,9 @@ class SimplifiedDualLidarOptimizer {
     Params &params() { return p_; }
     const Params &params() const { return p_; }
     // excavationAreaCallback (:164-178): GPU normals + 3-D cell grid from /excavation_area;
-    // an empty cloud keeps the previous grid (:168)
-    void excavationAreaCallback(const PointCloud2 &msg);
+    // an empty cloud keeps the previous grid (:168).  true: generateExcavationGrid3D ran to its
+    // end (:284-286) -- the shell then logs the grid size and publishes the grid markers
+    bool excavationAreaCallback(const PointCloud2 &msg);
     void terrainCallback(const PointCloud2 &msg);       // :180-192
     void zx120PointsCallback(const PointCloud2 &msg);   // :194-207
     // cells computed elsewhere (tests, replays): the valid cells of generateExcavationGrid3D
@@ -242,6 +243,7 @@ class SimplifiedDualLidarOptimizer {
     pcp_multi *multi_ = nullptr;   // non-null: poses sharded over its devices
     Params p_;
     bool terrain_cloud_ = false;   // terrain_cloud_ non-null (a message arrived)
+    size_t zx120_size_ = 0;        // zx120_cloud_->size() (:433-434)
     size_t n_cells_ = 0;
     double bbox_[6] = {0, 0, 0, 0, 0, 0};
     std::vector<uint8_t> flags_;   // GridCell flag state across ticks

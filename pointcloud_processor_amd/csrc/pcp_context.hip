@@ -295,6 +295,7 @@ int pcp_create(int device, pcp_ctx **out) {
         ctx->fan_npw = (v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 1;
     }
     if (const char *ho = std::getenv("PCP_FAN_HOST_OUT")) ctx->fan_host_out = std::atoi(ho) != 0;
+    if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
     if (const char *tf = std::getenv("PCP_TERRAIN_FINE")) ctx->terrain_fine = std::atoi(tf);
     if (const char *tt = std::getenv("PCP_FINE_TILE")) ctx->fine_tile = std::atoi(tt);
@@ -318,6 +319,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     prof_resolve(ctx);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->keys_ev) (void)hipEventDestroy(ctx->keys_ev);
     ctx->terrain.release();
     ctx->aux.release();
     ctx->exc_norm.release();

@@ -1283,8 +1283,8 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
     const bool emit_now = !(dev_out && upper > cap);
     const bool graphable = dev_in && dev_out && emit_now && ctx->use_graphs;
     // the centroid kernel emits the records itself: no kernel reads the sizes back, so they
-    // are stored straight into pinned memory (no D2H copy per frame; PCP_FAN_HOST_OUT)
-    const bool landed = emit_now && ctx->fan_host_out && emit_in_centroid(bts);
+    // are stored straight into pinned memory (no D2H copy per frame; PCP_FM_HOST_OUT)
+    const bool landed = emit_now && ctx->fm_host_out && emit_in_centroid(bts);
     if (landed) {
         PCP_HIP(ctx, ctx->fm_res_host.ensure(3 * kMaxClouds * sizeof(uint32_t)));
         res = ctx->fm_res_host.as<uint32_t>();

@@ -240,6 +240,10 @@ struct pcp_ctx {
     pcp::PinnedBuf fm_res_host;              // pcp_filter_merge's result sizes, stored by its
                                              // kernels themselves (fixed: a graph holds it)
     pcp::PinnedBuf small_host;               // pinned landing of small size readbacks
+    // pcp_raycast_fan_keys: the query's completion (a caller's stream waits on it) -- the next
+    // query waits for it before it reuses the pinned pose staging
+    hipEvent_t keys_ev = nullptr;
+    bool keys_pending = false;
     int32_t fan_naz = -1, fan_nel = -1;      // cached fan direction tables
     double fan_elmin = 0.0, fan_elmax = 0.0;
     double steps_end = -1e300;               // cached step table
@@ -249,6 +253,8 @@ struct pcp_ctx {
     int fan_npw = 8;                         // poses per wave of the fan kernel (PCP_FAN_NPW)
     bool fan_host_out = true;                // k_fan_reduce stores into the pinned landing
                                              // block, no D2H copy (PCP_FAN_HOST_OUT)
+    bool fm_host_out = true;                 // pcp_filter_merge's result sizes stored by its
+                                             // kernels into pinned memory (PCP_FM_HOST_OUT)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
     int fine_pack = 1;                       // fine-window entries as 12 bytes (PCP_FINE_PACK)
     int fine_tile = 2;                       // fine records: 0 x-fastest, 1 4 x 4 tiles, 2 split
@@ -317,7 +323,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
 // the block-major copy of a z-sorted index (GridView.bstart / bpts); no-op when built
 int build_blocks(pcp_ctx *ctx, GridIndex &g);
 // the fine-window copy of a z-sorted index (GridView.frec / wpts); no-op when built.  Marks
-// blk_fail (no retry) past its size caps or on an allocation failure.
+// fine_fail (no retry) past its size caps or on an allocation failure.
 int build_fine(pcp_ctx *ctx, GridIndex &g);
 // before a terrain query: build the terrain's block copy per PCP_TERRAIN_BLOCKS (0 never,
 // 1 at the second query after pcp_set_terrain -- a terrain that is queried once, as in the
@@ -372,8 +378,10 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
                   const pcp_vl_params *p, ScoreEnq &o, const uint8_t *cell_flags = nullptr,
                   bool fuse_tail = false);
 // key kernels of the pose-sharded search (pcp_vlidar.hip; used by pcp_multi.hip)
+// identity: the value of the other ranks' slots (~0 for ncclUint64 MIN, INT64_MAX for a signed
+// int64 MIN as torch.distributed reduces it)
 void launch_fan_keys(hipStream_t st, const uint32_t *blocked_d, uint32_t lo, uint32_t cnt,
-                     uint32_t P, unsigned long long *keys);
+                     uint32_t P, unsigned long long *keys, unsigned long long identity = ~0ull);
 void launch_score_keys(hipStream_t st, const ScoreEnq &o, int lo, int P, unsigned long long *v);
 void launch_flags_from_keys(hipStream_t st, const unsigned long long *v, const uint8_t *zbits,
                             int C, int P, uint8_t *flags, int32_t *stats);

@@ -9,24 +9,91 @@
 // The reduced vector lands on every rank; rank 0's copy gives the host the reference-exact
 // argmin / strict-'>' argmax (virtual_lidar.cpp:471-474) and the stale-flag colour statistics.
 //
-// Ranks that share a device (a rehearsal on fewer GPUs than ranks; RCCL refuses duplicate
-// devices in one communicator) combine their key vectors on that device instead: same keys,
-// same finalization, min / max by a kernel.
+// Ranks that all share ONE device (a rehearsal on one GPU; RCCL refuses duplicate devices in
+// one communicator) combine their key vectors on that device instead: same keys, same
+// finalization, min / max by a kernel.  A mixed list ({0, 0, 1}) is refused: the combine
+// kernel would read another device's buffers (no peer access is set up).
+//
+// The per-device index builds (pcp_multi_set_*) run on one host thread per device; a query
+// issues every rank's pose upload before any rank's launches.
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pcp_internal.hpp"
 
 using namespace pcp;
 
+namespace {
+// one host thread per rank (rank 0 = the caller's thread): every rank's work -- index builds,
+// a query's pose upload + launches -- is issued concurrently instead of rank after rank.
+// Only used when the ranks sit on distinct devices (one context per device per thread).
+class RankPool {
+   public:
+    void start(int n) {
+        for (int r = 1; r < n; ++r) th_.emplace_back([this, r] { loop(r); });
+    }
+    ~RankPool() {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    bool active() const { return !th_.empty(); }
+    // f(r) for every rank r, concurrently; returns when all are done
+    void run(const std::function<void(int)> &f) {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            job_ = &f;
+            pending_ = (int)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> l(mu_);
+        done_.wait(l, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+   private:
+    void loop(int r) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> l(mu_);
+            cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            const std::function<void(int)> *f = job_;
+            l.unlock();
+            (*f)(r);
+            l.lock();
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool stop_ = false;
+};
+}  // namespace
+
 struct pcp_multi {
     int n = 0;
+    RankPool pool;                      // threads of ranks 1..n-1 (distinct devices only)
     std::vector<pcp_ctx *> ctx;
     std::vector<ncclComm_t> comm;       // empty when ranks share a device
     std::vector<DevBuf> keys;           // per rank: the vector the collective reduces
@@ -51,6 +118,21 @@ int merr(pcp_multi *m, int code, const char *fmt, ...) {
 int from_ctx(pcp_multi *m, int r, int rc) {
     m->err = "rank " + std::to_string(r) + ": " + pcp_last_error(m->ctx[r]);
     return rc;
+}
+
+// f(r) -> status for every rank: concurrently on the rank threads when the ranks own distinct
+// devices, else in rank order; the first failing rank's status (its context has the message)
+int for_ranks(pcp_multi *m, const std::function<int(int)> &f) {
+    std::vector<int> rc(m->n, PCP_OK);
+    if (m->pool.active()) {
+        m->pool.run([&](int r) { rc[r] = f(r); });
+    } else {
+        for (int r = 0; r < m->n; ++r)
+            if ((rc[r] = f(r)) != PCP_OK) break;
+    }
+    for (int r = 0; r < m->n; ++r)
+        if (rc[r] != PCP_OK) return from_ctx(m, r, rc[r]);
+    return PCP_OK;
 }
 
 #define M_HIP(m, expr)                                                                    \
@@ -126,6 +208,11 @@ int pcp_multi_create(int n_dev, const int *devices, pcp_multi **out) {
         dev[r] = devices ? devices[r] : r;
         if (dev[r] < 0 || dev[r] >= have) return PCP_E_INVALID;
     }
+    std::vector<int> sorted = dev;
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    const bool one_device = sorted.front() == sorted.back();
+    if (!distinct && !one_device) return PCP_E_INVALID;   // mixed: no combine across devices
     pcp_multi *m = new (std::nothrow) pcp_multi();
     if (!m) return PCP_E_NOMEM;
     m->n = n_dev;
@@ -138,9 +225,6 @@ int pcp_multi_create(int n_dev, const int *devices, pcp_multi **out) {
             return rc;
         }
     }
-    std::vector<int> sorted = dev;
-    std::sort(sorted.begin(), sorted.end());
-    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
     if (distinct) {
         m->comm.resize(n_dev);
         if (ncclCommInitAll(m->comm.data(), n_dev, dev.data()) != ncclSuccess) {
@@ -148,6 +232,7 @@ int pcp_multi_create(int n_dev, const int *devices, pcp_multi **out) {
             pcp_multi_destroy(m);
             return PCP_E_HIP;
         }
+        m->pool.start(n_dev);
     }
     *out = m;
     return PCP_OK;
@@ -180,27 +265,21 @@ pcp_ctx *pcp_multi_ctx(pcp_multi *m, int rank) {
     return (m && rank >= 0 && rank < m->n) ? m->ctx[rank] : nullptr;
 }
 
-// the index builds run on every device from the host buffer (each takes ~1 ms per 1M points;
-// the per-frame state is small next to a collective's setup)
+// the index builds run on every device from the host buffer (each takes ~1 ms per 1M points),
+// all devices at once (one host thread per device)
 int pcp_multi_set_terrain(pcp_multi *m, const pcp_cloud_view *terrain) {
     if (!m) return PCP_E_INVALID;
-    for (int r = 0; r < m->n; ++r)
-        if (int rc = pcp_set_terrain(m->ctx[r], terrain)) return from_ctx(m, r, rc);
-    return PCP_OK;
+    return for_ranks(m, [&](int r) { return pcp_set_terrain(m->ctx[r], terrain); });
 }
 
 int pcp_multi_set_aux_cloud(pcp_multi *m, const pcp_cloud_view *aux) {
     if (!m) return PCP_E_INVALID;
-    for (int r = 0; r < m->n; ++r)
-        if (int rc = pcp_set_aux_cloud(m->ctx[r], aux)) return from_ctx(m, r, rc);
-    return PCP_OK;
+    return for_ranks(m, [&](int r) { return pcp_set_aux_cloud(m->ctx[r], aux); });
 }
 
 int pcp_multi_set_cells(pcp_multi *m, const double *xyz, const float *normals, uint64_t n) {
     if (!m) return PCP_E_INVALID;
-    for (int r = 0; r < m->n; ++r)
-        if (int rc = pcp_set_cells(m->ctx[r], xyz, normals, n)) return from_ctx(m, r, rc);
-    return PCP_OK;
+    return for_ranks(m, [&](int r) { return pcp_set_cells(m->ctx[r], xyz, normals, n); });
 }
 
 int pcp_multi_raycast_fan(pcp_multi *m, const double *poses5, uint64_t n,
@@ -217,18 +296,20 @@ int pcp_multi_raycast_fan(pcp_multi *m, const double *poses5, uint64_t n,
     if (int rc = ensure_keys(m, P)) return rc;
     std::vector<FanEnq> o(m->n);
     std::vector<uint64_t> lo(m->n), cnt(m->n);
-    for (int r = 0; r < m->n; ++r) {   // enqueue every rank before waiting on any
+    for (int r = 0; r < m->n; ++r) shard(n, m->n, r, lo[r], cnt[r]);
+    // every rank enqueued (on its own thread) before waiting on any
+    int erc = for_ranks(m, [&](int r) -> int {
         pcp_ctx *c = m->ctx[r];
-        shard(n, m->n, r, lo[r], cnt[r]);
-        if (cnt[r]) {
+        if (cnt[r])
             if (int rc = fan_enqueue(c, poses5 + 5 * lo[r], cnt[r], fan, false, false, false, o[r]))
-                return from_ctx(m, r, rc);
-        }
-        M_HIP(m, hipSetDevice(c->device));
+                return rc;
+        PCP_HIP(c, hipSetDevice(c->device));
         launch_fan_keys(c->stream, o[r].blocked_d, (uint32_t)lo[r], (uint32_t)cnt[r], P,
                         m->keys[r].as<unsigned long long>());
-        M_HIP(m, hipGetLastError());
-    }
+        PCP_CHECK_LAUNCH(c);
+        return PCP_OK;
+    });
+    if (erc) return erc;
     if (int rc = reduce_keys(m, P, false)) return rc;
     // rank 0's reduced keys and every rank's units into one pinned block
     M_HIP(m, m->host.ensure((size_t)P * 16 + 64));
@@ -277,14 +358,15 @@ int pcp_multi_score_poses(pcp_multi *m, const double *poses5, uint64_t n,
     if (int rc = ensure_keys(m, count)) return rc;
     std::vector<ScoreEnq> o(m->n);
     std::vector<uint64_t> lo(m->n), cnt(m->n);
-    for (int r = 0; r < m->n; ++r) {
+    for (int r = 0; r < m->n; ++r) shard(n, m->n, r, lo[r], cnt[r]);
+    int erc = for_ranks(m, [&](int r) -> int {
         pcp_ctx *c = m->ctx[r];
-        shard(n, m->n, r, lo[r], cnt[r]);
-        if (int rc = score_enqueue(c, poses5 + 5 * lo[r], cnt[r], zx120_pose5, p, o[r]))
-            return from_ctx(m, r, rc);
+        if (int rc = score_enqueue(c, poses5 + 5 * lo[r], cnt[r], zx120_pose5, p, o[r])) return rc;
         launch_score_keys(c->stream, o[r], (int)lo[r], P, m->keys[r].as<unsigned long long>());
-        M_HIP(m, hipGetLastError());
-    }
+        PCP_CHECK_LAUNCH(c);
+        return PCP_OK;
+    });
+    if (erc) return erc;
     if (int rc = reduce_keys(m, count, true)) return rc;
     // finalize on rank 0: the caller's flags, the reduced newest-pose keys, the zx120 bits
     pcp_ctx *c0 = m->ctx[0];

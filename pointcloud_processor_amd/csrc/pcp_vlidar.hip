@@ -322,7 +322,12 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
                 if (FN == 8) {   // skip the run's entries > r above q (pcp_fine.hip, k_frec)
                     const uint32_t ws = ld_u32o(g.fstart, ri);
                     const float h2 = __builtin_fmaf((float)iz + 1.5f, g.fzc, g.fzo);
-                    w0 = (ws & 0x0FFFFFFFu) + (qz + (rexit + 1e-4f) < h2 ? ws >> 28 : 0u);
+                    // h2 is the record's double height rounded through fzo, fzc and the fma
+                    // (a few ulps of the larger magnitude): the margin grows with it, so far
+                    // from the origin (|z| of km) the skip stays exact
+                    const float marg =
+                        1e-4f + 4.0f * FLT_EPSILON * (fabsf(h2) + fabsf(g.fzo) + fabsf(qz));
+                    w0 = (ws & 0x0FFFFFFFu) + (qz + (rexit + marg) < h2 ? ws >> 28 : 0u);
                 }
                 if (g.wpack ? scan_window3<STATS>(reinterpret_cast<const float *>(g.wpts), w0, qx,
                                                   qy, qz, r2, rexit, cnt)
@@ -862,12 +867,12 @@ __host__ __device__ constexpr int sum_flag_row_blocks(int P) {
 // argmin with ties to the lowest index
 __global__ void __launch_bounds__(kT)
 k_fan_keys(const uint32_t *__restrict__ blocked, uint32_t lo, uint32_t cnt, uint32_t P,
-           unsigned long long *__restrict__ keys) {
+           unsigned long long *__restrict__ keys, unsigned long long identity) {
     const uint32_t i = blockIdx.x * kT + threadIdx.x;
     if (i >= P) return;
     keys[i] = (i >= lo && i - lo < cnt)
                   ? (((unsigned long long)blocked[i - lo] << 32) | (unsigned long long)i)
-                  : ~0ull;
+                  : identity;
 }
 
 // reference mode: v = [P totals | P covered | C range | C fov | C vis], all-reduce(MAX).
@@ -957,9 +962,9 @@ k_keys_combine(unsigned long long *__restrict__ a, const unsigned long long *__r
 }
 
 void launch_fan_keys(hipStream_t st, const uint32_t *blocked_d, uint32_t lo, uint32_t cnt,
-                     uint32_t P, unsigned long long *keys) {
+                     uint32_t P, unsigned long long *keys, unsigned long long identity) {
     hipLaunchKernelGGL(k_fan_keys, dim3((P + kT - 1) / kT), dim3(kT), 0, st, blocked_d, lo, cnt,
-                       P, keys);
+                       P, keys, identity);
 }
 void launch_score_keys(hipStream_t st, const ScoreEnq &o, int lo, int P,
                        unsigned long long *v) {
@@ -1934,6 +1939,46 @@ int pcp_raycast_fan_stamps(pcp_ctx *ctx, const double *poses5, uint64_t n,
     std::vector<uint32_t> blocked(n ? n : 1);
     return raycast_fan_impl(ctx, poses5, n, fan, blocked.data(), nullptr, nullptr, nullptr,
                             nullptr, stamps);
+}
+
+// one rank's shard of a pose-sharded fan query whose collective the caller runs (one process
+// per GPU, torch.distributed over RCCL): keys stay on the device, in the caller's buffer
+int pcp_raycast_fan_keys(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                         const pcp_fan_params *fan, uint64_t lo, uint64_t p_total,
+                         int64_t *keys_dev, uint64_t *units_dev, void *wait_stream) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!fan || !keys_dev || (n && !poses5))
+        return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan_keys: null argument");
+    if (lo + n > p_total || p_total > 65535u * 64u)
+        return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan_keys: shard [%llu, %llu) of %llu poses",
+                       (unsigned long long)lo, (unsigned long long)(lo + n),
+                       (unsigned long long)p_total);
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    // the previous query's pose upload must be done before the pinned staging is rewritten
+    if (ctx->keys_pending) PCP_HIP(ctx, hipEventSynchronize(ctx->keys_ev));
+    ctx->keys_pending = false;
+    const uint32_t *blocked_d = nullptr;
+    if (n) {
+        FanEnq o;
+        if (int rc = fan_enqueue(ctx, poses5, n, fan, false, false, false, o)) return rc;
+        blocked_d = o.blocked_d;
+        if (units_dev)
+            PCP_HIP(ctx, hipMemcpyAsync(units_dev, o.units_d, n * sizeof(uint64_t),
+                                        hipMemcpyDeviceToDevice, st));
+    }
+    launch_fan_keys(st, blocked_d, (uint32_t)lo, (uint32_t)n, (uint32_t)p_total,
+                    reinterpret_cast<unsigned long long *>(keys_dev), 0x7fffffffffffffffull);
+    PCP_CHECK_LAUNCH(ctx);
+    if (!ctx->keys_ev) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->keys_ev, hipEventDisableTiming));
+    PCP_HIP(ctx, hipEventRecord(ctx->keys_ev, st));
+    if (wait_stream) {
+        PCP_HIP(ctx, hipStreamWaitEvent(static_cast<hipStream_t>(wait_stream), ctx->keys_ev, 0));
+        ctx->keys_pending = true;
+    } else {
+        PCP_HIP(ctx, hipEventSynchronize(ctx->keys_ev));
+    }
+    return PCP_OK;
 }
 
 }  // extern "C"

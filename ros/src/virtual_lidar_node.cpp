@@ -3,8 +3,8 @@
 // :454-548, :802-962.  Normals, the 3-D cell grid, candidate generation, the ray-fan
 // occlusion scoring and the argmax run in libpcp; this file only moves messages.
 //
-// PCP_DEVICES="0,1,2,3" shards the candidate poses over those GPUs (pcp_multi, one RCCL
-// all-gather per tick); unset, one GPU (PCP_DEVICE, default 0).
+// PCP_DEVICES="0,1,2,3" shards the candidate poses over those GPUs (pcp_multi: one RCCL
+// all-reduce of the per-pose score keys per tick); unset, one GPU (PCP_DEVICE, default 0).
 #include "pcp_ros.hpp"
 
 #include <algorithm>
@@ -38,7 +38,8 @@ class SimplifiedDualLidarOptimizerNode : public rclcpp::Node {
             core_ = std::make_unique<pcp::SimplifiedDualLidarOptimizer>(*multi_);
             dev_ = &multi_->rank0();
             RCLCPP_INFO(get_logger(), "Scoring sharded over %d GPUs (%s)", multi_->size(),
-                        multi_->usesRccl() ? "RCCL" : "host gather");
+                        multi_->usesRccl() ? "RCCL all-reduce"
+                                           : "one device: on-device key combine");
         } else {
             dev_ = &pcp_ros::device();
             core_ = std::make_unique<pcp::SimplifiedDualLidarOptimizer>(*dev_);
@@ -55,8 +56,16 @@ class SimplifiedDualLidarOptimizerNode : public rclcpp::Node {
 
         excavation_area_sub_ = create_subscription<sensor_msgs::msg::PointCloud2>(
             "/excavation_area", 10, [this](sensor_msgs::msg::PointCloud2::SharedPtr m) {
-                core_->excavationAreaCallback(pcp_ros::from_ros(*m));
-                report("Failed to process excavation area");
+                // generateExcavationGrid3D logs the grid and republishes the grid markers, from
+                // the fresh cells' flags, every time it runs (:284-286)
+                if (core_->excavationAreaCallback(pcp_ros::from_ros(*m))) {
+                    RCLCPP_INFO(get_logger(),
+                                "Generated 3D grid: %d valid cells across %d vertical layers",
+                                (int)core_->lastCells(), core_->params().vertical_layers);
+                    publishGridVisualization();
+                } else {
+                    report("Failed to process excavation area");
+                }
             });
         terrain_sub_ = create_subscription<sensor_msgs::msg::PointCloud2>(
             "/excavated_terrain", 10, [this](sensor_msgs::msg::PointCloud2::SharedPtr m) {
@@ -112,7 +121,7 @@ class SimplifiedDualLidarOptimizerNode : public rclcpp::Node {
         const auto stamp = now();
         publishOptimalPosition(r, stamp);
         publishCandidatePositions(r, stamp);
-        publishGridVisualization(stamp);
+        publishGridVisualization();
     }
 
     void publishOptimalPosition(const pcp::SimplifiedDualLidarOptimizer::Result &r,
@@ -169,7 +178,8 @@ class SimplifiedDualLidarOptimizerNode : public rclcpp::Node {
         candidate_positions_pub_->publish(arr);
     }
 
-    void publishGridVisualization(const rclcpp::Time &stamp) {   // :908-962
+    void publishGridVisualization() {   // :908-962 (each marker stamped now(), :920)
+        const rclcpp::Time stamp = now();
         uint64_t n = 0;
         pcp_get_cells(dev_->ctx(), nullptr, nullptr, 0, &n);
         std::vector<double> xyz(3 * n);

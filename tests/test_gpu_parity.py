@@ -503,6 +503,41 @@ def test_raycast_fan_clutter_and_odd_fans(oracle, n_az, n_el):
         ctx.close()
 
 
+@pytest.mark.parametrize("dz", [3000.0, -2500.0])
+def test_raycast_fan_far_from_origin(oracle, scene, cells, dz, monkeypatch):
+    """The terrain and the poses shifted by kilometres in z, where float spacing (~2.4e-4 m)
+    exceeds the fixed 1e-4 m margins: the split-record walk skip widens its margin with |z|
+    (pcp_vlidar.hip), so first hits, blocked counts and ray-hit tests stay exact on the
+    fine-window copy (built at the first query)."""
+    monkeypatch.setenv("PCP_TERRAIN_BLOCKS", "2")
+    terr = np.ascontiguousarray(scene.terrain.copy())
+    terr[:, 2] += np.float32(dz)
+    ctx = _abi.Context(0)
+    try:
+        ctx.set_terrain(terr, point_step=32)
+        p = _abi.default_vl_params(num_candidates=100)
+        g = _abi.Context(0)
+        try:
+            g.set_terrain(scene.terrain, point_step=32)
+            poses = g.generate_candidates(cells.grid_bbox, p, scene.zx120_pose5)[::9][:8].copy()
+        finally:
+            g.close()
+        poses[:, 2] += dz
+        fan = _abi.fan_params(n_az=256, n_el=64)
+        blocked, units, fh, _ = ctx.raycast_fan(poses, fan, want_first_hit=True)
+        assert ctx.terrain_info()["scan_layout"] == "fine"
+    finally:
+        ctx.close()
+    oracle.set_threads(8)
+    r_blocked, r_units, r_fh = oracle.raycast_fan(oracle.Cloud(terr), poses, 256, 64,
+                                                  fan.el_min, fan.el_max, fan.max_distance)
+    oracle.set_threads(1)
+    np.testing.assert_array_equal(fh, r_fh)
+    np.testing.assert_array_equal(blocked, r_blocked)
+    np.testing.assert_array_equal(units, r_units)
+    assert blocked.sum() > 0
+
+
 def test_raycast_fan_without_terrain_and_empty(oracle):
     """No terrain tree: every ray runs to the end unblocked (the reference's visible = true);
     zero poses: nothing to do, best index -1; an all-NaN terrain: an empty tree."""
@@ -980,7 +1015,66 @@ def test_fine_copy_dense_window(oracle, monkeypatch):
 
 
 # ---------------------------------------------------------------------------------- multi-GPU
-@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_fan_device_keys_match_reduce_fan(gpu, loaded, scene):
+    """bench.py --gpus N over RCCL: pcp_raycast_fan_keys writes each rank's keys into a torch
+    device vector (no host copy), the collective is an int64 MIN.  Four ranks' shards on one
+    device, their vectors combined by torch.minimum (the all-reduce's arithmetic): blocked
+    counts, units and the argmin bit-identical to the host path (raycast_fan ->
+    dist.reduce_fan)."""
+    import sys
+    from pathlib import Path
+
+    import torch
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    from pointcloud_processor_amd import dist as pd
+
+    poses, _ = bench._poses_for(gpu, bench._grid_bbox(scene.area), scene.zx120_pose5, 96)
+    fan = _abi.fan_params(n_az=256, n_el=64)
+    b1, u1, _, _ = gpu.raycast_fan(poses, fan)
+    P, world = poses.shape[0], 4
+    ref_keys, ref_best = pd.reduce_fan(b1, 0, P, P)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    vecs = []
+    units = torch.zeros(P, dtype=torch.int64, device=dev)
+    for r in range(world):
+        lo, hi = pd.shard(P, world, r)
+        k = torch.empty(P, dtype=torch.int64, device=dev)
+        sh = np.ascontiguousarray(poses[lo:hi])
+        gpu.raycast_fan_keys(sh, fan, lo, P, k.data_ptr(), units.data_ptr() + 8 * lo, stream)
+        vecs.append(k)
+    red = vecs[0]
+    for k in vecs[1:]:
+        red = torch.minimum(red, k)
+    kh = red.cpu().numpy()
+    np.testing.assert_array_equal(kh >> 32, ref_keys)
+    np.testing.assert_array_equal(kh & 0xFFFFFFFF, np.arange(P))
+    assert int(kh.min()) & 0xFFFFFFFF == ref_best
+    np.testing.assert_array_equal(units.cpu().numpy().astype(np.uint64), u1)
+    # one rank holding no poses writes only the identity
+    k = torch.zeros(P, dtype=torch.int64, device=dev)
+    gpu.raycast_fan_keys(poses[:0], fan, P, P, k.data_ptr(), None, None)
+    assert bool((k == np.iinfo(np.int64).max).all())
+
+
+def _need_devices(devices):
+    if len(set(devices)) > 1 and _abi.device_count() < len(set(devices)):
+        pytest.skip(f"needs {len(set(devices))} GPUs (RCCL over distinct devices); "
+                    f"{_abi.device_count()} visible")
+
+
+def test_multi_rejects_mixed_device_lists(gpu):
+    """Devices all distinct (RCCL) or all the same (on-device combine); a mixed list such as
+    {0, 0, 1} would combine buffers across devices without peer access: refused."""
+    with pytest.raises(_abi.PcpError):
+        _abi.Multi([0, 0, 1])
+    with pytest.raises(_abi.PcpError):
+        _abi.Multi([0, 1, 1])
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0], [0, 1], [0, 1, 2, 3]])
 def test_multi_fan_matches_single_context(gpu, loaded, scene, devices):
     """pcp_multi: the C2 poses sharded over the ranks, ONE all-reduce(MIN) over
     the (blocked << 32) | pose keys -- RCCL over one device, or three ranks sharing device 0
@@ -991,6 +1085,7 @@ def test_multi_fan_matches_single_context(gpu, loaded, scene, devices):
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
     import bench
 
+    _need_devices(devices)
     poses, _ = bench._poses_for(gpu, bench._grid_bbox(scene.area), scene.zx120_pose5, 256)
     fan = _abi.fan_params()
     b1, u1, _, best1 = gpu.raycast_fan(poses, fan)
@@ -1008,11 +1103,12 @@ def test_multi_fan_matches_single_context(gpu, loaded, scene, devices):
     assert best1 == int(np.argmin(b1))
 
 
-@pytest.mark.parametrize("devices", [[0], [0, 0]])
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 1]])
 def test_multi_score_matches_single_context(gpu, loaded, scene, cells, aux, devices):
     """pcp_multi_score_poses: totals, covered counts, strict-'>' best index, stale flags and the
     colour report over two ticks (the second starting from the first's flags), identical to
     pcp_score_poses on one context."""
+    _need_devices(devices)
     params = _abi.default_vl_params()
     poses = gpu.generate_candidates(cells.grid_bbox, _abi.default_vl_params(num_candidates=400),
                                     scene.zx120_pose5)
