@@ -1190,12 +1190,17 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, cons
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     PCP_HIP(ctx, ctx->out_d.ensure(total * 32));
     float4 *o = ctx->out_d.as<float4>();
+    // every cloud staged in its own region of f_in: all uploads and launches in flight, one
+    // synchronisation for the call
+    std::vector<size_t> soff(k + 1, 0);
+    for (int i = 0; i < k; ++i)
+        soff[i + 1] = soff[i] + align256(clouds[i].n * (uint64_t)clouds[i].point_step);
+    PCP_HIP(ctx, ctx->f_in.ensure(soff[k] + 256));
     uint64_t base = 0;
     for (int i = 0; i < k; ++i) {
         if (clouds[i].n == 0) continue;
-        PCP_HIP(ctx, ctx->f_in.ensure(clouds[i].n * (uint64_t)clouds[i].point_step + 256));
         CloudIn c;
-        int rc = stage_cloud(ctx, clouds[i], false, ctx->f_in, 0, c);
+        int rc = stage_cloud(ctx, clouds[i], false, ctx->f_in, soff[i], c);
         if (rc) return rc;
         const Rigid r = make_rigid(tf[i], rgb + 3 * i);
         {
@@ -1204,7 +1209,6 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, cons
                                ctx->stream, c, r, o + 2 * base);
             PCP_CHECK_LAUNCH(ctx);
         }
-        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));   // f_in is reused by the next cloud
         base += c.n;
     }
     PCP_HIP(ctx, hipMemcpyAsync(out, o, total * 32, hipMemcpyDeviceToHost, ctx->stream));

@@ -21,7 +21,7 @@
 #include <cfloat>
 #include <cmath>
 
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "pcp_grid.hpp"
 #include "pcp_internal.hpp"
@@ -260,9 +260,10 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     const float4 *pts = g.pts.as<const float4>();
     // 1. global z order
     size_t t1 = 0, t2 = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, (unsigned long long *)nullptr,
-                                       (unsigned long long *)nullptr, (uint32_t *)nullptr,
-                                       (uint32_t *)nullptr, (int)n, 0, 64, st);
+    // rocPRIM's onesweep radix sort, called directly (no CUB-compatibility layer)
+    (void)rocprim::radix_sort_pairs(nullptr, t1, (unsigned long long *)nullptr,
+                                    (unsigned long long *)nullptr, (uint32_t *)nullptr,
+                                    (uint32_t *)nullptr, n, 0u, 64u, st);
     PCP_HIP(ctx, ctx->scratch[2].ensure((size_t)n * 24 + 64));   // keys x2, vals x2
     unsigned long long *k0 = ctx->scratch[2].as<unsigned long long>(), *k1 = k0 + n;
     uint32_t *v0 = reinterpret_cast<uint32_t *>(k1 + n), *zord = v0 + n;
@@ -276,8 +277,8 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     const size_t tscan = scan_tmp_bytes(std::max<uint64_t>(n, nw)) +
                          (std::max<uint64_t>(n, nw) + 1) * sizeof(uint32_t);
     PCP_HIP(ctx, ctx->scratch[4].ensure(std::max(t1, tscan) + 256));
-    if (hipcub::DeviceRadixSort::SortPairs(ctx->scratch[4].p, t1, k0, k1, v0, zord, (int)n, 0, 64,
-                                           st) != hipSuccess)
+    if (rocprim::radix_sort_pairs(ctx->scratch[4].p, t1, k0, k1, v0, zord, n, 0u, 64u, st) !=
+        hipSuccess)
         return set_err(ctx, PCP_E_HIP, "build_fine: z sort failed");
     hipLaunchKernelGGL(k_win_count, dim3(gridn), dim3(kThreads), 0, st, pts, zord, n, f, pcount);
     PCP_CHECK_LAUNCH(ctx);
@@ -293,9 +294,9 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     // 4. pairs (window, z rank), stable sort by window
     int wbits = 1;
     while ((1ull << wbits) < nw) ++wbits;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t2, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                       (uint32_t *)nullptr, (uint32_t *)nullptr, (int)np, 0, wbits,
-                                       st);
+    (void)rocprim::radix_sort_pairs(nullptr, t2, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                    (uint32_t *)nullptr, (uint32_t *)nullptr, np, 0u,
+                                    (unsigned)wbits, st);
     PCP_HIP(ctx, ctx->scratch[5].ensure((size_t)np * 16 + 64));
     uint32_t *wk0 = ctx->scratch[5].as<uint32_t>(), *wk1 = wk0 + np, *rk0 = wk1 + np,
              *rk1 = rk0 + np;
@@ -303,8 +304,8 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     hipLaunchKernelGGL(k_win_emit, dim3(gridn), dim3(kThreads), 0, st, pts, zord, n, f,
                        (const uint32_t *)poff, wk0, rk0);
     PCP_CHECK_LAUNCH(ctx);
-    if (hipcub::DeviceRadixSort::SortPairs(ctx->scratch[6].p, t2, wk0, wk1, rk0, rk1, (int)np, 0,
-                                           wbits, st) != hipSuccess)
+    if (rocprim::radix_sort_pairs(ctx->scratch[6].p, t2, wk0, wk1, rk0, rk1, np, 0u,
+                                  (unsigned)wbits, st) != hipSuccess)
         return set_err(ctx, PCP_E_HIP, "build_fine: window sort failed");
     hipLaunchKernelGGL(k_win_bounds, dim3((unsigned)((nw + kThreads) / kThreads)), dim3(kThreads),
                        0, st, (const uint32_t *)wk1, np, (uint32_t)nw, cstart);
