@@ -251,6 +251,29 @@ k_keep_count(uint64_t n, const uint8_t *__restrict__ removed, uint32_t *__restri
     if (threadIdx.x == 0) counts[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
 }
 
+struct GenPoint {    // a generated point: position, height query, z recipe (reference order)
+    double x, y;
+    int32_t q;       // height query index
+    int32_t kind;    // 0: h - v   1: (h - depth) + v   (v as below)
+    double v;
+    float rgb;
+};
+
+// the generated records (generateExcavatedSurface / generateExcavationArea) from their height
+// queries, in the host's double expressions: record k at out + 2 * (base + k), base = *base_d
+// (the kept count, the generated surface goes after the kept points) or 0
+__global__ void __launch_bounds__(kCT)
+k_gen_emit(const GenPoint *__restrict__ gp, uint32_t ng, const double *__restrict__ h,
+           double depth, const uint32_t *__restrict__ base_d, float4 *__restrict__ out) {
+    const uint32_t k = blockIdx.x * kCT + threadIdx.x;
+    if (k >= ng) return;
+    const GenPoint g = gp[k];
+    const double z = g.kind == 0 ? h[g.q] - g.v : (h[g.q] - depth) + g.v;
+    const size_t o = (size_t)(base_d ? *base_d : 0u) + k;
+    out[2 * o] = make_float4((float)g.x, (float)g.y, (float)z, 1.0f);
+    out[2 * o + 1] = make_float4(g.rgb, 0.0f, 0.0f, 0.0f);
+}
+
 // kept points in input order as PointXYZRGB records (x, y, z, 1, rgb, 0, 0, 0)
 __global__ void __launch_bounds__(kCT)
 k_keep_emit(CarveArgs a, const uint8_t *__restrict__ removed, const uint32_t *__restrict__ counts,
@@ -345,14 +368,6 @@ static float pack_rgb(unsigned r, unsigned g, unsigned b) {
     std::memcpy(&f, &v, 4);
     return f;
 }
-
-struct GenPoint {    // a generated point: position, height query, z recipe (reference order)
-    double x, y;
-    int32_t q;       // height query index
-    int32_t kind;    // 0: h - v   1: (h - depth) + v   (v as below)
-    double v;
-    float rgb;
-};
 
 }  // namespace pcp
 
@@ -504,9 +519,10 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     uint8_t *removed = reinterpret_cast<uint8_t *>(base + qb + ib + hb + fb);
     uint32_t *tcount = reinterpret_cast<uint32_t *>(base + qb + ib + hb + fb + rb);
     uint32_t *ctr = reinterpret_cast<uint32_t *>(base + qb + ib + hb + fb + rb + cb);   // 4 words
-    PCP_HIP(ctx, ctx->out_d.ensure(n * 32 + 64));
+    const uint64_t nsurf = surf.size(), narea = area.size();
+    PCP_HIP(ctx, ctx->out_d.ensure((n + nsurf) * 32 + 64));
     float4 *kept = ctx->out_d.as<float4>();
-    PCP_HIP(ctx, hipMemcpyAsync(qxy, qv.data(), G * sizeof(double2), hipMemcpyHostToDevice, st));
+    if (int rc0 = upload_async(ctx, qxy, qv.data(), G * sizeof(double2), st)) return rc0;
     PCP_HIP(ctx, hipMemsetAsync(ctr, 0, 16, st));
     PCP_HIP(ctx, hipMemsetAsync(removed, 0, n ? n : 1, st));
     const float r2 = (float)(p->terrain_search_radius * p->terrain_search_radius);
@@ -533,19 +549,55 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
                            (const uint32_t *)tcount, kept, ctr + 2);
         PCP_CHECK_LAUNCH(ctx);
     }
-    std::vector<double> hg(G);
+    // the generated surface (after the kept points) and area records, on the device
+    PCP_HIP(ctx, ctx->out_a.ensure((nsurf + narea) * sizeof(GenPoint) + narea * 32 + 64));
+    GenPoint *gp = ctx->out_a.as<GenPoint>();
+    float4 *area_d = reinterpret_cast<float4 *>(gp + nsurf + narea);
+    if (nsurf && (rc = upload_async(ctx, gp, surf.data(), nsurf * sizeof(GenPoint), st))) return rc;
+    if (narea && (rc = upload_async(ctx, gp + nsurf, area.data(), narea * sizeof(GenPoint), st)))
+        return rc;
+    if (nsurf) {
+        hipLaunchKernelGGL(k_gen_emit, dim3((unsigned)((nsurf + kCT - 1) / kCT)), dim3(kCT), 0, st,
+                           (const GenPoint *)gp, (uint32_t)nsurf, (const double *)h, p->depth,
+                           n ? (const uint32_t *)(ctr + 2) : nullptr, kept);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    if (narea) {
+        hipLaunchKernelGGL(k_gen_emit, dim3((unsigned)((narea + kCT - 1) / kCT)), dim3(kCT), 0, st,
+                           (const GenPoint *)(gp + nsurf), (uint32_t)narea, (const double *)h,
+                           p->depth, nullptr, area_d);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    // the kept count and the centre height land in pinned memory; when the caller's buffers
+    // hold the worst case (n kept + the surface, pcp_excavate_bounds), the records go out in the
+    // same round trip: one synchronisation for the call
+    PCP_HIP(ctx, ctx->small_host.ensure(4096));
+    char *sm = ctx->small_host.as<char>();
+    PCP_HIP(ctx, hipMemcpyAsync(sm, ctr, 16, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipMemcpyAsync(sm + 16, h, sizeof(double), hipMemcpyDeviceToHost, st));
+    const bool one_trip = terrain_out && terrain_cap >= n + nsurf && (area_out || !narea) &&
+                          area_cap >= narea;
+    if (one_trip) {
+        if (n + nsurf)
+            PCP_HIP(ctx, hipMemcpyAsync(terrain_out, kept, (n + nsurf) * 32, hipMemcpyDeviceToHost,
+                                        st));
+        if (narea)
+            PCP_HIP(ctx, hipMemcpyAsync(area_out, area_d, narea * 32, hipMemcpyDeviceToHost, st));
+    }
+    PCP_HIP(ctx, hipStreamSynchronize(st));
     uint32_t cnt[4];
-    PCP_HIP(ctx, hipMemcpyAsync(hg.data(), h, G * sizeof(double), hipMemcpyDeviceToHost, st));
-    if (int rc0 = read_small(ctx, cnt, ctr, sizeof(cnt), st)) return rc0;   // also waits for hg
+    std::memcpy(cnt, sm, 16);
+    double h0;
+    std::memcpy(&h0, sm + 16, sizeof(double));
     const uint64_t nkept = n ? cnt[2] : 0;
     if (pose_out) {
         pose_out[0] = cx;
         pose_out[1] = cy;
-        pose_out[2] = hg[0];
+        pose_out[2] = h0;
         pose_out[3] = yaw;
     }
-    *n_terrain = nkept + surf.size();
-    *n_area = area.size();
+    *n_terrain = nkept + nsurf;
+    *n_area = narea;
     if (*n_terrain > terrain_cap || *n_area > area_cap) {
         prof_resolve(ctx);
         return set_err(ctx, PCP_E_CAPACITY, "pcp_excavate: need %llu / %llu records, cap %llu / %llu",
@@ -554,23 +606,14 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     }
     if ((*n_terrain && !terrain_out) || (*n_area && !area_out))
         return set_err(ctx, PCP_E_INVALID, "pcp_excavate: null output");
-    if (nkept)
-        PCP_HIP(ctx, hipMemcpyAsync(terrain_out, kept, nkept * 32, hipMemcpyDeviceToHost, st));
-    const double depth = p->depth;
-    auto put = [&hg, depth](const GenPoint &gp, float *o) {
-        const double z = gp.kind == 0 ? hg[gp.q] - gp.v : (hg[gp.q] - depth) + gp.v;
-        o[0] = (float)gp.x;
-        o[1] = (float)gp.y;
-        o[2] = (float)z;
-        o[3] = 1.0f;
-        o[4] = gp.rgb;
-        o[5] = o[6] = o[7] = 0.0f;
-    };
-    float *to = static_cast<float *>(terrain_out);
-    for (size_t k = 0; k < surf.size(); ++k) put(surf[k], to + 8 * (nkept + k));
-    float *ao = static_cast<float *>(area_out);
-    for (size_t k = 0; k < area.size(); ++k) put(area[k], ao + 8 * k);
-    PCP_HIP(ctx, hipStreamSynchronize(st));
+    if (!one_trip) {   // exact-size buffers: the records follow the sizes
+        if (*n_terrain)
+            PCP_HIP(ctx, hipMemcpyAsync(terrain_out, kept, *n_terrain * 32, hipMemcpyDeviceToHost,
+                                        st));
+        if (narea)
+            PCP_HIP(ctx, hipMemcpyAsync(area_out, area_d, narea * 32, hipMemcpyDeviceToHost, st));
+        PCP_HIP(ctx, hipStreamSynchronize(st));
+    }
     prof_resolve(ctx);
     return PCP_OK;
 }

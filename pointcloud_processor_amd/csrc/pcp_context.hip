@@ -52,6 +52,24 @@ uint64_t alloc_count(int which) {
     return which == 0 ? g_reallocs.load() : which == 1 ? g_pinned_reallocs.load() : g_alloc_bytes.load();
 }
 
+int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hipStream_t st) {
+    if (bytes == 0) return PCP_OK;
+    if (bytes > kUploadPinnedMax) {
+        PCP_HIP(ctx, hipMemcpyAsync(dst_d, src_h, bytes, hipMemcpyHostToDevice, st));
+        return PCP_OK;
+    }
+    const int k = ctx->up_next;
+    ctx->up_next = (k + 1) % pcp_ctx::kUpRing;
+    if (ctx->up_used[k]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[k]));   // its last DMA
+    if (!ctx->up_ev[k]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[k], hipEventDisableTiming));
+    PCP_HIP(ctx, ctx->up_buf[k].ensure(bytes));
+    std::memcpy(ctx->up_buf[k].p, src_h, bytes);
+    PCP_HIP(ctx, hipMemcpyAsync(dst_d, ctx->up_buf[k].p, bytes, hipMemcpyHostToDevice, st));
+    PCP_HIP(ctx, hipEventRecord(ctx->up_ev[k], st));
+    ctx->up_used[k] = true;
+    return PCP_OK;
+}
+
 int read_small(pcp_ctx *ctx, void *dst, const void *src_d, size_t bytes, hipStream_t st) {
     if (bytes > 4096) return set_err(ctx, PCP_E_INVALID, "read_small: %zu bytes", bytes);
     PCP_HIP(ctx, ctx->small_host.ensure(4096));
@@ -125,7 +143,14 @@ KernelTimer::~KernelTimer() {
 }
 
 void prof_resolve(pcp_ctx *ctx) {
+    // calls that return without a stream synchronisation (index builds) leave events in
+    // flight: those stay pending until a later call finds them complete
+    std::vector<PendingEvent> keep;
     for (auto &pe : ctx->pending) {
+        if (hipEventQuery(pe.b) == hipErrorNotReady) {
+            keep.push_back(pe);
+            continue;
+        }
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
             ctx->slots[pe.kid].total_ms += ms;
@@ -134,7 +159,7 @@ void prof_resolve(pcp_ctx *ctx) {
         ctx->event_pool.push_back(pe.a);
         ctx->event_pool.push_back(pe.b);
     }
-    ctx->pending.clear();
+    ctx->pending.swap(keep);
 }
 
 // ---- exclusive scan (uint32) ----------------------------------------------------------------
@@ -320,6 +345,11 @@ void pcp_destroy(pcp_ctx *ctx) {
     prof_resolve(ctx);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->keys_ev) (void)hipEventDestroy(ctx->keys_ev);
+    for (int k = 0; k < pcp_ctx::kUpRing; ++k) {
+        if (ctx->up_ev[k]) (void)hipEventDestroy(ctx->up_ev[k]);
+        ctx->up_buf[k].release();
+    }
+    ctx->cand_host.release();
     ctx->terrain.release();
     ctx->aux.release();
     ctx->exc_norm.release();

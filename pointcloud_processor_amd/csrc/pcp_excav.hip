@@ -145,16 +145,20 @@ __device__ __forceinline__ DD dd_merge(DD a, DD b) {
     return a;
 }
 
-// computeTerrainNormals: block per point (sorted index order; .w = input index).  The
-// second moments are double-double sums of exact float x float products: the exact sum for
-// these magnitudes, so the result does not depend on the (atomic) order of points in a cell.
+// computeTerrainNormals: block per point (sorted index order; .w = input index).  The shifted
+// second moments are summed as 64-bit fixed point (each double term rounded once to a multiple
+// of 2^-32, far below the float covariance's own rounding): integer sums are associative, so
+// the result does not depend on the (atomic) order of the points in a cell or on the reduction
+// tree -- deterministic run to run -- for fewer instructions than the double-double sums this
+// replaced (|term| <= 2.25 m^2 within the 1.5 m radius: 9e8 neighbours fit in int64).
+constexpr double kMomScale = 4294967296.0;   // 2^32
 __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, float *__restrict__ out) {
     const uint32_t qi = blockIdx.x;
     const float4 q = g.pts[qi];
     const uint32_t orig = __float_as_uint(q.w);
     uint32_t lo[4], hi[4];
-    DD acc[10];   // xx xy xz yy yz zz x y z count
-    for (int a = 0; a < 10; ++a) acc[a] = DD{0.0, 0.0};
+    long long acc[10];   // xx xy xz yy yz zz x y z count
+    for (int a = 0; a < 10; ++a) acc[a] = 0;
     if (stencil_ranges(g, q.x, q.y, q.z, lo, hi)) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -164,36 +168,33 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
                 // shifted by K = the first (nearest) neighbour = the query point itself
                 const double x = (double)(p.x - q.x), y = (double)(p.y - q.y),
                              z = (double)(p.z - q.z);
-                dd_add(acc[0], x * x);
-                dd_add(acc[1], x * y);
-                dd_add(acc[2], x * z);
-                dd_add(acc[3], y * y);
-                dd_add(acc[4], y * z);
-                dd_add(acc[5], z * z);
-                dd_add(acc[6], x);
-                dd_add(acc[7], y);
-                dd_add(acc[8], z);
-                acc[9].hi += 1.0;
+                acc[0] += __double2ll_rn(x * x * kMomScale);
+                acc[1] += __double2ll_rn(x * y * kMomScale);
+                acc[2] += __double2ll_rn(x * z * kMomScale);
+                acc[3] += __double2ll_rn(y * y * kMomScale);
+                acc[4] += __double2ll_rn(y * z * kMomScale);
+                acc[5] += __double2ll_rn(z * z * kMomScale);
+                acc[6] += __double2ll_rn(x * kMomScale);
+                acc[7] += __double2ll_rn(y * kMomScale);
+                acc[8] += __double2ll_rn(z * kMomScale);
+                acc[9] += 1;
             }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
-        for (int a = 0; a < 10; ++a) {
-            const DD t{__shfl_xor(acc[a].hi, o, 64), __shfl_xor(acc[a].lo, o, 64)};
-            acc[a] = dd_merge(acc[a], t);
-        }
-    __shared__ DD lds[10][kXT / 64];
+        for (int a = 0; a < 10; ++a) acc[a] += __shfl_xor(acc[a], o, 64);
+    __shared__ long long lds[10][kXT / 64];
     if (lane == 0)
         for (int a = 0; a < 10; ++a) lds[a][wid] = acc[a];
     __syncthreads();
     if (threadIdx.x != 0) return;
     double v[10];
     for (int a = 0; a < 10; ++a) {
-        DD t = lds[a][0];
-        for (int w = 1; w < kXT / 64; ++w) t = dd_merge(t, lds[a][w]);
-        v[a] = t.hi + t.lo;
+        long long t = lds[a][0];
+        for (int w = 1; w < kXT / 64; ++w) t += lds[a][w];
+        v[a] = a == 9 ? (double)t : (double)t / kMomScale;
     }
     float *o = out + 3 * (size_t)orig;
     if (v[9] < 3.0) {   // computePointNormal: < 3 neighbours -> NaN
@@ -300,67 +301,76 @@ k_lattice_compact(const uint8_t *__restrict__ flags, Lattice L, double *__restri
     if (threadIdx.x == 0) *n_out = run;
 }
 
-// computeCellSurfaceNormal: block per cell, neighbours within 1.5 m of the float cell position
+// computeCellSurfaceNormal: a block per cell (block-strided over the cells; their count is
+// read on the device, so the host never waits for the lattice), neighbours within 1.5 m of
+// the float cell position
 __global__ void __launch_bounds__(kXT)
 k_cell_normals(GridView g, float r2, const double *__restrict__ cells,
-               const float *__restrict__ area_nrm, float *__restrict__ out) {
-    const uint32_t c = blockIdx.x;
-    const float qx = (float)cells[3 * (size_t)c], qy = (float)cells[3 * (size_t)c + 1],
-                qz = (float)cells[3 * (size_t)c + 2];
-    DD s[3] = {{0, 0}, {0, 0}, {0, 0}};
-    uint32_t valid = 0;
-    uint32_t lo[4], hi[4];
-    if (stencil_ranges(g, qx, qy, qz, lo, hi)) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            for (uint32_t k = lo[r] + threadIdx.x; k < hi[r]; k += kXT) {
-                const float4 p = g.pts[k];
-                if (!flann_within(qx, qy, qz, p, r2)) continue;
-                const float *n = area_nrm + 3 * (size_t)__float_as_uint(p.w);
-                const float nx = n[0], ny = n[1], nz = n[2];
-                if (!(isfinite(nx) && isfinite(ny) && isfinite(nz))) continue;
-                dd_add(s[0], (double)nx);
-                dd_add(s[1], (double)ny);
-                dd_add(s[2], (double)nz);
-                ++valid;
-            }
-    }
+               const float *__restrict__ area_nrm, const uint32_t *__restrict__ n_cells,
+               float *__restrict__ out) {
+    const uint32_t nc = *n_cells;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            DD t{__shfl_xor(s[a].hi, o, 64), __shfl_xor(s[a].lo, o, 64)};
-            s[a] = dd_merge(s[a], t);
-        }
-        valid += __shfl_xor(valid, o, 64);
-    }
     __shared__ DD lds[3][kXT / 64];
     __shared__ uint32_t lv[kXT / 64];
-    if (lane == 0) {
-        for (int a = 0; a < 3; ++a) lds[a][wid] = s[a];
-        lv[wid] = valid;
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    DD t[3];
-    uint32_t nv = 0;
-    for (int a = 0; a < 3; ++a) {
-        t[a] = lds[a][0];
-        for (int w = 1; w < kXT / 64; ++w) t[a] = dd_merge(t[a], lds[a][w]);
-    }
-    for (int w = 0; w < kXT / 64; ++w) nv += lv[w];
-    float *o = out + 3 * (size_t)c;
-    o[0] = 0.0f;   // GridCell's default surface normal
-    o[1] = 0.0f;
-    o[2] = 1.0f;
-    if (nv == 0) return;
-    const double sx = t[0].hi + t[0].lo, sy = t[1].hi + t[1].lo, sz = t[2].hi + t[2].lo;
-    const double norm = sqrt(sx * sx + sy * sy + sz * sz);
-    if (norm > 1e-6) {
-        o[0] = (float)(sx / norm);
-        o[1] = (float)(sy / norm);
-        o[2] = (float)(sz / norm);
+    for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
+        const float qx = (float)cells[3 * (size_t)c], qy = (float)cells[3 * (size_t)c + 1],
+                    qz = (float)cells[3 * (size_t)c + 2];
+        DD s[3] = {{0, 0}, {0, 0}, {0, 0}};
+        uint32_t valid = 0;
+        uint32_t lo[4], hi[4];
+        if (stencil_ranges(g, qx, qy, qz, lo, hi)) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                for (uint32_t k = lo[r] + threadIdx.x; k < hi[r]; k += kXT) {
+                    const float4 p = g.pts[k];
+                    if (!flann_within(qx, qy, qz, p, r2)) continue;
+                    const float *n = area_nrm + 3 * (size_t)__float_as_uint(p.w);
+                    const float nx = n[0], ny = n[1], nz = n[2];
+                    if (!(isfinite(nx) && isfinite(ny) && isfinite(nz))) continue;
+                    dd_add(s[0], (double)nx);
+                    dd_add(s[1], (double)ny);
+                    dd_add(s[2], (double)nz);
+                    ++valid;
+                }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                DD t{__shfl_xor(s[a].hi, o, 64), __shfl_xor(s[a].lo, o, 64)};
+                s[a] = dd_merge(s[a], t);
+            }
+            valid += __shfl_xor(valid, o, 64);
+        }
+        if (lane == 0) {
+            for (int a = 0; a < 3; ++a) lds[a][wid] = s[a];
+            lv[wid] = valid;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            DD t[3];
+            uint32_t nv = 0;
+            for (int a = 0; a < 3; ++a) {
+                t[a] = lds[a][0];
+                for (int w = 1; w < kXT / 64; ++w) t[a] = dd_merge(t[a], lds[a][w]);
+            }
+            for (int w = 0; w < kXT / 64; ++w) nv += lv[w];
+            float *o = out + 3 * (size_t)c;
+            o[0] = 0.0f;   // GridCell's default surface normal
+            o[1] = 0.0f;
+            o[2] = 1.0f;
+            if (nv != 0) {
+                const double sx = t[0].hi + t[0].lo, sy = t[1].hi + t[1].lo,
+                             sz = t[2].hi + t[2].lo;
+                const double norm = sqrt(sx * sx + sy * sy + sz * sz);
+                if (norm > 1e-6) {
+                    o[0] = (float)(sx / norm);
+                    o[1] = (float)(sy / norm);
+                    o[2] = (float)(sz / norm);
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -390,7 +400,6 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     PCP_HIP(ctx, hipMemsetAsync(ctx->area_nrm.p, 0xff, n * 3 * sizeof(float), ctx->stream));
     ctx->area_n = n;
     if (ctx->exc_norm.n_pts == 0) {   // no finite point: no lattice bounds, no cells
-        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
         ctx->n_cells = 0;
         if (n_cells) *n_cells = 0;
         return PCP_OK;
@@ -438,15 +447,18 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
                        (const uint8_t *)ctx->stage.as<uint8_t>(), L, ctx->cells_xyz.as<double>(),
                        (uint32_t)total, n_d);
     PCP_CHECK_LAUNCH(ctx);
-    uint32_t nc = 0;
-    if (int rc0 = read_small(ctx, &nc, n_d, 4, ctx->stream)) return rc0;
-    if (nc) {
-        hipLaunchKernelGGL(k_cell_normals, dim3(nc), dim3(kXT), 0, ctx->stream, gn, r2n,
+    // the cell normals read the lattice count on the device; the count comes back once, at
+    // the end (one synchronisation for the whole call)
+    if (total) {
+        hipLaunchKernelGGL(k_cell_normals, dim3((unsigned)std::min<uint64_t>(total, 8192)),
+                           dim3(kXT), 0, ctx->stream, gn, r2n,
                            (const double *)ctx->cells_xyz.as<double>(),
-                           (const float *)ctx->area_nrm.as<float>(), ctx->cells_nrm.as<float>());
+                           (const float *)ctx->area_nrm.as<float>(), (const uint32_t *)n_d,
+                           ctx->cells_nrm.as<float>());
         PCP_CHECK_LAUNCH(ctx);
     }
-    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    uint32_t nc = 0;
+    if (int rc0 = read_small(ctx, &nc, n_d, 4, ctx->stream)) return rc0;
     ctx->n_cells = nc;
     if (n_cells) *n_cells = nc;
     prof_resolve(ctx);

@@ -1016,7 +1016,9 @@ static int stage_cloud(pcp_ctx *ctx, const pcp_cloud_view &v, bool device_in, De
     }
     const uint64_t bytes = v.n * (uint64_t)v.point_step;
     unsigned char *dst = buf.as<unsigned char>() + off;
-    PCP_HIP(ctx, hipMemcpyAsync(dst, v.data, bytes, hipMemcpyHostToDevice, ctx->stream));
+    // message-sized clouds through the pinned ring (no wait on the stream), C3-sized ones
+    // straight from pageable memory (the link, not the wait, sets their rate)
+    if (int rc = upload_async(ctx, dst, v.data, bytes, ctx->stream)) return rc;
     c.raw = dst;
     return PCP_OK;
 }

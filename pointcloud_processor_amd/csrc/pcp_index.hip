@@ -393,6 +393,33 @@ k_blk_fill(const float4 *__restrict__ pts, uint64_t n, const uint32_t *__restric
     }
 }
 
+// clouds up to this size get their bbox from the host (build_index)
+constexpr uint64_t kHostBboxMax = 1ull << 17;
+
+// min / max of the finite points and their count, as k_extract + k_bbox_final compute them
+static void host_bbox(const pcp_cloud_view &v, float bb[10], uint32_t &nfin) {
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    uint32_t c = 0;
+    const unsigned char *raw = static_cast<const unsigned char *>(v.data);
+    for (uint64_t i = 0; i < v.n; ++i) {
+        const unsigned char *p = raw + i * v.point_step;
+        float x, y, z;
+        memcpy(&x, p + v.off_x, 4);
+        memcpy(&y, p + v.off_y, 4);
+        memcpy(&z, p + v.off_z, 4);
+        if (!(std::isfinite(x) && std::isfinite(y) && std::isfinite(z))) continue;
+        ++c;
+        mn[0] = std::fmin(mn[0], x); mx[0] = std::fmax(mx[0], x);
+        mn[1] = std::fmin(mn[1], y); mx[1] = std::fmax(mx[1], y);
+        mn[2] = std::fmin(mn[2], z); mx[2] = std::fmax(mx[2], z);
+    }
+    for (int a = 0; a < 3; ++a) {
+        bb[a] = mn[a];
+        bb[3 + a] = mx[a];
+    }
+    nfin = c;
+}
+
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort,
                 bool occ) {
     const uint64_t n = v.n;
@@ -412,10 +439,10 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     g.blk_fail = false;
     g.fine_ok = false;
     g.fine_fail = false;
-    // 1. stage the raw AoS bytes (the PointCloud2 data blob)
+    // 1. stage the raw AoS bytes (the PointCloud2 data blob): pinned ring, no implicit wait
     const uint64_t raw_bytes = n * (uint64_t)v.point_step;
     PCP_HIP(ctx, ctx->stage.ensure(raw_bytes));
-    PCP_HIP(ctx, hipMemcpyAsync(ctx->stage.p, v.data, raw_bytes, hipMemcpyHostToDevice, st));
+    if (int rc0 = upload_async(ctx, ctx->stage.p, v.data, raw_bytes, st)) return rc0;
     // 2. extract + bbox
     const int nb = (int)std::min<uint64_t>((n + kThreads - 1) / kThreads, 1024);
     PCP_HIP(ctx, ctx->scratch[0].ensure(n * sizeof(float4)));
@@ -427,14 +454,21 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
                        n, v.point_step, v.off_x, v.off_y, v.off_z, ctx->scratch[0].as<float4>(),
                        part, part_n);
     PCP_CHECK_LAUNCH(ctx);
-    float *bb_d = ctx->stats_d.as<float>();
-    hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(kThreads), 0, st, part, part_n, nb, bb_d,
-                       reinterpret_cast<uint32_t *>(bb_d + 8));
-    PCP_CHECK_LAUNCH(ctx);
     float bb_h[10];
-    if (int rc0 = read_small(ctx, bb_h, bb_d, sizeof(bb_h), st)) return rc0;
     uint32_t nfin;
-    memcpy(&nfin, &bb_h[8], 4);
+    if (n <= kHostBboxMax) {
+        // a message-sized cloud: the grid geometry from the host's copy of the same bytes (the
+        // same float min / max over the finite points, order-free) while the device extracts --
+        // no round trip through the stream
+        host_bbox(v, bb_h, nfin);
+    } else {
+        float *bb_d = ctx->stats_d.as<float>();
+        hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(kThreads), 0, st, part, part_n, nb, bb_d,
+                           reinterpret_cast<uint32_t *>(bb_d + 8));
+        PCP_CHECK_LAUNCH(ctx);
+        if (int rc0 = read_small(ctx, bb_h, bb_d, sizeof(bb_h), st)) return rc0;
+        memcpy(&nfin, &bb_h[8], 4);
+    }
     g.r_q = r_q;
     g.n_pts = nfin;
     if (nfin == 0) {   // a tree over zero valid points: never returns neighbours
@@ -531,7 +565,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         PCP_CHECK_LAUNCH(ctx);
         g.occz_ok = true;
     }
-    PCP_HIP(ctx, hipStreamSynchronize(st));
+    // no synchronisation: the index is used by later work on the same stream
     g.present = true;
     return PCP_OK;
 }

@@ -244,6 +244,13 @@ struct pcp_ctx {
     // query waits for it before it reuses the pinned pose staging
     hipEvent_t keys_ev = nullptr;
     bool keys_pending = false;
+    // pinned upload ring (upload_async): host bytes copied here, then a stream-ordered DMA
+    static constexpr int kUpRing = 4;
+    pcp::PinnedBuf up_buf[kUpRing];
+    hipEvent_t up_ev[kUpRing] = {};
+    bool up_used[kUpRing] = {};
+    int up_next = 0;
+    pcp::PinnedBuf cand_host;                // generate_candidates: poses + count in one readback
     int32_t fan_naz = -1, fan_nel = -1;      // cached fan direction tables
     double fan_elmin = 0.0, fan_elmax = 0.0;
     double steps_end = -1e300;               // cached step table
@@ -397,6 +404,15 @@ int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what);
 // a small (<= 4 KB) device -> host readback through pinned memory; synchronizes the stream
 // (a pageable destination costs a staging copy per call)
 int read_small(pcp_ctx *ctx, void *dst, const void *src_d, size_t bytes, hipStream_t st);
+
+// host -> device copy of a caller's (pageable) buffer that does NOT wait for the stream: a
+// pageable hipMemcpyAsync returns only once the stream has drained up to it (an implicit
+// synchronisation in the middle of a chain).  Up to kUploadPinnedMax bytes are copied on the
+// host into a slot of a pinned ring and DMA'd stream-ordered (the slot is reused only after
+// its previous DMA completed); larger buffers take the pageable path.  The caller may reuse
+// src_h on return either way.
+constexpr size_t kUploadPinnedMax = 16u << 20;
+int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hipStream_t st);
 
 // the smallest float d with fl(d * d) >= r2: a point with dz = qz - pz >= d fails FLANN's
 // float test (its sum is >= fl(dz^2) >= r2), and so does every lower point of a z-descending

@@ -1369,13 +1369,12 @@ int pcp_set_cells(pcp_ctx *ctx, const double *xyz, const float *normals, uint64_
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     PCP_HIP(ctx, ctx->cells_xyz.ensure(n * 3 * sizeof(double) + 16));
     PCP_HIP(ctx, ctx->cells_nrm.ensure(n * 3 * sizeof(float) + 16));
-    if (n) {
-        PCP_HIP(ctx, hipMemcpyAsync(ctx->cells_xyz.p, xyz, n * 3 * sizeof(double),
-                                    hipMemcpyHostToDevice, ctx->stream));
-        PCP_HIP(ctx, hipMemcpyAsync(ctx->cells_nrm.p, normals, n * 3 * sizeof(float),
-                                    hipMemcpyHostToDevice, ctx->stream));
+    if (n) {   // through the pinned ring: no wait on the stream, the caller may reuse its arrays
+        if (int rc = upload_async(ctx, ctx->cells_xyz.p, xyz, n * 3 * sizeof(double), ctx->stream))
+            return rc;
+        if (int rc = upload_async(ctx, ctx->cells_nrm.p, normals, n * 3 * sizeof(float), ctx->stream))
+            return rc;
     }
-    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     ctx->n_cells = n;
     return PCP_OK;
 }
@@ -1424,24 +1423,35 @@ int pcp_generate_candidates(pcp_ctx *ctx, const double bb[6], const pcp_vl_param
                            ctx->out_a.as<const double>(), L, ctx->out_b.as<double>(), n_d);
         PCP_CHECK_LAUNCH(ctx);
     }
-    uint32_t nh = 0;
-    if (int rc0 = read_small(ctx, &nh, n_d, 4, ctx->stream)) return rc0;
-    *n_out = nh;
-    if (nh > cap) {
+    // the poses and their count are adjacent: one readback of the lattice's worst case into
+    // pinned memory, one synchronisation (huge lattices: the count first, then the poses)
+    const size_t span = (size_t)L * 5 * sizeof(double) + sizeof(uint32_t);
+    if (span > (4u << 20)) {
+        uint32_t nh = 0;
+        if (int rc0 = read_small(ctx, &nh, n_d, 4, ctx->stream)) return rc0;
+        *n_out = nh;
         prof_resolve(ctx);
+        if (nh > cap)
+            return set_err(ctx, PCP_E_CAPACITY, "pcp_generate_candidates: need %u poses, cap %llu",
+                           nh, (unsigned long long)cap);
+        if (nh)
+            PCP_HIP(ctx, hipMemcpyAsync(poses5, ctx->out_b.p, (size_t)nh * 5 * sizeof(double),
+                                        hipMemcpyDeviceToHost, ctx->stream));
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        return PCP_OK;
+    }
+    PCP_HIP(ctx, ctx->cand_host.ensure(span));
+    PCP_HIP(ctx, hipMemcpyAsync(ctx->cand_host.p, ctx->out_b.p, span, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    uint32_t nh = 0;
+    std::memcpy(&nh, ctx->cand_host.as<char>() + (size_t)L * 5 * sizeof(double), sizeof(nh));
+    *n_out = nh;
+    prof_resolve(ctx);
+    if (nh > cap)
         return set_err(ctx, PCP_E_CAPACITY, "pcp_generate_candidates: need %u poses, cap %llu", nh,
                        (unsigned long long)cap);
-    }
-    const size_t pbytes = (size_t)nh * 5 * sizeof(double);
-    if (nh && pbytes <= 4096) {   // the usual lattice (~100 poses): through pinned memory
-        if (int rc0 = read_small(ctx, poses5, ctx->out_b.p, pbytes, ctx->stream)) return rc0;
-    } else {
-        if (nh)
-            PCP_HIP(ctx, hipMemcpyAsync(poses5, ctx->out_b.p, pbytes, hipMemcpyDeviceToHost,
-                                        ctx->stream));
-        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    }
-    prof_resolve(ctx);
+    if (nh) std::memcpy(poses5, ctx->cand_host.p, (size_t)nh * 5 * sizeof(double));
     return PCP_OK;
 }
 
