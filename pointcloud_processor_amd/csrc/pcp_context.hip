@@ -321,6 +321,7 @@ int pcp_create(int device, pcp_ctx **out) {
     }
     if (const char *ho = std::getenv("PCP_FAN_HOST_OUT")) ctx->fan_host_out = std::atoi(ho) != 0;
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
+    if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff) != 0;
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
     if (const char *tf = std::getenv("PCP_TERRAIN_FINE")) ctx->terrain_fine = std::atoi(tf);
     if (const char *tt = std::getenv("PCP_FINE_TILE")) ctx->fine_tile = std::atoi(tt);

@@ -40,6 +40,7 @@ constexpr int kGroup = 16;          // sort tiles per prefix group (radix digit 
 constexpr int kDigitBits = 9;       // radix digit: 512 bins, 3 passes for the C3 crop box
 constexpr int kBins = 1 << kDigitBits;
 constexpr int kMaxPasses = 4;       // ceil(32 / 9)
+constexpr int kMaxCloudsDev = 64;   // result slots of a call (= kMaxClouds below)
 
 // diagnostic build only (make STAMPS=1): per-tile phase times, s_memrealtime (100 MHz)
 #ifdef PCP_STAMPS
@@ -222,7 +223,19 @@ struct CloudJob {
     VoxParams *vp;
     Rigid rig;            // pcp_filter_merge's transform + colour of this cloud
     int32_t slot;         // result slot (index of the cloud in the call)
+    // the fast chain (pcp_filter_merge when every cloud certainly voxelises, enqueue_fast):
+    // the crop forms BOX-relative voxel keys -- (floor(p * inv) - kb) per axis, mixed radix
+    // kdx, kdxy -- whose order is PCL's idx order (a constant shift per axis does not change
+    // the lexicographic (k, j, i) order), plus each crop tile's digit-0 counts; the first radix
+    // pass then reads the crop tiles in groups of kGroupTiles, no compaction, no parameters
+    int32_t fast;
+    float kinv, kb[3];
+    uint32_t kdx, kdxy;
+    uint32_t *skeys;      // [nb * kCropTile] keys in the crop tiles' slots
+    uint32_t *h0;         // [nb][kBins] digit-0 counts per crop tile
+    uint32_t ng;          // groups of kGroupTiles crop tiles (pass 0's sort tiles)
 };
+constexpr int kGroupTiles = 8;   // crop tiles per pass-0 sort tile (~10 % survive the C3 crop)
 
 // up to kBatch clouds per launch, passed BY VALUE: pointers loaded from kernel arguments are
 // known to be global (global_load, independent waits), which a table in memory would lose
@@ -239,8 +252,26 @@ struct JobBatch {
 #else
 #define PCP_CROP_ATTR
 #endif
-__global__ void __launch_bounds__(kCT) PCP_CROP_ATTR k_crop_tile(const JobBatch jobs) {
+template <bool KEYS>
+__global__ void __launch_bounds__(kCT) PCP_CROP_ATTR k_crop_tile(const JobBatch jobs,
+                                                                 uint32_t *__restrict__ res) {
     const CloudJob &J = jobs.j[blockIdx.y];
+    if constexpr (KEYS) {
+        // the fast chain's zeroing (k_compact_keys does it in the other chain): digit totals
+        // and group sums of every pass, the sort count (k_hist0 adds to it) and the result
+        // slots (a cloud with nothing cropped keeps 0 voxels)
+        for (uint32_t q = blockIdx.x * kCT + threadIdx.x; q < J.nzero; q += gridDim.x * kCT)
+            J.zero[q] = 0;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            VoxParams p{};
+            p.do_voxel = 1;
+            p.inv = J.kinv;
+            *J.vp = p;
+            res[J.slot] = 0;
+            res[kMaxCloudsDev + 2 * J.slot] = 0;
+            res[kMaxCloudsDev + 2 * J.slot + 1] = 0;
+        }
+    }
     if (blockIdx.x >= J.nb) return;
     const CloudIn c = J.in;
     const Box b = J.box;
@@ -267,7 +298,11 @@ __global__ void __launch_bounds__(kCT) PCP_CROP_ATTR k_crop_tile(const JobBatch 
         bal[j] = __ballot(k);
     }
     __shared__ uint32_t wo[kCropItems][kCT / 64];
-    const uint32_t tot = round_offsets(bal, wo);
+    __shared__ uint32_t h0s[KEYS ? kBins : 1];
+    if constexpr (KEYS) {
+        for (int q = threadIdx.x; q < kBins; q += kCT) h0s[q] = 0;
+    }
+    const uint32_t tot = round_offsets(bal, wo);   // (its barriers order the zeroing above)
     if (threadIdx.x == 0) counts[blockIdx.x] = tot;
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
 #pragma unroll
@@ -275,10 +310,27 @@ __global__ void __launch_bounds__(kCT) PCP_CROP_ATTR k_crop_tile(const JobBatch 
         if (!((keep >> j) & 1u)) continue;
         const uint32_t d = wo[j][wid] + (uint32_t)__popcll(bal[j] & lanemask_lt(lane));
         sparse[base + d] = make_float4(x[j], y[j], z[j], 1.0f);
-        if (sparse_idx) sparse_idx[base + d] = (uint32_t)(base + (uint64_t)j * kCT + threadIdx.x);
-        mn[0] = fminf(mn[0], x[j]); mx[0] = fmaxf(mx[0], x[j]);
-        mn[1] = fminf(mn[1], y[j]); mx[1] = fmaxf(mx[1], y[j]);
-        mn[2] = fminf(mn[2], z[j]); mx[2] = fmaxf(mx[2], z[j]);
+        if constexpr (KEYS) {
+            // applyFilter's float keying, shifted by the box floor (exact: integers < 2^24)
+            const uint32_t i0 = (uint32_t)(int)(floorf(x[j] * J.kinv) - J.kb[0]);
+            const uint32_t i1 = (uint32_t)(int)(floorf(y[j] * J.kinv) - J.kb[1]);
+            const uint32_t i2 = (uint32_t)(int)(floorf(z[j] * J.kinv) - J.kb[2]);
+            const uint32_t key = i0 + i1 * J.kdx + i2 * J.kdxy;
+            J.skeys[base + d] = key;
+            atomicAdd(&h0s[key & (kBins - 1)], 1u);
+        } else {
+            if (sparse_idx)
+                sparse_idx[base + d] = (uint32_t)(base + (uint64_t)j * kCT + threadIdx.x);
+            mn[0] = fminf(mn[0], x[j]); mx[0] = fmaxf(mx[0], x[j]);
+            mn[1] = fminf(mn[1], y[j]); mx[1] = fmaxf(mx[1], y[j]);
+            mn[2] = fminf(mn[2], z[j]); mx[2] = fmaxf(mx[2], z[j]);
+        }
+    }
+    if constexpr (KEYS) {   // the tile's digit-0 row (the fast chain needs no bbox)
+        __syncthreads();
+        for (int q = threadIdx.x; q < kBins; q += kCT)
+            J.h0[(size_t)blockIdx.x * kBins + q] = h0s[q];
+        return;
     }
     // bbox partials (used by the voxel stage; exact min/max, order-free)
 #pragma unroll
@@ -466,8 +518,10 @@ k_radix_scatter(const JobBatch jobs, int pass) {
     const bool odd = pass & 1;
     const uint32_t *kin = odd ? J.keys1 : J.keys0;
     uint32_t *kout = odd ? J.keys0 : J.keys1;
-    const float4 *pin = odd ? J.sparse : J.xyz;
-    float4 *pout = odd ? J.xyz : J.sparse;
+    // the fast chain's pass 0 wrote its payload to xyz (it read the crop tiles in sparse)
+    const bool sw = odd != (J.fast != 0);
+    const float4 *pin = sw ? J.sparse : J.xyz;
+    float4 *pout = sw ? J.xyz : J.sparse;
     const VoxParams *vpp = J.vp;
     const int shift = kDigitBits * pass;
     const uint32_t ntp = J.ntp;
@@ -578,6 +632,160 @@ k_radix_scatter(const JobBatch jobs, int pass) {
     }
 }
 
+// ---- the fast chain's pass 0 -------------------------------------------------------------
+// digit-0 counts of each group of kGroupTiles crop tiles (their rows summed), the pass's
+// totals and group sums, and the sort count m (k_vox_params's and k_compact_keys's jobs for the
+// sort, without their passes over the points)
+__global__ void __launch_bounds__(kST) k_hist0(const JobBatch jobs) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    const uint32_t g = blockIdx.x;
+    if (!J.fast || g >= J.ng) return;
+    static_assert(kBins == kST, "one digit per thread");
+    const uint32_t d = threadIdx.x;
+    const uint32_t c0 = g * kGroupTiles, c1 = min(c0 + (uint32_t)kGroupTiles, J.nb);
+    uint32_t v = 0;
+    for (uint32_t c = c0; c < c1; ++c) v += J.h0[(size_t)c * kBins + d];
+    J.rhist[(size_t)d * J.ntp + g] = v;
+    if (v) {
+        atomicAdd(&J.zero[d], v);   // pass 0's digit totals
+        atomicAdd(&J.zero[(size_t)kMaxPasses * kBins + (size_t)(g / kGroup) * kBins + d], v);
+    }
+    if (threadIdx.x < 64) {
+        uint32_t n = (c0 + threadIdx.x < c1) ? J.counts[c0 + threadIdx.x] : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+        if (threadIdx.x == 0 && n) atomicAdd(&J.vp->m, n);
+    }
+}
+
+// pass 0 of the fast chain: sort tile g = the kept points of crop tiles [8g, 8g + 8), read in
+// place from their sparse slots (input order = tile order, then slot order), in chunks of up to
+// kSortTile items; otherwise k_radix_scatter's stable ranking and run-wise stores, with each
+// digit's running count carried from chunk to chunk
+__global__ void __launch_bounds__(kST) k_radix_scatter0(const JobBatch jobs) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    if (!J.fast || J.passes <= 0) return;
+    const int shift = 0;
+    const uint32_t ntp = J.ntp;
+    const uint32_t *hist = J.rhist;
+    const uint32_t *totals = J.zero;
+    const uint32_t *gsum = J.zero + (size_t)kMaxPasses * kBins;
+    uint32_t *kout = J.keys1;
+    float4 *pout = J.xyz;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    constexpr int kWaveItems = kSortTile / kSW;
+    __shared__ uint32_t wh[kSW][kBins];
+    __shared__ uint32_t gbase[kBins];   // output position of the group's first item of digit d
+    __shared__ uint32_t tx[kBins];
+    __shared__ uint32_t lsa[kSW], lsb[kSW];
+    __shared__ uint32_t lk[kSortTile];
+    __shared__ float4 lp[kSortTile];
+    __shared__ uint32_t cpre[kGroupTiles + 1];
+    const uint32_t d = threadIdx.x;
+    for (uint32_t g = blockIdx.x; g < J.ng; g += gridDim.x) {
+        const uint32_t c0 = g * kGroupTiles;
+        if (threadIdx.x == 0) {
+            uint32_t a = 0;
+            cpre[0] = 0;
+            for (int c = 0; c < kGroupTiles; ++c) {
+                a += (c0 + c < J.nb) ? J.counts[c0 + c] : 0u;
+                cpre[c + 1] = a;
+            }
+        }
+        // earlier groups' count of digit d: whole 16-group sets, then the groups of g's set
+        const uint32_t grp = g / kGroup;
+        uint32_t pre = 0;
+#pragma unroll 8
+        for (uint32_t q = 0; q < grp; ++q) pre += gsum[(size_t)q * kBins + d];
+        {
+            const uint4 *row = reinterpret_cast<const uint4 *>(hist + (size_t)d * ntp + grp * kGroup);
+            const uint32_t nin = g - grp * kGroup;
+#pragma unroll
+            for (uint32_t qq = 0; qq < kGroup / 4; ++qq) {
+                if (4 * qq < nin) {
+                    const uint4 v = row[qq];
+                    const uint32_t b = 4 * qq;
+                    pre += v.x + (b + 1 < nin ? v.y : 0u) + (b + 2 < nin ? v.z : 0u) +
+                           (b + 3 < nin ? v.w : 0u);
+                }
+            }
+        }
+        const uint32_t base_d = block_excl_scan<kST>(totals[d], lsa);
+        gbase[d] = base_d + pre;
+        __syncthreads();
+        const uint32_t T = cpre[kGroupTiles];
+        for (uint32_t cb = 0; cb < T; cb += kSortTile) {
+            const uint32_t tn = min((uint32_t)kSortTile, T - cb);
+#pragma unroll
+            for (int w = 0; w < kSW; ++w) wh[w][d] = 0;
+            uint32_t k[kSortItems];
+            float4 pv[kSortItems];
+#pragma unroll
+            for (int j = 0; j < kSortItems; ++j) {
+                const uint32_t q = cb + (uint32_t)(wid * kWaveItems + j * 64 + lane);
+                k[j] = 0u;
+                pv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (q < T) {
+                    int c = 0;
+#pragma unroll
+                    for (int u = 1; u < kGroupTiles; ++u) c += q >= cpre[u] ? 1 : 0;
+                    const size_t sp = (size_t)(c0 + c) * kCropTile + (q - cpre[c]);
+                    k[j] = J.skeys[sp];
+                    pv[j] = J.sparse[sp];
+                }
+            }
+            __syncthreads();
+            uint32_t r[kSortItems];
+#pragma unroll
+            for (int j = 0; j < kSortItems; ++j) {
+                const bool act = cb + (uint32_t)(wid * kWaveItems + j * 64 + lane) < T;
+                const uint32_t dj = (k[j] >> shift) & (kBins - 1);
+                uint64_t same = __ballot(act);
+#pragma unroll
+                for (int bit = 0; bit < kDigitBits; ++bit) {
+                    const uint64_t bb = __ballot((dj >> bit) & 1u);
+                    same &= ((dj >> bit) & 1u) ? bb : ~bb;
+                }
+                const uint32_t lower = (uint32_t)__popcll(same & lanemask_lt(lane));
+                r[j] = act ? wh[wid][dj] + lower : 0u;
+                if (act && lower == 0) wh[wid][dj] += (uint32_t)__popcll(same);
+            }
+            __syncthreads();
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int w = 0; w < kSW; ++w) {
+                const uint32_t v = wh[w][d];
+                wh[w][d] = cnt;
+                cnt += v;
+            }
+            const uint32_t tx_d = block_excl_scan<kST>(cnt, lsb);
+            tx[d] = tx_d;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kSortItems; ++j) {
+                if (cb + (uint32_t)(wid * kWaveItems + j * 64 + lane) < T) {
+                    const uint32_t dj = (k[j] >> shift) & (kBins - 1);
+                    const uint32_t lpos = tx[dj] + wh[wid][dj] + r[j];
+                    lk[lpos] = k[j];
+                    lp[lpos] = pv[j];
+                }
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (uint32_t q = threadIdx.x; q < tn; q += kST) {
+                const uint32_t kk = lk[q];
+                const uint32_t dq = (kk >> shift) & (kBins - 1);
+                const uint32_t dst = gbase[dq] + (q - tx[dq]);
+                kout[dst] = kk;
+                pout[dst] = lp[q];
+            }
+            __syncthreads();
+            gbase[d] += cnt;   // the next chunk's items of digit d follow these
+            __syncthreads();
+        }
+    }
+}
+
 // ---- segments (voxels) of the sorted keys and their centroids ------------------------------
 // a sorted position starts a voxel iff its key differs from the previous one
 __device__ __forceinline__ bool seg_head(const uint32_t *keys, uint64_t i, uint32_t m) {
@@ -641,7 +849,7 @@ k_seg_centroid(const JobBatch jobs, uint32_t *__restrict__ res, float4 *__restri
     const CloudJob &J = jobs.j[blockIdx.y];
     if (J.passes == 0) return;
     const uint32_t *keys = (J.passes & 1) ? J.keys1 : J.keys0;
-    const float4 *pay = (J.passes & 1) ? J.sparse : J.xyz;
+    const float4 *pay = ((J.passes & 1) != (J.fast != 0)) ? J.sparse : J.xyz;
     const VoxParams *vpp = J.vp;
     const uint32_t *tcount = J.tcount, *fhead = J.fhead;
     float4 *out = J.out4;
@@ -681,7 +889,13 @@ k_seg_centroid(const JobBatch jobs, uint32_t *__restrict__ res, float4 *__restri
     FLT_STAMP(1, t, 1);
     const uint32_t tot = round_offsets(bal, wo);
     FLT_STAMP(1, t, 2);
-    if (t == nact - 1 && threadIdx.x == 0) res[slot] = pre + tot;
+    if (t == nact - 1 && threadIdx.x == 0) {
+        res[slot] = pre + tot;
+        if (J.fast) {   // no k_vox_params in the fast chain: the cropped count, no passthrough
+            res[kMaxCloudsDev + 2 * slot] = m;
+            res[kMaxCloudsDev + 2 * slot + 1] = 0;
+        }
+    }
     if (tot != 0) {   // uniform; 0: a tile inside one long voxel
     uint32_t loc[kSortItems];
 #pragma unroll
@@ -887,6 +1101,44 @@ static int make_job(pcp_ctx *ctx, int slot, const CloudIn &c, const Box &b, floa
     return PCP_OK;
 }
 
+// the fast chain's key geometry for job J (its box finite, leaf > 0, n > 0): box floor kb =
+// floor(lo * inv) - 2 per axis (a margin for the float product p * inv of a point just inside
+// the box), dims DX, DY, DZ past floor(hi * inv) + 1; false when the keys or the float
+// integers would not be exact (|values| >= 2^23, or DX * DY * DZ >= 2^31)
+static bool fast_geometry(pcp_ctx *ctx, int slot, CloudJob &J) {
+    if (J.in.n == 0 || !(J.leaf > 0.0f)) return false;
+    const float inv = 1.0f / J.leaf;
+    const double invd = (double)inv;
+    const double lo[3] = {J.box.x0, J.box.y0, J.box.z0}, hi[3] = {J.box.x1, J.box.y1, J.box.z1};
+    double dim[3];
+    for (int a = 0; a < 3; ++a) {
+        if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) return false;
+        const double f0 = std::floor(lo[a] * invd) - 2.0, f1 = std::floor(hi[a] * invd) + 2.0;
+        if (std::fabs(f0) >= 8388608.0 || std::fabs(f1) >= 8388608.0 || !(f1 > f0)) return false;
+        J.kb[a] = (float)f0;
+        dim[a] = f1 - f0 + 1.0;
+    }
+    const double nv = dim[0] * dim[1] * dim[2];
+    if (!(nv < 2147483647.0)) return false;
+    int bits = 0;
+    while (bits < 31 && std::ldexp(1.0, bits) < nv) ++bits;
+    const uint32_t nb = J.nb;
+    CloudBufs &B = ctx->fbuf[slot];
+    if (B.skeys.ensure((size_t)nb * kCropTile * 4 + (size_t)nb * kBins * 4 + 256) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    J.fast = 1;
+    J.kinv = inv;
+    J.kdx = (uint32_t)dim[0];
+    J.kdxy = (uint32_t)dim[0] * (uint32_t)dim[1];
+    J.passes = std::max(1, (bits + kDigitBits - 1) / kDigitBits);
+    J.skeys = B.skeys.as<uint32_t>();
+    J.h0 = J.skeys + (size_t)nb * kCropTile;
+    J.ng = (nb + kGroupTiles - 1) / kGroupTiles;
+    return true;
+}
+
 struct Batch {
     JobBatch jb{};
     int k = 0;
@@ -921,7 +1173,8 @@ static int enqueue_chain(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream
     {
         ProfScope ps(ctx, PCP_K_CROP, st);
         if (bt.max_nb) {
-            hipLaunchKernelGGL(k_crop_tile, dim3(bt.max_nb, k), dim3(kCT), 0, st, bt.jb);
+            hipLaunchKernelGGL(k_crop_tile<false>, dim3(bt.max_nb, k), dim3(kCT), 0, st, bt.jb,
+                               res);
             PCP_CHECK_LAUNCH(ctx);
         }
         hipLaunchKernelGGL(k_vox_params, dim3(1, k), dim3(kFT), 0, st, bt.jb, res,
@@ -949,6 +1202,42 @@ static int enqueue_chain(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream
         hipLaunchKernelGGL(k_seg_centroid, dim3(gx, k), dim3(kST), 0, st, bt.jb, res, emit);
         PCP_CHECK_LAUNCH(ctx);
     }
+    return PCP_OK;
+}
+
+// the fast chain of one batch whose clouds all certainly voxelise (make_job set J.fast): keyed
+// crop -> digit-0 group counts -> pass 0 from the crop tiles -> passes 1.. -> voxels -> the
+// centroids emitted as merged records.  No k_vox_params / k_compact_keys and their passes.
+static int enqueue_fast(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream_t st,
+                        float4 *emit) {
+    const unsigned k = (unsigned)bt.k;
+    uint32_t max_ng = 0;
+    for (int i = 0; i < bt.k; ++i) max_ng = std::max(max_ng, bt.jb.j[i].ng);
+    {
+        ProfScope ps(ctx, PCP_K_CROP, st);
+        hipLaunchKernelGGL(k_crop_tile<true>, dim3(std::max(bt.max_nb, 1u), k), dim3(kCT), 0, st,
+                           bt.jb, res);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    ProfScope ps(ctx, PCP_K_VOXEL, st);
+    hipLaunchKernelGGL(k_hist0, dim3(std::max(max_ng, 1u), k), dim3(kST), 0, st, bt.jb);
+    PCP_CHECK_LAUNCH(ctx);
+    const unsigned per_cu = (unsigned)std::max(1, 8192 / kSortTile);
+    const unsigned cap = per_cu * (unsigned)std::max(ctx->num_cus, 1) / k;
+    const unsigned g0 = std::max(1u, std::min<unsigned>(max_ng, cap));
+    hipLaunchKernelGGL(k_radix_scatter0, dim3(g0, k), dim3(kST), 0, st, bt.jb);
+    PCP_CHECK_LAUNCH(ctx);
+    const unsigned gx = std::max(1u, std::min<unsigned>(bt.max_nt, cap));
+    for (int pass = 1; pass < bt.max_passes; ++pass) {
+        hipLaunchKernelGGL(k_radix_hist, dim3(gx, k), dim3(kST), 0, st, bt.jb, pass);
+        PCP_CHECK_LAUNCH(ctx);
+        hipLaunchKernelGGL(k_radix_scatter, dim3(gx, k), dim3(kST), 0, st, bt.jb, pass);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    hipLaunchKernelGGL(k_seg_count, dim3(gx, k), dim3(kST), 0, st, bt.jb);
+    PCP_CHECK_LAUNCH(ctx);
+    hipLaunchKernelGGL(k_seg_centroid, dim3(gx, k), dim3(kST), 0, st, bt.jb, res, emit);
+    PCP_CHECK_LAUNCH(ctx);
     return PCP_OK;
 }
 
@@ -988,7 +1277,12 @@ static bool emit_in_centroid(const std::vector<Batch> &bts) {
 
 static int enqueue_all(pcp_ctx *ctx, const std::vector<Batch> &bts, uint32_t *res,
                        float4 *emit_out, hipStream_t st) {
-    if (emit_out && emit_in_centroid(bts)) return enqueue_chain(ctx, bts[0], res, st, emit_out);
+    if (emit_out && emit_in_centroid(bts)) {
+        bool fast = true;
+        for (int i = 0; i < bts[0].k; ++i) fast = fast && bts[0].jb.j[i].fast;
+        return fast ? enqueue_fast(ctx, bts[0], res, st, emit_out)
+                    : enqueue_chain(ctx, bts[0], res, st, emit_out);
+    }
     for (const Batch &bt : bts) {
         int rc = enqueue_chain(ctx, bt, res, st);
         if (rc) return rc;
@@ -1284,9 +1578,19 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
         if ((rc = make_job(ctx, i, c, b, leaf, false, make_rigid(tf[i], rgb + 3 * i), vp, jobs[i])))
             return rc;
     }
-    const std::vector<Batch> bts = batches_of(jobs);
+    std::vector<Batch> bts = batches_of(jobs);
     // the emit needs the sizes first when the output might not fit (device output only)
     const bool emit_now = !(dev_out && upper > cap);
+    // every cloud certainly voxelises: the fast chain (PCP_FM_FAST=0: the general chain)
+    if (emit_now && ctx->fm_fast && emit_in_centroid(bts)) {
+        std::vector<CloudJob> fj = jobs;
+        bool all = true;
+        for (int i = 0; i < k && all; ++i) all = fast_geometry(ctx, i, fj[i]);
+        if (all) {
+            jobs = fj;
+            bts = batches_of(jobs);
+        }
+    }
     const bool graphable = dev_in && dev_out && emit_now && ctx->use_graphs;
     // the centroid kernel emits the records itself: no kernel reads the sizes back, so they
     // are stored straight into pinned memory (no D2H copy per frame; PCP_FM_HOST_OUT)

@@ -195,7 +195,9 @@ struct ProfSlot {
 
 struct CloudBufs {                 // one cloud's filter-pipeline scratch
     DevBuf xyz, idx, keys[2], sparse, sparse_idx, hist, out;
+    DevBuf skeys;                  // the fast chain: crop tiles' keys + digit-0 rows
     void release() {
+        skeys.release();
         xyz.release();
         idx.release();
         for (int q = 0; q < 2; ++q) keys[q].release();
@@ -260,6 +262,7 @@ struct pcp_ctx {
     int fan_npw = 8;                         // poses per wave of the fan kernel (PCP_FAN_NPW)
     bool fan_host_out = true;                // k_fan_reduce stores into the pinned landing
                                              // block, no D2H copy (PCP_FAN_HOST_OUT)
+    bool fm_fast = true;                     // pcp_filter_merge's fast chain (PCP_FM_FAST)
     bool fm_host_out = true;                 // pcp_filter_merge's result sizes stored by its
                                              // kernels into pinned memory (PCP_FM_HOST_OUT)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)

@@ -226,6 +226,61 @@ def test_filter_merge_sparse_survivors(gpu, oracle, second):
         np.testing.assert_array_equal(out[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
 
 
+@pytest.mark.parametrize("case", ["dense_groups", "far_box", "one_pass", "fine_leaf"])
+def test_filter_merge_fast_chain(gpu, oracle, case, monkeypatch):
+    """The fast chain (box-relative keys formed in the crop, pass 0 straight from the crop
+    tiles in groups of 8) against the oracle and the general chain (PCP_FM_FAST=0):
+    dense_groups -- every point survives, so one pass-0 group holds 8 x 4096 items (8 chunks)
+    and one voxel holds 100 k points; far_box -- a box 2 km from the origin with negative
+    coordinates; one_pass -- a box of < 2^9 voxels (a single radix pass); fine_leaf -- leaf
+    0.013 m (four passes over the key)."""
+    rng = np.random.default_rng({"dense_groups": 1, "far_box": 2, "one_pass": 3,
+                                 "fine_leaf": 4}[case])
+    leaf = 0.05
+    if case == "dense_groups":
+        box = np.array([-1.0, 30.0, -10.0, 10.0, -3.0, 5.0])
+        a = np.zeros((200_000, 4), np.float32)
+        a[:, :3] = rng.uniform([0, -5, -1], [20, 5, 2], (200_000, 3))
+        a[50_000:150_000, :3] = [3.01, 2.02, 0.33]
+        b = synth.lidar_cloud(100_000, seed=8)
+    elif case == "far_box":
+        box = np.array([-2105.0, -2085.0, 1990.0, 2010.0, -1.5, 9.0])
+        a = np.zeros((400_000, 4), np.float32)
+        a[:, :3] = rng.uniform([-2110, 1985, -3], [-2080, 2015, 10], (400_000, 3))
+        b = a[::-1].copy()
+    elif case == "one_pass":
+        box = np.array([1.0, 1.3, -0.2, 0.1, 0.0, 0.2])
+        a = np.zeros((300_000, 4), np.float32)
+        a[:, :3] = rng.uniform([0.8, -0.4, -0.1], [1.5, 0.3, 0.3], (300_000, 3))
+        b = a.copy()
+        b[:, 2] += np.float32(0.05)
+    else:
+        leaf = 0.013
+        box = np.array([0.0, 15.0, -10.0, 10.0, -1.5, 1.5])
+        a = synth.lidar_cloud(600_000, seed=9)
+        b = synth.lidar_cloud(400_000, seed=10, sensor_height=3.5)
+    tfs = _tfs()
+    rgbs = [(255, 0, 0), (0, 0, 255)]
+    parts = []
+    for c, tf, rgb in zip([a, b], tfs, rgbs):
+        k = oracle.crop_box(c, box)
+        v, _, _, pt = oracle.voxel_grid(c[k], leaf)
+        assert not pt
+        parts.append(oracle.transform_rgb(v, *tf, rgb))
+    ref = np.concatenate(parts)
+    out, per = gpu.filter_merge([a, b], [box, box], leaf, tfs, rgbs)
+    assert list(per) == [p.shape[0] for p in parts]
+    np.testing.assert_array_equal(out[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
+    monkeypatch.setenv("PCP_FM_FAST", "0")
+    ctx = _abi.Context(0)
+    try:
+        out2, per2 = ctx.filter_merge([a, b], [box, box], leaf, tfs, rgbs)
+    finally:
+        ctx.close()
+    assert list(per2) == list(per)
+    np.testing.assert_array_equal(out2.view(np.uint32), out.view(np.uint32))
+
+
 def test_filter_merge_device_graph_replay(gpu, oracle):
     """Device-resident inputs: the pipeline is captured into a hipGraph and replayed; every
     replay must equal the eager host-path result and the oracle."""
