@@ -351,6 +351,7 @@ void pcp_destroy(pcp_ctx *ctx) {
         ctx->up_buf[k].release();
     }
     ctx->cand_host.release();
+    ctx->cv_host.release();
     ctx->terrain.release();
     ctx->aux.release();
     ctx->exc_norm.release();

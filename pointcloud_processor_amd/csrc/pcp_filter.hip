@@ -227,15 +227,18 @@ struct CloudJob {
     // the crop forms BOX-relative voxel keys -- (floor(p * inv) - kb) per axis, mixed radix
     // kdx, kdxy -- whose order is PCL's idx order (a constant shift per axis does not change
     // the lexicographic (k, j, i) order), plus each crop tile's digit-0 counts; the first radix
-    // pass then reads the crop tiles in groups of kGroupTiles, no compaction, no parameters
+    // pass then reads the crop tiles in groups of gt, no compaction, no parameters
     int32_t fast;
     float kinv, kb[3];
     uint32_t kdx, kdxy;
     uint32_t *skeys;      // [nb * kCropTile] keys in the crop tiles' slots
     uint32_t *h0;         // [nb][kBins] digit-0 counts per crop tile
-    uint32_t ng;          // groups of kGroupTiles crop tiles (pass 0's sort tiles)
+    uint32_t ng;          // groups of gt crop tiles (pass 0's sort tiles)
+    uint32_t gt;          // crop tiles per group: all groups of a batch in ONE round of blocks
 };
-constexpr int kGroupTiles = 8;   // crop tiles per pass-0 sort tile (~10 % survive the C3 crop)
+constexpr int kMaxGroupTiles = 32;   // crop tiles per pass-0 sort tile, at most
+constexpr int kS0Items = 10;         // pass-0 chunk: 5,120 items (a group of ~10 C3 crop tiles
+constexpr int kS0Tile = kST * kS0Items;   // holds ~4,000 +- 100: one chunk)
 
 // up to kBatch clouds per launch, passed BY VALUE: pointers loaded from kernel arguments are
 // known to be global (global_load, independent waits), which a table in memory would lose
@@ -633,7 +636,7 @@ k_radix_scatter(const JobBatch jobs, int pass) {
 }
 
 // ---- the fast chain's pass 0 -------------------------------------------------------------
-// digit-0 counts of each group of kGroupTiles crop tiles (their rows summed), the pass's
+// digit-0 counts of each group of gt crop tiles (their rows summed), the pass's
 // totals and group sums, and the sort count m (k_vox_params's and k_compact_keys's jobs for the
 // sort, without their passes over the points)
 __global__ void __launch_bounds__(kST) k_hist0(const JobBatch jobs) {
@@ -642,7 +645,7 @@ __global__ void __launch_bounds__(kST) k_hist0(const JobBatch jobs) {
     if (!J.fast || g >= J.ng) return;
     static_assert(kBins == kST, "one digit per thread");
     const uint32_t d = threadIdx.x;
-    const uint32_t c0 = g * kGroupTiles, c1 = min(c0 + (uint32_t)kGroupTiles, J.nb);
+    const uint32_t c0 = g * J.gt, c1 = min(c0 + J.gt, J.nb);
     uint32_t v = 0;
     for (uint32_t c = c0; c < c1; ++c) v += J.h0[(size_t)c * kBins + d];
     J.rhist[(size_t)d * J.ntp + g] = v;
@@ -658,7 +661,7 @@ __global__ void __launch_bounds__(kST) k_hist0(const JobBatch jobs) {
     }
 }
 
-// pass 0 of the fast chain: sort tile g = the kept points of crop tiles [8g, 8g + 8), read in
+// pass 0 of the fast chain: sort tile g = the kept points of crop tiles [g gt, (g + 1) gt), read in
 // place from their sparse slots (input order = tile order, then slot order), in chunks of up to
 // kSortTile items; otherwise k_radix_scatter's stable ranking and run-wise stores, with each
 // digit's running count carried from chunk to chunk
@@ -673,24 +676,28 @@ __global__ void __launch_bounds__(kST) k_radix_scatter0(const JobBatch jobs) {
     uint32_t *kout = J.keys1;
     float4 *pout = J.xyz;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    constexpr int kWaveItems = kSortTile / kSW;
+    constexpr int kWaveItems = kS0Tile / kSW;
     __shared__ uint32_t wh[kSW][kBins];
     __shared__ uint32_t gbase[kBins];   // output position of the group's first item of digit d
     __shared__ uint32_t tx[kBins];
     __shared__ uint32_t lsa[kSW], lsb[kSW];
-    __shared__ uint32_t lk[kSortTile];
-    __shared__ float4 lp[kSortTile];
-    __shared__ uint32_t cpre[kGroupTiles + 1];
+    __shared__ uint32_t lk[kS0Tile];
+    __shared__ float4 lp[kS0Tile];
+    __shared__ uint32_t cpre[kMaxGroupTiles + 1];
     const uint32_t d = threadIdx.x;
     for (uint32_t g = blockIdx.x; g < J.ng; g += gridDim.x) {
-        const uint32_t c0 = g * kGroupTiles;
-        if (threadIdx.x == 0) {
-            uint32_t a = 0;
-            cpre[0] = 0;
-            for (int c = 0; c < kGroupTiles; ++c) {
-                a += (c0 + c < J.nb) ? J.counts[c0 + c] : 0u;
-                cpre[c + 1] = a;
+        const uint32_t c0 = g * J.gt, gt = J.gt;
+        if (threadIdx.x < 64) {   // the group's crop-tile counts, prefix by one wave
+            const uint32_t v = (threadIdx.x < gt && c0 + threadIdx.x < J.nb) ? J.counts[c0 + threadIdx.x]
+                                                                          : 0u;
+            uint32_t incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t u = __shfl_up(incl, o, 64);
+                if ((int)threadIdx.x >= o) incl += u;
             }
+            if (threadIdx.x == 0) cpre[0] = 0;
+            if (threadIdx.x < gt) cpre[threadIdx.x + 1] = incl;
         }
         // earlier groups' count of digit d: whole 16-group sets, then the groups of g's set
         const uint32_t grp = g / kGroup;
@@ -713,31 +720,30 @@ __global__ void __launch_bounds__(kST) k_radix_scatter0(const JobBatch jobs) {
         const uint32_t base_d = block_excl_scan<kST>(totals[d], lsa);
         gbase[d] = base_d + pre;
         __syncthreads();
-        const uint32_t T = cpre[kGroupTiles];
-        for (uint32_t cb = 0; cb < T; cb += kSortTile) {
-            const uint32_t tn = min((uint32_t)kSortTile, T - cb);
+        const uint32_t T = cpre[gt];
+        for (uint32_t cb = 0; cb < T; cb += kS0Tile) {
+            const uint32_t tn = min((uint32_t)kS0Tile, T - cb);
 #pragma unroll
             for (int w = 0; w < kSW; ++w) wh[w][d] = 0;
-            uint32_t k[kSortItems];
-            float4 pv[kSortItems];
+            uint32_t k[kS0Items];
+            float4 pv[kS0Items];
 #pragma unroll
-            for (int j = 0; j < kSortItems; ++j) {
+            for (int j = 0; j < kS0Items; ++j) {
                 const uint32_t q = cb + (uint32_t)(wid * kWaveItems + j * 64 + lane);
                 k[j] = 0u;
                 pv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (q < T) {
-                    int c = 0;
-#pragma unroll
-                    for (int u = 1; u < kGroupTiles; ++u) c += q >= cpre[u] ? 1 : 0;
+                    uint32_t c = 0;
+                    for (uint32_t u = 1; u < gt; ++u) c += q >= cpre[u] ? 1u : 0u;
                     const size_t sp = (size_t)(c0 + c) * kCropTile + (q - cpre[c]);
                     k[j] = J.skeys[sp];
                     pv[j] = J.sparse[sp];
                 }
             }
             __syncthreads();
-            uint32_t r[kSortItems];
+            uint32_t r[kS0Items];
 #pragma unroll
-            for (int j = 0; j < kSortItems; ++j) {
+            for (int j = 0; j < kS0Items; ++j) {
                 const bool act = cb + (uint32_t)(wid * kWaveItems + j * 64 + lane) < T;
                 const uint32_t dj = (k[j] >> shift) & (kBins - 1);
                 uint64_t same = __ballot(act);
@@ -762,7 +768,7 @@ __global__ void __launch_bounds__(kST) k_radix_scatter0(const JobBatch jobs) {
             tx[d] = tx_d;
             __syncthreads();
 #pragma unroll
-            for (int j = 0; j < kSortItems; ++j) {
+            for (int j = 0; j < kS0Items; ++j) {
                 if (cb + (uint32_t)(wid * kWaveItems + j * 64 + lane) < T) {
                     const uint32_t dj = (k[j] >> shift) & (kBins - 1);
                     const uint32_t lpos = tx[dj] + wh[wid][dj] + r[j];
@@ -783,6 +789,7 @@ __global__ void __launch_bounds__(kST) k_radix_scatter0(const JobBatch jobs) {
             gbase[d] += cnt;   // the next chunk's items of digit d follow these
             __syncthreads();
         }
+        __syncthreads();   // cpre / gbase of this group are read above before the next one
     }
 }
 
@@ -1105,7 +1112,7 @@ static int make_job(pcp_ctx *ctx, int slot, const CloudIn &c, const Box &b, floa
 // floor(lo * inv) - 2 per axis (a margin for the float product p * inv of a point just inside
 // the box), dims DX, DY, DZ past floor(hi * inv) + 1; false when the keys or the float
 // integers would not be exact (|values| >= 2^23, or DX * DY * DZ >= 2^31)
-static bool fast_geometry(pcp_ctx *ctx, int slot, CloudJob &J) {
+static bool fast_geometry(pcp_ctx *ctx, int slot, CloudJob &J, int clouds = 1) {
     if (J.in.n == 0 || !(J.leaf > 0.0f)) return false;
     const float inv = 1.0f / J.leaf;
     const double invd = (double)inv;
@@ -1135,7 +1142,12 @@ static bool fast_geometry(pcp_ctx *ctx, int slot, CloudJob &J) {
     J.passes = std::max(1, (bits + kDigitBits - 1) / kDigitBits);
     J.skeys = B.skeys.as<uint32_t>();
     J.h0 = J.skeys + (size_t)nb * kCropTile;
-    J.ng = (nb + kGroupTiles - 1) / kGroupTiles;
+    // groups: every group of every cloud in one round of one-block-per-CU blocks (the pass-0
+    // scatter's LDS admits one per CU), at least 8 crop tiles each
+    const uint32_t cus = (uint32_t)std::max(ctx->num_cus, 1);
+    J.gt = std::min<uint32_t>(kMaxGroupTiles,
+                              std::max<uint32_t>(8, (nb * (uint32_t)clouds + cus - 1) / cus));
+    J.ng = (nb + J.gt - 1) / J.gt;
     return true;
 }
 
@@ -1277,6 +1289,11 @@ static bool emit_in_centroid(const std::vector<Batch> &bts) {
 
 static int enqueue_all(pcp_ctx *ctx, const std::vector<Batch> &bts, uint32_t *res,
                        float4 *emit_out, hipStream_t st) {
+    if (!emit_out && bts.size() == 1) {   // pcp_crop_voxel's fast chain (run_single)
+        bool fast = bts[0].k > 0;
+        for (int i = 0; i < bts[0].k; ++i) fast = fast && bts[0].jb.j[i].fast;
+        if (fast) return enqueue_fast(ctx, bts[0], res, st, nullptr);
+    }
     if (emit_out && emit_in_centroid(bts)) {
         bool fast = true;
         for (int i = 0; i < bts[0].k; ++i) fast = fast && bts[0].jb.j[i].fast;
@@ -1346,8 +1363,11 @@ static int read_results(pcp_ctx *ctx, const uint32_t *res_d, int k, ResultInfo *
 }
 
 // one host cloud through crop [-> voxel] (slot 0); results stay in ctx->fbuf[0]
+// fast_ok: the caller wants the centroids only (pcp_crop_voxel) -- a finite box then takes the
+// fast chain, whose centroid kernel stores the voxels and the result sizes straight into
+// pinned memory (J.out4 is then HOST memory): one round trip for the call
 static int run_single(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b, float leaf,
-                      bool want_idx, CloudJob &J, ResultInfo &ri) {
+                      bool want_idx, CloudJob &J, ResultInfo &ri, bool fast_ok = false) {
     VoxParams *vp;
     uint32_t *res;
     int rc = ensure_misc(ctx, vp, res);
@@ -1358,6 +1378,19 @@ static int run_single(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b, floa
     if ((rc = stage_cloud(ctx, *in, false, ctx->f_in, 0, c))) return rc;
     std::vector<CloudJob> jobs(1);
     if ((rc = make_job(ctx, 0, c, b, leaf, want_idx, Rigid{}, vp, jobs[0]))) return rc;
+    if (fast_ok && !want_idx && ctx->fm_fast && fast_geometry(ctx, 0, jobs[0])) {
+        CloudJob &F = jobs[0];
+        const uint64_t ncap = c.n ? c.n : 1;
+        const size_t res_b = align256(3 * kMaxClouds * sizeof(uint32_t));
+        PCP_HIP(ctx, ctx->cv_host.ensure(res_b + (ncap + 1) * sizeof(float4) + (2 * ncap + 8) * 4 + 256));
+        uint32_t *res_h = ctx->cv_host.as<uint32_t>();
+        F.out4 = reinterpret_cast<float4 *>(ctx->cv_host.as<char>() + res_b);
+        F.vidx = reinterpret_cast<uint32_t *>(F.out4 + ncap + 1);
+        F.vcnt = F.vidx + ncap + 1;
+        if ((rc = enqueue_all(ctx, batches_of(jobs), res_h, nullptr, ctx->stream))) return rc;
+        J = F;
+        return read_results(ctx, res_h, 1, &ri, true);
+    }
     if ((rc = enqueue_all(ctx, batches_of(jobs), res, nullptr, ctx->stream))) return rc;
     J = jobs[0];
     return read_results(ctx, res, 1, &ri);
@@ -1405,7 +1438,8 @@ static int crop_voxel_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b,
                            int32_t *passthrough) {
     CloudJob J;
     ResultInfo ri;
-    int rc = run_single(ctx, in, b, leaf, false, J, ri);
+    const bool fast_ok = voxel_idx == nullptr && voxel_count == nullptr;
+    int rc = run_single(ctx, in, b, leaf, false, J, ri, fast_ok);
     if (rc) return rc;
     const bool vox = leaf > 0.0f && !ri.overflow;
     if (passthrough) *passthrough = (leaf > 0.0f && ri.overflow) ? 1 : 0;
@@ -1415,6 +1449,11 @@ static int crop_voxel_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b,
         prof_resolve(ctx);
         return set_err(ctx, PCP_E_CAPACITY, "voxel output needs %u points, cap %llu", ri.n,
                        (unsigned long long)cap);
+    }
+    if (J.fast) {   // the voxels already sit in pinned memory (synchronised by read_results)
+        if (ri.n) std::memcpy(out_xyz16, J.out4, (size_t)ri.n * 16);
+        prof_resolve(ctx);
+        return PCP_OK;
     }
     if (ri.n) {
         const void *src = vox ? (const void *)J.out4 : (const void *)J.xyz;
@@ -1585,7 +1624,7 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
     if (emit_now && ctx->fm_fast && emit_in_centroid(bts)) {
         std::vector<CloudJob> fj = jobs;
         bool all = true;
-        for (int i = 0; i < k && all; ++i) all = fast_geometry(ctx, i, fj[i]);
+        for (int i = 0; i < k && all; ++i) all = fast_geometry(ctx, i, fj[i], k);
         if (all) {
             jobs = fj;
             bts = batches_of(jobs);

@@ -93,7 +93,11 @@ __device__ __forceinline__ float ld_f32(const unsigned char *base, uint32_t off)
 __global__ void __launch_bounds__(kThreads)
 k_extract(const unsigned char *__restrict__ raw, uint64_t n, uint32_t step, uint32_t ox,
           uint32_t oy, uint32_t oz, float4 *__restrict__ xyz, float *__restrict__ part,
-          uint32_t *__restrict__ part_n) {
+          uint32_t *__restrict__ part_n, uint32_t *__restrict__ zero_p, uint64_t zero_n) {
+    // the cell counters of the build, zeroed here instead of by a separate fill launch
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < zero_n;
+         i += (uint64_t)gridDim.x * kThreads)
+        zero_p[i] = 0;
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     uint32_t cnt = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n;
@@ -450,18 +454,21 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     PCP_HIP(ctx, ctx->stats_d.ensure(64));
     float *part = ctx->scratch[1].as<float>();
     uint32_t *part_n = reinterpret_cast<uint32_t *>(part + nb * 6);
-    hipLaunchKernelGGL(k_extract, dim3(nb), dim3(kThreads), 0, st, ctx->stage.as<unsigned char>(),
-                       n, v.point_step, v.off_x, v.off_y, v.off_z, ctx->scratch[0].as<float4>(),
-                       part, part_n);
-    PCP_CHECK_LAUNCH(ctx);
     float bb_h[10];
     uint32_t nfin;
-    if (n <= kHostBboxMax) {
-        // a message-sized cloud: the grid geometry from the host's copy of the same bytes (the
-        // same float min / max over the finite points, order-free) while the device extracts --
-        // no round trip through the stream
+    // a message-sized cloud: the grid geometry from the host's copy of the same bytes (the
+    // same float min / max over the finite points, order-free) -- no round trip through the
+    // stream; the extraction is launched below, once the cell count is known (it also zeroes
+    // the cell counters)
+    const bool host_bb = n <= kHostBboxMax;
+    if (host_bb) {
         host_bbox(v, bb_h, nfin);
     } else {
+        hipLaunchKernelGGL(k_extract, dim3(nb), dim3(kThreads), 0, st,
+                           ctx->stage.as<unsigned char>(), n, v.point_step, v.off_x, v.off_y,
+                           v.off_z, ctx->scratch[0].as<float4>(), part, part_n, nullptr,
+                           (uint64_t)0);
+        PCP_CHECK_LAUNCH(ctx);
         float *bb_d = ctx->stats_d.as<float>();
         hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(kThreads), 0, st, part, part_n, nb, bb_d,
                            reinterpret_cast<uint32_t *>(bb_d + 8));
@@ -515,7 +522,15 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     // 4. count per cell
     PCP_HIP(ctx, ctx->scratch[2].ensure(n * sizeof(uint32_t)));
     PCP_HIP(ctx, ctx->scratch[3].ensure((ncell + 1) * sizeof(uint32_t)));
-    PCP_HIP(ctx, hipMemsetAsync(ctx->scratch[3].p, 0, (ncell + 1) * sizeof(uint32_t), st));
+    if (host_bb) {
+        hipLaunchKernelGGL(k_extract, dim3(nb), dim3(kThreads), 0, st,
+                           ctx->stage.as<unsigned char>(), n, v.point_step, v.off_x, v.off_y,
+                           v.off_z, ctx->scratch[0].as<float4>(), part, part_n,
+                           ctx->scratch[3].as<uint32_t>(), ncell + 1);
+        PCP_CHECK_LAUNCH(ctx);
+    } else {
+        PCP_HIP(ctx, hipMemsetAsync(ctx->scratch[3].p, 0, (ncell + 1) * sizeof(uint32_t), st));
+    }
     const unsigned gridn = (unsigned)((n + kThreads - 1) / kThreads);
     hipLaunchKernelGGL(k_cell_count, dim3(gridn), dim3(kThreads), 0, st,
                        ctx->scratch[0].as<const float4>(), n, m, ctx->scratch[2].as<uint32_t>(),

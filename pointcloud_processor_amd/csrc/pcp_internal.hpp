@@ -253,6 +253,8 @@ struct pcp_ctx {
     bool up_used[kUpRing] = {};
     int up_next = 0;
     pcp::PinnedBuf cand_host;                // generate_candidates: poses + count in one readback
+    pcp::PinnedBuf cv_host;                  // pcp_crop_voxel's fast chain: centroids + result
+                                             // sizes stored by the kernels (one round trip)
     int32_t fan_naz = -1, fan_nel = -1;      // cached fan direction tables
     double fan_elmin = 0.0, fan_elmax = 0.0;
     double steps_end = -1e300;               // cached step table
