@@ -1070,48 +1070,61 @@ def test_fine_copy_dense_window(oracle, monkeypatch):
 
 
 # ---------------------------------------------------------------------------------- multi-GPU
-def test_fan_device_keys_match_reduce_fan(gpu, loaded, scene):
+_DEVICE_KEYS_CHECK = r"""
+import sys
+import numpy as np
+import torch
+torch.cuda.init()                      # torch's HIP runtime first, as in bench.py
+sys.path.insert(0, sys.argv[1])
+import bench
+from pointcloud_processor_amd import _abi, synth
+from pointcloud_processor_amd import dist as pd
+scene = synth.terrain_scene()
+gpu = _abi.Context(0)
+gpu.set_terrain(scene.terrain, point_step=32)
+poses, _ = bench._poses_for(gpu, bench._grid_bbox(scene.area), scene.zx120_pose5, 96)
+fan = _abi.fan_params(n_az=256, n_el=64)
+b1, u1, _, _ = gpu.raycast_fan(poses, fan)
+P, world = poses.shape[0], 4
+ref_keys, ref_best = pd.reduce_fan(b1, 0, P, P)
+dev = torch.device("cuda", 0)
+stream = torch.cuda.current_stream(dev).cuda_stream
+units = torch.zeros(P, dtype=torch.int64, device=dev)
+red = None
+for r in range(world):
+    lo, hi = pd.shard(P, world, r)
+    k = torch.empty(P, dtype=torch.int64, device=dev)
+    gpu.raycast_fan_keys(np.ascontiguousarray(poses[lo:hi]), fan, lo, P, k.data_ptr(),
+                         units.data_ptr() + 8 * lo, stream)
+    red = k if red is None else torch.minimum(red, k)
+kh = red.cpu().numpy()
+assert np.array_equal(kh >> 32, ref_keys)
+assert np.array_equal(kh & 0xFFFFFFFF, np.arange(P))
+assert int(kh.min()) & 0xFFFFFFFF == ref_best
+assert np.array_equal(units.cpu().numpy().astype(np.uint64), u1)
+k = torch.zeros(P, dtype=torch.int64, device=dev)
+gpu.raycast_fan_keys(poses[:0].copy(), fan, P, P, k.data_ptr(), None, None)
+assert bool((k == np.iinfo(np.int64).max).all())
+print("device keys ok", P, ref_best)
+"""
+
+
+def test_fan_device_keys_match_reduce_fan():
     """bench.py --gpus N over RCCL: pcp_raycast_fan_keys writes each rank's keys into a torch
     device vector (no host copy), the collective is an int64 MIN.  Four ranks' shards on one
     device, their vectors combined by torch.minimum (the all-reduce's arithmetic): blocked
     counts, units and the argmin bit-identical to the host path (raycast_fan ->
-    dist.reduce_fan)."""
+    dist.reduce_fan).  In its own process, torch's HIP runtime initialised first as in
+    bench.py (torch bundles its own ROCm runtime beside the one libpcp links)."""
+    import subprocess
     import sys
     from pathlib import Path
 
-    import torch
-
-    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-    import bench
-    from pointcloud_processor_amd import dist as pd
-
-    poses, _ = bench._poses_for(gpu, bench._grid_bbox(scene.area), scene.zx120_pose5, 96)
-    fan = _abi.fan_params(n_az=256, n_el=64)
-    b1, u1, _, _ = gpu.raycast_fan(poses, fan)
-    P, world = poses.shape[0], 4
-    ref_keys, ref_best = pd.reduce_fan(b1, 0, P, P)
-    dev = torch.device("cuda", 0)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    vecs = []
-    units = torch.zeros(P, dtype=torch.int64, device=dev)
-    for r in range(world):
-        lo, hi = pd.shard(P, world, r)
-        k = torch.empty(P, dtype=torch.int64, device=dev)
-        sh = np.ascontiguousarray(poses[lo:hi])
-        gpu.raycast_fan_keys(sh, fan, lo, P, k.data_ptr(), units.data_ptr() + 8 * lo, stream)
-        vecs.append(k)
-    red = vecs[0]
-    for k in vecs[1:]:
-        red = torch.minimum(red, k)
-    kh = red.cpu().numpy()
-    np.testing.assert_array_equal(kh >> 32, ref_keys)
-    np.testing.assert_array_equal(kh & 0xFFFFFFFF, np.arange(P))
-    assert int(kh.min()) & 0xFFFFFFFF == ref_best
-    np.testing.assert_array_equal(units.cpu().numpy().astype(np.uint64), u1)
-    # one rank holding no poses writes only the identity
-    k = torch.zeros(P, dtype=torch.int64, device=dev)
-    gpu.raycast_fan_keys(poses[:0], fan, P, P, k.data_ptr(), None, None)
-    assert bool((k == np.iinfo(np.int64).max).all())
+    root = str(Path(__file__).resolve().parents[1])
+    r = subprocess.run([sys.executable, "-c", _DEVICE_KEYS_CHECK, root], capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "device keys ok" in r.stdout
 
 
 def _need_devices(devices):

@@ -5,7 +5,10 @@ passes; FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half 
 wide coalesced streaming reads (doubled below, flagged as such: the fan kernel's gathers are
 an uncalibrated access width, so both the raw and the corrected read bytes are recorded).
 
-    python tools/pmc_traffic.py KEY KERNEL_SUBSTR FETCH_DIR WRITE_DIR [per_dispatch|steps=N]
+    python tools/pmc_traffic.py KEY KERNEL_SUBSTR FETCH_DIR WRITE_DIR [per_dispatch|steps=N] [OUT]
+
+OUT (default profiles/pmc_traffic.json): the JSON file the entry is merged into (round 3 writes
+profiles/r03_pmc_traffic.json, which bench.py reads first).
 
 per_dispatch (default): average over the matching dispatches (one kernel per launch);
 steps=N: sum of every matching dispatch / N (a multi-kernel pipeline run N times).
@@ -32,6 +35,7 @@ def per_dispatch(d: Path, counter: str, substr: str):
 def main():
     key, substr, fdir, wdir = sys.argv[1:5]
     mode = sys.argv[5] if len(sys.argv) > 5 else "per_dispatch"
+    out_name = sys.argv[6] if len(sys.argv) > 6 else "pmc_traffic.json"
     fetch = per_dispatch(Path(fdir), "FETCH_SIZE", substr)
     write = per_dispatch(Path(wdir), "WRITE_SIZE", substr)
     if not fetch or not write:
@@ -41,7 +45,7 @@ def main():
         fk, wk = sum(fetch) / n, sum(write) / n
     else:
         fk, wk = sum(fetch) / len(fetch), sum(write) / len(write)
-    out_f = ROOT / "profiles" / "pmc_traffic.json"
+    out_f = ROOT / "profiles" / out_name
     data = json.loads(out_f.read_text()) if out_f.exists() else {}
     data[key] = {
         "kernel": substr,
