@@ -10,6 +10,13 @@
 namespace pcp {
 
 // ---- PointCloud2 helpers -------------------------------------------------------------------
+// a landing buffer of at least n elements: grown when short, otherwise reused as is
+template <class T>
+static T *landing(std::vector<T> &v, size_t n) {
+    if (v.size() < n) v.resize(n);
+    return v.data();
+}
+
 static PointCloud2 make_cloud(const void *rec, size_t n, uint32_t step,
                               std::vector<PointField> fields, const std::string &frame) {
     PointCloud2 m;
@@ -19,8 +26,8 @@ static PointCloud2 make_cloud(const void *rec, size_t n, uint32_t step,
     m.fields = std::move(fields);
     m.point_step = step;
     m.row_step = step * m.width;
-    m.data.resize(n * step);
-    if (n) std::memcpy(m.data.data(), rec, n * step);
+    const uint8_t *b = static_cast<const uint8_t *>(rec);
+    if (n) m.data.assign(b, b + n * step);   // one pass: no zero-fill before the copy
     m.is_dense = true;
     return m;
 }
@@ -102,15 +109,15 @@ PointCloud2 SimplifiedScanMatcher::processCloudSimple(const PointCloud2 &in,
     PointCloud2 out = make_xyz_cloud(nullptr, 0, in.frame_id);
     out.stamp = in.stamp;   // output_msg->header = input_msg->header (:79)
     if (!cloud_view(in, v, &err_)) return out;
-    std::vector<float> buf(4 * (v.n ? v.n : 1));
+    float *buf = landing(out_, 4 * (v.n ? v.n : 1));
     uint64_t n_out = 0, n_crop = 0;
-    if (pcp_crop_voxel(dev_.ctx(), &v, box, (float)p_.voxel_leaf_size, buf.data(), v.n, &n_out,
+    if (pcp_crop_voxel(dev_.ctx(), &v, box, (float)p_.voxel_leaf_size, buf, v.n, &n_out,
                        &n_crop) != PCP_OK) {
         err_ = dev_.error();
         return out;
     }
     last_cropped_ = n_crop;
-    out = make_xyz_cloud(buf.data(), n_out, in.frame_id);
+    out = make_xyz_cloud(buf, n_out, in.frame_id);
     out.stamp = in.stamp;
     return out;
 }
@@ -144,16 +151,16 @@ GnssGicpMatcher::Output GnssGicpMatcher::processPointClouds(bool origin_set,
     }
     uint64_t total = 0;
     for (int i = 0; i < k; ++i) total += v[i].n;
-    std::vector<uint8_t> buf(32 * (total ? total : 1));
+    uint8_t *buf = landing(out_, 32 * (total ? total : 1));
     uint64_t n = 0;
-    if (k && pcp_transform_concat(dev_.ctx(), k, v, tf, rgb, buf.data(), total, &n) != PCP_OK) {
+    if (k && pcp_transform_concat(dev_.ctx(), k, v, tf, rgb, buf, total, &n) != PCP_OK) {
         err_ = dev_.error();
         return o;
     }
-    o.merged = make_xyzrgb_cloud(buf.data(), n, "map");
+    o.merged = make_xyzrgb_cloud(buf, n, "map");
     uint64_t base = 0;
     for (int i = 0; i < k; ++i) {
-        PointCloud2 part = make_xyzrgb_cloud(buf.data() + 32 * base, v[i].n, "map");
+        PointCloud2 part = make_xyzrgb_cloud(buf + 32 * base, v[i].n, "map");
         (which[i] == 0 ? o.robot_colored : o.backhoe_colored) = std::move(part);
         base += v[i].n;
     }
@@ -372,16 +379,15 @@ ExcavationTerrainGenerator::Output ExcavationTerrainGenerator::matchedCloudCallb
         o.excavated_terrain = msg;
         return o;
     }
-    std::vector<uint8_t> terr(nt * 32), area(na * 32);
-    if (pcp_excavate(dev_.ctx(), &v, &p_, &tf, terr.data(), nt, &nt, area.data(), na, &na, pose) !=
-        PCP_OK) {
+    uint8_t *terr = landing(terr_, nt * 32 + 32), *area = landing(area_, na * 32 + 32);
+    if (pcp_excavate(dev_.ctx(), &v, &p_, &tf, terr, nt, &nt, area, na, &na, pose) != PCP_OK) {
         err_ = dev_.error();
         o.excavated_terrain = msg;
         return o;
     }
-    o.excavated_terrain = make_xyzrgb_cloud(terr.data(), nt, "map");   // header kept, frame map
+    o.excavated_terrain = make_xyzrgb_cloud(terr, nt, "map");   // header kept, frame map
     o.excavated_terrain.stamp = msg.stamp;
-    o.excavation_area = make_xyzrgb_cloud(area.data(), na, "map");
+    o.excavation_area = make_xyzrgb_cloud(area, na, "map");
     o.excavation_area.stamp = msg.stamp;
     o.area_published = true;
     o.center[0] = pose[0];

@@ -111,6 +111,7 @@ class SimplifiedScanMatcher {
     Device &dev_;
     Params p_;
     size_t last_cropped_ = 0;
+    std::vector<float> out_;   // result landing, reused (grown, never re-zeroed per message)
     std::string err_;
 };
 
@@ -132,6 +133,7 @@ class GnssGicpMatcher {
     Device &dev_;
     PointCloud2 robot_, backhoe_;
     bool have_robot_ = false, have_backhoe_ = false;
+    std::vector<uint8_t> out_;   // result landing, reused
     std::string err_;
 };
 
@@ -161,6 +163,9 @@ class ExcavationTerrainGenerator {
    private:
     Device &dev_;
     Params p_;
+    // result landings sized by pcp_excavate_bounds (MBs: the generated-point capacities), reused
+    // so no message pays for zero-filling them
+    std::vector<uint8_t> terr_, area_;
     std::string err_;
 };
 

@@ -226,6 +226,11 @@ static int cmd_replay(Device &dev, char **a) {
     const Transform zx_base{{0.0, 0.0, 0.0}, {0, 0, 0, 1}};
     std::vector<double> lat;
     std::vector<double> lat_frame;   // in frame order (the sorted copy gives the percentiles)
+    // per-callback wall time (ms): filter x2, merger, carve, area, terrain, zx120 cloud, tick
+    constexpr int kStages = 7;
+    static const char *kStageName[kStages] = {"filter", "merge", "carve", "area",
+                                              "terrain", "zx120", "tick"};
+    std::vector<double> stage[kStages];
     size_t merged_n = 0, best = 0, cells_n = cn;
     uint64_t realloc_after_warmup = 0, ra0 = 0;
     std::string dumped;
@@ -235,12 +240,20 @@ static int cmd_replay(Device &dev, char **a) {
         PointCloud2 rm = make_xyz_cloud(rs.data(), npts, "four_wheel_robot/velodyne_link");
         PointCloud2 zm = make_xyz_cloud(zs.data(), npts, "zx120/velodyne_link");
         const auto t0 = std::chrono::steady_clock::now();
+        double st[kStages] = {};
+        auto lap = [&st, last = t0](int k) mutable {
+            const auto now = std::chrono::steady_clock::now();
+            st[k] = std::chrono::duration<double, std::milli>(now - last).count();
+            last = now;
+        };
         // pointcloud_filter: both sensors; pointcloud_merger: 10 Hz tick; virtual_lidar: zx120
         // filtered cloud + the pose search
         PointCloud2 rf = filt.robotCloudCallback(rm), zf = filt.backhoeCloudCallback(zm);
+        lap(0);
         merger.robotCloudCallback(rf);
         merger.backhoeCloudCallback(zf);
         auto o = merger.processPointClouds(true, &robot_tf, &zx_tf);
+        lap(1);
         ExcavationTerrainGenerator::Output e;
         if (chain) {
             e = gen.matchedCloudCallback(o.merged, &zx_base);
@@ -248,13 +261,20 @@ static int cmd_replay(Device &dev, char **a) {
                 std::fprintf(stderr, "replay: carve failed: %s\n", gen.lastError().c_str());
                 return 1;
             }
+            lap(2);
             vl.excavationAreaCallback(e.excavation_area);
+            lap(3);
             vl.terrainCallback(e.excavated_terrain);
+            lap(4);
             cells_n = vl.lastCells();
         }
         vl.zx120PointsCallback(zf);
+        lap(5);
         auto r = vl.runOptimization(&zx_base);
+        lap(6);
         const auto t1 = std::chrono::steady_clock::now();
+        if (f >= 2)
+            for (int k = 0; k < kStages; ++k) stage[k].push_back(st[k]);
         if (!r.ran) {
             std::fprintf(stderr, "replay: pose search did not run: %s\n", vl.lastError().c_str());
             return 1;
@@ -308,12 +328,22 @@ static int cmd_replay(Device &dev, char **a) {
     }
     std::sort(lat.begin(), lat.end());
     auto q = [&lat](double p) { return lat[std::min(lat.size() - 1, (size_t)(p * lat.size()))]; };
+    std::string stage_s;
+    for (int k = 0; k < kStages; ++k) {
+        auto &v = stage[k];
+        std::sort(v.begin(), v.end());
+        char b[64];
+        std::snprintf(b, sizeof(b), "%s\"%s\": %.4f", k ? ", " : "", kStageName[k],
+                      v.empty() ? 0.0 : v[v.size() / 2]);
+        stage_s += b;
+    }
     std::printf("{\"frames\": %zu, \"points_per_scan\": %zu, \"chain\": %d, \"p50_ms\": %.4f, "
                 "\"p99_ms\": %.4f, \"max_ms\": %.4f, \"merged_points\": %zu, \"cells\": %zu, "
                 "\"best_idx\": %zu, \"reallocs_after_warmup\": %llu, \"dumped\": [%s], "
-                "\"lat_ms\": [%s]}\n",
+                "\"stage_p50_ms\": {%s}, \"lat_ms\": [%s]}\n",
                 lat.size(), npts, chain ? 1 : 0, q(0.5), q(0.99), lat.back(), merged_n, cells_n,
-                best, (unsigned long long)realloc_after_warmup, dumped.c_str(), lat_s.c_str());
+                best, (unsigned long long)realloc_after_warmup, dumped.c_str(), stage_s.c_str(),
+                lat_s.c_str());
     return 0;
 }
 

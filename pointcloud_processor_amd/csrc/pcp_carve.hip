@@ -264,8 +264,16 @@ struct GenPoint {    // a generated point: position, height query, z recipe (ref
 // (the kept count, the generated surface goes after the kept points) or 0
 __global__ void __launch_bounds__(kCT)
 k_gen_emit(const GenPoint *__restrict__ gp, uint32_t ng, const double *__restrict__ h,
-           double depth, const uint32_t *__restrict__ base_d, float4 *__restrict__ out) {
+           double depth, const uint32_t *__restrict__ base_d, float4 *__restrict__ out,
+           const uint32_t *__restrict__ ctr, uint32_t *__restrict__ sm_host) {
     const uint32_t k = blockIdx.x * kCT + threadIdx.x;
+    // the counters and the centre height into the pinned landing (in place of two small DMAs);
+    // every kernel that writes them ran before this one
+    if (sm_host && k == 0) {
+        for (int w = 0; w < 4; ++w) sm_host[w] = ctr[w];
+        const double h0 = h[0];
+        __builtin_memcpy(sm_host + 4, &h0, sizeof(double));
+    }
     if (k >= ng) return;
     const GenPoint g = gp[k];
     const double z = g.kind == 0 ? h[g.q] - g.v : (h[g.q] - depth) + g.v;
@@ -426,59 +434,77 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     const int n_x = (int)((mxx - mnx) / dens) + 1;
     const int n_y = (int)((mxy - mny) / dens) + 1;
     const double cyaw = std::cos(yaw), syaw = std::sin(yaw);
-    std::vector<double2> qv;          // 0: the centre; then the lattice bottoms; then walls
-    qv.push_back(make_double2(cx, cy));
-    std::vector<GenPoint> surf, area;
-    const float rgb_bottom = pack_rgb(0, 139, 0), rgb_slope = pack_rgb(144, 238, 144);
-    const float rgb_abot = pack_rgb(255, 255, 0), rgb_aslope = pack_rgb(200, 200, 0);
-    const int n_slope = (int)(slope_offset / dens) + 1;
-    const int n_depth = (int)(p->depth / dens);
-    auto wall_offset = [&](double xl, double yl, double off, double &ofx, double &ofy) {
-        ofx = 0.0;
-        ofy = 0.0;
-        if (!inside_any(xl + dens, yl, box, nbox)) ofx = off;
-        else if (!inside_any(xl - dens, yl, box, nbox)) ofx = -off;
-        if (!inside_any(xl, yl + dens, box, nbox)) ofy = off;
-        else if (!inside_any(xl, yl - dens, box, nbox)) ofy = -off;
+    const uint64_t n = in->n;
+    // the generated lattice is a function of these alone (the excavation pose and the
+    // parameters): an unchanged key reuses the device copy of the last call
+    const double key[16] = {p->depth, p->slope_angle_deg, p->offset_x, p->offset_y, dens,
+                            (double)p->l_shape_enabled, p->arm1_length, p->arm1_width,
+                            p->arm2_length, p->arm2_width, p->width, p->length, cx, cy, yaw, 0.0};
+    auto gen_bytes = [n](uint64_t g, uint64_t ns, uint64_t na, size_t &gpb, size_t &qxb) {
+        gpb = ((ns + na) * sizeof(GenPoint) + 255) & ~(size_t)255;
+        qxb = ((g + n) * sizeof(double2) + 255) & ~(size_t)255;
+        return gpb + qxb + na * 32 + 256;
     };
-    for (int i = 0; i <= n_x; ++i)   // generateExcavatedSurface bottom (:518-535) + area (:367-)
-        for (int j = 0; j <= n_y; ++j) {
-            const double xl = mnx + i * dens, yl = mny + j * dens;
-            if (!inside_any(xl, yl, box, nbox)) continue;
-            const double xg = cx + xl * cyaw - yl * syaw;
-            const double yg = cy + xl * syaw + yl * cyaw;
-            const int q = (int)qv.size();
-            qv.push_back(make_double2(xg, yg));
-            surf.push_back(GenPoint{xg, yg, q, 0, p->depth, rgb_bottom});   // h - depth
-            area.push_back(GenPoint{xg, yg, q, 0, p->depth, rgb_abot});
-            if (!outer_edge(xl, yl, box, nbox, dens)) continue;
-            for (int k = 1; k < n_depth; ++k) {   // area walls use the lattice point's height
-                const double z_ratio = (double)k / n_depth;
-                double ofx, ofy;
-                wall_offset(xl, yl, slope_offset * z_ratio, ofx, ofy);
-                const double xs2 = xl + ofx, ys2 = yl + ofy;
-                area.push_back(GenPoint{cx + xs2 * cyaw - ys2 * syaw, cy + xs2 * syaw + ys2 * cyaw,
-                                        q, 1, k * dens, rgb_aslope});   // (h - depth) + k*dens
-            }
-        }
-    for (int i = 0; i <= n_x; ++i)   // generateExcavatedSurface walls (:538-583)
-        for (int j = 0; j <= n_y; ++j) {
-            const double xl = mnx + i * dens, yl = mny + j * dens;
-            if (!outer_edge(xl, yl, box, nbox, dens)) continue;
-            for (int k = 0; k <= n_slope; ++k) {
-                const double z_ratio = (double)k / n_slope;
-                double ofx, ofy;
-                wall_offset(xl, yl, slope_offset * z_ratio, ofx, ofy);
-                const double xs2 = xl + ofx, ys2 = yl + ofy;
-                const double xg = cx + xs2 * cyaw - ys2 * syaw;
-                const double yg = cy + xs2 * syaw + ys2 * cyaw;
+    size_t gpb = 0, qxb = 0;
+    bool gen_hit = ctx->carve_gen_ok && std::memcmp(key, ctx->carve_key, sizeof(key)) == 0 &&
+                   ctx->carve_gen.cap >= gen_bytes(ctx->carve_G, ctx->carve_nsurf,
+                                                   ctx->carve_narea, gpb, qxb);
+    std::vector<double2> qv;          // 0: the centre; then the lattice bottoms; then walls
+    std::vector<GenPoint> surf, area;
+    if (!gen_hit) {
+        qv.push_back(make_double2(cx, cy));
+        const float rgb_bottom = pack_rgb(0, 139, 0), rgb_slope = pack_rgb(144, 238, 144);
+        const float rgb_abot = pack_rgb(255, 255, 0), rgb_aslope = pack_rgb(200, 200, 0);
+        const int n_slope = (int)(slope_offset / dens) + 1;
+        const int n_depth = (int)(p->depth / dens);
+        auto wall_offset = [&](double xl, double yl, double off, double &ofx, double &ofy) {
+            ofx = 0.0;
+            ofy = 0.0;
+            if (!inside_any(xl + dens, yl, box, nbox)) ofx = off;
+            else if (!inside_any(xl - dens, yl, box, nbox)) ofx = -off;
+            if (!inside_any(xl, yl + dens, box, nbox)) ofy = off;
+            else if (!inside_any(xl, yl - dens, box, nbox)) ofy = -off;
+        };
+        for (int i = 0; i <= n_x; ++i)   // generateExcavatedSurface bottom (:518-535) + area (:367-)
+            for (int j = 0; j <= n_y; ++j) {
+                const double xl = mnx + i * dens, yl = mny + j * dens;
+                if (!inside_any(xl, yl, box, nbox)) continue;
+                const double xg = cx + xl * cyaw - yl * syaw;
+                const double yg = cy + xl * syaw + yl * cyaw;
                 const int q = (int)qv.size();
                 qv.push_back(make_double2(xg, yg));
-                surf.push_back(GenPoint{xg, yg, q, 0, p->depth * (1.0 - z_ratio), rgb_slope});
+                surf.push_back(GenPoint{xg, yg, q, 0, p->depth, rgb_bottom});   // h - depth
+                area.push_back(GenPoint{xg, yg, q, 0, p->depth, rgb_abot});
+                if (!outer_edge(xl, yl, box, nbox, dens)) continue;
+                for (int k = 1; k < n_depth; ++k) {   // area walls use the lattice point's height
+                    const double z_ratio = (double)k / n_depth;
+                    double ofx, ofy;
+                    wall_offset(xl, yl, slope_offset * z_ratio, ofx, ofy);
+                    const double xs2 = xl + ofx, ys2 = yl + ofy;
+                    area.push_back(GenPoint{cx + xs2 * cyaw - ys2 * syaw, cy + xs2 * syaw + ys2 * cyaw,
+                                            q, 1, k * dens, rgb_aslope});   // (h - depth) + k*dens
+                }
             }
-        }
-    const uint32_t G = (uint32_t)qv.size();
-    const uint64_t n = in->n;
+        for (int i = 0; i <= n_x; ++i)   // generateExcavatedSurface walls (:538-583)
+            for (int j = 0; j <= n_y; ++j) {
+                const double xl = mnx + i * dens, yl = mny + j * dens;
+                if (!outer_edge(xl, yl, box, nbox, dens)) continue;
+                for (int k = 0; k <= n_slope; ++k) {
+                    const double z_ratio = (double)k / n_slope;
+                    double ofx, ofy;
+                    wall_offset(xl, yl, slope_offset * z_ratio, ofx, ofy);
+                    const double xs2 = xl + ofx, ys2 = yl + ofy;
+                    const double xg = cx + xs2 * cyaw - ys2 * syaw;
+                    const double yg = cy + xs2 * syaw + ys2 * cyaw;
+                    const int q = (int)qv.size();
+                    qv.push_back(make_double2(xg, yg));
+                    surf.push_back(GenPoint{xg, yg, q, 0, p->depth * (1.0 - z_ratio), rgb_slope});
+                }
+            }
+    }
+    const uint32_t G = gen_hit ? ctx->carve_G : (uint32_t)qv.size();
+    const uint64_t nsurf = gen_hit ? ctx->carve_nsurf : surf.size();
+    const uint64_t narea = gen_hit ? ctx->carve_narea : area.size();
     // ---- index of the input (radius = terrain_search_radius); the raw records stay staged
     // in ctx->stage (build_index's H2D copy) for the per-point passes below
     if ((rc = build_index(ctx, ctx->carve, *in, p->terrain_search_radius, false, false))) return rc;
@@ -500,11 +526,11 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     a.box[0] = box[0];
     a.box[1] = box[1];
     a.nbox = nbox;
-    // device scratch: queries (G + n), candidate indices (n), heights, fallback list, removed
-    // flags, tile counts, kept records
+    // device scratch: candidate indices (n), heights, fallback list, removed flags, tile
+    // counts, kept records (the queries live in carve_gen)
     const uint64_t nq_max = G + n;
     const uint32_t nb = (uint32_t)((n + kKeepTile - 1) / kKeepTile);
-    const size_t qb = (nq_max * sizeof(double2) + 255) & ~(size_t)255;
+    const size_t qb = 0;
     const size_t ib = (n * 4 + 256) & ~(size_t)255;
     const size_t hb = (nq_max * 8 + 255) & ~(size_t)255;
     const size_t fb = (nq_max * 4 + 256) & ~(size_t)255;
@@ -512,17 +538,43 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     const size_t cb = ((size_t)(nb + 1) * 4 + 256) & ~(size_t)255;
     PCP_HIP(ctx, ctx->carve_buf.ensure(qb + ib + hb + fb + rb + cb + 256));
     char *base = ctx->carve_buf.as<char>();
-    double2 *qxy = reinterpret_cast<double2 *>(base);
     uint32_t *qidx = reinterpret_cast<uint32_t *>(base + qb);
     double *h = reinterpret_cast<double *>(base + qb + ib);
     uint32_t *fb_list = reinterpret_cast<uint32_t *>(base + qb + ib + hb);
     uint8_t *removed = reinterpret_cast<uint8_t *>(base + qb + ib + hb + fb);
     uint32_t *tcount = reinterpret_cast<uint32_t *>(base + qb + ib + hb + fb + rb);
     uint32_t *ctr = reinterpret_cast<uint32_t *>(base + qb + ib + hb + fb + rb + cb);   // 4 words
-    const uint64_t nsurf = surf.size(), narea = area.size();
-    PCP_HIP(ctx, ctx->out_d.ensure((n + nsurf) * 32 + 64));
-    float4 *kept = ctx->out_d.as<float4>();
-    if (int rc0 = upload_async(ctx, qxy, qv.data(), G * sizeof(double2), st)) return rc0;
+    // the records: straight into pinned memory for message-sized results (the kernels store
+    // them there, no D2H copy), else a device buffer copied out
+    const size_t land_b = (n + nsurf + narea) * 32;
+    const bool land = ctx->zc_in && land_b <= kPinDirectMax * 8;
+    float4 *kept;
+    if (land) {
+        PCP_HIP(ctx, ctx->tc_host.ensure(land_b + 256));
+        kept = ctx->tc_host.as<float4>();
+    } else {
+        PCP_HIP(ctx, ctx->out_d.ensure((n + nsurf) * 32 + 64));
+        kept = ctx->out_d.as<float4>();
+    }
+    const size_t gen_need = gen_bytes(G, nsurf, narea, gpb, qxb);
+    if (!gen_hit) {   // surface + area records and the generated queries: one DMA
+        ctx->carve_gen_ok = false;
+        PCP_HIP(ctx, ctx->carve_gen.ensure(gen_need));
+        const HostPiece pc[3] = {{0, surf.data(), nsurf * sizeof(GenPoint)},
+                                 {nsurf * sizeof(GenPoint), area.data(), narea * sizeof(GenPoint)},
+                                 {gpb, qv.data(), G * sizeof(double2)}};
+        if (int rc0 = upload_pieces(ctx, ctx->carve_gen.p, pc, 3, gpb + G * sizeof(double2), st))
+            return rc0;
+        std::memcpy(ctx->carve_key, key, sizeof(key));
+        ctx->carve_G = G;
+        ctx->carve_nsurf = nsurf;
+        ctx->carve_narea = narea;
+        ctx->carve_gen_ok = true;
+    }
+    char *gbase = ctx->carve_gen.as<char>();
+    GenPoint *gp = reinterpret_cast<GenPoint *>(gbase);
+    double2 *qxy = reinterpret_cast<double2 *>(gbase + gpb);
+    float4 *area_d = land ? kept + 2 * (n + nsurf) : reinterpret_cast<float4 *>(gbase + gpb + qxb);
     PCP_HIP(ctx, hipMemsetAsync(ctr, 0, 16, st));
     PCP_HIP(ctx, hipMemsetAsync(removed, 0, n ? n : 1, st));
     const float r2 = (float)(p->terrain_search_radius * p->terrain_search_radius);
@@ -550,33 +602,34 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
         PCP_CHECK_LAUNCH(ctx);
     }
     // the generated surface (after the kept points) and area records, on the device
-    PCP_HIP(ctx, ctx->out_a.ensure((nsurf + narea) * sizeof(GenPoint) + narea * 32 + 64));
-    GenPoint *gp = ctx->out_a.as<GenPoint>();
-    float4 *area_d = reinterpret_cast<float4 *>(gp + nsurf + narea);
-    if (nsurf && (rc = upload_async(ctx, gp, surf.data(), nsurf * sizeof(GenPoint), st))) return rc;
-    if (narea && (rc = upload_async(ctx, gp + nsurf, area.data(), narea * sizeof(GenPoint), st)))
-        return rc;
+    PCP_HIP(ctx, ctx->small_host.ensure(4096));
+    char *sm = ctx->small_host.as<char>();
+    // landed: the first k_gen_emit stores the counters and the centre height too
+    uint32_t *sm_k = land ? reinterpret_cast<uint32_t *>(sm) : nullptr;
     if (nsurf) {
         hipLaunchKernelGGL(k_gen_emit, dim3((unsigned)((nsurf + kCT - 1) / kCT)), dim3(kCT), 0, st,
                            (const GenPoint *)gp, (uint32_t)nsurf, (const double *)h, p->depth,
-                           n ? (const uint32_t *)(ctr + 2) : nullptr, kept);
+                           n ? (const uint32_t *)(ctr + 2) : nullptr, kept,
+                           (const uint32_t *)ctr, sm_k);
         PCP_CHECK_LAUNCH(ctx);
+        sm_k = nullptr;
     }
     if (narea) {
         hipLaunchKernelGGL(k_gen_emit, dim3((unsigned)((narea + kCT - 1) / kCT)), dim3(kCT), 0, st,
                            (const GenPoint *)(gp + nsurf), (uint32_t)narea, (const double *)h,
-                           p->depth, nullptr, area_d);
+                           p->depth, nullptr, area_d, (const uint32_t *)ctr, sm_k);
         PCP_CHECK_LAUNCH(ctx);
+        sm_k = nullptr;
     }
     // the kept count and the centre height land in pinned memory; when the caller's buffers
     // hold the worst case (n kept + the surface, pcp_excavate_bounds), the records go out in the
     // same round trip: one synchronisation for the call
-    PCP_HIP(ctx, ctx->small_host.ensure(4096));
-    char *sm = ctx->small_host.as<char>();
-    PCP_HIP(ctx, hipMemcpyAsync(sm, ctr, 16, hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipMemcpyAsync(sm + 16, h, sizeof(double), hipMemcpyDeviceToHost, st));
-    const bool one_trip = terrain_out && terrain_cap >= n + nsurf && (area_out || !narea) &&
-                          area_cap >= narea;
+    if (!land || sm_k) {   // not stored by a kernel above
+        PCP_HIP(ctx, hipMemcpyAsync(sm, ctr, 16, hipMemcpyDeviceToHost, st));
+        PCP_HIP(ctx, hipMemcpyAsync(sm + 16, h, sizeof(double), hipMemcpyDeviceToHost, st));
+    }
+    const bool one_trip = !land && terrain_out && terrain_cap >= n + nsurf &&
+                          (area_out || !narea) && area_cap >= narea;
     if (one_trip) {
         if (n + nsurf)
             PCP_HIP(ctx, hipMemcpyAsync(terrain_out, kept, (n + nsurf) * 32, hipMemcpyDeviceToHost,
@@ -606,7 +659,10 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     }
     if ((*n_terrain && !terrain_out) || (*n_area && !area_out))
         return set_err(ctx, PCP_E_INVALID, "pcp_excavate: null output");
-    if (!one_trip) {   // exact-size buffers: the records follow the sizes
+    if (land) {   // the records sit in pinned memory already
+        if (*n_terrain) std::memcpy(terrain_out, kept, *n_terrain * 32);
+        if (narea) std::memcpy(area_out, area_d, narea * 32);
+    } else if (!one_trip) {   // exact-size buffers: the records follow the sizes
         if (*n_terrain)
             PCP_HIP(ctx, hipMemcpyAsync(terrain_out, kept, *n_terrain * 32, hipMemcpyDeviceToHost,
                                         st));

@@ -70,6 +70,60 @@ int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hip
     return PCP_OK;
 }
 
+int upload_pieces(pcp_ctx *ctx, void *dst_d, const HostPiece *pc, int k, size_t bytes,
+                  hipStream_t st) {
+    if (bytes == 0) return PCP_OK;
+    if (bytes > kUploadPinnedMax) {   // pageable, piece by piece
+        for (int i = 0; i < k; ++i)
+            if (pc[i].bytes)
+                PCP_HIP(ctx, hipMemcpyAsync(static_cast<char *>(dst_d) + pc[i].off, pc[i].src,
+                                            pc[i].bytes, hipMemcpyHostToDevice, st));
+        return PCP_OK;
+    }
+    const int s = ctx->up_next;
+    ctx->up_next = (s + 1) % pcp_ctx::kUpRing;
+    if (ctx->up_used[s]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[s]));
+    if (!ctx->up_ev[s]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[s], hipEventDisableTiming));
+    PCP_HIP(ctx, ctx->up_buf[s].ensure(bytes));
+    for (int i = 0; i < k; ++i)
+        if (pc[i].bytes) std::memcpy(static_cast<char *>(ctx->up_buf[s].p) + pc[i].off, pc[i].src,
+                                     pc[i].bytes);
+    PCP_HIP(ctx, hipMemcpyAsync(dst_d, ctx->up_buf[s].p, bytes, hipMemcpyHostToDevice, st));
+    PCP_HIP(ctx, hipEventRecord(ctx->up_ev[s], st));
+    ctx->up_used[s] = true;
+    return PCP_OK;
+}
+
+int pin_stage(pcp_ctx *ctx, const HostPiece *pc, int k, size_t bytes, const void **dev) {
+    if (ctx->pin_held >= 0) {   // an unreleased slot (an error path): drain, then drop it
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        ctx->pin_held = -1;
+    }
+    const int s = ctx->up_next;
+    ctx->up_next = (s + 1) % pcp_ctx::kUpRing;
+    if (ctx->up_used[s]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[s]));
+    ctx->up_used[s] = false;
+    if (!ctx->up_ev[s]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[s], hipEventDisableTiming));
+    PCP_HIP(ctx, ctx->up_buf[s].ensure(bytes + 256));
+    for (int i = 0; i < k; ++i)
+        if (pc[i].bytes) std::memcpy(static_cast<char *>(ctx->up_buf[s].p) + pc[i].off, pc[i].src,
+                                     pc[i].bytes);
+    ctx->pin_held = s;
+    *dev = ctx->up_buf[s].p;
+    return PCP_OK;
+}
+
+void pin_release(pcp_ctx *ctx, hipStream_t st) {
+    const int s = ctx->pin_held;
+    if (s < 0) return;
+    ctx->pin_held = -1;
+    if (hipEventRecord(ctx->up_ev[s], st) == hipSuccess) {
+        ctx->up_used[s] = true;
+    } else {   // no event: make sure no kernel still reads the slot
+        (void)hipStreamSynchronize(st);
+    }
+}
+
 int read_small(pcp_ctx *ctx, void *dst, const void *src_d, size_t bytes, hipStream_t st) {
     if (bytes > 4096) return set_err(ctx, PCP_E_INVALID, "read_small: %zu bytes", bytes);
     PCP_HIP(ctx, ctx->small_host.ensure(4096));
@@ -322,6 +376,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *ho = std::getenv("PCP_FAN_HOST_OUT")) ctx->fan_host_out = std::atoi(ho) != 0;
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
     if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff) != 0;
+    if (const char *zc = std::getenv("PCP_ZC_IN")) ctx->zc_in = std::atoi(zc) != 0;
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
     if (const char *tf = std::getenv("PCP_TERRAIN_FINE")) ctx->terrain_fine = std::atoi(tf);
     if (const char *tt = std::getenv("PCP_FINE_TILE")) ctx->fine_tile = std::atoi(tt);
@@ -351,6 +406,7 @@ void pcp_destroy(pcp_ctx *ctx) {
         ctx->up_buf[k].release();
     }
     ctx->cand_host.release();
+    ctx->tc_host.release();
     ctx->cv_host.release();
     ctx->terrain.release();
     ctx->aux.release();
@@ -359,6 +415,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->area_nrm.release();
     ctx->carve.release();
     ctx->carve_buf.release();
+    ctx->carve_gen.release();
     ctx->fan_host.release();
     ctx->res_host.release();
     ctx->fm_res_host.release();

@@ -152,12 +152,21 @@ __device__ __forceinline__ DD dd_merge(DD a, DD b) {
 // tree -- deterministic run to run -- for fewer instructions than the double-double sums this
 // replaced (|term| <= 2.25 m^2 within the 1.5 m radius: 9e8 neighbours fit in int64).
 constexpr double kMomScale = 4294967296.0;   // 2^32
+// round-to-nearest-even of t * 2^32 to an integer, as the bit pattern of 1.5 * 2^52 + that
+// integer: one FMA instead of the emulated double -> int64 conversion.  |t * 2^32| < 2^51, so
+// the sum stays in [2^52, 2^53) where the double's ulp is 1 and the bits are linear in the
+// integer; the accumulated 1.5 * 2^52 terms come off once at the end (count * kMagicBits)
+constexpr double kMagic = 6755399441055744.0;   // 1.5 * 2^52
+constexpr unsigned long long kMagicBits = 0x4338000000000000ull;
+__device__ __forceinline__ unsigned long long fx_bits(double t) {
+    return (unsigned long long)__double_as_longlong(fma(t, kMomScale, kMagic));
+}
 __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, float *__restrict__ out) {
     const uint32_t qi = blockIdx.x;
     const float4 q = g.pts[qi];
     const uint32_t orig = __float_as_uint(q.w);
     uint32_t lo[4], hi[4];
-    long long acc[10];   // xx xy xz yy yz zz x y z count
+    unsigned long long acc[10];   // xx xy xz yy yz zz x y z (biased bits) count
     for (int a = 0; a < 10; ++a) acc[a] = 0;
     if (stencil_ranges(g, q.x, q.y, q.z, lo, hi)) {
 #pragma unroll
@@ -165,18 +174,19 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
             for (uint32_t k = lo[r] + threadIdx.x; k < hi[r]; k += kXT) {
                 const P3 p = ld_p3(g.pts, k);
                 if (!flann_within(q.x, q.y, q.z, p, r2)) continue;
-                // shifted by K = the first (nearest) neighbour = the query point itself
+                // shifted by K = the first (nearest) neighbour = the query point itself; the
+                // products of two float-valued doubles are exact
                 const double x = (double)(p.x - q.x), y = (double)(p.y - q.y),
                              z = (double)(p.z - q.z);
-                acc[0] += __double2ll_rn(x * x * kMomScale);
-                acc[1] += __double2ll_rn(x * y * kMomScale);
-                acc[2] += __double2ll_rn(x * z * kMomScale);
-                acc[3] += __double2ll_rn(y * y * kMomScale);
-                acc[4] += __double2ll_rn(y * z * kMomScale);
-                acc[5] += __double2ll_rn(z * z * kMomScale);
-                acc[6] += __double2ll_rn(x * kMomScale);
-                acc[7] += __double2ll_rn(y * kMomScale);
-                acc[8] += __double2ll_rn(z * kMomScale);
+                acc[0] += fx_bits(x * x);
+                acc[1] += fx_bits(x * y);
+                acc[2] += fx_bits(x * z);
+                acc[3] += fx_bits(y * y);
+                acc[4] += fx_bits(y * z);
+                acc[5] += fx_bits(z * z);
+                acc[6] += fx_bits(x);
+                acc[7] += fx_bits(y);
+                acc[8] += fx_bits(z);
                 acc[9] += 1;
             }
     }
@@ -185,16 +195,19 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
     for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
         for (int a = 0; a < 10; ++a) acc[a] += __shfl_xor(acc[a], o, 64);
-    __shared__ long long lds[10][kXT / 64];
+    __shared__ unsigned long long lds[10][kXT / 64];
     if (lane == 0)
         for (int a = 0; a < 10; ++a) lds[a][wid] = acc[a];
     __syncthreads();
     if (threadIdx.x != 0) return;
     double v[10];
+    unsigned long long cnt = 0;
+    for (int w = 0; w < kXT / 64; ++w) cnt += lds[9][w];
     for (int a = 0; a < 10; ++a) {
-        long long t = lds[a][0];
+        unsigned long long t = lds[a][0];
         for (int w = 1; w < kXT / 64; ++w) t += lds[a][w];
-        v[a] = a == 9 ? (double)t : (double)t / kMomScale;
+        // modulo-2^64 sums: the bias comes off exactly
+        v[a] = a == 9 ? (double)t : (double)(long long)(t - cnt * kMagicBits) / kMomScale;
     }
     float *o = out + 3 * (size_t)orig;
     if (v[9] < 3.0) {   // computePointNormal: < 3 neighbours -> NaN

@@ -1014,6 +1014,26 @@ __global__ void __launch_bounds__(kFT) k_xform_raw(CloudIn c, Rigid r, float4 *_
     xform_store(r, x, y, z, out + 2 * i);
 }
 
+// several raw blobs in one launch (pcp_transform_concat): block b belongs to the cloud whose
+// tile range [tile0[i], tile0[i+1]) holds it; cloud i's records land at out + 2 * base[i]
+constexpr int kXfMax = 8;
+struct XformBatch {
+    int k;
+    CloudIn c[kXfMax];
+    Rigid r[kXfMax];
+    uint64_t base[kXfMax];
+    uint32_t tile0[kXfMax + 1];
+};
+__global__ void __launch_bounds__(kFT) k_xform_batch(XformBatch B, float4 *__restrict__ out) {
+    int i = 0;
+    while (i + 1 < B.k && blockIdx.x >= B.tile0[i + 1]) ++i;
+    const uint64_t j = (uint64_t)(blockIdx.x - B.tile0[i]) * kFT + threadIdx.x;
+    if (j >= B.c[i].n) return;
+    float x, y, z;
+    load_xyz(B.c[i], j, x, y, z);
+    xform_store(B.r[i], x, y, z, out + 2 * (B.base[i] + j));
+}
+
 // =========================================================================================
 // host orchestration: one job per cloud in a device table; every stage is one batched launch
 // (grid.y = clouds) on ctx->stream with sizes kept on the device, so a whole crop -> voxel ->
@@ -1373,9 +1393,20 @@ static int run_single(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b, floa
     int rc = ensure_misc(ctx, vp, res);
     if (rc) return rc;
     if (ctx->fbuf.empty()) ctx->fbuf.resize(1);
-    PCP_HIP(ctx, ctx->f_in.ensure(in->n * (uint64_t)in->point_step + 256));
     CloudIn c;
-    if ((rc = stage_cloud(ctx, *in, false, ctx->f_in, 0, c))) return rc;
+    // a message-sized cloud on the fast chain: read in place from the pinned ring (no DMA)
+    const uint64_t in_bytes = in->n * (uint64_t)in->point_step;
+    const bool zc = fast_ok && ctx->zc_in && ctx->fm_fast && in_bytes <= kPinDirectMax;
+    if (zc) {
+        if ((rc = stage_cloud(ctx, *in, true, ctx->f_in, 0, c))) return rc;   // fields only
+        const HostPiece pc{0, in->data, in_bytes};
+        const void *dv = nullptr;
+        if ((rc = pin_stage(ctx, &pc, 1, in_bytes, &dv))) return rc;
+        c.raw = static_cast<const unsigned char *>(dv);
+    } else {
+        PCP_HIP(ctx, ctx->f_in.ensure(in_bytes + 256));
+        if ((rc = stage_cloud(ctx, *in, false, ctx->f_in, 0, c))) return rc;
+    }
     std::vector<CloudJob> jobs(1);
     if ((rc = make_job(ctx, 0, c, b, leaf, want_idx, Rigid{}, vp, jobs[0]))) return rc;
     if (fast_ok && !want_idx && ctx->fm_fast && fast_geometry(ctx, 0, jobs[0])) {
@@ -1388,10 +1419,12 @@ static int run_single(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b, floa
         F.vidx = reinterpret_cast<uint32_t *>(F.out4 + ncap + 1);
         F.vcnt = F.vidx + ncap + 1;
         if ((rc = enqueue_all(ctx, batches_of(jobs), res_h, nullptr, ctx->stream))) return rc;
+        if (zc) pin_release(ctx, ctx->stream);
         J = F;
         return read_results(ctx, res_h, 1, &ri, true);
     }
     if ((rc = enqueue_all(ctx, batches_of(jobs), res, nullptr, ctx->stream))) return rc;
+    if (zc) pin_release(ctx, ctx->stream);
     J = jobs[0];
     return read_results(ctx, res, 1, &ri);
 }
@@ -1523,13 +1556,53 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, cons
     if (total == 0) return PCP_OK;
     if (!out) return set_err(ctx, PCP_E_INVALID, "pcp_transform_concat: null output");
     PCP_HIP(ctx, hipSetDevice(ctx->device));
+    std::vector<size_t> soff(k + 1, 0);
+    for (int i = 0; i < k; ++i)
+        soff[i + 1] = soff[i] + align256(clouds[i].n * (uint64_t)clouds[i].point_step);
+    if (ctx->zc_in && k <= kXfMax && soff[k] <= kPinDirectMax) {
+        // message-sized: every cloud read in place from one pinned slot, one launch, the
+        // records stored straight into pinned memory -- no DMA either way, one synchronisation
+        std::vector<HostPiece> pc(k);
+        for (int i = 0; i < k; ++i)
+            pc[i] = HostPiece{soff[i], clouds[i].data, clouds[i].n * (uint64_t)clouds[i].point_step};
+        PCP_HIP(ctx, ctx->tc_host.ensure(total * 32 + 256));
+        float4 *o = ctx->tc_host.as<float4>();
+        const void *dv = nullptr;
+        if (int rc = pin_stage(ctx, pc.data(), k, soff[k], &dv)) return rc;
+        XformBatch B{};
+        B.k = k;
+        uint64_t base = 0;
+        uint32_t tiles = 0;
+        for (int i = 0; i < k; ++i) {
+            CloudIn &c = B.c[i];
+            c.n = clouds[i].n;
+            c.step = clouds[i].point_step;
+            c.ox = clouds[i].off_x;
+            c.oy = clouds[i].off_y;
+            c.oz = clouds[i].off_z;
+            c.raw = static_cast<const unsigned char *>(dv) + soff[i];
+            B.r[i] = make_rigid(tf[i], rgb + 3 * i);
+            B.base[i] = base;
+            B.tile0[i] = tiles;
+            base += c.n;
+            tiles += (uint32_t)((c.n + kFT - 1) / kFT);
+        }
+        B.tile0[k] = tiles;
+        {
+            ProfScope ps(ctx, PCP_K_TRANSFORM);
+            hipLaunchKernelGGL(k_xform_batch, dim3(tiles), dim3(kFT), 0, ctx->stream, B, o);
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        pin_release(ctx, ctx->stream);
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        std::memcpy(out, o, total * 32);
+        prof_resolve(ctx);
+        return PCP_OK;
+    }
     PCP_HIP(ctx, ctx->out_d.ensure(total * 32));
     float4 *o = ctx->out_d.as<float4>();
     // every cloud staged in its own region of f_in: all uploads and launches in flight, one
     // synchronisation for the call
-    std::vector<size_t> soff(k + 1, 0);
-    for (int i = 0; i < k; ++i)
-        soff[i + 1] = soff[i] + align256(clouds[i].n * (uint64_t)clouds[i].point_step);
     PCP_HIP(ctx, ctx->f_in.ensure(soff[k] + 256));
     uint64_t base = 0;
     for (int i = 0; i < k; ++i) {

@@ -234,6 +234,15 @@ struct pcp_ctx {
     // excavated-terrain carve (pcp_excavate): index of the input cloud + scratch
     pcp::GridIndex carve;
     pcp::DevBuf carve_buf;
+    // the generated lattice (surface + area records, their height queries) on the device:
+    // [GenPoint surf | GenPoint area | queries (G generated + n input) | area records].  It
+    // depends on the parameters and the excavation pose alone; while carve_key matches, the
+    // next call neither regenerates nor uploads it
+    pcp::DevBuf carve_gen;
+    double carve_key[16] = {};
+    bool carve_gen_ok = false;
+    uint32_t carve_G = 0;
+    uint64_t carve_nsurf = 0, carve_narea = 0;
     // scratch
     pcp::DevBuf stage, scratch[8];
     pcp::DevBuf fan_tab, poses_d, steps_d, out_a, out_b, out_c, out_d, stats_d;
@@ -252,6 +261,11 @@ struct pcp_ctx {
     hipEvent_t up_ev[kUpRing] = {};
     bool up_used[kUpRing] = {};
     int up_next = 0;
+    int pin_held = -1;                       // ring slot held by pin_stage until pin_release
+    bool zc_in = true;                       // message-sized inputs read in place from pinned
+                                             // memory (PCP_ZC_IN; 0: DMA'd first)
+    pcp::PinnedBuf tc_host;                  // transform_concat / carve: records stored by the
+                                             // kernels straight into pinned memory
     pcp::PinnedBuf cand_host;                // generate_candidates: poses + count in one readback
     pcp::PinnedBuf cv_host;                  // pcp_crop_voxel's fast chain: centroids + result
                                              // sizes stored by the kernels (one round trip)
@@ -418,6 +432,24 @@ int read_small(pcp_ctx *ctx, void *dst, const void *src_d, size_t bytes, hipStre
 // src_h on return either way.
 constexpr size_t kUploadPinnedMax = 16u << 20;
 int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hipStream_t st);
+// several host pieces into one pinned slot at their byte offsets, then ONE DMA of `bytes`
+// (the gaps between pieces are don't-care bytes on the device)
+struct HostPiece {
+    size_t off;
+    const void *src;
+    size_t bytes;
+};
+int upload_pieces(pcp_ctx *ctx, void *dst_d, const HostPiece *pc, int k, size_t bytes,
+                  hipStream_t st);
+// zero-copy staging of message-sized inputs (<= kPinDirectMax bytes): the pieces are copied on
+// the host into a slot of the pinned ring and the kernels read them there, over the host link
+// -- no DMA, so no copy-engine hand-off in front of the first kernel.  *dev = the slot (a
+// device-readable host pointer).  The slot stays held until pin_release records, on st, the
+// point after the last kernel that reads it (a call that stages twice without releasing
+// drains the stream first).
+constexpr size_t kPinDirectMax = 4u << 20;
+int pin_stage(pcp_ctx *ctx, const HostPiece *pc, int k, size_t bytes, const void **dev);
+void pin_release(pcp_ctx *ctx, hipStream_t st);
 
 // the smallest float d with fl(d * d) >= r2: a point with dz = qz - pz >= d fails FLANN's
 // float test (its sum is >= fl(dz^2) >= r2), and so does every lower point of a z-descending

@@ -910,20 +910,26 @@ def _matched_cloud(seed=3):
 
 def test_excavate_matches_oracle(gpu, oracle):
     """pcp_excavate against the CPU restatement: kept points (order, bytes), the generated
-    excavated surface and /excavation_area records, and the marker pose, all bit-exact."""
-    c = _matched_cloud()
-    yaw = math.radians(20.0)
-    t, q = (0.3, -0.2, 0.1), (0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2))
-    terr, area, pose = gpu.excavate(c, (t, q))
-    keep, surf, r_area, r_pose = oracle.excavate(c, t, q)
-    np.testing.assert_array_equal(pose, r_pose)
-    nk = int(keep.sum())
-    assert 0 < nk < c.shape[0] and terr.shape[0] == nk + surf.shape[0]
-    kept = c[keep]
-    np.testing.assert_array_equal(terr[:nk, :3].view(np.uint32), kept[:, :3].view(np.uint32))
-    np.testing.assert_array_equal(terr[:nk, 4].view(np.uint32), kept[:, 4].view(np.uint32))
-    np.testing.assert_array_equal(terr[nk:, [0, 1, 2, 4]].view(np.uint32), surf.view(np.uint32))
-    np.testing.assert_array_equal(area[:, [0, 1, 2, 4]].view(np.uint32), r_area.view(np.uint32))
+    excavated surface and /excavation_area records, and the marker pose, all bit-exact.  The
+    sequence covers the device copy of the generated lattice: reused for a new cloud under the
+    same pose, regenerated for a new pose, and for a cloud that outgrows its buffer."""
+    for seed, yaw_deg, twice in ((3, 20.0, False), (4, 20.0, False), (3, -35.0, False),
+                                 (7, -35.0, True), (3, 20.0, False)):
+        c = _matched_cloud(seed)
+        if twice:
+            c = np.concatenate([c, _matched_cloud(seed + 1)])
+        yaw = math.radians(yaw_deg)
+        t, q = (0.3, -0.2, 0.1), (0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2))
+        terr, area, pose = gpu.excavate(c, (t, q))
+        keep, surf, r_area, r_pose = oracle.excavate(c, t, q)
+        np.testing.assert_array_equal(pose, r_pose)
+        nk = int(keep.sum())
+        assert 0 < nk < c.shape[0] and terr.shape[0] == nk + surf.shape[0]
+        kept = c[keep]
+        np.testing.assert_array_equal(terr[:nk, :3].view(np.uint32), kept[:, :3].view(np.uint32))
+        np.testing.assert_array_equal(terr[:nk, 4].view(np.uint32), kept[:, 4].view(np.uint32))
+        np.testing.assert_array_equal(terr[nk:, [0, 1, 2, 4]].view(np.uint32), surf.view(np.uint32))
+        np.testing.assert_array_equal(area[:, [0, 1, 2, 4]].view(np.uint32), r_area.view(np.uint32))
 
 
 def test_excavate_bounds_hold(gpu):
