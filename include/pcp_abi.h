@@ -272,6 +272,17 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
                     const pcp_vl_params *p, uint8_t *cell_flags, double *total_score,
                     int32_t *covered, pcp_vl_report *rep);
 
+/* runOptimization's device part in one call (:455-519): pcp_generate_candidates then
+ * pcp_score_poses on those candidates, identical results, one synchronisation -- the scoring
+ * reads the candidates and their count where the generation left them on the device (the
+ * reference's generateCandidatePositions + candidate loop).  poses5 (cap poses) receives the
+ * candidates, *n_out their count; the rest as pcp_score_poses.  Lattices past 65,535 points
+ * run as the two calls. */
+int pcp_generate_and_score(pcp_ctx *ctx, const double grid_bbox[6], const pcp_vl_params *p,
+                           const double zx120_pose5[5], double *poses5, uint64_t cap,
+                           uint64_t *n_out, uint8_t *cell_flags, double *total_score,
+                           int32_t *covered, pcp_vl_report *rep);
+
 /* Dense ray fan (BASELINE configs[1]): per pose, n_az x n_el rays, ray (i, j) with local
  * direction (cos e_j cos a_i, cos e_j sin a_i, sin e_j), a_i = 2*pi*i/n_az,
  * e_j = el_min + (el_max-el_min)*(j+0.5)/n_el, rotated by the pose yaw, marched with

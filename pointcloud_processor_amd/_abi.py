@@ -128,6 +128,8 @@ _SIGS = [
                                           C.POINTER(C.c_uint64)]),
     ("pcp_score_poses", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams), _P, _P, _P,
                                   C.POINTER(VlReport)]),
+    ("pcp_generate_and_score", C.c_int, [_P, _P, C.POINTER(VlParams), _P, _P, C.c_uint64,
+                                         C.POINTER(C.c_uint64), _P, _P, _P, C.POINTER(VlReport)]),
     ("pcp_raycast_fan", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P, _P, _P,
                                   C.POINTER(C.c_int64)]),
     ("pcp_raycast_fan_stats", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), _P]),
@@ -558,6 +560,27 @@ class Context:
                                              _ptr(cell_flags), _ptr(tot), _ptr(cov),
                                              C.byref(rep)), "pcp_score_poses")
         return tot[:P].copy(), cov[:P].copy(), rep
+
+    def generate_and_score(self, grid_bbox, params: VlParams, zx120_pose5,
+                           cell_flags: np.ndarray):
+        """runOptimization's device part in one call (pcp_generate_and_score): returns
+        (poses [n, 5], totals, covered, report); cell_flags updated in place."""
+        bb = np.ascontiguousarray(grid_bbox, np.float64)
+        zx = np.ascontiguousarray(zx120_pose5, np.float64)
+        assert cell_flags.dtype == np.uint8 and cell_flags.flags.c_contiguous
+        gs = int(np.ceil(np.sqrt(float(params.num_candidates))))
+        cap = max(gs * gs, 1)
+        poses = np.empty((cap, 5), np.float64)
+        tot = np.empty(cap, np.float64)
+        cov = np.empty(cap, np.int32)
+        n = C.c_uint64()
+        rep = VlReport()
+        self._check(self.lib.pcp_generate_and_score(self.h, _ptr(bb), C.byref(params), _ptr(zx),
+                                                    _ptr(poses), cap, C.byref(n),
+                                                    _ptr(cell_flags), _ptr(tot), _ptr(cov),
+                                                    C.byref(rep)), "pcp_generate_and_score")
+        P = n.value
+        return poses[:P].copy(), tot[:P].copy(), cov[:P].copy(), rep
 
     def score_poses_into(self, poses5: np.ndarray, zx120_pose5: np.ndarray, params: VlParams,
                          cell_flags: np.ndarray, tot: np.ndarray, cov: np.ndarray,

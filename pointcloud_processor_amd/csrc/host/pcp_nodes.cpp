@@ -269,18 +269,22 @@ SimplifiedDualLidarOptimizer::Result SimplifiedDualLidarOptimizer::runOptimizati
     const int gs = (int)std::ceil(std::sqrt((double)p_.num_candidates));
     std::vector<double> poses(5 * (size_t)std::max(1, gs * gs));
     uint64_t n = 0;
-    if (pcp_generate_candidates(dev_.ctx(), bbox_, &p, zx, poses.data(), poses.size() / 5, &n) !=
-        PCP_OK) {
-        err_ = dev_.error();
-        return r;
+    std::vector<double> totals(poses.size() / 5);
+    int rc;
+    if (multi_) {
+        if (pcp_generate_candidates(dev_.ctx(), bbox_, &p, zx, poses.data(), poses.size() / 5,
+                                    &n) != PCP_OK) {
+            err_ = dev_.error();
+            return r;
+        }
+        // the candidate loop (:467-475) sharded over multi_'s devices, one collective
+        // (identical results)
+        rc = pcp_multi_score_poses(multi_, poses.data(), n, zx, &p, flags_.data(), totals.data(),
+                                   nullptr, &r.report);
+    } else {   // generateCandidatePositions + the candidate loop, one round trip
+        rc = pcp_generate_and_score(dev_.ctx(), bbox_, &p, zx, poses.data(), poses.size() / 5, &n,
+                                    flags_.data(), totals.data(), nullptr, &r.report);
     }
-    std::vector<double> totals(n ? n : 1);
-    // the candidate loop (:467-475): on one device, or sharded over multi_'s devices with one
-    // collective (identical results)
-    const int rc = multi_ ? pcp_multi_score_poses(multi_, poses.data(), n, zx, &p, flags_.data(),
-                                                  totals.data(), nullptr, &r.report)
-                          : pcp_score_poses(dev_.ctx(), poses.data(), n, zx, &p, flags_.data(),
-                                            totals.data(), nullptr, &r.report);
     if (rc != PCP_OK) {
         err_ = multi_ ? pcp_multi_last_error(multi_) : dev_.error();
         return r;

@@ -506,11 +506,22 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     const uint64_t nsurf = gen_hit ? ctx->carve_nsurf : surf.size();
     const uint64_t narea = gen_hit ? ctx->carve_narea : area.size();
     // ---- index of the input (radius = terrain_search_radius); the raw records stay staged
-    // in ctx->stage (build_index's H2D copy) for the per-point passes below
-    if ((rc = build_index(ctx, ctx->carve, *in, p->terrain_search_radius, false, false))) return rc;
+    // (build_index's pinned slot or ctx->stage) for the per-point passes below, the slot held
+    // until the last of them is enqueued
+    // (DMA'd, not read in place: three passes below re-read the records, which over the host
+    // link cost more than the copy -- k_keep_emit 16 -> 36 us measured)
+    const unsigned char *raw = nullptr;
+    if (n) {
+        const size_t raw_b = n * (size_t)in->point_step;
+        PCP_HIP(ctx, ctx->stage.ensure(raw_b));
+        if (int rc0 = upload_async(ctx, ctx->stage.p, in->data, raw_b, st)) return rc0;
+        raw = ctx->stage.as<unsigned char>();
+    }
+    if ((rc = build_index(ctx, ctx->carve, *in, p->terrain_search_radius, false, false, &raw)))
+        return rc;
     const GridView g = ctx->carve.view();
     CarveArgs a{};
-    a.raw = ctx->stage.as<const unsigned char>();
+    a.raw = raw;
     a.n = n;
     a.step = in->point_step;
     a.ox = in->off_x;
@@ -601,6 +612,7 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
                            (const uint32_t *)tcount, kept, ctr + 2);
         PCP_CHECK_LAUNCH(ctx);
     }
+    pin_release(ctx, st);   // k_keep_emit was the raw records' last reader
     // the generated surface (after the kept points) and area records, on the device
     PCP_HIP(ctx, ctx->small_host.ensure(4096));
     char *sm = ctx->small_host.as<char>();

@@ -52,14 +52,21 @@ uint64_t alloc_count(int which) {
     return which == 0 ? g_reallocs.load() : which == 1 ? g_pinned_reallocs.load() : g_alloc_bytes.load();
 }
 
+// the next ring slot, never the one pin_stage holds (kernels may still read it)
+static int next_slot(pcp_ctx *ctx) {
+    int k = ctx->up_next;
+    if (k == ctx->pin_held) k = (k + 1) % pcp_ctx::kUpRing;
+    ctx->up_next = (k + 1) % pcp_ctx::kUpRing;
+    return k;
+}
+
 int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hipStream_t st) {
     if (bytes == 0) return PCP_OK;
     if (bytes > kUploadPinnedMax) {
         PCP_HIP(ctx, hipMemcpyAsync(dst_d, src_h, bytes, hipMemcpyHostToDevice, st));
         return PCP_OK;
     }
-    const int k = ctx->up_next;
-    ctx->up_next = (k + 1) % pcp_ctx::kUpRing;
+    const int k = next_slot(ctx);
     if (ctx->up_used[k]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[k]));   // its last DMA
     if (!ctx->up_ev[k]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[k], hipEventDisableTiming));
     PCP_HIP(ctx, ctx->up_buf[k].ensure(bytes));
@@ -80,8 +87,7 @@ int upload_pieces(pcp_ctx *ctx, void *dst_d, const HostPiece *pc, int k, size_t 
                                             pc[i].bytes, hipMemcpyHostToDevice, st));
         return PCP_OK;
     }
-    const int s = ctx->up_next;
-    ctx->up_next = (s + 1) % pcp_ctx::kUpRing;
+    const int s = next_slot(ctx);
     if (ctx->up_used[s]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[s]));
     if (!ctx->up_ev[s]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[s], hipEventDisableTiming));
     PCP_HIP(ctx, ctx->up_buf[s].ensure(bytes));
@@ -99,8 +105,7 @@ int pin_stage(pcp_ctx *ctx, const HostPiece *pc, int k, size_t bytes, const void
         PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
         ctx->pin_held = -1;
     }
-    const int s = ctx->up_next;
-    ctx->up_next = (s + 1) % pcp_ctx::kUpRing;
+    const int s = next_slot(ctx);
     if (ctx->up_used[s]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[s]));
     ctx->up_used[s] = false;
     if (!ctx->up_ev[s]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[s], hipEventDisableTiming));

@@ -283,7 +283,7 @@ k_lattice_flags(GridView g, float r2, Lattice L, uint8_t *__restrict__ flags) {
 // one block: the flagged lattice points in order -> cells (double xyz); *n_out = count
 __global__ void __launch_bounds__(1024)
 k_lattice_compact(const uint8_t *__restrict__ flags, Lattice L, double *__restrict__ cells,
-                  uint32_t cap, uint32_t *__restrict__ n_out) {
+                  uint32_t cap, uint32_t *__restrict__ n_out, uint32_t *__restrict__ n_host) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     __shared__ uint32_t wc[16];
     uint32_t run = 0;
@@ -311,7 +311,10 @@ k_lattice_compact(const uint8_t *__restrict__ flags, Lattice L, double *__restri
         run += tot;
         __syncthreads();
     }
-    if (threadIdx.x == 0) *n_out = run;
+    if (threadIdx.x == 0) {
+        *n_out = run;
+        if (n_host) *n_host = run;   // the pinned landing: no readback copy
+    }
 }
 
 // computeCellSurfaceNormal: a block per cell (block-strided over the cells; their count is
@@ -405,8 +408,12 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     if (area->n == 0) return PCP_OK;   // :168, nothing is rebuilt; the previous cells stay
     ProfScope prof(ctx, PCP_K_EXCAV_SETUP);
     const double r_near = grid_resolution * 1.5;
-    if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius, false, false))) return rc;
-    if ((rc = build_index(ctx, ctx->exc_near, *area, r_near, false, false))) return rc;
+    // both indices read the same staged bytes (staged once)
+    const unsigned char *raw = nullptr;
+    if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius, false, false, &raw))) return rc;
+    rc = build_index(ctx, ctx->exc_near, *area, r_near, false, false, &raw);
+    pin_release(ctx, ctx->stream);
+    if (rc) return rc;
     const uint64_t n = area->n;
     PCP_HIP(ctx, ctx->area_nrm.ensure(n * 3 * sizeof(float) + 16));
     // non-finite points are not in the index: PCL gives them a NaN normal
@@ -456,9 +463,11 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
                            0, ctx->stream, gq, r2q, L, ctx->stage.as<uint8_t>());
         PCP_CHECK_LAUNCH(ctx);
     }
+    PCP_HIP(ctx, ctx->small_host.ensure(4096));
+    uint32_t *n_h = ctx->small_host.as<uint32_t>();
     hipLaunchKernelGGL(k_lattice_compact, dim3(1), dim3(1024), 0, ctx->stream,
                        (const uint8_t *)ctx->stage.as<uint8_t>(), L, ctx->cells_xyz.as<double>(),
-                       (uint32_t)total, n_d);
+                       (uint32_t)total, n_d, n_h);
     PCP_CHECK_LAUNCH(ctx);
     // the cell normals read the lattice count on the device; the count comes back once, at
     // the end (one synchronisation for the whole call)
@@ -470,8 +479,8 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
                            ctx->cells_nrm.as<float>());
         PCP_CHECK_LAUNCH(ctx);
     }
-    uint32_t nc = 0;
-    if (int rc0 = read_small(ctx, &nc, n_d, 4, ctx->stream)) return rc0;
+    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const uint32_t nc = *n_h;
     ctx->n_cells = nc;
     if (n_cells) *n_cells = nc;
     prof_resolve(ctx);

@@ -425,7 +425,7 @@ static void host_bbox(const pcp_cloud_view &v, float bb[10], uint32_t &nfin) {
 }
 
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort,
-                bool occ) {
+                bool occ, const unsigned char **raw_io) {
     const uint64_t n = v.n;
     hipStream_t st = ctx->stream;
     // the query kernels address points and cells with 32-bit byte offsets (pcp_stencil.hpp)
@@ -443,10 +443,28 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     g.blk_fail = false;
     g.fine_ok = false;
     g.fine_fail = false;
-    // 1. stage the raw AoS bytes (the PointCloud2 data blob): pinned ring, no implicit wait
+    // 1. the raw AoS bytes (the PointCloud2 data blob), device-readable: given by the caller,
+    //    read in place from the pinned ring (message-sized), or DMA'd into ctx->stage
     const uint64_t raw_bytes = n * (uint64_t)v.point_step;
-    PCP_HIP(ctx, ctx->stage.ensure(raw_bytes));
-    if (int rc0 = upload_async(ctx, ctx->stage.p, v.data, raw_bytes, st)) return rc0;
+    const unsigned char *raw = raw_io ? *raw_io : nullptr;
+    bool pinned = false;
+    if (!raw && n && ctx->zc_in && raw_bytes <= kPinDirectMax) {
+        const HostPiece pc{0, v.data, raw_bytes};
+        const void *dv = nullptr;
+        if (int rc0 = pin_stage(ctx, &pc, 1, raw_bytes, &dv)) return rc0;
+        raw = static_cast<const unsigned char *>(dv);
+        pinned = true;
+    }
+    if (!raw) {
+        PCP_HIP(ctx, ctx->stage.ensure(raw_bytes));
+        if (int rc0 = upload_async(ctx, ctx->stage.p, v.data, raw_bytes, st)) return rc0;
+        raw = ctx->stage.as<unsigned char>();
+    }
+    if (raw_io) *raw_io = raw;
+    // the extraction is the index's only reader of the raw bytes
+    auto release_raw = [&]() {
+        if (pinned && !raw_io) pin_release(ctx, st);
+    };
     // 2. extract + bbox
     const int nb = (int)std::min<uint64_t>((n + kThreads - 1) / kThreads, 1024);
     PCP_HIP(ctx, ctx->scratch[0].ensure(n * sizeof(float4)));
@@ -464,11 +482,11 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     if (host_bb) {
         host_bbox(v, bb_h, nfin);
     } else {
-        hipLaunchKernelGGL(k_extract, dim3(nb), dim3(kThreads), 0, st,
-                           ctx->stage.as<unsigned char>(), n, v.point_step, v.off_x, v.off_y,
-                           v.off_z, ctx->scratch[0].as<float4>(), part, part_n, nullptr,
-                           (uint64_t)0);
+        hipLaunchKernelGGL(k_extract, dim3(nb), dim3(kThreads), 0, st, raw, n, v.point_step,
+                           v.off_x, v.off_y, v.off_z, ctx->scratch[0].as<float4>(), part, part_n,
+                           nullptr, (uint64_t)0);
         PCP_CHECK_LAUNCH(ctx);
+        release_raw();
         float *bb_d = ctx->stats_d.as<float>();
         hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(kThreads), 0, st, part, part_n, nb, bb_d,
                            reinterpret_cast<uint32_t *>(bb_d + 8));
@@ -479,6 +497,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     g.r_q = r_q;
     g.n_pts = nfin;
     if (nfin == 0) {   // a tree over zero valid points: never returns neighbours
+        release_raw();
         g.c = 1.0;
         g.nx = g.ny = g.nz = 1;
         for (int a = 0; a < 3; ++a) g.bmin[a] = g.bmax[a] = 0.0;
@@ -523,11 +542,11 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     PCP_HIP(ctx, ctx->scratch[2].ensure(n * sizeof(uint32_t)));
     PCP_HIP(ctx, ctx->scratch[3].ensure((ncell + 1) * sizeof(uint32_t)));
     if (host_bb) {
-        hipLaunchKernelGGL(k_extract, dim3(nb), dim3(kThreads), 0, st,
-                           ctx->stage.as<unsigned char>(), n, v.point_step, v.off_x, v.off_y,
-                           v.off_z, ctx->scratch[0].as<float4>(), part, part_n,
+        hipLaunchKernelGGL(k_extract, dim3(nb), dim3(kThreads), 0, st, raw, n, v.point_step,
+                           v.off_x, v.off_y, v.off_z, ctx->scratch[0].as<float4>(), part, part_n,
                            ctx->scratch[3].as<uint32_t>(), ncell + 1);
         PCP_CHECK_LAUNCH(ctx);
+        release_raw();
     } else {
         PCP_HIP(ctx, hipMemsetAsync(ctx->scratch[3].p, 0, (ncell + 1) * sizeof(uint32_t), st));
     }

@@ -344,8 +344,13 @@ struct KernelTimer {
 // zsort: points of each cell in descending z (needed by scan_stencil's early exit: the
 // terrain and aux indices); the other indices' queries are order-free
 // occ: build the dilated occupancy bits (stencil_any: the aux index; the fan's A/B variant 2)
+// raw_io (nullable): *raw_io non-null = the cloud's bytes already device-readable there (a
+// previous build's, or a caller's staging); on return *raw_io = where the bytes were read.  A
+// message-sized cloud is read in place from the pinned ring (pin_stage): without raw_io the
+// slot is released behind the extraction; with raw_io the caller releases it (pin_release)
+// after its own last reader.  Larger clouds are DMA'd into ctx->stage.
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
-                bool zsort = true, bool occ = true);
+                bool zsort = true, bool occ = true, const unsigned char **raw_io = nullptr);
 // the block-major copy of a z-sorted index (GridView.bstart / bpts); no-op when built
 int build_blocks(pcp_ctx *ctx, GridIndex &g);
 // the fine-window copy of a z-sorted index (GridView.frec / wpts); no-op when built.  Marks
@@ -391,7 +396,10 @@ struct ScoreEnq {
     uint8_t *flags_d = nullptr;    // [C] cell flag bytes (caller fills)
     double *tot_d = nullptr;       // [P + 1] totals, row P = zx120
     int32_t *cov_d = nullptr;      // [P + 1]
-    int32_t *stats = nullptr;      // 64 colour-statistics slots
+    int32_t *stats = nullptr;      // 64 colour-statistics slots (device: atomics)
+    int32_t *stats_host = nullptr; // zc: where the last flag block copies the finished stats
+    bool zc = false;               // flags / totals / covered live in the pinned block itself
+    const uint32_t *P_dev = nullptr;   // the device's pose count (rows P = capacity)
     // the query's block (poses_d on the device, res_host pinned, same offsets): poses at 0,
     // cell flags at fl_off, totals + covered (tc_bytes) ending at most at st_off, stats at
     // st_off, blk_bytes in all
@@ -400,9 +408,15 @@ struct ScoreEnq {
 // cell_flags (C bytes) travel with the poses when given (pcp_score_poses); k_score_cells zeroes
 // the statistics
 // fuse_tail: the row sums are left to the caller's k_sum_flags launch (pcp_score_poses)
+// zc: the kernels read the poses and flags from the pinned block and store the flags, totals,
+// covered counts and (via the last flag block) the statistics back into it -- no copies (only
+// with fuse_tail and cells present)
+// P_dev / poses_dev: the poses are on the device already (generated in the same stream), n =
+// the rows' capacity and *P_dev their count (pcp_generate_and_score)
 int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
                   const pcp_vl_params *p, ScoreEnq &o, const uint8_t *cell_flags = nullptr,
-                  bool fuse_tail = false);
+                  bool fuse_tail = false, bool zc = false, const uint32_t *P_dev = nullptr,
+                  const double *poses_dev = nullptr);
 // key kernels of the pose-sharded search (pcp_vlidar.hip; used by pcp_multi.hip)
 // identity: the value of the other ranks' slots (~0 for ncclUint64 MIN, INT64_MAX for a signed
 // int64 MIN as torch.distributed reduces it)

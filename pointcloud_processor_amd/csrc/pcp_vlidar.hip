@@ -499,7 +499,7 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
               const double *__restrict__ poses5, int P, const double *__restrict__ zx5,
               double *__restrict__ sm_out, uint8_t *__restrict__ mbits,
               double *__restrict__ score_z, uint8_t *__restrict__ zbits,
-              int32_t *__restrict__ stats) {
+              int32_t *__restrict__ stats, const uint32_t *__restrict__ P_dev) {
     const int c = blockIdx.x * kT + threadIdx.x;
     // the colour-statistics slots k_cell_flags accumulates into (it runs after this kernel)
     if (stats && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) stats[threadIdx.x] = 0;
@@ -511,7 +511,9 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
     const double *steps = SL ? s_steps : E.steps;
     if (c >= C) return;
     const int p = blockIdx.y;
-    const bool zrow = p == P;
+    const bool zrow = p == P;   // the last row (P = the rows' capacity with P_dev)
+    // P_dev: the pose count is the device's (candidates generated in the same stream)
+    if (P_dev && !zrow && p >= (int)*P_dev) return;
     const double *Q = zrow ? zx5 : poses5 + 5 * (size_t)p;
     uint32_t bits;
     const double s = eval_cell(E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1],
@@ -769,10 +771,14 @@ enum {
 
 // stale-flag resolution (virtual_lidar.cpp:487-501 read flags written by the LAST
 // evaluation that reached each assignment, :662-687) + colour statistics
+// stats_host (nullable): the last of the nblk flag blocks to finish copies the finished
+// statistics there (ticket in stats[63], zeroed with the rest by k_score_cells)
 __device__ __forceinline__ void cell_flags_body(const uint8_t *__restrict__ zbits,
                                                 const uint8_t *__restrict__ mbits, int C, int P,
                                                 uint8_t *__restrict__ flags,
-                                                int32_t *__restrict__ stats, int blk) {
+                                                int32_t *__restrict__ stats, int blk,
+                                                int32_t *__restrict__ stats_host = nullptr,
+                                                int nblk = 0) {
     const int c = blk * kT + threadIdx.x;
     __shared__ int32_t bst[S_N];
     if (threadIdx.x < S_N) bst[threadIdx.x] = 0;
@@ -822,6 +828,13 @@ __device__ __forceinline__ void cell_flags_body(const uint8_t *__restrict__ zbit
     }
     __syncthreads();
     if (threadIdx.x < S_N && bst[threadIdx.x]) atomicAdd(&stats[threadIdx.x], bst[threadIdx.x]);
+    if (!stats_host) return;
+    __threadfence();   // this block's statistics adds before its ticket
+    __syncthreads();
+    __shared__ int last;
+    if (threadIdx.x == 0) last = atomicAdd(&stats[63], 1) == nblk - 1;
+    __syncthreads();
+    if (last && threadIdx.x < S_N) stats_host[threadIdx.x] = atomicAdd(&stats[threadIdx.x], 0);
 }
 
 __global__ void __launch_bounds__(kT)
@@ -838,21 +851,27 @@ __global__ void __launch_bounds__(kT)
 k_sum_flags(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
             double *__restrict__ total, int32_t *__restrict__ covered,
             const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbits,
-            uint8_t *__restrict__ flags, int32_t *__restrict__ stats) {
+            uint8_t *__restrict__ flags, int32_t *__restrict__ stats,
+            int32_t *__restrict__ stats_host, const uint32_t *__restrict__ P_dev) {
+    // P: the rows the grid was sized for; Pa: the poses (the device's count with P_dev, the
+    // row blocks past it idle)
+    const int Pa = P_dev ? (int)*P_dev : P;
 #if PCP_ROW_SUM_LANES
     const int nr = sum_groups(P);
     if ((int)blockIdx.x < nr) {
-        row_group_body(sm, score_z, C, P, total, covered, blockIdx.x);
+        if ((int)blockIdx.x < sum_groups(Pa)) row_group_body(sm, score_z, C, Pa, total, covered, blockIdx.x);
         return;
     }
 #else
     const int nr = P + 1;
     if ((int)blockIdx.x < nr) {
-        if (threadIdx.x < 64) row_sum_body(sm, score_z, C, P, total, covered, blockIdx.x);
+        if (threadIdx.x < 64 && (int)blockIdx.x <= Pa)
+            row_sum_body(sm, score_z, C, Pa, total, covered, blockIdx.x);
         return;
     }
 #endif
-    cell_flags_body(zbits, mbits, C, P, flags, stats, (int)blockIdx.x - nr);
+    cell_flags_body(zbits, mbits, C, Pa, flags, stats, (int)blockIdx.x - nr, stats_host,
+                    (int)gridDim.x - nr);
 }
 __host__ __device__ constexpr int sum_flag_row_blocks(int P) {
     return PCP_ROW_SUM_LANES ? sum_groups(P) : P + 1;
@@ -1074,7 +1093,8 @@ __global__ void __launch_bounds__(kT) k_candidates(CandArgs a) {
 
 // order-preserving compaction of the lattice (single block)
 __global__ void __launch_bounds__(1024)
-k_cand_compact(const double *__restrict__ lat, int L, double *__restrict__ out, uint32_t *n_out) {
+k_cand_compact(const double *__restrict__ lat, int L, double *__restrict__ out, uint32_t *n_out,
+               double *__restrict__ out_h = nullptr, uint32_t *__restrict__ n_h = nullptr) {
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t base_s;
     if (threadIdx.x == 0) base_s = 0;
@@ -1095,13 +1115,20 @@ k_cand_compact(const double *__restrict__ lat, int L, double *__restrict__ out, 
         }
         if (v) {
             const uint32_t d = off + pre;
-            for (int q = 0; q < 5; ++q) out[5 * (size_t)d + q] = lat[6 * (size_t)l + 1 + q];
+            for (int q = 0; q < 5; ++q) {
+                const double x = lat[6 * (size_t)l + 1 + q];
+                out[5 * (size_t)d + q] = x;
+                if (out_h) out_h[5 * (size_t)d + q] = x;   // the host's copy (pinned)
+            }
         }
         __syncthreads();
         if (threadIdx.x == 0) base_s += tot;
         __syncthreads();
     }
-    if (threadIdx.x == 0) *n_out = base_s;
+    if (threadIdx.x == 0) {
+        *n_out = base_s;
+        if (n_h) *n_h = base_s;
+    }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1379,17 +1406,12 @@ int pcp_set_cells(pcp_ctx *ctx, const double *xyz, const float *normals, uint64_
     return PCP_OK;
 }
 
-int pcp_generate_candidates(pcp_ctx *ctx, const double bb[6], const pcp_vl_params *p,
-                            const double zx[5], double *poses5, uint64_t cap, uint64_t *n_out) {
-    if (!ctx) return PCP_E_INVALID;
-    if (!bb || !p || !zx || !n_out || (cap && !poses5))
-        return set_err(ctx, PCP_E_INVALID, "pcp_generate_candidates: null argument");
-    PCP_HIP(ctx, hipSetDevice(ctx->device));
-    *n_out = 0;
-    const int gs = (int)std::ceil(std::sqrt((double)p->num_candidates));
-    if (gs <= 0) return PCP_OK;
-    if ((int64_t)gs * gs > (1 << 24))
-        return set_err(ctx, PCP_E_INVALID, "pcp_generate_candidates: num_candidates too large");
+}  // extern "C"
+
+namespace pcp {
+// generateCandidatePositions' kernel arguments (:357-415)
+static CandArgs cand_args(pcp_ctx *ctx, const double bb[6], const pcp_vl_params *p,
+                          const double zx[5], int gs) {
     CandArgs a{};
     a.ground_enabled = (ctx->terrain_cloud_n > 0 && ctx->terrain.present) ? 1 : 0;
     if (a.ground_enabled) a.g = ctx->terrain.view();
@@ -1410,23 +1432,52 @@ int pcp_generate_candidates(pcp_ctx *ctx, const double bb[6], const pcp_vl_param
     a.zxx = zx[0];
     a.zxy = zx[1];
     a.sensor_height = p->sensor_height;
+    return a;
+}
+
+}  // namespace pcp
+
+extern "C" {
+
+int pcp_generate_candidates(pcp_ctx *ctx, const double bb[6], const pcp_vl_params *p,
+                            const double zx[5], double *poses5, uint64_t cap, uint64_t *n_out) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!bb || !p || !zx || !n_out || (cap && !poses5))
+        return set_err(ctx, PCP_E_INVALID, "pcp_generate_candidates: null argument");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    *n_out = 0;
+    const int gs = (int)std::ceil(std::sqrt((double)p->num_candidates));
+    if (gs <= 0) return PCP_OK;
+    if ((int64_t)gs * gs > (1 << 24))
+        return set_err(ctx, PCP_E_INVALID, "pcp_generate_candidates: num_candidates too large");
+    CandArgs a = cand_args(ctx, bb, p, zx, gs);
     const int L = gs * gs;
     PCP_HIP(ctx, ctx->out_a.ensure((size_t)L * 6 * sizeof(double)));
-    PCP_HIP(ctx, ctx->out_b.ensure((size_t)L * 5 * sizeof(double) + 64));
     a.lat = ctx->out_a.as<double>();
-    uint32_t *n_d = reinterpret_cast<uint32_t *>(ctx->out_b.as<char>() + (size_t)L * 5 * sizeof(double));
+    // the poses and their count are adjacent: k_cand_compact stores them straight into pinned
+    // memory (one synchronisation, no copy); huge lattices go through a device buffer, the
+    // count first, then the poses
+    const size_t span = (size_t)L * 5 * sizeof(double) + sizeof(uint32_t);
+    const bool land = span <= (4u << 20);
+    double *outp;
+    if (land) {
+        PCP_HIP(ctx, ctx->cand_host.ensure(span));
+        outp = ctx->cand_host.as<double>();
+    } else {
+        PCP_HIP(ctx, ctx->out_b.ensure((size_t)L * 5 * sizeof(double) + 64));
+        outp = ctx->out_b.as<double>();
+    }
+    uint32_t *n_d = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(outp) +
+                                                 (size_t)L * 5 * sizeof(double));
     {
         ProfScope ps(ctx, PCP_K_CANDIDATES);
         hipLaunchKernelGGL(k_candidates, dim3(L), dim3(kT), 0, ctx->stream, a);
         PCP_CHECK_LAUNCH(ctx);
         hipLaunchKernelGGL(k_cand_compact, dim3(1), dim3(1024), 0, ctx->stream,
-                           ctx->out_a.as<const double>(), L, ctx->out_b.as<double>(), n_d);
+                           ctx->out_a.as<const double>(), L, outp, n_d);
         PCP_CHECK_LAUNCH(ctx);
     }
-    // the poses and their count are adjacent: one readback of the lattice's worst case into
-    // pinned memory, one synchronisation (huge lattices: the count first, then the poses)
-    const size_t span = (size_t)L * 5 * sizeof(double) + sizeof(uint32_t);
-    if (span > (4u << 20)) {
+    if (!land) {
         uint32_t nh = 0;
         if (int rc0 = read_small(ctx, &nh, n_d, 4, ctx->stream)) return rc0;
         *n_out = nh;
@@ -1435,23 +1486,20 @@ int pcp_generate_candidates(pcp_ctx *ctx, const double bb[6], const pcp_vl_param
             return set_err(ctx, PCP_E_CAPACITY, "pcp_generate_candidates: need %u poses, cap %llu",
                            nh, (unsigned long long)cap);
         if (nh)
-            PCP_HIP(ctx, hipMemcpyAsync(poses5, ctx->out_b.p, (size_t)nh * 5 * sizeof(double),
+            PCP_HIP(ctx, hipMemcpyAsync(poses5, outp, (size_t)nh * 5 * sizeof(double),
                                         hipMemcpyDeviceToHost, ctx->stream));
         PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
         return PCP_OK;
     }
-    PCP_HIP(ctx, ctx->cand_host.ensure(span));
-    PCP_HIP(ctx, hipMemcpyAsync(ctx->cand_host.p, ctx->out_b.p, span, hipMemcpyDeviceToHost,
-                                ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     uint32_t nh = 0;
-    std::memcpy(&nh, ctx->cand_host.as<char>() + (size_t)L * 5 * sizeof(double), sizeof(nh));
+    std::memcpy(&nh, n_d, sizeof(nh));
     *n_out = nh;
     prof_resolve(ctx);
     if (nh > cap)
         return set_err(ctx, PCP_E_CAPACITY, "pcp_generate_candidates: need %u poses, cap %llu", nh,
                        (unsigned long long)cap);
-    if (nh) std::memcpy(poses5, ctx->cand_host.p, (size_t)nh * 5 * sizeof(double));
+    if (nh) std::memcpy(poses5, outp, (size_t)nh * 5 * sizeof(double));
     return PCP_OK;
 }
 
@@ -1482,7 +1530,7 @@ namespace pcp {
 // [P+1] (row P = zx120); the caller synchronizes.  Validation is the caller's.
 int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
                   const pcp_vl_params *p, ScoreEnq &o, const uint8_t *cell_flags,
-                  bool fuse_tail) {
+                  bool fuse_tail, bool zc, const uint32_t *P_dev, const double *poses_dev) {
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
     const int C = (int)ctx->n_cells, P = (int)n;
@@ -1518,15 +1566,29 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
     PCP_HIP(ctx, ctx->res_host.ensure(o.blk_bytes + 64));
     char *pin = ctx->res_host.as<char>();
     // the candidates, then the zx120 pose behind them (row P of k_score_cells), then the
-    // caller's cell flags: one upload
-    if (P) std::memcpy(pin, poses5, (size_t)P * 5 * sizeof(double));
+    // caller's cell flags: one upload -- or none (zc: the kernels read the pinned block)
+    if (P && poses5) std::memcpy(pin, poses5, (size_t)P * 5 * sizeof(double));
+    o.P_dev = P_dev;
     std::memcpy(pin + (size_t)P * 5 * sizeof(double), zx, 5 * sizeof(double));
     size_t up = (size_t)(P + 1) * 5 * sizeof(double);
     if (cell_flags && C) {
         std::memcpy(pin + o.fl_off, cell_flags, C);
         up = o.fl_off + C;
     }
-    PCP_HIP(ctx, hipMemcpyAsync(blk, pin, up, hipMemcpyHostToDevice, st));
+    o.zc = zc && fuse_tail && C > 0;
+    const char *pose_blk = blk;
+    if (o.zc) {
+        pose_blk = pin;
+        o.flags_d = reinterpret_cast<uint8_t *>(pin + o.fl_off);
+        o.tot_d = reinterpret_cast<double *>(pin + to_off);
+        o.cov_d = reinterpret_cast<int32_t *>(o.tot_d + (P + 1));
+        o.stats_host = reinterpret_cast<int32_t *>(pin + o.st_off);
+    } else {
+        PCP_HIP(ctx, hipMemcpyAsync(blk, pin, up, hipMemcpyHostToDevice, st));
+    }
+    const double *poses_k = reinterpret_cast<const double *>(pose_blk);
+    const double *zx_k = poses_k + 5 * (size_t)P;
+    if (poses_dev) poses_k = poses_dev;   // (the zx120 pose stays in the block)
     const unsigned cb = (unsigned)((C + kT - 1) / kT);
     if (C) {
         {
@@ -1535,17 +1597,13 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
             if (E.K <= kStepLds)
                 hipLaunchKernelGGL(k_score_cells<true>, g, dim3(kT), 0, st, E,
                                    ctx->cells_xyz.as<const double>(),
-                                   ctx->cells_nrm.as<const float>(), C,
-                                   ctx->poses_d.as<const double>(), P,
-                                   ctx->poses_d.as<const double>() + 5 * (size_t)P, o.comb,
-                                   o.mbits, score_z, o.zbits, o.stats);
+                                   ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
+                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev);
             else
                 hipLaunchKernelGGL(k_score_cells<false>, g, dim3(kT), 0, st, E,
                                    ctx->cells_xyz.as<const double>(),
-                                   ctx->cells_nrm.as<const float>(), C,
-                                   ctx->poses_d.as<const double>(), P,
-                                   ctx->poses_d.as<const double>() + 5 * (size_t)P, o.comb,
-                                   o.mbits, score_z, o.zbits, o.stats);
+                                   ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
+                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev);
             PCP_CHECK_LAUNCH(ctx);
         }
         o.score_z = score_z;
@@ -1599,7 +1657,7 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
         return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: null argument");
     if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: at most 65535 poses per call");
     ScoreEnq o;
-    if (int rc = score_enqueue(ctx, poses5, n, zx, p, o, cell_flags, true)) return rc;
+    if (int rc = score_enqueue(ctx, poses5, n, zx, p, o, cell_flags, true, ctx->zc_in)) return rc;
     hipStream_t st = ctx->stream;
     const int C = o.C, P = o.P;
     char *pin = ctx->res_host.as<char>();
@@ -1610,15 +1668,19 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
                            0,
                            st, (const double *)o.comb, (const double *)o.score_z, C, P, o.tot_d,
                            o.cov_d, (const uint8_t *)o.zbits, (const uint8_t *)o.mbits, o.flags_d,
-                           o.stats);
+                           o.stats, o.stats_host, o.P_dev);
         PCP_CHECK_LAUNCH(ctx);
     }
     // flags, totals, covered counts and statistics are one span of the block: one download
-    PCP_HIP(ctx, hipMemcpyAsync(pin + o.fl_off, reinterpret_cast<const char *>(o.flags_d),
-                                o.blk_bytes - o.fl_off, hipMemcpyDeviceToHost, st));
+    // (zc: the kernels stored them in the pinned block)
+    if (!o.zc)
+        PCP_HIP(ctx, hipMemcpyAsync(pin + o.fl_off, reinterpret_cast<const char *>(o.flags_d),
+                                    o.blk_bytes - o.fl_off, hipMemcpyDeviceToHost, st));
     PCP_HIP(ctx, hipStreamSynchronize(st));
-    const double *tot_h = reinterpret_cast<const double *>(
-        pin + (reinterpret_cast<const char *>(o.tot_d) - ctx->poses_d.as<const char>()));
+    const double *tot_h = o.zc ? o.tot_d
+                               : reinterpret_cast<const double *>(
+                                     pin + (reinterpret_cast<const char *>(o.tot_d) -
+                                            ctx->poses_d.as<const char>()));
     const int32_t *cov_h = reinterpret_cast<const int32_t *>(tot_h + (P + 1));
     const int32_t *st_h = reinterpret_cast<const int32_t *>(pin + o.st_off);
     if (C) std::memcpy(cell_flags, pin + o.fl_off, C);
@@ -1627,6 +1689,91 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     double best = -INFINITY;
     int64_t best_idx = -1;
     for (int k = 0; k < P; ++k) {
+        if (total_score) total_score[k] = tot_h[k];
+        if (covered) covered[k] = cov_h[k];
+        if (tot_h[k] > best) {
+            best = tot_h[k];
+            best_idx = k;
+        }
+    }
+    fill_report(st_h, tot_h[P], best_idx, best, rep);
+    return PCP_OK;
+}
+
+int pcp_generate_and_score(pcp_ctx *ctx, const double bb[6], const pcp_vl_params *p,
+                           const double zx[5], double *poses5, uint64_t cap, uint64_t *n_out,
+                           uint8_t *cell_flags, double *total_score, int32_t *covered,
+                           pcp_vl_report *rep) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!bb || !p || !zx || !n_out || !rep || (cap && !poses5) || (ctx->n_cells && !cell_flags))
+        return set_err(ctx, PCP_E_INVALID, "pcp_generate_and_score: null argument");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    *n_out = 0;
+    const int gs = (int)std::ceil(std::sqrt((double)p->num_candidates));
+    const int64_t L = gs > 0 ? (int64_t)gs * gs : 0;
+    if (L == 0 || L > 65535 || !ctx->zc_in) {   // the two calls (one synchronisation each)
+        uint64_t n = 0;
+        if (int rc = pcp_generate_candidates(ctx, bb, p, zx, poses5, cap, &n)) return rc;
+        *n_out = n;
+        return pcp_score_poses(ctx, poses5, n, zx, p, cell_flags, total_score, covered, rep);
+    }
+    // candidates -> device poses + their count (and the host's pinned copies), scoring sized
+    // for the whole lattice with the count read on the device: one synchronisation
+    CandArgs a = cand_args(ctx, bb, p, zx, gs);
+    PCP_HIP(ctx, ctx->out_a.ensure((size_t)L * 6 * sizeof(double)));
+    a.lat = ctx->out_a.as<double>();
+    PCP_HIP(ctx, ctx->out_d.ensure((size_t)L * 5 * sizeof(double) + 64));
+    double *poses_d = ctx->out_d.as<double>();
+    uint32_t *n_d = reinterpret_cast<uint32_t *>(poses_d + 5 * (size_t)L);
+    const size_t span = (size_t)L * 5 * sizeof(double) + sizeof(uint32_t);
+    PCP_HIP(ctx, ctx->cand_host.ensure(span));
+    double *poses_h = ctx->cand_host.as<double>();
+    uint32_t *n_h = reinterpret_cast<uint32_t *>(poses_h + 5 * (size_t)L);
+    {
+        ProfScope ps(ctx, PCP_K_CANDIDATES);
+        hipLaunchKernelGGL(k_candidates, dim3((unsigned)L), dim3(kT), 0, ctx->stream, a);
+        PCP_CHECK_LAUNCH(ctx);
+        hipLaunchKernelGGL(k_cand_compact, dim3(1), dim3(1024), 0, ctx->stream,
+                           ctx->out_a.as<const double>(), (int)L, poses_d, n_d, poses_h, n_h);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    ScoreEnq o;
+    if (int rc = score_enqueue(ctx, nullptr, (uint64_t)L, zx, p, o, cell_flags, true, true, n_d,
+                               poses_d))
+        return rc;
+    hipStream_t st = ctx->stream;
+    const int C = o.C;
+    char *pin = ctx->res_host.as<char>();
+    if (C) {
+        ProfScope ps(ctx, PCP_K_POSE_SUM);
+        hipLaunchKernelGGL(k_sum_flags,
+                           dim3((unsigned)(sum_flag_row_blocks((int)L) + (C + kT - 1) / kT)),
+                           dim3(kT), 0, st, (const double *)o.comb, (const double *)o.score_z, C,
+                           (int)L, o.tot_d, o.cov_d, (const uint8_t *)o.zbits,
+                           (const uint8_t *)o.mbits, o.flags_d, o.stats, o.stats_host, n_d);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    if (!o.zc)   // no cells: the zeroed totals and statistics
+        PCP_HIP(ctx, hipMemcpyAsync(pin + o.fl_off, reinterpret_cast<const char *>(o.flags_d),
+                                    o.blk_bytes - o.fl_off, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    const uint32_t P = *n_h;
+    *n_out = P;
+    prof_resolve(ctx);
+    if (P > cap)
+        return set_err(ctx, PCP_E_CAPACITY, "pcp_generate_and_score: need %u poses, cap %llu", P,
+                       (unsigned long long)cap);
+    if (P) std::memcpy(poses5, poses_h, (size_t)P * 5 * sizeof(double));
+    const double *tot_h = o.zc ? o.tot_d
+                               : reinterpret_cast<const double *>(
+                                     pin + (reinterpret_cast<const char *>(o.tot_d) -
+                                            ctx->poses_d.as<const char>()));
+    const int32_t *cov_h = reinterpret_cast<const int32_t *>(tot_h + (L + 1));
+    const int32_t *st_h = reinterpret_cast<const int32_t *>(pin + o.st_off);
+    if (C) std::memcpy(cell_flags, pin + o.fl_off, C);
+    double best = -INFINITY;
+    int64_t best_idx = -1;
+    for (uint32_t k = 0; k < P; ++k) {   // :464-475, strict '>' keeps the first maximum
         if (total_score) total_score[k] = tot_h[k];
         if (covered) covered[k] = cov_h[k];
         if (tot_h[k] > best) {

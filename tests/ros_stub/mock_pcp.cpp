@@ -142,6 +142,12 @@ int pcp_score_poses(pcp_ctx *c, const double *, uint64_t n, const double *, cons
     }
     return PCP_OK;
 }
+int pcp_generate_and_score(pcp_ctx *c, const double bb[6], const pcp_vl_params *pp,
+                           const double *zx, double *poses5, uint64_t cap, uint64_t *n,
+                           uint8_t *f, double *t, int32_t *cv, pcp_vl_report *r) {
+    if (int rc = pcp_generate_candidates(c, bb, pp, zx, poses5, cap, n)) return rc;
+    return pcp_score_poses(c, poses5, *n, zx, pp, f, t, cv, r);
+}
 int pcp_multi_score_poses(pcp_multi *m, const double *p, uint64_t n, const double *zx,
                           const pcp_vl_params *pp, uint8_t *f, double *t, int32_t *cv,
                           pcp_vl_report *r) {

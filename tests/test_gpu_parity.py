@@ -747,6 +747,35 @@ def test_score_poses_matches_reference_loop(gpu, oracle, loaded, scene, cells):
     assert rep2.best_idx == r_rep2.best_idx
 
 
+def test_generate_and_score_matches_two_calls(gpu, loaded, scene, cells):
+    """pcp_generate_and_score (one round trip: the scoring reads the candidates and their count
+    where the generation left them) against pcp_generate_candidates + pcp_score_poses on the
+    same context: poses, totals, covered counts, flags and the report bit-identical over ticks
+    whose flags carry over, lattice sizes that change between calls, and a context without
+    cells."""
+    fa = np.zeros(cells.xyz.shape[0], np.uint8)
+    fb = fa.copy()
+    for nc in (None, 400, 100, None):
+        params = _abi.default_vl_params() if nc is None else _abi.default_vl_params(num_candidates=nc)
+        poses = gpu.generate_candidates(cells.grid_bbox, params, scene.zx120_pose5)
+        tot, cov, rep = gpu.score_poses(poses, scene.zx120_pose5, params, fa)
+        p2, tot2, cov2, rep2 = gpu.generate_and_score(cells.grid_bbox, params, scene.zx120_pose5, fb)
+        np.testing.assert_array_equal(p2, poses)
+        np.testing.assert_array_equal(tot2.view(np.uint64), tot.view(np.uint64))
+        np.testing.assert_array_equal(cov2, cov)
+        np.testing.assert_array_equal(fb, fa)
+        assert rep2.as_dict() == rep.as_dict()
+    with _abi.Context(0) as ctx:   # no cells, no terrain: the zeroed report, flat candidates
+        params = _abi.default_vl_params(num_candidates=9)
+        f0 = np.zeros(0, np.uint8)
+        poses = ctx.generate_candidates(cells.grid_bbox, params, scene.zx120_pose5)
+        tot, cov, rep = ctx.score_poses(poses, scene.zx120_pose5, params, f0)
+        p2, tot2, cov2, rep2 = ctx.generate_and_score(cells.grid_bbox, params, scene.zx120_pose5, f0)
+        np.testing.assert_array_equal(p2, poses)
+        np.testing.assert_array_equal(tot2, tot)
+        assert rep2.as_dict() == rep.as_dict()
+
+
 def test_score_fov_boundary(oracle):
     """The FOV decision (virtual_lidar.cpp:665-672, |elevation - pitch| <= fov / 2) at and around
     its boundary: cells straight below and above a pose (elevation exactly -pi/2, +pi/2) and a
