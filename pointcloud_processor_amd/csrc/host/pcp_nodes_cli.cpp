@@ -230,7 +230,7 @@ static int cmd_replay(Device &dev, char **a) {
     constexpr int kStages = 7;
     static const char *kStageName[kStages] = {"filter", "merge", "carve", "area",
                                               "terrain", "zx120", "tick"};
-    std::vector<double> stage[kStages];
+    std::vector<double> stage[kStages], stage_frame[kStages];   // sorted later / frame order
     size_t merged_n = 0, best = 0, cells_n = cn;
     uint64_t realloc_after_warmup = 0, ra0 = 0;
     std::string dumped;
@@ -274,7 +274,10 @@ static int cmd_replay(Device &dev, char **a) {
         lap(6);
         const auto t1 = std::chrono::steady_clock::now();
         if (f >= 2)
-            for (int k = 0; k < kStages; ++k) stage[k].push_back(st[k]);
+            for (int k = 0; k < kStages; ++k) {
+                stage[k].push_back(st[k]);
+                stage_frame[k].push_back(st[k]);
+            }
         if (!r.ran) {
             std::fprintf(stderr, "replay: pose search did not run: %s\n", vl.lastError().c_str());
             return 1;
@@ -326,6 +329,25 @@ static int cmd_replay(Device &dev, char **a) {
         std::snprintf(b, sizeof(b), "%s%.4f", i ? ", " : "", lat_frame[i]);
         lat_s += b;
     }
+    // the stage times of the slowest frames (what the tail is made of)
+    std::string slow_s;
+    {
+        std::vector<size_t> ord(lat_frame.size());
+        for (size_t i = 0; i < ord.size(); ++i) ord[i] = i;
+        std::sort(ord.begin(), ord.end(),
+                  [&lat_frame](size_t a, size_t b) { return lat_frame[a] > lat_frame[b]; });
+        for (size_t r = 0; r < std::min<size_t>(4, ord.size()); ++r) {
+            char b[96];
+            std::snprintf(b, sizeof(b), "%s{\"frame\": %zu, \"ms\": %.4f", r ? ", " : "", ord[r],
+                          lat_frame[ord[r]]);
+            slow_s += b;
+            for (int k = 0; k < kStages; ++k) {
+                std::snprintf(b, sizeof(b), ", \"%s\": %.4f", kStageName[k], stage_frame[k][ord[r]]);
+                slow_s += b;
+            }
+            slow_s += "}";
+        }
+    }
     std::sort(lat.begin(), lat.end());
     auto q = [&lat](double p) { return lat[std::min(lat.size() - 1, (size_t)(p * lat.size()))]; };
     std::string stage_s;
@@ -340,10 +362,10 @@ static int cmd_replay(Device &dev, char **a) {
     std::printf("{\"frames\": %zu, \"points_per_scan\": %zu, \"chain\": %d, \"p50_ms\": %.4f, "
                 "\"p99_ms\": %.4f, \"max_ms\": %.4f, \"merged_points\": %zu, \"cells\": %zu, "
                 "\"best_idx\": %zu, \"reallocs_after_warmup\": %llu, \"dumped\": [%s], "
-                "\"stage_p50_ms\": {%s}, \"lat_ms\": [%s]}\n",
+                "\"stage_p50_ms\": {%s}, \"slowest\": [%s], \"lat_ms\": [%s]}\n",
                 lat.size(), npts, chain ? 1 : 0, q(0.5), q(0.99), lat.back(), merged_n, cells_n,
                 best, (unsigned long long)realloc_after_warmup, dumped.c_str(), stage_s.c_str(),
-                lat_s.c_str());
+                slow_s.c_str(), lat_s.c_str());
     return 0;
 }
 

@@ -70,11 +70,12 @@ __device__ __forceinline__ void dds_add(DDs &a, double x) {
 // for every z_rel it accepts).  Writes the query (x, y) and the point index.
 __global__ void __launch_bounds__(kCT)
 k_carve_cand(CarveArgs a, double2 *__restrict__ qxy, uint32_t *__restrict__ qidx,
-             uint32_t *__restrict__ count, uint32_t qbase) {
+             uint32_t *__restrict__ count, uint32_t qbase, uint8_t *__restrict__ removed) {
     const uint64_t i = (uint64_t)blockIdx.x * kCT + threadIdx.x;
     bool cand = false;
     float x = 0.f, y = 0.f, z = 0.f;
     if (i < a.n) {
+        removed[i] = 0;   // (k_carve_decide sets the carved ones)
         load_p(a, i, x, y, z);
         const double dx = (double)x - a.cx, dy = (double)y - a.cy;
         const double xl = dx * a.cos_my - dy * a.sin_my;
@@ -587,11 +588,10 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     double2 *qxy = reinterpret_cast<double2 *>(gbase + gpb);
     float4 *area_d = land ? kept + 2 * (n + nsurf) : reinterpret_cast<float4 *>(gbase + gpb + qxb);
     PCP_HIP(ctx, hipMemsetAsync(ctr, 0, 16, st));
-    PCP_HIP(ctx, hipMemsetAsync(removed, 0, n ? n : 1, st));
     const float r2 = (float)(p->terrain_search_radius * p->terrain_search_radius);
     const unsigned gn = (unsigned)((n + kCT - 1) / kCT);
     if (n) {
-        hipLaunchKernelGGL(k_carve_cand, dim3(gn), dim3(kCT), 0, st, a, qxy, qidx, ctr, G);
+        hipLaunchKernelGGL(k_carve_cand, dim3(gn), dim3(kCT), 0, st, a, qxy, qidx, ctr, G, removed);
         PCP_CHECK_LAUNCH(ctx);
     }
     const unsigned gq = (unsigned)((nq_max + kCT / 64 - 1) / (kCT / 64));   // a wave per query

@@ -161,8 +161,27 @@ constexpr unsigned long long kMagicBits = 0x4338000000000000ull;
 __device__ __forceinline__ unsigned long long fx_bits(double t) {
     return (unsigned long long)__double_as_longlong(fma(t, kMomScale, kMagic));
 }
-__global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, float *__restrict__ out) {
+// the raw input (the index holds its finite points only): the blocks past the index's points
+// give the non-finite ones their NaN normal
+struct RawIn {
+    const unsigned char *raw;
+    uint64_t n;
+    uint32_t step, ox, oy, oz;
+};
+__global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, float *__restrict__ out,
+                                                      RawIn in) {
     const uint32_t qi = blockIdx.x;
+    if (qi >= g.n_pts) {
+        const uint64_t i = (uint64_t)(qi - g.n_pts) * kXT + threadIdx.x;
+        if (i >= in.n) return;
+        const unsigned char *p = in.raw + i * in.step;
+        const float x = *reinterpret_cast<const float *>(p + in.ox),
+                    y = *reinterpret_cast<const float *>(p + in.oy),
+                    z = *reinterpret_cast<const float *>(p + in.oz);
+        if (!(isfinite(x) && isfinite(y) && isfinite(z)))
+            out[3 * i] = out[3 * i + 1] = out[3 * i + 2] = NAN;
+        return;
+    }
     const float4 q = g.pts[qi];
     const uint32_t orig = __float_as_uint(q.w);
     uint32_t lo[4], hi[4];
@@ -412,24 +431,27 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     const unsigned char *raw = nullptr;
     if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius, false, false, &raw))) return rc;
     rc = build_index(ctx, ctx->exc_near, *area, r_near, false, false, &raw);
-    pin_release(ctx, ctx->stream);
-    if (rc) return rc;
+    if (rc) return rc;   // (a held slot is drained by the next pin_stage)
     const uint64_t n = area->n;
     PCP_HIP(ctx, ctx->area_nrm.ensure(n * 3 * sizeof(float) + 16));
-    // non-finite points are not in the index: PCL gives them a NaN normal
-    PCP_HIP(ctx, hipMemsetAsync(ctx->area_nrm.p, 0xff, n * 3 * sizeof(float), ctx->stream));
     ctx->area_n = n;
     if (ctx->exc_norm.n_pts == 0) {   // no finite point: no lattice bounds, no cells
+        PCP_HIP(ctx, hipMemsetAsync(ctx->area_nrm.p, 0xff, n * 3 * sizeof(float), ctx->stream));
+        pin_release(ctx, ctx->stream);
         ctx->n_cells = 0;
         if (n_cells) *n_cells = 0;
         return PCP_OK;
     }
     const GridView gn = ctx->exc_norm.view(), gq = ctx->exc_near.view();
     const float r2n = (float)(kNormalRadius * kNormalRadius), r2q = (float)(r_near * r_near);
-    hipLaunchKernelGGL(k_area_normals, dim3((unsigned)ctx->exc_norm.n_pts), dim3(kXT), 0,
-                       ctx->stream, gn, r2n,
-                       ctx->area_nrm.as<float>());
+    // non-finite points are not in the index: PCL gives them a NaN normal (the kernel's blocks
+    // past the index's points)
+    const RawIn rin{raw, n, area->point_step, area->off_x, area->off_y, area->off_z};
+    hipLaunchKernelGGL(k_area_normals,
+                       dim3((unsigned)(ctx->exc_norm.n_pts + (n + kXT - 1) / kXT)), dim3(kXT), 0,
+                       ctx->stream, gn, r2n, ctx->area_nrm.as<float>(), rin);
     PCP_CHECK_LAUNCH(ctx);
+    pin_release(ctx, ctx->stream);   // k_area_normals read the raw records last
     // grid bounds (:239-256): min/max of the float coordinates as doubles, then the margin
     const double *bmin = ctx->exc_norm.bmin, *bmax = ctx->exc_norm.bmax;
     Lattice L;

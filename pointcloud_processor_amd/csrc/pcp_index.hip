@@ -262,14 +262,9 @@ k_cell_rank_z(const float4 *__restrict__ in, uint64_t n, CellMap m,
 // the lowest).  Rounded outwards by one extra step and clamped to the open-ended codes, so
 // zb + lo*kZq*c <= every point z <= zb + hi*kZq*c holds for the block's points whatever the
 // rounding of their cell assignment (zb = the block's floor, oz + iz*c).
-__global__ void __launch_bounds__(kThreads)
-k_occz(const uint32_t *__restrict__ start, const float4 *__restrict__ pts, CellMap m, double c,
-       uint64_t ncell, uint16_t *__restrict__ occz) {
-    const uint64_t lin = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (lin >= ncell) return;
-    const int ix = (int)(lin % m.nx);
-    const int iy = (int)((lin / m.nx) % m.ny);
-    const int iz = (int)(lin / ((uint64_t)m.nx * m.ny));
+__device__ __forceinline__ uint16_t occz_at(const uint32_t *__restrict__ start,
+                                            const float4 *__restrict__ pts, const CellMap &m,
+                                            double c, int ix, int iy, int iz) {
     float zmax = -FLT_MAX, zmin = FLT_MAX;
     bool any = false;
     for (int dz = 0; dz < 2; ++dz)
@@ -286,7 +281,43 @@ k_occz(const uint32_t *__restrict__ start, const float4 *__restrict__ pts, CellM
                 }
             }
         }
-    occz[lin] = any ? zband_code(zmax, zmin, m.oz + (double)iz * c, c) : 0x00FFu;
+    return any ? zband_code(zmax, zmin, m.oz + (double)iz * c, c) : (uint16_t)0x00FFu;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_occz(const uint32_t *__restrict__ start, const float4 *__restrict__ pts, CellMap m, double c,
+       uint64_t ncell, uint16_t *__restrict__ occz) {
+    const uint64_t lin = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (lin >= ncell) return;
+    const int ix = (int)(lin % m.nx);
+    const int iy = (int)((lin / m.nx) % m.ny);
+    const int iz = (int)(lin / ((uint64_t)m.nx * m.ny));
+    occz[lin] = occz_at(start, pts, m, c, ix, iy, iz);
+}
+
+// the same bands for a sparse grid (far more cells than points; the array preset to the empty
+// code 0x00FF): the first point of each occupied cell writes the bands of the 8 corners whose
+// 2x2x2 block holds that cell -- every corner with a point in its block, and no other, differs
+// from the preset.  A corner shared by several occupied cells gets the same value from each.
+__global__ void __launch_bounds__(kThreads)
+k_occz_sparse(const uint32_t *__restrict__ start, const float4 *__restrict__ pts, CellMap m,
+              double c, uint64_t npts, uint16_t *__restrict__ occz) {
+    // thread = (point, corner): the corners of one cell are independent (one occz_at each, no
+    // chain of eight)
+    const uint64_t t = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    const uint64_t j = t >> 3;
+    const int d = (int)(t & 7);
+    if (j >= npts) return;
+    const float4 p = pts[j];
+    const uint32_t cc = cell_of(m, p.x, p.y, p.z);
+    if (start[cc] != (uint32_t)j) return;
+    const int ix = (int)(cc % (uint32_t)m.nx);
+    const int iy = (int)((cc / (uint32_t)m.nx) % (uint32_t)m.ny);
+    const int iz = (int)(cc / ((uint32_t)m.nx * (uint32_t)m.ny));
+    const int tx = ix - (d & 1), ty = iy - ((d >> 1) & 1), tz = iz - (d >> 2);
+    if (tx < 0 || ty < 0 || tz < 0) return;
+    const uint64_t lin = (uint64_t)tx + (uint64_t)m.nx * ((uint64_t)ty + (uint64_t)m.ny * tz);
+    occz[lin] = occz_at(start, pts, m, c, tx, ty, tz);
 }
 
 // dilated occupancy: bit for lower corner (ix,iy,iz) = any point in the 2x2x2 block
@@ -396,6 +427,9 @@ k_blk_fill(const float4 *__restrict__ pts, uint64_t n, const uint32_t *__restric
         bpts[bstart[K] + pos] = p;
     }
 }
+
+// z bands of grids with more than this many cells per point: only around the occupied cells
+constexpr uint64_t kSparseCells = 32;
 
 // clouds up to this size get their bbox from the host (build_index)
 constexpr uint64_t kHostBboxMax = 1ull << 17;
@@ -593,9 +627,17 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     g.occz_ok = false;
     if (zsort) {
         PCP_HIP(ctx, g.occz.ensure(ncell * sizeof(uint16_t)));
-        hipLaunchKernelGGL(k_occz, dim3((unsigned)((ncell + kThreads - 1) / kThreads)),
-                           dim3(kThreads), 0, st, g.start.as<const uint32_t>(),
-                           g.pts.as<const float4>(), m, c, ncell, g.occz.as<uint16_t>());
+        if (ncell > kSparseCells * (uint64_t)nfin) {   // mostly empty: preset + occupied cells
+            PCP_HIP(ctx, hipMemsetD16Async(g.occz.p, 0x00FFu, ncell, st));
+            hipLaunchKernelGGL(k_occz_sparse, dim3((unsigned)((8 * (uint64_t)nfin + kThreads - 1) / kThreads)),
+                               dim3(kThreads), 0, st, g.start.as<const uint32_t>(),
+                               g.pts.as<const float4>(), m, c, (uint64_t)nfin,
+                               g.occz.as<uint16_t>());
+        } else {
+            hipLaunchKernelGGL(k_occz, dim3((unsigned)((ncell + kThreads - 1) / kThreads)),
+                               dim3(kThreads), 0, st, g.start.as<const uint32_t>(),
+                               g.pts.as<const float4>(), m, c, ncell, g.occz.as<uint16_t>());
+        }
         PCP_CHECK_LAUNCH(ctx);
         g.occz_ok = true;
     }
