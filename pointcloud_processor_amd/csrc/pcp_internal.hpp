@@ -37,6 +37,8 @@ constexpr double kQueryMargin = 1e-3;
 void note_realloc(size_t bytes, bool pinned);
 uint64_t alloc_count(int which);   // 0 device, 1 pinned reallocations, 2 bytes allocated
 
+constexpr size_t kHeadroomMax = 16u << 20;   // first allocations below this get +25 %
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -47,7 +49,9 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
         size_t want = bytes < 256 ? 256 : bytes;
-        if (grow) want = std::max<size_t>(want + want / 4, 64u << 10);
+        // message-sized buffers start with the headroom a growth would add: streamed clouds
+        // vary by a few percent frame to frame, and each growth is a free + malloc in a frame
+        if (grow || want < kHeadroomMax) want = std::max<size_t>(want + want / 4, 64u << 10);
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
         note_realloc(want, false);
@@ -73,7 +77,7 @@ struct PinnedBuf {
         p = nullptr;
         cap = 0;
         size_t want = bytes < 4096 ? 4096 : bytes;
-        if (grow) want = std::max<size_t>(want + want / 4, 64u << 10);
+        if (grow || want < kHeadroomMax) want = std::max<size_t>(want + want / 4, 64u << 10);
         hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
         if (e == hipSuccess) cap = want;
         note_realloc(want, true);
