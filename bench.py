@@ -16,7 +16,7 @@ poses_per_s_reference_mode (runOptimization over the excavation cells, virtual_l
 of K steps, and CPU baselines (the oracle restatement, 1 thread and the host's CPU share) for
 all three on rank 0 at N = 1.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode all|fan|filter|cells]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode all|fan|filter|cells|c1|c5]
 
 --gpus N without WORLD_SIZE starts N ranks itself (one process per GPU).
 """
@@ -848,6 +848,60 @@ def run_c1(args, local, cpu: bool):
     return out
 
 
+def run_c5(args, torch, dist, world, rank, local, backend=None):
+    """BASELINE configs[4] (8 GPUs x 60k-pt streams): C5 is replicas only -- each
+    rank streams its own frames through the C++ node cores (pcp_nodes_cli replay, full chain:
+    filter x2 -> merge -> carve -> normals + grid -> terrain index -> pose search), nothing is
+    exchanged on the data path.  value = frames/s of all replicas (each rank's frames over its
+    mean frame latency, summed by one reduction at the end); p50/p99 = the worst rank's."""
+    import subprocess
+    import tempfile
+
+    from pointcloud_processor_amd import synth
+
+    sc = synth.terrain_scene()
+    cells = synth.excavation_cells(sc.area)
+    d = Path(tempfile.mkdtemp(prefix=f"pcp_c5_r{rank}_"))
+    np.ascontiguousarray(sc.terrain).tofile(d / "t.f32")
+    np.ascontiguousarray(cells.xyz).tofile(d / "c.f64")
+    np.ascontiguousarray(cells.normals).tofile(d / "n.f32")
+    bb = ",".join(repr(float(v)) for v in cells.grid_bbox)
+    cli = Path(__file__).resolve().parent / "pointcloud_processor_amd" / "_lib" / "pcp_nodes_cli"
+    env = dict(os.environ)
+    ndev = torch.cuda.device_count()
+    if ndev:   # the replica's own GPU (device 0 of the child)
+        env["HIP_VISIBLE_DEVICES"] = str(local % ndev)
+    frames = max(args.steps, 20)
+    if dist is not None:
+        dist.barrier()
+    r = subprocess.run([str(cli), "replay", str(d / "t.f32"), str(sc.terrain.shape[0]),
+                        str(d / "c.f64"), str(d / "n.f32"), str(cells.xyz.shape[0]), bb,
+                        str(frames), "60032", "1"], env=env, capture_output=True, text=True,
+                       timeout=600)
+    if r.returncode != 0:
+        raise SystemExit(f"bench.py --mode c5: replay failed (rank {rank}): {r.stderr[-400:]}")
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    lat = np.array(res["lat_ms"])
+    vals = [1e3 / float(lat.mean()), res["p50_ms"], res["p99_ms"]]
+    if dist is not None:
+        t = torch.tensor(vals, dtype=torch.float64,
+                         device=f"cuda:{local}" if backend == "nccl" else "cpu")
+        s = t.clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        m = t.clone()
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        vals = [float(s[0]), float(m[1]), float(m[2])]
+    return {"metric": "C5 frames/s (full chain, replicas)", "value": vals[0], "unit": "frames/s",
+            "n_gpus": world, "steps": frames, "warmup": 2, "ms_per_step": vals[1],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32 points / f64 scoring", "data": "synthetic 60,032-pt HDL-64-like scans",
+            "config": {"workload": "C5: 60k-pt stream per GPU, filter x2 -> merge -> carve -> "
+                                   "normals + grid -> terrain index -> pose search",
+                       "parallelism": f"replicas x{world}"},
+            "p50_ms_worst_rank": vals[1], "p99_ms_worst_rank": vals[2],
+            "stage_p50_ms_rank0": res.get("stage_p50_ms")}
+
+
 def run_cells(args, torch, dist, world, rank, local, backend=None):
     """Reference-mode scoring (runOptimization) alone: poses/s."""
     a = argparse.Namespace(**vars(args))
@@ -866,11 +920,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--mode", choices=["all", "fan", "filter", "cells", "c1", "launch-check"],
+    ap.add_argument("--mode", choices=["all", "fan", "filter", "cells", "c1", "c5",
+                                       "launch-check"],
                     default="all",
                     help="all (default): the fan line with reference-mode scoring and C3 as "
                          "extra keys; fan: the fan alone (profiling); filter: C3 with PCIe and "
-                         "stage breakdown; cells: reference mode alone")
+                         "stage breakdown; cells: reference mode alone; c1 / c5: the streaming "
+                         "chain (configs[0] / configs[4], replicas)")
     ap.add_argument("--poses-per-gpu", type=int, default=256)
     ap.add_argument("--n-az", type=int, default=1024)
     ap.add_argument("--n-el", type=int, default=256)
@@ -895,6 +951,8 @@ def main():
         out = run_cells(args, torch, dist, world, rank, local, backend)
     elif args.mode == "c1":
         out = run_c1(args, local, cpu=not args.no_cpu_baseline)
+    elif args.mode == "c5":
+        out = run_c5(args, torch, dist, world, rank, local, backend)
     else:
         out = run_all(args, torch, dist, world, rank, local, backend)
     if rank == 0:
