@@ -844,6 +844,45 @@ def test_score_poses_clutter(oracle):
         ctx.close()
 
 
+def test_score_poses_sparse_terrain(oracle):
+    """A sparse terrain (a few thousand points over 40 m x 40 m, like the chain's carved
+    terrain) takes the sparse z-band build and the coarse occupancy map that the cell march
+    reads from LDS before each probe: flags and covered counts exact, totals to 1e-12 relative,
+    against the oracle.  Pillars between the poses and the cells make some rays blocked."""
+    rng = np.random.default_rng(11)
+    ground = np.c_[rng.uniform(-20, 20, (2_500, 2)), rng.normal(0.0, 0.05, 2_500)]
+    pillars = [np.c_[x + rng.normal(0, 0.05, 300), y + rng.normal(0, 0.05, 300),
+                     rng.uniform(0.0, 3.0, 300)] for x, y in ((3.0, 2.0), (-4.0, 5.0), (6.0, -6.0),
+                                                            (0.5, 0.5))]
+    pts = np.concatenate([ground] + pillars).astype(np.float32)
+    cloud = np.zeros((pts.shape[0], 4), np.float32)
+    cloud[:, :3] = pts
+    xyz = np.c_[rng.uniform(-8, 8, (400, 2)), rng.uniform(-0.3, 0.6, 400)]
+    nrm = rng.normal(size=(400, 3)).astype(np.float32)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    poses = np.array([[0.0, 0.0, 2.5, -0.6, 0.0], [-6.0, -6.0, 1.5, -0.3, 0.8],
+                      [7.0, 1.0, 3.0, -0.9, 3.1], [1.0, 7.0, 1.2, 0.0, -1.57]])
+    zx = np.array([-9.0, 9.0, 2.0, -0.5, -0.7])
+    params = _abi.default_vl_params()
+    with _abi.Context(0) as ctx:
+        ctx.set_terrain(cloud)
+        ctx.set_cells(xyz, nrm)
+        fg = np.zeros(400, np.uint8)
+        fr = fg.copy()
+        T = oracle.Cloud(cloud)
+        for tick in range(2):
+            tot, cov, rep = ctx.score_poses(poses, zx, params, fg)
+            r_tot, r_cov, r_rep = oracle.score_poses(T, None, xyz, nrm, poses, zx,
+                                                     oracle.vl_params(), fr)
+            np.testing.assert_array_equal(fg, fr)
+            np.testing.assert_array_equal(cov, r_cov)
+            assert _rel_close(tot, r_tot)
+            assert rep.best_idx == r_rep.best_idx
+        info = ctx.terrain_info()
+        assert info["dims"][0] * info["dims"][1] * info["dims"][2] > 32 * cloud.shape[0]   # sparse
+        assert cov.max() > 0
+
+
 def test_score_poses_edge_states(oracle, scene, cells, aux):
     """No terrain (visible), no aux cloud, zero poses, zero cells, stale terrain tree."""
     params = _abi.default_vl_params(max_distance=12.0)
