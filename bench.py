@@ -441,14 +441,17 @@ def run_all(args, torch, dist, world, rank, local, backend):
     units_h = np.zeros(max(poses.shape[0], 1), np.uint64)
     # N > 1 over RCCL: the per-pose keys never leave the device before the collective --
     # pcp_raycast_fan_keys writes (blocked << 32) | pose into a torch int64 vector (INT64_MAX
-    # in the other ranks' slots) on the library's stream, torch's stream waits on it, one
+    # in the other ranks' slots) on the library's stream and returns once they are written, one
     # all_reduce(MIN) in place, and only the reduced vector comes back D2H.  The gloo
     # rehearsal (ranks sharing one GPU) keeps the host-side vector of dist.reduce_fan.
     dev_keys = dist is not None and on_gpu and backend == "nccl"
     if dev_keys:
         keys_t = torch.empty(P_total, dtype=torch.int64, device=dev)
         units_t = torch.zeros(max(poses.shape[0], 1), dtype=torch.int64, device=dev)
-        stream_ptr = torch.cuda.current_stream(dev).cuda_stream
+        # no stream handle: torch's wheel carries its own HIP runtime, whose hipStream_t means
+        # nothing to libpcp's (/opt/rocm) -- the call waits for its keys before it returns, and
+        # the keys stay on the device for the collective
+        stream_ptr = None
         units_step = {}
 
         def fan_step():

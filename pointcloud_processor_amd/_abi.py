@@ -622,7 +622,8 @@ class Context:
         """pcp_raycast_fan_keys: this rank's poses [lo, lo + P) of p_total as int64 keys
         (blocked << 32) | pose in the DEVICE buffer at keys_dev_ptr (p_total entries, INT64_MAX
         in other ranks' slots), e.g. a torch int64 tensor's data_ptr(); wait_stream: a
-        hipStream_t (torch.cuda.current_stream().cuda_stream) made to wait for the keys."""
+        hipStream_t of libpcp's OWN HIP runtime made to wait for the keys, or None (the call
+        returns once they are written) -- never a torch stream handle (the wheel's runtime)."""
         P = poses5.shape[0]
         if (poses5.dtype != np.float64 or not poses5.flags.c_contiguous or poses5.ndim != 2
                 or poses5.shape[1] != 5):

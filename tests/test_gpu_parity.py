@@ -1162,14 +1162,14 @@ b1, u1, _, _ = gpu.raycast_fan(poses, fan)
 P, world = poses.shape[0], 4
 ref_keys, ref_best = pd.reduce_fan(b1, 0, P, P)
 dev = torch.device("cuda", 0)
-stream = torch.cuda.current_stream(dev).cuda_stream
 units = torch.zeros(P, dtype=torch.int64, device=dev)
 red = None
 for r in range(world):
     lo, hi = pd.shard(P, world, r)
     k = torch.empty(P, dtype=torch.int64, device=dev)
+    # no stream handle: torch's runtime is not libpcp's (the call returns with the keys written)
     gpu.raycast_fan_keys(np.ascontiguousarray(poses[lo:hi]), fan, lo, P, k.data_ptr(),
-                         units.data_ptr() + 8 * lo, stream)
+                         units.data_ptr() + 8 * lo, None)
     red = k if red is None else torch.minimum(red, k)
 kh = red.cpu().numpy()
 assert np.array_equal(kh >> 32, ref_keys)
