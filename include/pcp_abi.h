@@ -326,9 +326,11 @@ int pcp_raycast_fan_stamps(pcp_ctx *ctx, const double *poses5, uint64_t n,
  * keys_dev[p_total] (int64; INT64_MAX in the other ranks' slots), so one all-reduce(MIN) over
  * int64 gives every rank the blocked count of every pose and the argmin (ties: lowest index;
  * virtual_lidar.cpp:467-475).  units_dev (device, nullable, n entries): ray-hit tests per pose.
- * wait_stream (a hipStream_t of the same device, nullable): that stream is made to wait for
- * the keys (hipStreamWaitEvent) and the call returns without a host synchronisation; NULL:
- * the call returns once the keys are written.  No host copy of the results is made. */
+ * wait_stream (a hipStream_t of the same device, created through the SAME HIP runtime that
+ * libpcp links -- not a handle from a framework that bundles its own, such as a PyTorch
+ * wheel; nullable): that stream is made to wait for the keys (hipStreamWaitEvent) and the call
+ * returns without a host synchronisation; NULL: the call returns once the keys are written.
+ * No host copy of the results is made. */
 int pcp_raycast_fan_keys(pcp_ctx *ctx, const double *poses5, uint64_t n,
                          const pcp_fan_params *fan, uint64_t lo, uint64_t p_total,
                          int64_t *keys_dev, uint64_t *units_dev, void *wait_stream);
