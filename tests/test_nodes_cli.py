@@ -139,21 +139,24 @@ def test_excavation_area_node(tmp_path, oracle, small_scene):
     assert res["best_idx"] == rep.best_idx
 
 
-def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells):
+@pytest.mark.parametrize("zc", ["1", "0"])
+def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc):
     """C5 with the launch file's whole chain per frame: filter x2 -> merge ->
     excavated_surface_generator (/excavated_terrain, /excavation_area) -> virtual_lidar
     (terrain index, normals + cell grid, pose search).  Frames 0, 1, 2 and the last one are
     re-run through the oracle from their raw scans: filtered clouds, merged cloud, carved
     terrain and excavation area bit-exact; cells exact, cell normals within 1e-4; candidate
     poses exact (angles 1e-12); totals 1e-12 and the best pose exact (scored with the node's
-    own normals).  Scratch reallocations settle after the first frames."""
+    own normals).  Scratch reallocations settle after the first frames.  Both staging modes:
+    message-sized data read / stored in place in pinned memory (PCP_ZC_IN=1, the default) and
+    DMA'd both ways (0)."""
     np.ascontiguousarray(scene.terrain).tofile(tmp_path / "t.f32")
     np.ascontiguousarray(cells.xyz).tofile(tmp_path / "c.f64")
     np.ascontiguousarray(cells.normals).tofile(tmp_path / "n.f32")
     frames = 8
     res = _run("replay", tmp_path / "t.f32", scene.terrain.shape[0], tmp_path / "c.f64",
                tmp_path / "n.f32", cells.xyz.shape[0], _t(cells.grid_bbox), frames, 60032, 1,
-               tmp_path)
+               tmp_path, env={"PCP_ZC_IN": zc})
     assert res["frames"] == frames and res["chain"] == 1
     assert res["cells"] > 0 and res["merged_points"] > 0 and res["best_idx"] >= 0
     assert 0 < res["p50_ms"] <= res["p99_ms"]
