@@ -60,6 +60,19 @@ static int next_slot(pcp_ctx *ctx) {
     return k;
 }
 
+// slot s must hold `bytes`: when it has to grow, every slot of the ring grows with it (their
+// earlier transfers drained first), so a stream of same-sized messages pays the pinned
+// allocations once, on its first message, not on each slot's first turn
+static int ring_ensure(pcp_ctx *ctx, int s, size_t bytes) {
+    if (bytes <= ctx->up_buf[s].cap) return PCP_OK;
+    for (int k = 0; k < pcp_ctx::kUpRing; ++k) {
+        if (k == ctx->pin_held || ctx->up_buf[k].cap >= bytes) continue;
+        if (ctx->up_used[k]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[k]));
+        PCP_HIP(ctx, ctx->up_buf[k].ensure(bytes));
+    }
+    return PCP_OK;
+}
+
 int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hipStream_t st) {
     if (bytes == 0) return PCP_OK;
     if (bytes > kUploadPinnedMax) {
@@ -69,7 +82,7 @@ int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hip
     const int k = next_slot(ctx);
     if (ctx->up_used[k]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[k]));   // its last DMA
     if (!ctx->up_ev[k]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[k], hipEventDisableTiming));
-    PCP_HIP(ctx, ctx->up_buf[k].ensure(bytes));
+    if (int rc = ring_ensure(ctx, k, bytes)) return rc;
     std::memcpy(ctx->up_buf[k].p, src_h, bytes);
     PCP_HIP(ctx, hipMemcpyAsync(dst_d, ctx->up_buf[k].p, bytes, hipMemcpyHostToDevice, st));
     PCP_HIP(ctx, hipEventRecord(ctx->up_ev[k], st));
@@ -90,7 +103,7 @@ int upload_pieces(pcp_ctx *ctx, void *dst_d, const HostPiece *pc, int k, size_t 
     const int s = next_slot(ctx);
     if (ctx->up_used[s]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[s]));
     if (!ctx->up_ev[s]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[s], hipEventDisableTiming));
-    PCP_HIP(ctx, ctx->up_buf[s].ensure(bytes));
+    if (int rc = ring_ensure(ctx, s, bytes)) return rc;
     for (int i = 0; i < k; ++i)
         if (pc[i].bytes) std::memcpy(static_cast<char *>(ctx->up_buf[s].p) + pc[i].off, pc[i].src,
                                      pc[i].bytes);
@@ -109,7 +122,7 @@ int pin_stage(pcp_ctx *ctx, const HostPiece *pc, int k, size_t bytes, const void
     if (ctx->up_used[s]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[s]));
     ctx->up_used[s] = false;
     if (!ctx->up_ev[s]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[s], hipEventDisableTiming));
-    PCP_HIP(ctx, ctx->up_buf[s].ensure(bytes + 256));
+    if (int rc = ring_ensure(ctx, s, bytes + 256)) return rc;
     for (int i = 0; i < k; ++i)
         if (pc[i].bytes) std::memcpy(static_cast<char *>(ctx->up_buf[s].p) + pc[i].off, pc[i].src,
                                      pc[i].bytes);
@@ -274,7 +287,7 @@ k_scan_tile_sums(const uint32_t *__restrict__ in, uint64_t n, uint32_t *__restri
 // them) receives a second copy of out[0 .. n)
 __global__ void __launch_bounds__(kScanThreads)
 k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
-             uint32_t *__restrict__ out, uint32_t *out2) {
+             uint32_t *__restrict__ out, uint32_t *out2, int zero2) {
     __shared__ uint32_t lds4[4];
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
     uint32_t v[kScanItems];
@@ -292,7 +305,7 @@ k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
         const uint64_t k = base + i;
         if (k < n) {
             out[k] = run;
-            if (out2) out2[k] = run;
+            if (out2) out2[k] = zero2 ? 0u : run;   // zero2: leave out2 (= in) cleared
         }
         run += v[i];
     }
@@ -311,7 +324,7 @@ size_t scan_tmp_bytes(uint64_t n) {
 }
 
 int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp,
-                       uint32_t *out2) {
+                       uint32_t *out2, bool zero2) {
     if (n == 0) {
         PCP_HIP(ctx, hipMemsetAsync(out, 0, sizeof(uint32_t), ctx->stream));
         return PCP_OK;
@@ -319,7 +332,7 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
     const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
     if (tiles == 1) {
         hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, ctx->stream, in, n,
-                           (const uint32_t *)nullptr, out, out2);
+                           (const uint32_t *)nullptr, out, out2, zero2 ? 1 : 0);
         PCP_CHECK_LAUNCH(ctx);
         return PCP_OK;
     }
@@ -332,7 +345,7 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
     int rc = exclusive_scan_u32(ctx, sums, sums_scan, tiles, next);
     if (rc) return rc;
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(kScanThreads), 0, ctx->stream, in,
-                       n, (const uint32_t *)sums_scan, out, out2);
+                       n, (const uint32_t *)sums_scan, out, out2, zero2 ? 1 : 0);
     PCP_CHECK_LAUNCH(ctx);
     return PCP_OK;
 }
@@ -420,6 +433,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->area_nrm.release();
     ctx->carve.release();
     ctx->carve_buf.release();
+    ctx->cell_cnt.release();
     ctx->carve_gen.release();
     ctx->fan_host.release();
     ctx->res_host.release();

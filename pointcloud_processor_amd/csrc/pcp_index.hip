@@ -200,38 +200,59 @@ __device__ __forceinline__ uint64_t peer_mask(uint32_t key) {
     return same;
 }
 
-__global__ void __launch_bounds__(kThreads)
-k_cell_count(const float4 *__restrict__ xyz, uint64_t n, CellMap m, uint32_t *__restrict__ cid,
-             uint32_t *__restrict__ count) {
-    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
-    const float4 p = xyz[i];
-    if (__float_as_uint(p.w) == 0xFFFFFFFFu) {
-        cid[i] = 0xFFFFFFFFu;
-        return;
-    }
-    const uint32_t c = cell_of(m, p.x, p.y, p.z);
-    cid[i] = c;
-    const uint64_t peers = peer_mask(c);
-    if ((threadIdx.x & 63) == (uint32_t)(__ffsll((long long)peers) - 1))
-        atomicAdd(&count[c], (uint32_t)__popcll(peers));
-}
-
-__global__ void __launch_bounds__(kThreads)
-k_cell_scatter(const float4 *__restrict__ xyz, uint64_t n, const uint32_t *__restrict__ cid,
-               uint32_t *__restrict__ cursor, float4 *__restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t c = cid[i];
-    if (c == 0xFFFFFFFFu) return;
-    // one atomic per group of lanes sharing the cell (the order inside a cell is free: z-sorted
-    // indices re-rank by (z, index), the others are queried order-free)
+// a point's cell and its slot in the cell: the count's atomic hands out the slots (one atomic
+// per group of lanes sharing the cell; the order inside a cell is free: z-sorted indices
+// re-rank by (z, index), the others are queried order-free)
+__device__ __forceinline__ void count_ranked(const CellMap &m, float x, float y, float z,
+                                             bool fin, uint32_t *__restrict__ count, uint2 &cr) {
+    const uint32_t c = fin ? cell_of(m, x, y, z) : 0xFFFFFFFFu;
     const uint64_t peers = peer_mask(c);
     const int lane = threadIdx.x & 63, leader = __ffsll((long long)peers) - 1;
     uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&cursor[c], (uint32_t)__popcll(peers));
+    if (fin && lane == leader) base = atomicAdd(&count[c], (uint32_t)__popcll(peers));
     base = __shfl(base, leader, 64);
-    out[base + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull))] = xyz[i];
+    cr = make_uint2(c, base + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull)));
+}
+
+// message-sized clouds (grid geometry from the host's bbox): extraction, cell and slot in one
+// pass over the raw records
+__global__ void __launch_bounds__(kThreads)
+k_extract_count(const unsigned char *__restrict__ raw, uint64_t n, uint32_t step, uint32_t ox,
+                uint32_t oy, uint32_t oz, CellMap m, float4 *__restrict__ xyz,
+                uint32_t *__restrict__ count, uint2 *__restrict__ cr) {
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;   // (whole waves: the peer masks below see only live lanes)
+    const unsigned char *p = raw + i * step;
+    const float x = ld_f32(p, ox), y = ld_f32(p, oy), z = ld_f32(p, oz);
+    const bool fin = isfinite(x) && isfinite(y) && isfinite(z);
+    xyz[i] = make_float4(x, y, z, __uint_as_float(fin ? (uint32_t)i : 0xFFFFFFFFu));
+    uint2 c;
+    count_ranked(m, x, y, z, fin, count, c);
+    cr[i] = c;
+}
+
+// the same after a device-side bbox (large clouds: k_extract + k_bbox_final first)
+__global__ void __launch_bounds__(kThreads)
+k_cell_count_ranked(const float4 *__restrict__ xyz, uint64_t n, CellMap m,
+                    uint32_t *__restrict__ count, uint2 *__restrict__ cr) {
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = xyz[i];
+    const bool fin = __float_as_uint(p.w) != 0xFFFFFFFFu;
+    uint2 c;
+    count_ranked(m, p.x, p.y, p.z, fin, count, c);
+    cr[i] = c;
+}
+
+// each point to its cell's start + its slot: no cursors, no atomics
+__global__ void __launch_bounds__(kThreads)
+k_cell_place(const float4 *__restrict__ xyz, uint64_t n, const uint2 *__restrict__ cr,
+             const uint32_t *__restrict__ start, float4 *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint2 c = cr[i];
+    if (c.x == 0xFFFFFFFFu) return;
+    out[start[c.x] + c.y] = xyz[i];
 }
 
 // points of each cell in descending z: lets a query stop scanning a cell at the first point
@@ -510,8 +531,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     uint32_t nfin;
     // a message-sized cloud: the grid geometry from the host's copy of the same bytes (the
     // same float min / max over the finite points, order-free) -- no round trip through the
-    // stream; the extraction is launched below, once the cell count is known (it also zeroes
-    // the cell counters)
+    // stream; the extraction is launched below, fused with the cell count
     const bool host_bb = n <= kHostBboxMax;
     if (host_bb) {
         host_bbox(v, bb_h, nfin);
@@ -572,38 +592,46 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     g.c = c;
     const GridView gv = g.view();
     CellMap m{gv.ox, gv.oy, gv.oz, gv.inv_c, g.nx, g.ny, g.nz};
-    // 4. count per cell
-    PCP_HIP(ctx, ctx->scratch[2].ensure(n * sizeof(uint32_t)));
-    PCP_HIP(ctx, ctx->scratch[3].ensure((ncell + 1) * sizeof(uint32_t)));
-    if (host_bb) {
-        hipLaunchKernelGGL(k_extract, dim3(nb), dim3(kThreads), 0, st, raw, n, v.point_step,
-                           v.off_x, v.off_y, v.off_z, ctx->scratch[0].as<float4>(), part, part_n,
-                           ctx->scratch[3].as<uint32_t>(), ncell + 1);
+    // 4. each point's cell and slot in it.  The counters are all zero between builds (the scan
+    //    below clears what this build counts), so nothing zeroes them here; a new or grown
+    //    buffer, or one left dirty by a build that stopped early, is cleared first
+    const size_t cnt_b = (ncell + 1) * sizeof(uint32_t);
+    if (ctx->cell_cnt.cap < cnt_b || ctx->cell_cnt_dirty) {
+        PCP_HIP(ctx, ctx->cell_cnt.ensure(cnt_b));
+        PCP_HIP(ctx, hipMemsetAsync(ctx->cell_cnt.p, 0, ctx->cell_cnt.cap, st));
+        ctx->cell_cnt_dirty = false;
+    }
+    uint32_t *cnt = ctx->cell_cnt.as<uint32_t>();
+    PCP_HIP(ctx, ctx->scratch[2].ensure(n * sizeof(uint2)));
+    uint2 *cr = ctx->scratch[2].as<uint2>();
+    const unsigned gridn = (unsigned)((n + kThreads - 1) / kThreads);
+    ctx->cell_cnt_dirty = true;
+    if (host_bb) {   // one pass over the raw records: extraction, cell, slot
+        hipLaunchKernelGGL(k_extract_count, dim3(gridn), dim3(kThreads), 0, st, raw, n,
+                           v.point_step, v.off_x, v.off_y, v.off_z, m,
+                           ctx->scratch[0].as<float4>(), cnt, cr);
         PCP_CHECK_LAUNCH(ctx);
         release_raw();
     } else {
-        PCP_HIP(ctx, hipMemsetAsync(ctx->scratch[3].p, 0, (ncell + 1) * sizeof(uint32_t), st));
+        hipLaunchKernelGGL(k_cell_count_ranked, dim3(gridn), dim3(kThreads), 0, st,
+                           ctx->scratch[0].as<const float4>(), n, m, cnt, cr);
+        PCP_CHECK_LAUNCH(ctx);
     }
-    const unsigned gridn = (unsigned)((n + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(k_cell_count, dim3(gridn), dim3(kThreads), 0, st,
-                       ctx->scratch[0].as<const float4>(), n, m, ctx->scratch[2].as<uint32_t>(),
-                       ctx->scratch[3].as<uint32_t>());
-    PCP_CHECK_LAUNCH(ctx);
-    // 5. prefix -> start
+    // 5. prefix -> start; the scan clears the counters behind it
     PCP_HIP(ctx, g.start.ensure((ncell + 1) * sizeof(uint32_t)));
     PCP_HIP(ctx, ctx->scratch[4].ensure(scan_tmp_bytes(ncell) + (ncell + 1) * sizeof(uint32_t)));
-    // 6. scatter cursors = a copy of start, written by the scan over the counts in place (no
-    //    device-to-device copy)
-    int rc = exclusive_scan_u32(ctx, ctx->scratch[3].as<const uint32_t>(), g.start.as<uint32_t>(),
-                                ncell, ctx->scratch[4].p, ctx->scratch[3].as<uint32_t>());
+    int rc = exclusive_scan_u32(ctx, cnt, g.start.as<uint32_t>(), ncell, ctx->scratch[4].p, cnt,
+                                true);
     if (rc) return rc;
+    ctx->cell_cnt_dirty = false;
+    // 6. every point to its cell's start + its slot
     PCP_HIP(ctx, g.pts.ensure((size_t)nfin * sizeof(float4)));
-    // (with zsort the scatter lands in a temporary and the rank pass writes g.pts)
+    // (with zsort the points land in a temporary and the rank pass writes g.pts)
     if (zsort) PCP_HIP(ctx, ctx->scratch[5].ensure((size_t)nfin * sizeof(float4)));
     float4 *scat = zsort ? ctx->scratch[5].as<float4>() : g.pts.as<float4>();
-    hipLaunchKernelGGL(k_cell_scatter, dim3(gridn), dim3(kThreads), 0, st,
-                       ctx->scratch[0].as<const float4>(), n, ctx->scratch[2].as<const uint32_t>(),
-                       ctx->scratch[3].as<uint32_t>(), scat);
+    hipLaunchKernelGGL(k_cell_place, dim3(gridn), dim3(kThreads), 0, st,
+                       ctx->scratch[0].as<const float4>(), n, (const uint2 *)cr,
+                       g.start.as<const uint32_t>(), scat);
     PCP_CHECK_LAUNCH(ctx);
     // 7. descending z inside each cell (the ray-march indices only)
     if (zsort) {

@@ -238,6 +238,11 @@ struct pcp_ctx {
     // excavated-terrain carve (pcp_excavate): index of the input cloud + scratch
     pcp::GridIndex carve;
     pcp::DevBuf carve_buf;
+    // the index builds' per-cell counters: all zero between builds (the build's scan clears what
+    // it counted), so no build zeroes them; cell_cnt_dirty marks a build that stopped between
+    // its count and its scan (the next one clears the buffer first)
+    pcp::DevBuf cell_cnt;
+    bool cell_cnt_dirty = false;
     // the generated lattice (surface + area records, their height queries) on the device:
     // [GenPoint surf | GenPoint area | queries (G generated + n input) | area records].  It
     // depends on the parameters and the excavation pose alone; while carve_key matches, the
@@ -368,9 +373,10 @@ int terrain_blocks_before_query(pcp_ctx *ctx);
 // scan: exclusive prefix sum of n uint32 values into out (n + 1 entries, out[n] = total).
 // tmp must hold scan_tmp_bytes(n).
 size_t scan_tmp_bytes(uint64_t n);
-// out2 (optional, may alias in): a second copy of out[0 .. n), e.g. a scatter's cursors
+// out2 (optional, may alias in): a second copy of out[0 .. n), e.g. a scatter's cursors; with
+// zero2 it is cleared instead (out2 = in: counters left zero for their next use)
 int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp,
-                       uint32_t *out2 = nullptr);
+                       uint32_t *out2 = nullptr, bool zero2 = false);
 
 // fan query up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip): device results
 // in flight on return, the caller synchronizes.  n > 0.
