@@ -60,6 +60,36 @@ static int next_slot(pcp_ctx *ctx) {
     return k;
 }
 
+// host (pinned) -> device copy by a kernel on the stream itself: no copy-engine hand-off
+// before the next kernel (a DMA's submission and the engine switch cost ~15 + ~14 us here)
+__global__ void __launch_bounds__(256)
+k_copy_pinned(const unsigned char *__restrict__ src, unsigned char *__restrict__ dst,
+              uint64_t bytes) {
+    const uint64_t n16 = bytes >> 4;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride)
+        reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+    if (blockIdx.x == 0 && threadIdx.x < (bytes & 15))
+        dst[(n16 << 4) + threadIdx.x] = src[(n16 << 4) + threadIdx.x];
+}
+
+int copy_pinned_async(pcp_ctx *ctx, void *dst_d, const void *src_pinned, size_t bytes,
+                      hipStream_t st) {
+    if (!bytes) return PCP_OK;
+    // both 16-byte aligned (device allocations and pinned slots are; offsets are the caller's)
+    if (!ctx->copy_kernel || (((uintptr_t)dst_d | (uintptr_t)src_pinned) & 15u)) {
+        PCP_HIP(ctx, hipMemcpyAsync(dst_d, src_pinned, bytes, hipMemcpyHostToDevice, st));
+        return PCP_OK;
+    }
+    const uint64_t n16 = (bytes + 15) / 16;
+    const unsigned g = (unsigned)std::min<uint64_t>((n16 + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_copy_pinned, dim3(g), dim3(256), 0, st,
+                       static_cast<const unsigned char *>(src_pinned),
+                       static_cast<unsigned char *>(dst_d), (uint64_t)bytes);
+    PCP_CHECK_LAUNCH(ctx);
+    return PCP_OK;
+}
+
 // slot s must hold `bytes`: when it has to grow, every slot of the ring grows with it (their
 // earlier transfers drained first), so a stream of same-sized messages pays the pinned
 // allocations once, on its first message, not on each slot's first turn
@@ -84,7 +114,7 @@ int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hip
     if (!ctx->up_ev[k]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[k], hipEventDisableTiming));
     if (int rc = ring_ensure(ctx, k, bytes)) return rc;
     std::memcpy(ctx->up_buf[k].p, src_h, bytes);
-    PCP_HIP(ctx, hipMemcpyAsync(dst_d, ctx->up_buf[k].p, bytes, hipMemcpyHostToDevice, st));
+    if (int rc = copy_pinned_async(ctx, dst_d, ctx->up_buf[k].p, bytes, st)) return rc;
     PCP_HIP(ctx, hipEventRecord(ctx->up_ev[k], st));
     ctx->up_used[k] = true;
     return PCP_OK;
@@ -107,7 +137,7 @@ int upload_pieces(pcp_ctx *ctx, void *dst_d, const HostPiece *pc, int k, size_t 
     for (int i = 0; i < k; ++i)
         if (pc[i].bytes) std::memcpy(static_cast<char *>(ctx->up_buf[s].p) + pc[i].off, pc[i].src,
                                      pc[i].bytes);
-    PCP_HIP(ctx, hipMemcpyAsync(dst_d, ctx->up_buf[s].p, bytes, hipMemcpyHostToDevice, st));
+    if (int rc = copy_pinned_async(ctx, dst_d, ctx->up_buf[s].p, bytes, st)) return rc;
     PCP_HIP(ctx, hipEventRecord(ctx->up_ev[s], st));
     ctx->up_used[s] = true;
     return PCP_OK;
@@ -395,6 +425,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
     if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff) != 0;
     if (const char *zc = std::getenv("PCP_ZC_IN")) ctx->zc_in = std::atoi(zc) != 0;
+    if (const char *ck = std::getenv("PCP_COPY_KERNEL")) ctx->copy_kernel = std::atoi(ck) != 0;
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
     if (const char *tf = std::getenv("PCP_TERRAIN_FINE")) ctx->terrain_fine = std::atoi(tf);
     if (const char *tt = std::getenv("PCP_FINE_TILE")) ctx->fine_tile = std::atoi(tt);

@@ -271,6 +271,8 @@ struct pcp_ctx {
     bool up_used[kUpRing] = {};
     int up_next = 0;
     int pin_held = -1;                       // ring slot held by pin_stage until pin_release
+    bool copy_kernel = true;                 // pinned -> device uploads by a copy kernel on the
+                                             // stream (PCP_COPY_KERNEL; 0: DMA)
     bool zc_in = true;                       // message-sized inputs read in place from pinned
                                              // memory (PCP_ZC_IN; 0: DMA'd first)
     pcp::PinnedBuf tc_host;                  // transform_concat / carve: records stored by the
@@ -456,6 +458,10 @@ int read_small(pcp_ctx *ctx, void *dst, const void *src_d, size_t bytes, hipStre
 // src_h on return either way.
 constexpr size_t kUploadPinnedMax = 16u << 20;
 int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hipStream_t st);
+// pinned host -> device by a copy kernel on st (no copy-engine hand-off); unaligned pointers
+// take hipMemcpyAsync
+int copy_pinned_async(pcp_ctx *ctx, void *dst_d, const void *src_pinned, size_t bytes,
+                      hipStream_t st);
 // several host pieces into one pinned slot at their byte offsets, then ONE DMA of `bytes`
 // (the gaps between pieces are don't-care bytes on the device)
 struct HostPiece {

@@ -1845,8 +1845,8 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
                                : stats ? ((size_t)P * waves * 4 + 4) * sizeof(uint64_t)
                                        : 64 * sizeof(uint64_t);
     PCP_HIP(ctx, ctx->stats_d.ensure(stats_bytes));
-    PCP_HIP(ctx, hipMemcpyAsync(ctx->poses_d.p, pose8, (size_t)P * 8 * sizeof(double),
-                                hipMemcpyHostToDevice, st));
+    if (int rc0 = copy_pinned_async(ctx, ctx->poses_d.p, pose8, (size_t)P * 8 * sizeof(double), st))
+        return rc0;
     // results land in device memory, or (host_out) straight in the pinned block behind the
     // staged poses: one copy and its dispatch fewer per query
     unsigned long long *units_d =

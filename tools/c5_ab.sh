@@ -5,8 +5,10 @@ set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out/replay
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_nodes_cli.py -x -q --timeout 300 --timeout-method thread > gpurun_out/c5ab_tests.log 2>&1 || { tail -40 gpurun_out/c5ab_tests.log; exit 1; }
-tail -1 gpurun_out/c5ab_tests.log
+if [ -z "${SKIP_TESTS:-}" ]; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_nodes_cli.py -x -q --timeout 300 --timeout-method thread > gpurun_out/c5ab_tests.log 2>&1 || { tail -40 gpurun_out/c5ab_tests.log; exit 1; }
+  tail -1 gpurun_out/c5ab_tests.log
+fi
 FRAMES=2 timeout -k 10 300 bash tools/replay.sh > /dev/null 2>&1 || exit 1   # writes the inputs
 read TN CN BB < gpurun_out/replay/args
 for r in 1 2; do for v in $VALUES; do
