@@ -120,9 +120,15 @@ k_heights(GridView g, float r2, double radius, const double2 *__restrict__ qxy,
     if (g.n_pts && stencil_cell3_f(g, qx, qy, qz, ix, iy, iz)) {
         const uint32_t nx = (uint32_t)g.nx, nxy = nx * (uint32_t)g.ny;
         const uint32_t lin = ix + nx * iy + nxy * iz;
+        uint32_t lo4[4], hi4[4];   // the 4 rows' ranges first: 8 independent loads
+#pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t row = lin + (r & 1) * nx + (r >> 1) * nxy;
-            const uint32_t lo = g.start[row], hi = g.start[row + 2];
+            lo4[r] = g.start[row];
+            hi4[r] = g.start[row + 2];
+        }
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t lo = lo4[r], hi = hi4[r];
             for (uint32_t k = lo + lane; k < hi; k += 64) {
                 const P3 p = ld_p3(g.pts, k);
                 if (!flann_within(qx, qy, qz, p, r2)) continue;
@@ -163,18 +169,31 @@ k_nearest(GridView g, const double2 *__restrict__ qxy, const uint32_t *__restric
         const float qx = (float)xy.x, qy = (float)xy.y, qz = 0.0f;
         float bd = INFINITY;
         uint32_t bi = UINT32_MAX, bk = 0;
-        for (uint32_t k = threadIdx.x; k < g.n_pts; k += kCT) {
-            const float4 p = g.pts[k];
-            const float d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
-            float acc = 0.0f;
-            acc = acc + d0 * d0;
-            acc = acc + d1 * d1;
-            acc = acc + d2 * d2;
-            const uint32_t oi = __float_as_uint(p.w);
-            if (acc < bd || (acc == bd && oi < bi)) {
-                bd = acc;
-                bi = oi;
-                bk = k;
+        // four independent loads in flight per step (the minimum of (distance, index) does not
+        // depend on the order the points are taken in)
+        constexpr int kU = 4;
+        for (uint32_t k0 = threadIdx.x; k0 < g.n_pts; k0 += kU * kCT) {
+            float4 pu[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint32_t k = k0 + u * kCT;
+                pu[u] = g.pts[k < g.n_pts ? k : k0];
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint32_t k = k0 + u * kCT;
+                const float4 p = pu[u];
+                const float d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
+                float acc = 0.0f;
+                acc = acc + d0 * d0;
+                acc = acc + d1 * d1;
+                acc = acc + d2 * d2;
+                const uint32_t oi = __float_as_uint(p.w);
+                if (k < g.n_pts && (acc < bd || (acc == bd && oi < bi))) {
+                    bd = acc;
+                    bi = oi;
+                    bk = k;
+                }
             }
         }
 #pragma unroll

@@ -1020,7 +1020,10 @@ struct CandArgs {
     double *lat;           // gs*gs x 6: valid, x, y, z, pitch, yaw
 };
 
-__global__ void __launch_bounds__(kT) k_candidates(CandArgs a) {
+// 1,024 threads per lattice point: the ground query's rows of cells (~600 for a 0.12 m terrain
+// grid) one per thread, so a block's latency is one row walk, not three
+constexpr int kCandT = 1024;
+__global__ void __launch_bounds__(kCandT) k_candidates(CandArgs a) {
     const int l = blockIdx.x;
     const int i = l / a.gs, j = l - i * a.gs;
     const double x = a.exminx + i * a.xs;
@@ -1049,7 +1052,7 @@ __global__ void __launch_bounds__(kT) k_candidates(CandArgs a) {
         rng(-2.0 - m, 2.0 + m, g.oz, g.nz, z0, z1);
         if (x0 <= x1 && y0 <= y1 && z0 <= z1) {
             const int ny_r = y1 - y0 + 1, rows = ny_r * (z1 - z0 + 1);
-            for (int r = threadIdx.x; r < rows; r += kT) {
+            for (int r = threadIdx.x; r < rows; r += kCandT) {
                 const int iy = y0 + r % ny_r, iz = z0 + r / ny_r;
                 const size_t row = (size_t)g.nx * ((size_t)iy + (size_t)g.ny * iz);
                 const uint32_t s = g.start[row + x0], e = g.start[row + x1 + 1];
@@ -1063,13 +1066,13 @@ __global__ void __launch_bounds__(kT) k_candidates(CandArgs a) {
         }
     }
     // block max
-    __shared__ double red[kT / 64];
+    __shared__ double red[kCandT / 64];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mz = fmax(mz, __shfl_xor(mz, o, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mz;
     __syncthreads();
     if (threadIdx.x != 0) return;
-    for (int w = 1; w < kT / 64; ++w) mz = fmax(mz, red[w]);
+    for (int w = 1; w < kCandT / 64; ++w) mz = fmax(mz, red[w]);
     const double ground = (mz != -DBL_MAX) ? mz : 0.0;
     const double z = ground + a.sensor_height;
     const double dx = a.cx - x, dy = a.cy - y, dz = a.cz - z;
@@ -1471,7 +1474,7 @@ int pcp_generate_candidates(pcp_ctx *ctx, const double bb[6], const pcp_vl_param
                                                  (size_t)L * 5 * sizeof(double));
     {
         ProfScope ps(ctx, PCP_K_CANDIDATES);
-        hipLaunchKernelGGL(k_candidates, dim3(L), dim3(kT), 0, ctx->stream, a);
+        hipLaunchKernelGGL(k_candidates, dim3(L), dim3(kCandT), 0, ctx->stream, a);
         PCP_CHECK_LAUNCH(ctx);
         hipLaunchKernelGGL(k_cand_compact, dim3(1), dim3(1024), 0, ctx->stream,
                            ctx->out_a.as<const double>(), L, outp, n_d);
@@ -1731,7 +1734,7 @@ int pcp_generate_and_score(pcp_ctx *ctx, const double bb[6], const pcp_vl_params
     uint32_t *n_h = reinterpret_cast<uint32_t *>(poses_h + 5 * (size_t)L);
     {
         ProfScope ps(ctx, PCP_K_CANDIDATES);
-        hipLaunchKernelGGL(k_candidates, dim3((unsigned)L), dim3(kT), 0, ctx->stream, a);
+        hipLaunchKernelGGL(k_candidates, dim3((unsigned)L), dim3(kCandT), 0, ctx->stream, a);
         PCP_CHECK_LAUNCH(ctx);
         hipLaunchKernelGGL(k_cand_compact, dim3(1), dim3(1024), 0, ctx->stream,
                            ctx->out_a.as<const double>(), (int)L, poses_d, n_d, poses_h, n_h);
