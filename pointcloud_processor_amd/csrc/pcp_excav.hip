@@ -299,32 +299,54 @@ k_lattice_flags(GridView g, float r2, Lattice L, uint8_t *__restrict__ flags) {
     if (lane == 0) flags[li] = hit ? 1 : 0;
 }
 
-// one block: the flagged lattice points in order -> cells (double xyz); *n_out = count
+// one block: the flagged lattice points in order -> cells (double xyz); *n_out = count.  Each
+// thread takes 4 consecutive lattice points per round (one 4-byte load of their flags), so a
+// round covers 4,096 points: a quarter of the dependent rounds of one point per thread
 __global__ void __launch_bounds__(1024)
 k_lattice_compact(const uint8_t *__restrict__ flags, Lattice L, double *__restrict__ cells,
                   uint32_t cap, uint32_t *__restrict__ n_out, uint32_t *__restrict__ n_host) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     __shared__ uint32_t wc[16];
     uint32_t run = 0;
-    for (uint32_t base = 0; base < L.total; base += 1024) {
-        const uint32_t li = base + threadIdx.x;
-        const bool f = li < L.total && flags[li];
-        const uint64_t bal = __ballot(f);
-        if (lane == 0) wc[wid] = (uint32_t)__popcll(bal);
+    for (uint32_t base = 0; base < L.total; base += 4096) {
+        const uint32_t li0 = base + 4 * threadIdx.x;
+        uint32_t f4 = 0;
+        if (li0 + 3 < L.total) {
+            f4 = *reinterpret_cast<const uint32_t *>(flags + li0);   // 4-aligned: base, 4 t
+        } else {
+            for (int j = 0; j < 4; ++j)
+                if (li0 + j < L.total && flags[li0 + j]) f4 |= 1u << (8 * j);
+        }
+        uint32_t fl = 0;   // bit j: lattice point li0 + j flagged
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fl |= ((f4 >> (8 * j)) & 0xFFu) ? (1u << j) : 0u;
+        const uint32_t c = (uint32_t)__popc(fl);
+        // exclusive scan of c over the block: within the wave, then the waves' totals
+        uint32_t inc = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += v;
+        }
+        if (lane == 63) wc[wid] = inc;
         __syncthreads();
         uint32_t pre = 0, tot = 0;
         for (int w = 0; w < 16; ++w) {
             pre += w < wid ? wc[w] : 0u;
             tot += wc[w];
         }
-        if (f) {
-            const uint32_t d = run + pre + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-            if (d < cap) {
-                double x, y, z;
-                lattice_xyz(L, li, x, y, z);
-                cells[3 * (size_t)d] = x;
-                cells[3 * (size_t)d + 1] = y;
-                cells[3 * (size_t)d + 2] = z;
+        uint32_t d = run + pre + inc - c;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if ((fl >> j) & 1u) {
+                if (d < cap) {
+                    double x, y, z;
+                    lattice_xyz(L, li0 + j, x, y, z);
+                    cells[3 * (size_t)d] = x;
+                    cells[3 * (size_t)d + 1] = y;
+                    cells[3 * (size_t)d + 2] = z;
+                }
+                ++d;
             }
         }
         run += tot;
