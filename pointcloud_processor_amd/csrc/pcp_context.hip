@@ -429,6 +429,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
     if (const char *tf = std::getenv("PCP_TERRAIN_FINE")) ctx->terrain_fine = std::atoi(tf);
     if (const char *tt = std::getenv("PCP_FINE_TILE")) ctx->fine_tile = std::atoi(tt);
+    if (const char *fs = std::getenv("PCP_FINE_SKIP")) ctx->fine_skip = std::atoi(fs) == 2 ? 2 : 1;
     if (const char *fp = std::getenv("PCP_FINE_PACK")) ctx->fine_pack = std::atoi(fp) != 0;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&

@@ -137,7 +137,8 @@ k_win_place(const float4 *__restrict__ pts, const uint32_t *__restrict__ zord,
 __global__ void __launch_bounds__(kThreads)
 k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ cstart, CellMap m, double c,
        uint32_t fnx, uint32_t fny, uint32_t rz, uint32_t tsteps, int tile,
-       uint2 *__restrict__ frec, uint16_t *__restrict__ fband, uint32_t *__restrict__ fstart) {
+       int skip2, uint2 *__restrict__ frec, uint16_t *__restrict__ fband,
+       uint32_t *__restrict__ fstart) {
     const uint32_t nw = fnx * fny, w = blockIdx.x * kThreads + threadIdx.x;
     // tiles of T x T records: 4 x 4 8-byte records (tile 1) or 8 x 8 split records (tile 2),
     // 128 bytes of probe data each
@@ -169,8 +170,8 @@ k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ cstart, CellMap m
                           __uint_as_float(0xFFFFFFFFu));
     // one pass down the run: jt / jb advance monotonically, each entry's z and coarse z cell
     // loaded once per pointer (the walk of every level reuses them)
-    uint32_t jt = s, jb = s, j2 = s;
-    float zt = wpts[s].z, zb = zt, zlast = zt, z2 = zt;
+    uint32_t jt = s, jb = s, j2 = s, j3 = s;
+    float zt = wpts[s].z, zb = zt, zlast = zt, z2 = zt, z3 = zt;
     int ct = s < e ? cell_z(m, zt) : -1, cb = ct;
     for (int iz = (int)rz - 1; iz >= 0; --iz) {
         while (jt < e && ct > iz + 1) {
@@ -198,18 +199,30 @@ k_frec(float4 *__restrict__ wpts, const uint32_t *__restrict__ cstart, CellMap m
             band = lo2 | (hi2 << 8);
         }
         // split records: the entries from jt that lie at or above oz + (iz + 1.5) c (at most
-        // 15 of them) can be skipped by a query more than r below that height (march, FN 8)
-        uint32_t skip = 0;
+        // 15 of them) can be skipped by a query more than r below that height (march, FN 8).
+        // skip2: two thresholds, iz + 1.375 and iz + 1.6875 (exact in float), at most 15 and 7
+        // entries, with a 25-bit start (build_fine: below 2^25 entries)
+        uint32_t word = jt;
         if (tile == 2) {
             if (j2 < jt) {
                 j2 = jt;
                 z2 = zt;
             }
-            const double h2 = m.oz + ((double)iz + 1.5) * c;
+            const double h2 = m.oz + ((double)iz + (skip2 ? 1.375 : 1.5)) * c;
             while (j2 < e && (double)z2 >= h2) z2 = wpts[++j2].z;
-            skip = min(j2 - jt, 15u);
+            if (skip2) {
+                if (j3 < jt) {
+                    j3 = jt;
+                    z3 = zt;
+                }
+                const double h3 = m.oz + ((double)iz + 1.6875) * c;
+                while (j3 < e && (double)z3 >= h3) z3 = wpts[++j3].z;
+                word = jt | (min(j2 - jt, 15u) << 25) | (min(j3 - jt, 7u) << 29);
+            } else {
+                word = jt | (min(j2 - jt, 15u) << 28);
+            }
         }
-        put((size_t)iz * plane + base, jt | (skip << 28), band);
+        put((size_t)iz * plane + base, word, band);
     }
 }
 
@@ -234,11 +247,13 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     const CellMap m{gv.ox, gv.oy, gv.oz, gv.inv_c, g.nx, g.ny, g.nz};
     const int F = std::max(2, std::min(ctx->terrain_fine, 8));
     const uint64_t fnx = (uint64_t)F * g.nx, fny = (uint64_t)F * g.ny;
-    const uint64_t rz = (uint64_t)(g.nz > 1 ? g.nz - 1 : 0), nw = fnx * fny;
+    const uint64_t rz = (uint64_t)(g.nz > 1 ? g.nz - 1 : 0);
     // caps: 32-bit record byte offsets (< 2^29 records), 24-bit probe multiplies, window keys
     const int tile = ctx->fine_tile == 2 ? 2 : ctx->fine_tile ? 1 : 0;
     const uint64_t T = tile == 2 ? 8 : 4;
-    const uint64_t nrec = tile ? ((fnx + T - 1) / T) * ((fny + T - 1) / T) * T * T * rz : nw * rz;
+    const uint64_t nrec = tile ? ((fnx + T - 1) / T) * ((fny + T - 1) / T) * T * T * rz
+                               : fnx * fny * rz;
+    const uint64_t nw = fnx * fny;   // windows (the runs)
     const size_t band_bytes = ((size_t)nrec * 2 + 255) & ~(size_t)255;
     const size_t rec_bytes = tile == 2 ? band_bytes + (size_t)nrec * 4 : (size_t)nrec * sizeof(uint2);
     if (rz == 0 || nrec >= (1ull << 29) || fnx >= (1ull << 24) || fny * rz >= (1ull << 24)) {
@@ -328,12 +343,15 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
                        pts, (const uint32_t *)zord, (const uint32_t *)wk1, (const uint32_t *)rk1,
                        np, went);
     PCP_CHECK_LAUNCH(ctx);
-    // 5. records (and the sentinels)
+    // 5. records (and the sentinels), one thread per window; two skip thresholds need a 25-bit
+    // walk start
+    const bool skip2 = tile == 2 && ctx->fine_skip == 2 && nent < (1ull << 25);
     const uint32_t tsteps = (uint32_t)std::ceil((g.r_q + 2e-3) / g.c / (double)kZq);
     const uint64_t nthr = std::max<uint64_t>(nw, tile ? nrec / rz : 0);
     hipLaunchKernelGGL(k_frec, dim3((unsigned)((nthr + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                        st, went, (const uint32_t *)cstart, m, g.c, (uint32_t)fnx,
-                       (uint32_t)fny, (uint32_t)rz, tsteps, tile, g.frec.as<uint2>(),
+                       (uint32_t)fny, (uint32_t)rz, tsteps, tile, skip2 ? 1 : 0,
+                       g.frec.as<uint2>(),
                        g.frec.as<uint16_t>(),
                        reinterpret_cast<uint32_t *>(g.frec.as<char>() + band_bytes));
     PCP_CHECK_LAUNCH(ctx);
@@ -349,6 +367,7 @@ int build_fine(pcp_ctx *ctx, GridIndex &g) {
     g.frz = (uint32_t)rz;
     g.ffine = (float)F;
     g.ftile = tile;
+    g.fskip = skip2 ? 2 : 1;
     g.fstart_off = tile == 2 ? band_bytes : 0;
     g.fine_ok = true;
     return PCP_OK;

@@ -75,6 +75,7 @@ GridView GridIndex::view() const {
                    ? reinterpret_cast<const uint32_t *>(frec.as<const char>() + fstart_off)
                    : nullptr;
     v.fus_off = (float)(rm * v.inv_c / (double)kZq);
+    v.fskip = fine_ok ? fskip : 1;
     return v;
 }
 

@@ -140,9 +140,12 @@ struct GridView {               // POD passed to kernels by value
     // ftile 2: the record split in two arrays of 8 x 8 xy tiles -- the probe's 2-byte
     // thresholds (one 128-byte line per tile) and the 4-byte walk start, read by candidates only
     const uint16_t *fband;
-    const uint32_t *fstart;     // walk start (28 bits) | skip (4 bits, << 28): entries of the
-                                // run at or above oz + (iz + 1.5) c, skipped by a candidate
-                                // whose q lies more than r below that height
+    const uint32_t *fstart;     // fskip 1: walk start (28 bits) | skip (4 bits, << 28): entries
+                                // of the run at or above oz + (iz + 1.5) c, skipped by a
+                                // candidate whose q lies more than r below that height; fskip 2:
+                                // start (25 bits) | skips at iz + 1.375 (4 bits, << 25) and
+                                // iz + 1.6875 (3 bits, << 29)
+    int32_t fskip;
     float fzc, fzo;             // c and oz in float (the skip test)
     int32_t wpack;              // wpts entries packed to 12 bytes (x, y, z), PCP_FINE_PACK
 };
@@ -166,6 +169,7 @@ struct GridIndex {
     int32_t wpack = 0;           // wpts as 12-byte (x, y, z) entries
     float ffine = 0.0f;
     int32_t ftile = 0;
+    int32_t fskip = 1;           // walk-start skip thresholds (PCP_FINE_SKIP)
     size_t fstart_off = 0;       // ftile 2: byte offset of the start array inside frec
     bool occ2_ok = false;        // occ2 built (only indices queried by stencil_any need it)
     GridView view() const;
@@ -294,6 +298,7 @@ struct pcp_ctx {
                                              // kernels into pinned memory (PCP_FM_HOST_OUT)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
     int fine_pack = 1;                       // fine-window entries as 12 bytes (PCP_FINE_PACK)
+    int fine_skip = 2;                       // split records' skip thresholds: 1 or 2
     int fine_tile = 2;                       // fine records: 0 x-fastest, 1 4 x 4 tiles, 2 split
                                              // in 8 x 8 tiles (PCP_FINE_TILE)
     int terrain_fine = 2;                    // fine-window layout of that copy, cells of c / F

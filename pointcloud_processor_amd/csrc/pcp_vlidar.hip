@@ -145,6 +145,9 @@ __device__ __forceinline__ bool scan_window3(const float *pts, uint32_t k, float
         const P3 p = P3{f[0], f[1], f[2]};
         ++k;
         if (STATS) cnt[2] += 1;
+#ifdef PCP_WALK_CENSUS
+        if (STATS && p.z - qz >= rexit) cnt[3] += 1;   // an entry r above q: a later start skips it
+#endif
         within = flann_within(qx, qy, qz, p, r2);
         stop = within | (qz - p.z >= rexit);
     } while (!stop);
@@ -160,6 +163,9 @@ __device__ __forceinline__ bool scan_window(const float4 *pts, uint32_t k, float
     do {   // one exit condition: simple exec-mask bookkeeping per step
         const P3 p = ld_p3o(pts, k++);
         if (STATS) cnt[2] += 1;
+#ifdef PCP_WALK_CENSUS
+        if (STATS && p.z - qz >= rexit) cnt[3] += 1;
+#endif
         within = flann_within(qx, qy, qz, p, r2);
         stop = within | (qz - p.z >= rexit);
     } while (!stop);
@@ -321,13 +327,24 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
                 uint32_t w0 = R.x;
                 if (FN == 8) {   // skip the run's entries > r above q (pcp_fine.hip, k_frec)
                     const uint32_t ws = ld_u32o(g.fstart, ri);
-                    const float h2 = __builtin_fmaf((float)iz + 1.5f, g.fzc, g.fzo);
-                    // h2 is the record's double height rounded through fzo, fzc and the fma
-                    // (a few ulps of the larger magnitude): the margin grows with it, so far
-                    // from the origin (|z| of km) the skip stays exact
-                    const float marg =
-                        1e-4f + 4.0f * FLT_EPSILON * (fabsf(h2) + fabsf(g.fzo) + fabsf(qz));
-                    w0 = (ws & 0x0FFFFFFFu) + (qz + (rexit + marg) < h2 ? ws >> 28 : 0u);
+                    // the thresholds are the record's double heights rounded through fzo, fzc
+                    // and the fma (a few ulps of the larger magnitude): the margin grows with
+                    // them, so far from the origin (|z| of km) the skip stays exact
+                    if (g.fskip == 2) {
+                        const float ha = __builtin_fmaf((float)iz + 1.375f, g.fzc, g.fzo);
+                        const float hb = __builtin_fmaf((float)iz + 1.6875f, g.fzc, g.fzo);
+                        const float marg = 1e-4f + 4.0f * FLT_EPSILON *
+                                                       (fmaxf(fabsf(ha), fabsf(hb)) +
+                                                        fabsf(g.fzo) + fabsf(qz));
+                        const float v = qz + (rexit + marg);
+                        w0 = (ws & 0x01FFFFFFu) +
+                             (v < ha ? (ws >> 25) & 15u : v < hb ? ws >> 29 : 0u);
+                    } else {
+                        const float h2 = __builtin_fmaf((float)iz + 1.5f, g.fzc, g.fzo);
+                        const float marg =
+                            1e-4f + 4.0f * FLT_EPSILON * (fabsf(h2) + fabsf(g.fzo) + fabsf(qz));
+                        w0 = (ws & 0x0FFFFFFFu) + (qz + (rexit + marg) < h2 ? ws >> 28 : 0u);
+                    }
                 }
                 if (g.wpack ? scan_window3<STATS>(reinterpret_cast<const float *>(g.wpts), w0, qx,
                                                   qy, qz, r2, rexit, cnt)
@@ -1215,7 +1232,7 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p0, uint32_t
     unsigned long long t0 = 0, t1 = 0, t2 = 0;
     if (MODE == FAN_STAMPS) t0 = __builtin_amdgcn_s_memtime();
     int hit = -1;
-    uint32_t cnt[3] = {0, 0, 0};
+    uint32_t cnt[4] = {0, 0, 0, 0};   // [3]: PCP_WALK_CENSUS builds only
     if (active && a.present) {
         const double *P = a.pose + 8 * (size_t)p;
         const double cy = P[5], sy = P[6];
@@ -1245,7 +1262,8 @@ __device__ __forceinline__ void fan_body(const FanArgs &a, uint32_t p0, uint32_t
 #pragma unroll
         for (int c = 0; c < 4; ++c) {   // [3] directory loads: one per scan (none: FN, the
                                         // probe's record is the directory)
-            unsigned long long v = c < 3 ? cnt[c] : (FN ? 0u : cnt[1]);
+            // (a PCP_WALK_CENSUS build: FN's [3] = the walks' tests of entries r above q)
+            unsigned long long v = c < 3 ? cnt[c] : (FN ? cnt[3] : cnt[1]);
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
             if ((threadIdx.x & 63) == 0 && wid < a.waves) a.stats[c * nw + wslot] = v;

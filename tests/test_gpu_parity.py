@@ -468,12 +468,15 @@ def test_into_wrappers_match(gpu, loaded, scene, cells):
     assert r2.best_idx == rep.best_idx and r2.green == rep.green
 
 
-@pytest.mark.parametrize("npw,tile", [("1", "2"), ("2", "2"), ("8", "2"), ("8", "1")])
-def test_raycast_fan_poses_per_wave(oracle, loaded, scene, cells, npw, tile, monkeypatch):
+@pytest.mark.parametrize("npw,tile,skip", [("1", "2", "1"), ("2", "2", "1"), ("8", "2", "1"),
+                                           ("8", "1", "1"), ("8", "2", "2")])
+def test_raycast_fan_poses_per_wave(oracle, loaded, scene, cells, npw, tile, skip, monkeypatch):
     """64 poses (P % 64 == 0: the XCD-chunk kernel with NPW poses per wave, its step table in
-    LDS) on split and 8-byte fine records: blocked counts, units and first hits exact."""
+    LDS) on split and 8-byte fine records, split records with one or two walk-start skip
+    thresholds (PCP_FINE_SKIP): blocked counts, units and first hits exact."""
     T, _ = loaded
     monkeypatch.setenv("PCP_FAN_NPW", npw)
+    monkeypatch.setenv("PCP_FINE_SKIP", skip)
     monkeypatch.setenv("PCP_FINE_TILE", tile.rstrip("u"))
     monkeypatch.setenv("PCP_FINE_PACK", "0" if tile.endswith("u") else "1")
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", "2")
@@ -558,13 +561,15 @@ def test_raycast_fan_clutter_and_odd_fans(oracle, n_az, n_el):
         ctx.close()
 
 
-@pytest.mark.parametrize("dz", [3000.0, -2500.0])
-def test_raycast_fan_far_from_origin(oracle, scene, cells, dz, monkeypatch):
+@pytest.mark.parametrize("dz,skip", [(3000.0, "1"), (-2500.0, "1"), (3000.0, "2"),
+                                     (-2500.0, "2")])
+def test_raycast_fan_far_from_origin(oracle, scene, cells, dz, skip, monkeypatch):
     """The terrain and the poses shifted by kilometres in z, where float spacing (~2.4e-4 m)
     exceeds the fixed 1e-4 m margins: the split-record walk skip widens its margin with |z|
     (pcp_vlidar.hip), so first hits, blocked counts and ray-hit tests stay exact on the
-    fine-window copy (built at the first query)."""
+    fine-window copy (built at the first query), with one or two skip thresholds."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", "2")
+    monkeypatch.setenv("PCP_FINE_SKIP", skip)
     terr = np.ascontiguousarray(scene.terrain.copy())
     terr[:, 2] += np.float32(dz)
     ctx = _abi.Context(0)
@@ -1119,10 +1124,13 @@ def test_terrain_block_copy_dense_and_tiny(oracle, mode, fine, tile, layout, mon
             ctx.close()
 
 
-def test_fine_copy_dense_window(oracle, monkeypatch):
+@pytest.mark.parametrize("skip", ["1", "2"])
+def test_fine_copy_dense_window(oracle, monkeypatch, skip):
     """70,000 points in a 5 cm cube: fine windows of 70 k points (the walks end at the first
-    point r below or at the window's sentinel, no stored count), bit-exact."""
+    point r below or at the window's sentinel, no stored count; the skip counts at their caps),
+    bit-exact."""
     monkeypatch.setenv("PCP_TERRAIN_BLOCKS", "2")
+    monkeypatch.setenv("PCP_FINE_SKIP", skip)
     rng = np.random.default_rng(5)
     n = 70_000
     cube = np.column_stack([rng.uniform(1.0, 1.05, n), rng.uniform(0.0, 0.05, n),
