@@ -94,6 +94,8 @@ enum pcp_kernel_id {
     PCP_K_FILTER_MERGE,      /* whole crop->voxel->transform pipeline (graph replay)   */
     PCP_K_EXCAVATE,          /* excavated-terrain carve: heights + pit test + compaction */
     PCP_K_EXCAV_SETUP,       /* excavation-area normals + cell grid                    */
+    PCP_K_VOXEL_REDO,        /* bucket-chain frames redone by the LSD chain (a bucket past
+                              * its LDS capacity); launches = frames redone             */
     PCP_K_COUNT
 };
 int pcp_profile_enable(pcp_ctx *ctx, int enable);

@@ -29,7 +29,7 @@ F_RANGE_Z, F_FOV_Z, F_VIS_Z, F_RANGE_M, F_FOV_M, F_VIS_M = 1, 2, 4, 8, 16, 32
 
 KERNELS = ["raycast_fan", "score_cells", "zx120_cells", "pose_sum", "cell_flags",
            "candidates", "index_build", "crop", "voxel", "transform", "filter_merge", "excavate",
-           "excav_setup"]
+           "excav_setup", "voxel_redo"]
 
 
 class PcpError(RuntimeError):

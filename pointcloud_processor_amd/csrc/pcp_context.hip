@@ -244,6 +244,10 @@ KernelTimer::~KernelTimer() {
     if (a && b) ctx->pending.push_back({kid, a, b});
 }
 
+void prof_count(pcp_ctx *ctx, int kid) {
+    if (kid >= 0 && kid < PCP_K_COUNT) ctx->slots[kid].launches += 1;
+}
+
 void prof_resolve(pcp_ctx *ctx) {
     // calls that return without a stream synchronisation (index builds) leave events in
     // flight: those stay pending until a later call finds them complete
@@ -423,7 +427,7 @@ int pcp_create(int device, pcp_ctx **out) {
     }
     if (const char *ho = std::getenv("PCP_FAN_HOST_OUT")) ctx->fan_host_out = std::atoi(ho) != 0;
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
-    if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff) != 0;
+    if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff);
     if (const char *zc = std::getenv("PCP_ZC_IN")) ctx->zc_in = std::atoi(zc) != 0;
     if (const char *ck = std::getenv("PCP_COPY_KERNEL")) ctx->copy_kernel = std::atoi(ck) != 0;
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);
@@ -474,7 +478,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage, &ctx->fan_tab,
                       &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,
                       &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->f_in,
-                      &ctx->f_misc};
+                      &ctx->f_misc,    &ctx->bk_stat};
     for (DevBuf *b : bufs) b->release();
     for (auto &b : ctx->scratch) b.release();
     for (auto &b : ctx->fbuf) b.release();
@@ -574,7 +578,7 @@ const char *pcp_kernel_name(int kid) {
                                              "pose_sum",    "cell_flags",  "candidates",
                                              "index_build", "crop",        "voxel",
                                              "transform",   "filter_merge", "excavate",
-                                             "excav_setup"};
+                                             "excav_setup", "voxel_redo"};
     if (kid < 0 || kid >= PCP_K_COUNT) return "unknown";
     return names[kid];
 }

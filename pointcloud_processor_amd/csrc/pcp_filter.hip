@@ -135,6 +135,61 @@ __device__ __forceinline__ uint32_t block_prefix_sum(const uint32_t *__restrict_
     return t;
 }
 
+// wave64 inclusive scan by DPP (row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast 15
+// / 31 across rows): VALU moves, no LDS-crossbar (ds_bpermute) round trips as __shfl_up takes
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_dpp(x), 63);
+}
+// wave min / max of floats by the same DPP pattern (identity in the lanes without a source)
+template <bool MAX>
+__device__ __forceinline__ float wave_minmax_dpp(float x) {
+    const int id = __float_as_int(MAX ? -FLT_MAX : FLT_MAX);
+#define PCP_MM_STEP(ctrl, rm)                                                                    \
+    {                                                                                            \
+        const float y = __int_as_float(__builtin_amdgcn_update_dpp(id, __float_as_int(x), ctrl, \
+                                                                   rm, 0xF, false));            \
+        x = MAX ? fmaxf(x, y) : fminf(x, y);                                                     \
+    }
+    PCP_MM_STEP(0x111, 0xF) PCP_MM_STEP(0x112, 0xF) PCP_MM_STEP(0x114, 0xF)
+    PCP_MM_STEP(0x118, 0xF) PCP_MM_STEP(0x142, 0xA) PCP_MM_STEP(0x143, 0xC)
+#undef PCP_MM_STEP
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+// exclusive block scan (thread order) with DPP wave scans; every thread gets its prefix
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan_dpp(uint32_t v, uint32_t *lds) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan_dpp(v);
+    if (lane == 63) lds[wid] = incl;
+    __syncthreads();
+    uint32_t ex = incl - v;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) ex += w < wid ? lds[w] : 0u;
+    return ex;
+}
+
+// sum of one value per thread over the block; every thread gets it (lds: NT / 64 words)
+template <int NT>
+__device__ __forceinline__ uint32_t block_prefix_sum_reg(uint32_t s, uint32_t *lds) {
+    s = wave_sum_dpp(s);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = s;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) t += lds[w];
+    return t;
+}
+
 // exclusive block scan of one value per thread (thread order); every thread gets its prefix
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds) {
@@ -190,7 +245,42 @@ struct VoxParams {
     int32_t div_b[3];
     uint32_t mul1, mul2;
     uint64_t nvox;       // div product (key upper bound)
+    uint32_t bs, nbk;    // the bucket chain: key bits below the bucket, buckets (0: none)
 };
+
+// applyFilter's parameters from the cropped count and bbox (float, as PCL computes them)
+__device__ __forceinline__ VoxParams vox_params_from(uint32_t m, const float (&mn)[3],
+                                                     const float (&mx)[3], float leaf) {
+    VoxParams p{};
+    p.m = m;
+    p.do_voxel = leaf > 0.0f ? 1 : 0;
+    const float inv = p.do_voxel ? 1.0f / leaf : 0.0f;
+    p.inv = inv;
+    if (p.m != 0 && p.do_voxel) {
+        const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
+        const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
+        const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
+        p.overflow = (dx * dy * dz > (int64_t)INT32_MAX) ? 1 : 0;
+        for (int a = 0; a < 3; ++a) {
+            p.min_b[a] = (int32_t)floorf(mn[a] * inv);
+            const int32_t max_b = (int32_t)floorf(mx[a] * inv);
+            p.div_b[a] = max_b - p.min_b[a] + 1;
+        }
+        p.mul1 = (uint32_t)p.div_b[0];
+        p.mul2 = (uint32_t)p.div_b[0] * (uint32_t)p.div_b[1];
+        p.nvox = (uint64_t)(uint32_t)p.div_b[0] * (uint64_t)(uint32_t)p.div_b[1] *
+                 (uint64_t)(uint32_t)p.div_b[2];
+    }
+    return p;
+}
+
+// PCL's voxel index of a point (applyFilter: ijk in float relative to min_b, then idx)
+__device__ __forceinline__ uint32_t vox_key(const VoxParams &vp, float x, float y, float z) {
+    const int ijk0 = (int)(floorf(x * vp.inv) - (float)vp.min_b[0]);
+    const int ijk1 = (int)(floorf(y * vp.inv) - (float)vp.min_b[1]);
+    const int ijk2 = (int)(floorf(z * vp.inv) - (float)vp.min_b[2]);
+    return (uint32_t)ijk0 + (uint32_t)ijk1 * vp.mul1 + (uint32_t)ijk2 * vp.mul2;
+}
 
 // points that go through the sort: all cropped points when voxelising without overflow
 __device__ __forceinline__ uint32_t sort_count(const VoxParams &vp) {
@@ -235,6 +325,11 @@ struct CloudJob {
     uint32_t *h0;         // [nb][kBins] digit-0 counts per crop tile
     uint32_t ng;          // groups of gt crop tiles (pass 0's sort tiles)
     uint32_t gt;          // crop tiles per group: all groups of a batch in ONE round of blocks
+    // the bucket chain (k_bk_group -> k_bk_sort -> k_bk_emit): groups of gt crop tiles sorted by
+    // bucket (PCL idx >> vp.bs) into xyz, one row of bucket starts per group
+    int32_t bk;
+    uint32_t nbkcap;      // buckets the rows and the look-back words are sized for
+    uint32_t *brows;      // [ng][nbk + 1] compact position of the group's first item of bucket b
 };
 constexpr int kMaxGroupTiles = 32;   // crop tiles per pass-0 sort tile, at most
 constexpr int kS0Items = 10;         // pass-0 chunk: 5,120 items (a group of ~10 C3 crop tiles
@@ -275,6 +370,8 @@ __global__ void __launch_bounds__(kCT) PCP_CROP_ATTR k_crop_tile(const JobBatch 
             res[kMaxCloudsDev + 2 * J.slot + 1] = 0;
         }
     }
+    else if (J.bk && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        res[3 * kMaxCloudsDev] = 0;   // the bucket chain's redo flag (k_bk_* set it)
     if (blockIdx.x >= J.nb) return;
     const CloudIn c = J.in;
     const Box b = J.box;
@@ -403,26 +500,7 @@ k_vox_params(const JobBatch jobs, uint32_t *__restrict__ res,
         mn[a] = s[a][0];
         mx[a] = s[3 + a][0];
     }
-    VoxParams p{};
-    p.m = m;
-    p.do_voxel = leaf > 0.0f ? 1 : 0;
-    const float inv = p.do_voxel ? 1.0f / leaf : 0.0f;
-    p.inv = inv;
-    if (p.m != 0 && p.do_voxel) {
-        const int64_t dx = (int64_t)((mx[0] - mn[0]) * inv) + 1;
-        const int64_t dy = (int64_t)((mx[1] - mn[1]) * inv) + 1;
-        const int64_t dz = (int64_t)((mx[2] - mn[2]) * inv) + 1;
-        p.overflow = (dx * dy * dz > (int64_t)INT32_MAX) ? 1 : 0;
-        for (int a = 0; a < 3; ++a) {
-            p.min_b[a] = (int32_t)floorf(mn[a] * inv);
-            const int32_t max_b = (int32_t)floorf(mx[a] * inv);
-            p.div_b[a] = max_b - p.min_b[a] + 1;
-        }
-        p.mul1 = (uint32_t)p.div_b[0];
-        p.mul2 = (uint32_t)p.div_b[0] * (uint32_t)p.div_b[1];
-        p.nvox = (uint64_t)(uint32_t)p.div_b[0] * (uint64_t)(uint32_t)p.div_b[1] *
-                 (uint64_t)(uint32_t)p.div_b[2];
-    }
+    const VoxParams p = vox_params_from(m, mn, mx, leaf);
     *vp = p;
     const bool vox = p.do_voxel && !p.overflow;
     res[slot] = vox ? 0u : m;
@@ -454,12 +532,7 @@ __global__ void __launch_bounds__(kFT) k_compact_keys(const JobBatch jobs) {
         const float4 p = sparse[sb + j];
         xyz[pre + j] = p;
         if (kept_idx) kept_idx[pre + j] = sparse_idx[sb + j];
-        if (sort) {
-            const int ijk0 = (int)(floorf(p.x * vp.inv) - (float)vp.min_b[0]);
-            const int ijk1 = (int)(floorf(p.y * vp.inv) - (float)vp.min_b[1]);
-            const int ijk2 = (int)(floorf(p.z * vp.inv) - (float)vp.min_b[2]);
-            keys[pre + j] = (uint32_t)ijk0 + (uint32_t)ijk1 * vp.mul1 + (uint32_t)ijk2 * vp.mul2;
-        }
+        if (sort) keys[pre + j] = vox_key(vp, p.x, p.y, p.z);
     }
 }
 
@@ -986,6 +1059,489 @@ k_seg_centroid(const JobBatch jobs, uint32_t *__restrict__ res, float4 *__restri
     }
 }
 
+// =========================================================================================
+// The bucket chain (round 4, pcp_filter_merge / pcp_crop_voxel when every cloud certainly
+// voxelises): crop -> k_bk_group -> k_bk_sort -> k_bk_emit, three launches for the voxel stage.
+// PCL's idx order is the order of (bucket = idx >> bs, sub = idx & (2^bs - 1)).
+//  k_bk_group : one block per group of gt crop tiles (~4 k kept points): the cloud's parameters
+//               from the crop's counts and bbox partials, then a counting sort of the group's
+//               points by bucket in LDS -- written to xyz at the group's compact offset, one row
+//               of bucket starts per group (no global atomics, no cross-block prefix)
+//  k_bk_sort  : one block per bucket (consecutive over the clouds): gathers the bucket's runs
+//               of every group, counting-sorts them by sub in LDS (unstable), puts each voxel's
+//               points back in input order by their crop-slot position (stored in .w), sums
+//               them in that order; centroids at the bucket's item offset, voxel count per bucket
+//  k_bk_emit  : output offset of each bucket (voxels of the earlier buckets), the centroids
+//               copied there -- as merged records (transform + colour) for pcp_filter_merge
+// A bucket past kBkCap points (or a parameter past the sizes the host allotted) sets the redo
+// flag (res[3 * kMaxCloudsDev]); the host then runs the frame again on the LSD chain.
+// =========================================================================================
+constexpr int kBkT = 512;                 // threads of the bucket kernels
+#ifndef PCP_BK_BITS
+#define PCP_BK_BITS 11
+#endif
+#ifndef PCP_BK_SUB
+#define PCP_BK_SUB 12
+#endif
+constexpr int kBkBits = PCP_BK_BITS;      // target: ~2^kBkBits buckets per cloud
+constexpr int kBkSubMax = PCP_BK_SUB;     // sub-key bits at most (LDS table of 2^kBkSubMax + 1)
+constexpr int kBkMax = 4096;              // buckets per cloud at most
+constexpr int kBkCap = 4096;              // points per bucket at most
+// bkv layout: [0, kBkChunkOff) per-bucket (voxels, item offset), then per-64-bucket voxel sums
+constexpr uint32_t kBkChunkOff = kBatch * kBkMax;
+constexpr int kBkGt = 15;                 // crop tiles per group at most
+constexpr int kBkGItems = 12;             // per thread and chunk in k_bk_group
+
+__device__ __forceinline__ void bk_redo(uint32_t *res) { res[3 * kMaxCloudsDev] = 1u; }
+
+// crop tile u of the group holding item q: the last u with cpre[u] <= q (cpre ascending)
+__device__ __forceinline__ uint32_t bk_tile_of(const uint32_t *cpre, uint32_t gt, uint32_t q) {
+    uint32_t lo = 0, hi = gt;   // cpre[lo] <= q < cpre[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cpre[mid] <= q) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(kBkT)
+k_bk_group(const JobBatch jobs, uint32_t *__restrict__ res, uint2 *__restrict__ bkv) {
+    const CloudJob &J = jobs.j[blockIdx.y];
+    // k_bk_sort's per-64-bucket voxel sums start at 0
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (uint32_t q = threadIdx.x; q < (uint32_t)kBatch * kBkMax / 64; q += kBkT)
+            bkv[kBkChunkOff + q] = make_uint2(0u, 0u);
+    const uint32_t g = blockIdx.x;
+    if (!J.bk || g >= J.ng) return;
+    [[maybe_unused]] const uint32_t stt = blockIdx.y * gridDim.x + blockIdx.x;   // stamp slot
+    FLT_STAMP(0, stt, 0);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t nb = J.nb, c0 = g * J.gt, c1 = min(c0 + J.gt, nb), gt = c1 - c0;
+    // the cloud's cropped count, the points of tiles before the group, the cropped bbox
+    uint32_t tot = 0, pre = 0;
+    float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    // the group's crop-tile counts (wave 0), issued with the loads below
+    const uint32_t gcnt = (threadIdx.x < 64 && threadIdx.x < gt) ? J.counts[c0 + threadIdx.x] : 0u;
+    // four tiles per thread and round, every load of a round issued before any is used
+    for (uint32_t t0 = threadIdx.x; t0 < nb; t0 += 4 * kBkT) {
+        uint32_t v[4];
+        float2 pa[4], pb[4], pc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t t = min(t0 + u * kBkT, nb - 1);
+            v[u] = J.counts[t];
+            pa[u] = reinterpret_cast<const float2 *>(J.part)[3 * t];
+            pb[u] = reinterpret_cast<const float2 *>(J.part)[3 * t + 1];
+            pc[u] = reinterpret_cast<const float2 *>(J.part)[3 * t + 2];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t t = t0 + u * kBkT;
+            if (t >= nb) continue;   // (a clamped duplicate: min/max only, never counted)
+            tot += v[u];
+            pre += t < c0 ? v[u] : 0u;
+            mn[0] = fminf(mn[0], pa[u].x); mn[1] = fminf(mn[1], pa[u].y);
+            mn[2] = fminf(mn[2], pb[u].x); mx[0] = fmaxf(mx[0], pb[u].y);
+            mx[1] = fmaxf(mx[1], pc[u].x); mx[2] = fmaxf(mx[2], pc[u].y);
+        }
+    }
+    tot = wave_sum_dpp(tot);
+    pre = wave_sum_dpp(pre);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        mn[a] = wave_minmax_dpp<false>(mn[a]);
+        mx[a] = wave_minmax_dpp<true>(mx[a]);
+    }
+    __shared__ float sred[8][kBkT / 64];
+    __shared__ uint32_t cpre[kBkGt + 1];
+    __shared__ uint32_t h[kBkMax + 1];
+    if (lane == 0) {
+        sred[0][wid] = __uint_as_float(tot);
+        sred[1][wid] = __uint_as_float(pre);
+        for (int a = 0; a < 3; ++a) {
+            sred[2 + a][wid] = mn[a];
+            sred[5 + a][wid] = mx[a];
+        }
+    }
+    if (threadIdx.x < 64) {   // the group's crop-tile counts, prefix by one wave
+        const uint32_t incl = wave_incl_scan_dpp(gcnt);
+        if (threadIdx.x == 0) cpre[0] = 0;
+        if (threadIdx.x < gt) cpre[threadIdx.x + 1] = incl;
+    }
+    __syncthreads();
+    tot = 0;
+    pre = 0;
+#pragma unroll
+    for (int w = 0; w < kBkT / 64; ++w) {
+        tot += __float_as_uint(sred[0][w]);
+        pre += __float_as_uint(sred[1][w]);
+        for (int a = 0; a < 3; ++a) {
+            mn[a] = fminf(mn[a], sred[2 + a][w]);
+            mx[a] = fmaxf(mx[a], sred[5 + a][w]);
+        }
+    }
+    VoxParams p = vox_params_from(tot, mn, mx, J.leaf);
+    // buckets: bs = clamp(bits(nvox) - kBkBits, 0, kBkSubMax), nbk = ceil(nvox / 2^bs)
+    bool redo = p.overflow != 0;
+    if (tot != 0 && !redo) {
+        int bits = 0;
+        while (bits < 40 && (1ull << bits) < p.nvox) ++bits;
+        p.bs = (uint32_t)min(max(bits - kBkBits, 0), kBkSubMax);
+        const uint64_t nbk = (p.nvox + (1ull << p.bs) - 1) >> p.bs;
+        if (nbk > J.nbkcap) redo = true;
+        else p.nbk = (uint32_t)nbk;
+    }
+    if (redo) p.nbk = 0;
+    if (g == 0 && threadIdx.x == 0) {
+        *J.vp = p;
+        res[J.slot] = 0;   // k_bk_emit writes it when the cloud has buckets
+        res[kMaxCloudsDev + 2 * J.slot] = tot;
+        res[kMaxCloudsDev + 2 * J.slot + 1] = 0;
+        if (redo) bk_redo(res);
+    }
+    if (p.nbk == 0) return;   // uniform: nothing cropped, or the frame is redone
+    FLT_STAMP(0, stt, 1);
+    const uint32_t nbk = p.nbk, bs = p.bs;
+    const uint32_t T = cpre[gt];
+    for (uint32_t b = threadIdx.x; b <= nbk; b += kBkT) h[b] = 0;
+    __syncthreads();
+    constexpr uint32_t kChunk = (uint32_t)kBkT * kBkGItems;
+    const uint32_t nch = (T + kChunk - 1) / kChunk;
+    float4 v[kBkGItems];
+    uint32_t bk[kBkGItems];
+    // pass A: bucket counts (the last chunk stays in registers for pass B); a chunk's loads
+    // are all issued before its LDS atomics
+    uint32_t spj[kBkGItems];
+    for (uint32_t ch = 0; ch < nch; ++ch) {
+#pragma unroll
+        for (int j = 0; j < kBkGItems; ++j) {
+            const uint32_t q = ch * kChunk + (uint32_t)j * kBkT + threadIdx.x;
+            const uint32_t qc = min(q, T - 1);
+            const uint32_t u = bk_tile_of(cpre, gt, qc);
+            spj[j] = (c0 + u) * (uint32_t)kCropTile + (qc - cpre[u]);
+            v[j] = J.sparse[spj[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < kBkGItems; ++j) {
+            const uint32_t q = ch * kChunk + (uint32_t)j * kBkT + threadIdx.x;
+            v[j].w = __uint_as_float(spj[j]);
+            bk[j] = vox_key(p, v[j].x, v[j].y, v[j].z) >> bs;
+            if (q < T) atomicAdd(&h[bk[j]], 1u);
+        }
+    }
+    __syncthreads();
+    FLT_STAMP(0, stt, 2);
+    // exclusive scan of the counts -> starts (contiguous runs of B buckets per thread)
+    {
+        __shared__ uint32_t lsc[kBkT / 64];
+        const uint32_t per = (nbk + kBkT - 1) / kBkT;
+        const uint32_t b0 = min(threadIdx.x * per, nbk), b1 = min(b0 + per, nbk);
+        uint32_t loc = 0;
+        for (uint32_t b = b0; b < b1; ++b) loc += h[b];
+        uint32_t ex = block_excl_scan_dpp<kBkT>(loc, lsc);
+        uint32_t *row = J.brows + (size_t)g * (nbk + 1);
+        for (uint32_t b = b0; b < b1; ++b) {
+            const uint32_t c = h[b];
+            h[b] = ex;
+            row[b] = pre + ex;
+            ex += c;
+        }
+        if (threadIdx.x == 0) row[nbk] = pre + T;
+    }
+    __syncthreads();
+    FLT_STAMP(0, stt, 3);
+    // pass B: each point to its bucket's next slot (LDS arrival order: not stable, k_bk_sort
+    // restores input order inside each voxel from the slot position in .w)
+    float4 *gout = J.xyz + pre;
+    for (int32_t ch = (int32_t)nch - 1; ch >= 0; --ch) {
+#pragma unroll
+        for (int j = 0; j < kBkGItems; ++j) {
+            const uint32_t q = (uint32_t)ch * kChunk + (uint32_t)j * kBkT + threadIdx.x;
+            if (q < T) {
+                if ((uint32_t)ch != nch - 1) {   // (only groups past one chunk)
+                    const uint32_t u = bk_tile_of(cpre, gt, q);
+                    const uint32_t sp = (c0 + u) * (uint32_t)kCropTile + (q - cpre[u]);
+                    const float4 a = J.sparse[sp];
+                    v[j] = make_float4(a.x, a.y, a.z, __uint_as_float(sp));
+                    bk[j] = vox_key(p, a.x, a.y, a.z) >> bs;
+                }
+                gout[atomicAdd(&h[bk[j]], 1u)] = v[j];
+            }
+        }
+    }
+    FLT_STAMP(0, stt, 4);
+}
+
+// the cloud of look-back position f and its first position b0 (the clouds' buckets follow one
+// another); -1: past the last bucket
+__device__ __forceinline__ int bk_cloud_of(const JobBatch &jobs, int k, uint32_t f, uint32_t &b0) {
+    b0 = 0;
+    for (int y = 0; y < k; ++y) {
+        const uint32_t nb = jobs.j[y].bk ? jobs.j[y].vp->nbk : 0u;
+        if (f < b0 + nb) return y;
+        b0 += nb;
+    }
+    return -1;
+}
+
+// k_bk_sort: one block per bucket.  The bucket's runs of every group gathered (one point per
+// thread and round, registers), counted per sub-key in LDS (arrival order), one packed scan ->
+// (start | voxel rank << 16) per sub-key, slots by arrival, then each point's rank among its
+// voxel's points by crop-slot position (input order), and the voxel sums in that order by the
+// voxel's first point.  The centroids land at the bucket's item offset in the cloud (sparse is
+// free after k_bk_group), (voxels, offset) in bkv[f]; k_bk_emit places them.
+#ifndef PCP_BK_T3
+#define PCP_BK_T3 512
+#endif
+constexpr int kBkT3 = PCP_BK_T3;
+// 64 VGPRs: 8 waves per SIMD, four 512-thread blocks per CU (LDS admits four); build knob
+// PCP_BK_W8=0 lets the compiler take 68 (three blocks per CU): 0.104 vs 0.101 ms per frame
+#ifndef PCP_BK_W8
+#define PCP_BK_W8 1
+#endif
+#if PCP_BK_W8
+#define PCP_BK_SORT_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#else
+#define PCP_BK_SORT_ATTR
+#endif
+constexpr int kBkItems3 = kBkCap / kBkT3;
+constexpr int kBkNg = kBkT3;              // groups per cloud at most (one per k_bk_sort thread)
+__global__ void __launch_bounds__(kBkT3) PCP_BK_SORT_ATTR
+k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restrict__ bkv,
+          int idx_out) {
+    const uint32_t f = blockIdx.x;
+    uint32_t b0;
+    const int c = bk_cloud_of(jobs, k, f, b0);
+    if (c < 0) return;
+    FLT_STAMP(1, f, 0);
+    const CloudJob &J = jobs.j[c];
+    const VoxParams P = *J.vp;
+    const uint32_t b = f - b0, bs = P.bs, nsub = 1u << bs, stride = P.nbk + 1;
+    const uint32_t ng = J.ng;
+    __shared__ uint32_t og[kBkNg + 1], sg[kBkNg];
+    __shared__ uint32_t tab[(1 << kBkSubMax) + 1];   // counts, then start | voxel rank << 16
+    __shared__ uint32_t p1[kBkCap];                  // slot -> crop-slot position, then
+                                                     // input-order slot -> xyz index
+    __shared__ uint32_t lsa[kBkT3 / 64], lsb[kBkT3 / 64];
+    // the bucket's run in every group, and its item offset in the cloud (points of the earlier
+    // buckets: sum over the groups of row[b] - row[0])
+    uint32_t gc = 0, gsum = 0;
+    if (threadIdx.x < ng) {
+        const uint32_t *row = J.brows + (size_t)threadIdx.x * stride;
+        const uint32_t r0 = row[0], rb = row[b], rb1 = row[b + 1];
+        gsum = rb - r0;
+        gc = rb1 - rb;
+        sg[threadIdx.x] = rb;
+    }
+    gsum = wave_sum_dpp(gsum);
+    if ((threadIdx.x & 63) == 0) lsb[threadIdx.x >> 6] = gsum;
+    const uint32_t gex = block_excl_scan_dpp<kBkT3>(gc, lsa);
+    if (threadIdx.x < ng) og[threadIdx.x] = gex;
+    if (threadIdx.x == kBkT3 - 1) og[ng] = gex + gc;
+    for (uint32_t e = threadIdx.x; e <= nsub; e += kBkT3) tab[e] = 0;
+    __syncthreads();
+    uint32_t ioff = 0;
+#pragma unroll
+    for (int w = 0; w < kBkT3 / 64; ++w) ioff += lsb[w];
+    const uint32_t n = og[ng];
+    const bool fits = n <= (uint32_t)kBkCap;
+    FLT_STAMP(1, f, 1);
+    uint32_t pos[kBkItems3], sxi[kBkItems3], sub[kBkItems3], arr[kBkItems3];
+    if (fits) {
+        float4 a[kBkItems3];
+#pragma unroll
+        for (int j = 0; j < kBkItems3; ++j) {
+            const uint32_t q = (uint32_t)j * kBkT3 + threadIdx.x;
+            if (q < n) {
+                uint32_t lo = 0, hi = ng;   // og[lo] <= q < og[hi]
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (og[mid] <= q) lo = mid; else hi = mid;
+                }
+                sxi[j] = sg[lo] + (q - og[lo]);
+                a[j] = J.xyz[sxi[j]];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kBkItems3; ++j) {
+            const uint32_t q = (uint32_t)j * kBkT3 + threadIdx.x;
+            if (q < n) {
+                pos[j] = __float_as_uint(a[j].w);
+                sub[j] = vox_key(P, a[j].x, a[j].y, a[j].z) & (nsub - 1u);
+                arr[j] = atomicAdd(&tab[sub[j]], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    FLT_STAMP(1, f, 2);
+    if (!fits) {   // uniform: the host redoes the frame on the LSD chain
+        if (threadIdx.x == 0) {
+            bk_redo(res);
+            bkv[f] = make_uint2(0u, ioff);
+        }
+        return;
+    }
+    // one packed exclusive scan of the table: points (low 16 bits) and occupied sub-keys (high
+    // 16).  Wave w scans the contiguous segment [w S, (w + 1) S) 64 entries per round (lane l
+    // reads entry r + l: no bank conflicts), segment totals first, then the scan with carries
+    uint32_t nvox;
+    {
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        const uint32_t S = max(64u, nsub / (uint32_t)(kBkT3 / 64));
+        const uint32_t e0 = (uint32_t)wid * S;
+        uint32_t tsum = 0;
+        if (e0 < nsub) {
+            for (uint32_t r = 0; r < S; r += 64) {
+                const uint32_t e = e0 + r + lane;
+                const uint32_t t = e < nsub ? tab[e] : 0u;
+                tsum += t | (t ? 0x10000u : 0u);
+            }
+            tsum = wave_sum_dpp(tsum);
+        }
+        if (lane == 0) lsa[wid] = tsum;
+        __syncthreads();
+        uint32_t off = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < kBkT3 / 64; ++w) {
+            off += w < wid ? lsa[w] : 0u;
+            all += lsa[w];
+        }
+        nvox = all >> 16;
+        if (e0 < nsub) {
+            for (uint32_t r = 0; r < S; r += 64) {
+                const uint32_t e = e0 + r + lane;
+                const uint32_t t = e < nsub ? tab[e] : 0u;
+                const uint32_t v = t | (t ? 0x10000u : 0u);
+                const uint32_t incl = wave_incl_scan_dpp(v);
+                if (e < nsub) tab[e] = off + incl - v;
+                off += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            }
+        }
+        if (threadIdx.x == 0) tab[nsub] = n | (nvox << 16);
+    }
+    __syncthreads();
+    FLT_STAMP(1, f, 3);
+    // slots in sub-key order, arrival order inside a voxel
+#pragma unroll
+    for (int j = 0; j < kBkItems3; ++j) {
+        const uint32_t q = (uint32_t)j * kBkT3 + threadIdx.x;
+        if (q < n) p1[(tab[sub[j]] & 0xffffu) + arr[j]] = pos[j];
+    }
+    __syncthreads();
+    FLT_STAMP(1, f, 4);
+    // input order inside each voxel: rank by crop-slot position among the voxel's points
+    uint32_t head = 0, fin[kBkItems3];
+#pragma unroll
+    for (int j = 0; j < kBkItems3; ++j) {
+        const uint32_t q = (uint32_t)j * kBkT3 + threadIdx.x;
+        if (q < n) {
+            const uint32_t st = tab[sub[j]] & 0xffffu;
+            const uint32_t cnt = (tab[sub[j] + 1] & 0xffffu) - st;
+            uint32_t r = 0;
+            for (uint32_t u = st; cnt > 1 && u < st + cnt; ++u) r += p1[u] < pos[j] ? 1u : 0u;
+            fin[j] = st + r;
+            head |= (r == 0 ? 1u : 0u) << j;
+        }
+    }
+    __syncthreads();   // every rank read p1 before it holds xyz indices
+#pragma unroll
+    for (int j = 0; j < kBkItems3; ++j) {
+        const uint32_t q = (uint32_t)j * kBkT3 + threadIdx.x;
+        if (q < n) p1[fin[j]] = sxi[j];
+    }
+    __syncthreads();
+    FLT_STAMP(1, f, 5);
+    // each voxel's first point (in input order) sums the voxel in input order
+    float4 *tmp = J.sparse + ioff;
+#pragma unroll
+    for (int j = 0; j < kBkItems3; ++j) {
+        if (!((head >> j) & 1u)) continue;
+        const uint32_t t0 = tab[sub[j]], st = t0 & 0xffffu, vr = t0 >> 16;
+        const uint32_t cnt = (tab[sub[j] + 1] & 0xffffu) - st;
+        float sx = 0.f, sy = 0.f, sz = 0.f;
+        for (uint32_t u = st; u < st + cnt; ++u) {
+            const float4 a = J.xyz[p1[u]];
+            sx = sx + a.x;
+            sy = sy + a.y;
+            sz = sz + a.z;
+        }
+        const float fc = (float)cnt;
+        tmp[vr] = make_float4(sx / fc, sy / fc, sz / fc, 1.0f);
+        if (idx_out) {   // pcp_crop_voxel: idx and count beside the centroid
+            J.keys0[ioff + vr] = (b << bs) | sub[j];
+            J.keys1[ioff + vr] = cnt;
+        }
+    }
+    if (threadIdx.x == 0) {
+        bkv[f] = make_uint2(nvox, ioff);
+        if (nvox) atomicAdd(&bkv[kBkChunkOff + (f >> 6)].x, nvox);   // k_bk_emit's chunk sums
+    }
+    FLT_STAMP(1, f, 6);
+}
+
+// k_bk_emit: one block per bucket.  Output offset = voxels of every earlier bucket of the call:
+// the per-64-bucket sums k_bk_sort accumulated before f's chunk + the buckets of f's chunk
+// before f (one load per lane of one wave); the centroids copied there (emit: through the
+// cloud's transform + colour as merged records); the cloud's last bucket writes its count.
+constexpr int kBkTE = 256;
+__device__ __forceinline__ uint32_t bk_voxels_before(const uint2 *bkv, uint32_t f) {
+    // wave 0 only (full wave): lanes sum chunk sums [0, f / 64) and buckets [f & ~63, f)
+    const uint32_t lane = threadIdx.x & 63, nch = f >> 6, c0 = f & ~63u;
+    uint32_t s = 0;
+    for (uint32_t q = lane; q < nch; q += 64) s += bkv[kBkChunkOff + q].x;
+    if (c0 + lane < f) s += bkv[c0 + lane].x;
+    return wave_sum_dpp(s);
+}
+__global__ void __launch_bounds__(kBkTE)
+k_bk_emit(const JobBatch jobs, int k, uint32_t *__restrict__ res, float4 *__restrict__ emit,
+          const uint2 *__restrict__ bkv) {
+    const uint32_t f = blockIdx.x;
+    uint32_t b0;
+    const int c = bk_cloud_of(jobs, k, f, b0);
+    if (c < 0) return;
+    const CloudJob &J = jobs.j[c];
+    __shared__ uint32_t sh[2];
+    if (threadIdx.x < 64) {
+        const uint32_t e = bk_voxels_before(bkv, f);
+        if (threadIdx.x == 0) sh[0] = e;
+    }
+    __syncthreads();
+    const uint32_t e = sh[0];
+    const uint2 kv = bkv[f];
+    const float4 *tmp = J.sparse + kv.y;
+    for (uint32_t v0 = 0; v0 < kv.x; v0 += 4 * kBkTE) {
+        float4 a[4];
+        uint32_t iv[4], cv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t v = v0 + u * kBkTE + threadIdx.x;
+            if (v < kv.x) {
+                a[u] = tmp[v];
+                if (!emit) {
+                    iv[u] = J.keys0[kv.y + v];
+                    cv[u] = J.keys1[kv.y + v];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t v = v0 + u * kBkTE + threadIdx.x;
+            if (v >= kv.x) continue;
+            if (emit) {
+                xform_store(J.rig, a[u].x, a[u].y, a[u].z, emit + 2 * ((size_t)e + v));
+            } else {
+                J.out4[e + v] = a[u];
+                J.vidx[e + v] = iv[u];
+                J.vcnt[e + v] = cv[u];
+            }
+        }
+    }
+    if (f - b0 == J.vp->nbk - 1 && threadIdx.x < 64) {   // the cloud's last bucket
+        const uint32_t before = bk_voxels_before(bkv, b0);
+        if (threadIdx.x == 0) res[J.slot] = e + kv.x - before;
+    }
+}
+
 // transform + colour of every cloud's result into the concatenated output (cloud order: the
 // robot first), counts[] = result counts of the clouds
 __global__ void __launch_bounds__(kFT)
@@ -1041,6 +1597,9 @@ __global__ void __launch_bounds__(kFT) k_xform_batch(XformBatch B, float4 *__res
 // pcp_filter_merge when its inputs are device-resident).
 // =========================================================================================
 constexpr int kMaxClouds = 64;
+// result words of a call: counts [kMaxClouds], (cropped, passthrough) [2 kMaxClouds], the bucket
+// chain's redo flag
+constexpr int kResWords = 3 * kMaxClouds + 4;
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -1048,7 +1607,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // res[kMaxClouds] result counts and info[2*kMaxClouds] (cropped count, passthrough flag)
 static int ensure_misc(pcp_ctx *ctx, VoxParams *&vp, uint32_t *&res) {
     const size_t vb = align256(kMaxClouds * sizeof(VoxParams));
-    PCP_HIP(ctx, ctx->f_misc.ensure(vb + 3 * kMaxClouds * 4));
+    PCP_HIP(ctx, ctx->f_misc.ensure(vb + kResWords * 4));
     vp = reinterpret_cast<VoxParams *>(ctx->f_misc.as<char>());
     res = reinterpret_cast<uint32_t *>(ctx->f_misc.as<char>() + vb);
     return PCP_OK;
@@ -1171,6 +1730,43 @@ static bool fast_geometry(pcp_ctx *ctx, int slot, CloudJob &J, int clouds = 1) {
     return true;
 }
 
+// the bucket chain's sizes for job J (finite box, leaf > 0, n > 0, box keys below 2^31): groups
+// of gt crop tiles (<= kBkNg per cloud), rows for the most buckets the cropped bbox can need
+static bool bucket_geometry(pcp_ctx *ctx, int slot, CloudJob &J, int clouds = 1) {
+    if (J.in.n == 0 || !(J.leaf > 0.0f)) return false;
+    const double lo[3] = {J.box.x0, J.box.y0, J.box.z0}, hi[3] = {J.box.x1, J.box.y1, J.box.z1};
+    double nv = 1.0;
+    for (int a = 0; a < 3; ++a) {
+        if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) return false;
+        nv *= std::floor((hi[a] - lo[a]) / (double)J.leaf) + 3.0;
+    }
+    if (!(nv < 2147483647.0)) return false;
+    const uint32_t nb = J.nb;
+    const uint32_t cus = (uint32_t)std::max(ctx->num_cus, 1);
+    // one round of blocks for all groups of the call, at most kBkGt tiles (< 64 Ki points) each
+    uint32_t gt = std::max<uint32_t>(1, (nb * (uint32_t)clouds + cus - 1) / cus);
+    gt = std::min<uint32_t>(gt, kBkGt);
+    const uint32_t ng = (nb + gt - 1) / gt;
+    if (ng > (uint32_t)kBkNg) return false;
+    // device: bs = clamp(bits(nvox) - kBkBits, 0, kBkSubMax), nbk = ceil(nvox / 2^bs)
+    const double cap = std::max(std::ldexp(1.0, kBkBits), std::ceil(nv / std::ldexp(1.0, kBkSubMax)));
+    const uint32_t nbkcap = (uint32_t)std::min<double>(cap, (double)kBkMax);
+    CloudBufs &B = ctx->fbuf[slot];
+    // rows, and the look-back words of a call's clouds (sized here: enqueue may be capturing)
+    if (B.skeys.ensure((size_t)ng * (nbkcap + 1) * 4 + 256) != hipSuccess ||
+        ctx->bk_stat.ensure(((size_t)kBkChunkOff + kBatch * kBkMax / 64) * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    J.bk = 1;
+    J.gt = gt;
+    J.ng = ng;
+    J.nbkcap = nbkcap;
+    J.brows = B.skeys.as<uint32_t>();
+    J.fast = 0;
+    return true;
+}
+
 struct Batch {
     JobBatch jb{};
     int k = 0;
@@ -1273,6 +1869,38 @@ static int enqueue_fast(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream_
     return PCP_OK;
 }
 
+// the bucket chain of one batch whose clouds all certainly voxelise (bucket_geometry): crop ->
+// k_bk_group -> k_bk_sort -> k_bk_emit (emit: the centroids as merged records)
+static int enqueue_bucket(pcp_ctx *ctx, const Batch &bt, uint32_t *res, hipStream_t st,
+                          float4 *emit) {
+    const unsigned k = (unsigned)bt.k;
+    uint32_t max_ng = 0, nseq = 0;
+    for (int i = 0; i < bt.k; ++i) {
+        max_ng = std::max(max_ng, bt.jb.j[i].ng);
+        nseq += bt.jb.j[i].nbkcap;
+    }
+    if (ctx->bk_stat.cap < ((size_t)kBkChunkOff + kBatch * kBkMax / 64) * 8)   // bucket_geometry
+        return set_err(ctx, PCP_E_STATE, "bucket chain: bucket words not allocated");
+    uint2 *bkv = ctx->bk_stat.as<uint2>();
+    {
+        ProfScope ps(ctx, PCP_K_CROP, st);
+        hipLaunchKernelGGL(k_crop_tile<false>, dim3(std::max(bt.max_nb, 1u), k), dim3(kCT), 0, st,
+                           bt.jb, res);
+        PCP_CHECK_LAUNCH(ctx);
+    }
+    ProfScope ps(ctx, PCP_K_VOXEL, st);
+    hipLaunchKernelGGL(k_bk_group, dim3(std::max(max_ng, 1u), k), dim3(kBkT), 0, st, bt.jb, res,
+                       bkv);
+    PCP_CHECK_LAUNCH(ctx);
+    hipLaunchKernelGGL(k_bk_sort, dim3(std::max(nseq, 1u)), dim3(kBkT3), 0, st, bt.jb, (int)k,
+                       res, bkv, emit ? 0 : 1);
+    PCP_CHECK_LAUNCH(ctx);
+    hipLaunchKernelGGL(k_bk_emit, dim3(std::max(nseq, 1u)), dim3(kBkTE), 0, st, bt.jb, (int)k, res,
+                       emit, bkv);
+    PCP_CHECK_LAUNCH(ctx);
+    return PCP_OK;
+}
+
 // transform + colour + concat of one batch (after every batch's chain: offsets need all counts)
 static int enqueue_emit(pcp_ctx *ctx, const Batch &bt, const uint32_t *res, float4 *out,
                         hipStream_t st) {
@@ -1307,8 +1935,16 @@ static bool emit_in_centroid(const std::vector<Batch> &bts) {
     return true;
 }
 
+static bool all_bucket(const std::vector<Batch> &bts) {
+    if (bts.size() != 1 || bts[0].k == 0) return false;
+    for (int i = 0; i < bts[0].k; ++i)
+        if (!bts[0].jb.j[i].bk) return false;
+    return true;
+}
+
 static int enqueue_all(pcp_ctx *ctx, const std::vector<Batch> &bts, uint32_t *res,
                        float4 *emit_out, hipStream_t st) {
+    if (all_bucket(bts)) return enqueue_bucket(ctx, bts[0], res, st, emit_out);
     if (!emit_out && bts.size() == 1) {   // pcp_crop_voxel's fast chain (run_single)
         bool fast = bts[0].k > 0;
         for (int i = 0; i < bts[0].k; ++i) fast = fast && bts[0].jb.j[i].fast;
@@ -1361,16 +1997,16 @@ struct ResultInfo {
 };
 
 static int read_results(pcp_ctx *ctx, const uint32_t *res_d, int k, ResultInfo *ri,
-                        bool landed = false) {
+                        bool landed = false, uint32_t *redo = nullptr) {
     // pinned landing buffer: the per-frame size readback is one small DMA, no staging copy;
     // landed: the kernels stored the sizes in pinned memory themselves (res_d is host memory)
     uint32_t *buf;
     if (landed) {
         buf = const_cast<uint32_t *>(res_d);
     } else {
-        PCP_HIP(ctx, ctx->res_host.ensure(3 * kMaxClouds * sizeof(uint32_t)));
+        PCP_HIP(ctx, ctx->res_host.ensure(kResWords * sizeof(uint32_t)));
         buf = ctx->res_host.as<uint32_t>();
-        PCP_HIP(ctx, hipMemcpyAsync(buf, res_d, 3 * kMaxClouds * sizeof(uint32_t),
+        PCP_HIP(ctx, hipMemcpyAsync(buf, res_d, kResWords * sizeof(uint32_t),
                                     hipMemcpyDeviceToHost, ctx->stream));
     }
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -1379,6 +2015,7 @@ static int read_results(pcp_ctx *ctx, const uint32_t *res_d, int k, ResultInfo *
         ri[i].m = buf[kMaxClouds + 2 * i];
         ri[i].overflow = buf[kMaxClouds + 2 * i + 1];
     }
+    if (redo) *redo = buf[3 * kMaxClouds];
     return PCP_OK;
 }
 
@@ -1409,19 +2046,30 @@ static int run_single(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b, floa
     }
     std::vector<CloudJob> jobs(1);
     if ((rc = make_job(ctx, 0, c, b, leaf, want_idx, Rigid{}, vp, jobs[0]))) return rc;
-    if (fast_ok && !want_idx && ctx->fm_fast && fast_geometry(ctx, 0, jobs[0])) {
-        CloudJob &F = jobs[0];
+    // the bucket chain (PCP_FM_FAST 2), else the LSD fast chain; a bucket chain that set its redo
+    // flag runs again on the LSD chain (the input stays where it was staged until then)
+    for (int mode = ctx->fm_fast; fast_ok && !want_idx && mode > 0; --mode) {
+        CloudJob F = jobs[0];
+        const bool geo = mode == 2 ? bucket_geometry(ctx, 0, F) : fast_geometry(ctx, 0, F);
+        if (!geo) continue;
         const uint64_t ncap = c.n ? c.n : 1;
-        const size_t res_b = align256(3 * kMaxClouds * sizeof(uint32_t));
+        const size_t res_b = align256(kResWords * sizeof(uint32_t));
         PCP_HIP(ctx, ctx->cv_host.ensure(res_b + (ncap + 1) * sizeof(float4) + (2 * ncap + 8) * 4 + 256));
         uint32_t *res_h = ctx->cv_host.as<uint32_t>();
         F.out4 = reinterpret_cast<float4 *>(ctx->cv_host.as<char>() + res_b);
         F.vidx = reinterpret_cast<uint32_t *>(F.out4 + ncap + 1);
         F.vcnt = F.vidx + ncap + 1;
-        if ((rc = enqueue_all(ctx, batches_of(jobs), res_h, nullptr, ctx->stream))) return rc;
+        std::vector<CloudJob> fj(1, F);
+        if ((rc = enqueue_all(ctx, batches_of(fj), res_h, nullptr, ctx->stream))) return rc;
+        uint32_t redo = 0;
+        if ((rc = read_results(ctx, res_h, 1, &ri, true, &redo))) return rc;
+        if (mode == 2 && redo) {
+            prof_count(ctx, PCP_K_VOXEL_REDO);
+            continue;
+        }
         if (zc) pin_release(ctx, ctx->stream);
         J = F;
-        return read_results(ctx, res_h, 1, &ri, true);
+        return PCP_OK;
     }
     if ((rc = enqueue_all(ctx, batches_of(jobs), res, nullptr, ctx->stream))) return rc;
     if (zc) pin_release(ctx, ctx->stream);
@@ -1694,21 +2342,28 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
     // the emit needs the sizes first when the output might not fit (device output only)
     const bool emit_now = !(dev_out && upper > cap);
     // every cloud certainly voxelises: the fast chain (PCP_FM_FAST=0: the general chain)
-    if (emit_now && ctx->fm_fast && emit_in_centroid(bts)) {
-        std::vector<CloudJob> fj = jobs;
+    // (2: the bucket chain, the LSD fast chain when a bucket chain frame has to be redone)
+    const std::vector<CloudJob> plain = jobs;
+    auto lsd_jobs = [&]() {
+        std::vector<CloudJob> fj = plain;
         bool all = true;
         for (int i = 0; i < k && all; ++i) all = fast_geometry(ctx, i, fj[i], k);
-        if (all) {
-            jobs = fj;
-            bts = batches_of(jobs);
-        }
+        return all ? fj : plain;
+    };
+    bool bucket = false;
+    if (emit_now && ctx->fm_fast && emit_in_centroid(bts)) {
+        std::vector<CloudJob> fj = plain;
+        bucket = ctx->fm_fast == 2;
+        for (int i = 0; i < k && bucket; ++i) bucket = bucket_geometry(ctx, i, fj[i], k);
+        jobs = bucket ? fj : lsd_jobs();
+        bts = batches_of(jobs);
     }
     const bool graphable = dev_in && dev_out && emit_now && ctx->use_graphs;
     // the centroid kernel emits the records itself: no kernel reads the sizes back, so they
     // are stored straight into pinned memory (no D2H copy per frame; PCP_FM_HOST_OUT)
     const bool landed = emit_now && ctx->fm_host_out && emit_in_centroid(bts);
     if (landed) {
-        PCP_HIP(ctx, ctx->fm_res_host.ensure(3 * kMaxClouds * sizeof(uint32_t)));
+        PCP_HIP(ctx, ctx->fm_res_host.ensure(kResWords * sizeof(uint32_t)));
         res = ctx->fm_res_host.as<uint32_t>();
     }
     if (graphable) {
@@ -1744,7 +2399,18 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
         if (rc) return rc;
     }
     std::vector<ResultInfo> ri(k);
-    if ((rc = read_results(ctx, res, k, ri.data(), landed))) return rc;
+    uint32_t redo = 0;
+    if ((rc = read_results(ctx, res, k, ri.data(), landed, &redo))) return rc;
+    if (bucket && redo) {   // a bucket past its LDS capacity: the frame again on the LSD chain
+        prof_count(ctx, PCP_K_VOXEL_REDO);
+        jobs = lsd_jobs();
+        bts = batches_of(jobs);
+        {
+            ProfScope ps(ctx, PCP_K_FILTER_MERGE);
+            if ((rc = enqueue_all(ctx, bts, res, obuf, ctx->stream))) return rc;
+        }
+        if ((rc = read_results(ctx, res, k, ri.data(), landed))) return rc;
+    }
     uint64_t total = 0;
     for (int i = 0; i < k; ++i) {
         const uint64_t ni = clouds[i].n ? ri[i].n : 0;

@@ -293,7 +293,9 @@ struct pcp_ctx {
     int fan_npw = 8;                         // poses per wave of the fan kernel (PCP_FAN_NPW)
     bool fan_host_out = true;                // k_fan_reduce stores into the pinned landing
                                              // block, no D2H copy (PCP_FAN_HOST_OUT)
-    bool fm_fast = true;                     // pcp_filter_merge's fast chain (PCP_FM_FAST)
+    int fm_fast = 2;                         // pcp_filter_merge's voxel chain (PCP_FM_FAST): 2 the
+                                             // bucket chain, 1 the LSD fast chain, 0 the general one
+    pcp::DevBuf bk_stat;                     // the bucket chain's look-back words
     bool fm_host_out = true;                 // pcp_filter_merge's result sizes stored by its
                                              // kernels into pinned memory (PCP_FM_HOST_OUT)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
@@ -344,6 +346,7 @@ struct ProfScope {
     ~ProfScope();
 };
 void prof_resolve(pcp_ctx *ctx);   // after a stream sync
+void prof_count(pcp_ctx *ctx, int kid);   // one event of kid (launches + 1, no time), always
 
 // profiling of ONE kernel through the events hipExtLaunchKernelGGL records around its own
 // execution: unlike stream-ordered events on an idle queue, the interval excludes the host's

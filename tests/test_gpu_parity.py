@@ -281,6 +281,86 @@ def test_filter_merge_fast_chain(gpu, oracle, case, monkeypatch):
     np.testing.assert_array_equal(out2.view(np.uint32), out.view(np.uint32))
 
 
+@pytest.mark.parametrize("case", ["lidar", "three_clouds", "tiny", "one_bucket", "dense_redo",
+                                  "near_cap"])
+def test_filter_merge_bucket_chain(oracle, case, monkeypatch):
+    """The bucket chain (PCP_FM_FAST=2, the default: crop -> per-group counting sort by bucket ->
+    per-bucket LDS sort + input-order sums + look-back offsets) against the oracle and the LSD
+    fast chain (PCP_FM_FAST=1).  lidar: two LiDAR clouds; three_clouds: a middle cloud with
+    nothing cropped (no buckets) between two that voxelise; tiny: 5 points; one_bucket: a box of
+    < 2^11 voxels (one bucket, bs = 0); dense_redo: one voxel of 60 k points (its bucket passes
+    the LDS capacity, the frame is redone on the LSD chain: voxel_redo counts it); near_cap: a
+    dense cluster whose bucket stays just under the capacity."""
+    rng = np.random.default_rng(50 + len(case))
+    tfs = _tfs()
+    rgbs = [(255, 0, 0), (0, 0, 255)]
+    box = BOX
+    redo = 0
+    if case == "lidar":
+        clouds = [synth.lidar_cloud(700_000, seed=31), synth.lidar_cloud(500_000, seed=32,
+                                                                         sensor_height=3.5)]
+    elif case == "three_clouds":
+        far = rng.uniform(30, 40, (50_000, 4)).astype(np.float32)
+        clouds = [synth.lidar_cloud(200_000, seed=33), far, synth.lidar_cloud(90_000, seed=34)]
+        tfs = [tfs[0], tfs[1], tfs[0]]
+        rgbs = [(255, 0, 0), (0, 255, 0), (0, 0, 255)]
+    elif case == "tiny":
+        clouds = [np.array([[1, 1, 1, 0], [1.01, 1.01, 1.01, 0], [5, -3, 2, 0], [2, 2, 2, 0],
+                            [1.02, 1.0, 1.03, 0]], np.float32), synth.lidar_cloud(1000, seed=35)]
+    elif case == "one_bucket":
+        box = np.array([1.0, 1.5, -0.2, 0.3, 0.0, 0.2])
+        a = np.zeros((200_000, 4), np.float32)
+        a[:, :3] = rng.uniform([0.9, -0.3, -0.1], [1.6, 0.4, 0.3], (200_000, 3))
+        clouds = [a, a[::-1].copy()]
+    elif case == "dense_redo":
+        a = synth.lidar_cloud(300_000, seed=36)
+        a[100_000:160_000, :3] = [3.01, 2.02, 0.33]
+        clouds = [a, synth.lidar_cloud(100_000, seed=37)]
+        redo = 1
+    else:   # near_cap: ~3,500 points in one voxel of an otherwise sparse cloud
+        a = synth.lidar_cloud(200_000, seed=38)
+        a[50_000:53_500, :3] = [7.51, -1.02, 0.43]
+        clouds = [a, synth.lidar_cloud(100_000, seed=39)]
+    parts = []
+    for c, tf, rgb in zip(clouds, tfs, rgbs):
+        k = oracle.crop_box(c, box)
+        if k.size == 0:
+            parts.append(np.zeros((0, 8), np.float32))
+            continue
+        v, _, _, pt = oracle.voxel_grid(c[k], 0.05)
+        assert not pt
+        parts.append(oracle.transform_rgb(v, *tf, rgb))
+    ref = np.concatenate(parts)
+    outs = {}
+    for mode in ("2", "1"):
+        monkeypatch.setenv("PCP_FM_FAST", mode)
+        ctx = _abi.Context(0)
+        try:
+            for _ in range(2):
+                out, per = ctx.filter_merge(clouds, [box] * len(clouds), 0.05, tfs, rgbs)
+                assert list(per) == [p.shape[0] for p in parts]
+                np.testing.assert_array_equal(out[:, :5].view(np.uint32),
+                                              ref[:, :5].view(np.uint32))
+            outs[mode] = out
+            if mode == "2":
+                assert ctx.profile_get("voxel_redo")[1] == 2 * redo
+        finally:
+            ctx.close()
+    np.testing.assert_array_equal(outs["2"].view(np.uint32), outs["1"].view(np.uint32))
+
+
+def test_crop_voxel_bucket_chain_voxel_order(gpu, oracle):
+    """pcp_voxel_grid's idx / count outputs come from the general chain; pcp_crop_voxel's
+    centroids from the bucket chain (run_single): the same centroids, in PCL idx order."""
+    a = synth.lidar_cloud(400_000, seed=41)
+    out, ncrop = gpu.crop_voxel(a, BOX, 0.05)
+    kept = oracle.crop_box(a, BOX)
+    r_xyz, r_idx, r_cnt, _ = oracle.voxel_grid(a[kept], 0.05)
+    assert ncrop == kept.size
+    np.testing.assert_array_equal(out[:, :3], r_xyz)
+    assert np.all(np.diff(r_idx.astype(np.int64)) > 0)
+
+
 def test_filter_merge_device_graph_replay(gpu, oracle):
     """Device-resident inputs: the pipeline is captured into a hipGraph and replayed; every
     replay must equal the eager host-path result and the oracle."""
