@@ -715,8 +715,13 @@ def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=Fal
                      "hbm_gbs": hbm_gbs,
                      "hbm_frac": hbm_gbs / HBM_PEAK_GBS if hbm_gbs else None,
                      "traffic_over_alg": traffic / alg if traffic else None,
-                     "limiter": "crop streams at ~4.8 TB/s; the voxel stage (sort of the ~1 M "
-                                "cropped points) is launch- and latency-bound",
+                     "limiter": "crop streams its 160 MB at ~5 TB/s (1/3 of the frame); the "
+                                "voxel stage -- bucket chain: k_bk_group (per-group counting sort "
+                                "by bucket), k_bk_sort (per-bucket LDS sort + input-order sums), "
+                                "k_bk_emit -- is three dependent launches of latency-bound "
+                                "blocks (global round trips + barriers), not bytes",
+                     "chain": {1: "LSD", 2: "bucket"}.get(
+                         int(os.environ.get("PCP_FM_FAST", "2") or 2), "general"),
                      "kernel": "filter_merge graph (all stages)", "avg_kernel_ms": step_dev_ms,
                      "model": "achieved = 12 B/input point + 16 B/output point (SURVEY 8d) / "
                               "device time of the frame; hbm_frac = traffic (PMC FETCH_SIZE x2 "

@@ -1086,7 +1086,10 @@ constexpr int kBkT = 512;                 // threads of the bucket kernels
 constexpr int kBkBits = PCP_BK_BITS;      // target: ~2^kBkBits buckets per cloud
 constexpr int kBkSubMax = PCP_BK_SUB;     // sub-key bits at most (LDS table of 2^kBkSubMax + 1)
 constexpr int kBkMax = 4096;              // buckets per cloud at most
-constexpr int kBkCap = 4096;              // points per bucket at most
+#ifndef PCP_BK_CAP
+#define PCP_BK_CAP 4096
+#endif
+constexpr int kBkCap = PCP_BK_CAP;        // points per bucket at most (LDS of k_bk_sort)
 // bkv layout: [0, kBkChunkOff) per-bucket (voxels, item offset), then per-64-bucket voxel sums
 constexpr uint32_t kBkChunkOff = kBatch * kBkMax;
 constexpr int kBkGt = 15;                 // crop tiles per group at most
