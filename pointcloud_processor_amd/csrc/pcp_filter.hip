@@ -222,12 +222,7 @@ __device__ __forceinline__ uint32_t round_offsets(const uint64_t (&bal)[J], uint
         const int j = threadIdx.x / W, w = threadIdx.x % W;
         const bool in = threadIdx.x < J * W;
         const uint32_t v = in ? wo[j][w] : 0u;
-        uint32_t incl = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t u = __shfl_up(incl, o, 64);
-            if (threadIdx.x >= o) incl += u;
-        }
+        const uint32_t incl = wave_incl_scan_dpp(v);
         if (in) wo[j][w] = incl - v;
         if (threadIdx.x == 63) tot = incl;
     }
@@ -432,14 +427,11 @@ __global__ void __launch_bounds__(kCT) PCP_CROP_ATTR k_crop_tile(const JobBatch 
             J.h0[(size_t)blockIdx.x * kBins + q] = h0s[q];
         return;
     }
-    // bbox partials (used by the voxel stage; exact min/max, order-free)
+    // bbox partials (used by the voxel stage; exact min/max, order-free), DPP wave reductions
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            mn[a] = fminf(mn[a], __shfl_xor(mn[a], o, 64));
-            mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], o, 64));
-        }
+    for (int a = 0; a < 3; ++a) {
+        mn[a] = wave_minmax_dpp<false>(mn[a]);
+        mx[a] = wave_minmax_dpp<true>(mx[a]);
     }
     __shared__ float s[6][kCT / 64];
     if (lane == 0)
