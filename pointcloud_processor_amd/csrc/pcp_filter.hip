@@ -1086,6 +1086,9 @@ constexpr int kBkCap = PCP_BK_CAP;        // points per bucket at most (LDS of k
 constexpr uint32_t kBkChunkOff = kBatch * kBkMax;
 constexpr int kBkGt = 15;                 // crop tiles per group at most
 constexpr int kBkGItems = 12;             // per thread and chunk in k_bk_group
+#ifndef PCP_BK_STAGE
+#define PCP_BK_STAGE 1                    // k_bk_group places a one-chunk group in LDS first
+#endif
 
 __device__ __forceinline__ void bk_redo(uint32_t *res) { res[3 * kMaxCloudsDev] = 1u; }
 
@@ -1248,6 +1251,20 @@ k_bk_group(const JobBatch jobs, uint32_t *__restrict__ res, uint2 *__restrict__ 
     // pass B: each point to its bucket's next slot (LDS arrival order: not stable, k_bk_sort
     // restores input order inside each voxel from the slot position in .w)
     float4 *gout = J.xyz + pre;
+#if PCP_BK_STAGE
+    if (nch == 1) {   // uniform: the group fits one chunk -- placed in LDS, stored coalesced
+        __shared__ float4 stg[kChunk];
+#pragma unroll
+        for (int j = 0; j < kBkGItems; ++j) {
+            const uint32_t q = (uint32_t)j * kBkT + threadIdx.x;
+            if (q < T) stg[atomicAdd(&h[bk[j]], 1u)] = v[j];
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < T; q += kBkT) gout[q] = stg[q];
+        FLT_STAMP(0, stt, 4);
+        return;
+    }
+#endif
     for (int32_t ch = (int32_t)nch - 1; ch >= 0; --ch) {
 #pragma unroll
         for (int j = 0; j < kBkGItems; ++j) {
@@ -1377,23 +1394,40 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
         return;
     }
     // one packed exclusive scan of the table: points (low 16 bits) and occupied sub-keys (high
-    // 16).  Wave w scans the contiguous segment [w S, (w + 1) S) 64 entries per round (lane l
-    // reads entry r + l: no bank conflicts), segment totals first, then the scan with carries
+    // 16).  Wave w owns the contiguous segment [w S, (w + 1) S); round r covers its entries
+    // r * 64 + lane (no bank conflicts).  All rounds' loads and DPP scans are independent of
+    // each other (ILP), the rounds' totals chain in scalar adds, one barrier for the waves
     uint32_t nvox;
     {
+        constexpr int kR = ((1 << kBkSubMax) + kBkT3 - 1) / kBkT3;   // rounds per wave at most
         const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
         const uint32_t S = max(64u, nsub / (uint32_t)(kBkT3 / 64));
         const uint32_t e0 = (uint32_t)wid * S;
-        uint32_t tsum = 0;
-        if (e0 < nsub) {
-            for (uint32_t r = 0; r < S; r += 64) {
-                const uint32_t e = e0 + r + lane;
-                const uint32_t t = e < nsub ? tab[e] : 0u;
-                tsum += t | (t ? 0x10000u : 0u);
+        uint32_t wtot = 0;
+        constexpr int kH = kR < 4 ? kR : 4;   // rounds in flight together (register pressure)
+#pragma unroll
+        for (int r0 = 0; r0 < kR; r0 += kH) {
+            uint32_t v[kH];
+#pragma unroll
+            for (int h = 0; h < kH; ++h) {
+                const int r = r0 + h;
+                const uint32_t e = e0 + (uint32_t)r * 64 + lane;
+                const uint32_t t = (r < kR && (uint32_t)r * 64 < S && e < nsub) ? tab[e] : 0u;
+                v[h] = t | (t ? 0x10000u : 0u);
             }
-            tsum = wave_sum_dpp(tsum);
+#pragma unroll
+            for (int h = 0; h < kH; ++h) {
+                if (r0 + h >= kR) continue;
+                const uint32_t x = wave_incl_scan_dpp(v[h]);
+                const uint32_t rt = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+                const int r = r0 + h;
+                const uint32_t e = e0 + (uint32_t)r * 64 + lane;
+                if ((uint32_t)r * 64 < S && e < nsub)
+                    tab[e] = x - v[h] + wtot;   // exclusive within the wave's segment
+                wtot += rt;
+            }
         }
-        if (lane == 0) lsa[wid] = tsum;
+        if (lane == 0) lsa[wid] = wtot;
         __syncthreads();
         uint32_t off = 0, all = 0;
 #pragma unroll
@@ -1402,14 +1436,11 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
             all += lsa[w];
         }
         nvox = all >> 16;
-        if (e0 < nsub) {
-            for (uint32_t r = 0; r < S; r += 64) {
-                const uint32_t e = e0 + r + lane;
-                const uint32_t t = e < nsub ? tab[e] : 0u;
-                const uint32_t v = t | (t ? 0x10000u : 0u);
-                const uint32_t incl = wave_incl_scan_dpp(v);
-                if (e < nsub) tab[e] = off + incl - v;
-                off += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (off) {   // wave-uniform: the segments after the first get their wave's offset
+#pragma unroll
+            for (int r = 0; r < kR; ++r) {
+                const uint32_t e = e0 + (uint32_t)r * 64 + lane;
+                if ((uint32_t)r * 64 < S && e < nsub) tab[e] += off;
             }
         }
         if (threadIdx.x == 0) tab[nsub] = n | (nvox << 16);
