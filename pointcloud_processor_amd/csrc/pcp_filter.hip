@@ -27,7 +27,10 @@ constexpr int kFT = 256;            // threads per block
 #define PCP_CROP_THREADS 256
 #endif
 constexpr int kCT = PCP_CROP_THREADS;   // threads of a crop block (build knob)
-constexpr int kCropTile = 4096;         // points per crop tile
+#ifndef PCP_CROP_TILE
+#define PCP_CROP_TILE 4096
+#endif
+constexpr int kCropTile = PCP_CROP_TILE;   // points per crop tile (build knob)
 constexpr int kCropItems = kCropTile / kCT;   // points per thread per crop tile
 constexpr int kST = 512;            // threads of the sort-tile kernels (8 waves)
 constexpr int kSW = kST / 64;
