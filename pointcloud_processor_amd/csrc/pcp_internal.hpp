@@ -295,7 +295,9 @@ struct pcp_ctx {
                                              // block, no D2H copy (PCP_FAN_HOST_OUT)
     int fm_fast = 2;                         // pcp_filter_merge's voxel chain (PCP_FM_FAST): 2 the
                                              // bucket chain, 1 the LSD fast chain, 0 the general one
-    pcp::DevBuf bk_stat;                     // the bucket chain's look-back words
+    pcp::DevBuf bk_stat;                     // the bucket chain's per-bucket words
+    int bk_gt = 0;                           // crop tiles per k_bk_group group (PCP_BK_GT; 0: one
+                                             // round of blocks)
     bool fm_host_out = true;                 // pcp_filter_merge's result sizes stored by its
                                              // kernels into pinned memory (PCP_FM_HOST_OUT)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
