@@ -408,6 +408,54 @@ def test_filter_merge_device_graph_replay(gpu, oracle):
                                   np.concatenate(parts)[:, :5].view(np.uint32))
 
 
+def test_filter_merge_device_graph_redo(oracle):
+    """Device-resident inputs through the captured graph when the bucket chain must redo the
+    frame (one 30 k-point voxel: its bucket passes the LDS capacity): every replay redoes the
+    frame on the LSD chain inside the call and returns the oracle's bytes; a later frame whose
+    buckets fit replays the same graph without a redo."""
+    a = synth.lidar_cloud(200_000, seed=61)
+    a[20_000:50_000, :3] = [4.01, -2.02, 0.51]
+    b = synth.lidar_cloud(100_000, seed=62, sensor_height=3.5)
+    tfs = _tfs()
+    rgbs = [(255, 0, 0), (0, 0, 255)]
+    parts = []
+    for c, tf, rgb in zip([a, b], tfs, rgbs):
+        k = oracle.crop_box(c, BOX)
+        v, _, _, _ = oracle.voxel_grid(c[k], 0.05)
+        parts.append(oracle.transform_rgb(v, *tf, rgb))
+    ref = np.concatenate(parts)
+    ctx = _abi.Context(0)
+    dp = [ctx.dev_alloc(c.nbytes) for c in (a, b)]
+    cap = a.shape[0] + b.shape[0]
+    out_d = ctx.dev_alloc(cap * 32)
+    try:
+        for p, c in zip(dp, (a, b)):
+            ctx.h2d(p, c)
+        views = [_abi.CloudView(p, c.shape[0], 16, 0, 4, 8) for p, c in zip(dp, (a, b))]
+        for i in range(3):   # capture, then replays
+            n, per = ctx.filter_merge_device(views, [BOX, BOX], 0.05, tfs, rgbs, out_d, cap)
+            assert n == ref.shape[0] and list(per) == [p.shape[0] for p in parts]
+            got = np.empty((n, 8), np.float32)
+            ctx.d2h(got, out_d)
+            np.testing.assert_array_equal(got[:, :5].view(np.uint32), ref[:, :5].view(np.uint32))
+            assert ctx.profile_get("voxel_redo")[1] == i + 1
+        # the dense voxel gone (same views, same graph): no redo
+        a2 = synth.lidar_cloud(200_000, seed=61)
+        ctx.h2d(dp[0], a2)
+        n2, _ = ctx.filter_merge_device(views, [BOX, BOX], 0.05, tfs, rgbs, out_d, cap)
+        assert ctx.profile_get("voxel_redo")[1] == 3
+        k2 = oracle.crop_box(a2, BOX)
+        v2, _, _, _ = oracle.voxel_grid(a2[k2], 0.05)
+        ref2 = np.concatenate([oracle.transform_rgb(v2, *tfs[0], rgbs[0]), parts[1]])
+        got = np.empty((n2, 8), np.float32)
+        ctx.d2h(got, out_d)
+        np.testing.assert_array_equal(got[:, :5].view(np.uint32), ref2[:, :5].view(np.uint32))
+    finally:
+        for p in dp + [out_d]:
+            ctx.dev_free(p)
+        ctx.close()
+
+
 def test_filter_merge_pinned_staging(gpu):
     """PointCloud2 boundary with page-locked buffers: clouds and the output pinned in place
     (pcp_host_register) and a pcp_host_alloc block must give the pageable path's bytes."""
