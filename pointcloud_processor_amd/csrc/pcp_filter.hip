@@ -1488,11 +1488,19 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
         const uint32_t t0 = tab[sub[j]], st = t0 & 0xffffu, vr = t0 >> 16;
         const uint32_t cnt = (tab[sub[j] + 1] & 0xffffu) - st;
         float sx = 0.f, sy = 0.f, sz = 0.f;
-        for (uint32_t u = st; u < st + cnt; ++u) {
-            const float4 a = J.xyz[p1[u]];
-            sx = sx + a.x;
-            sy = sy + a.y;
-            sz = sz + a.z;
+        // four loads in flight, then the adds in input order (bit-identical)
+        for (uint32_t u = st; u < st + cnt; u += 4) {
+            float4 a[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h)
+                if (u + h < st + cnt) a[h] = J.xyz[p1[u + h]];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                if (u + h >= st + cnt) break;
+                sx = sx + a[h].x;
+                sy = sy + a[h].y;
+                sz = sz + a[h].z;
+            }
         }
         const float fc = (float)cnt;
         tmp[vr] = make_float4(sx / fc, sy / fc, sz / fc, 1.0f);
