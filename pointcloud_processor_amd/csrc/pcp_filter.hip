@@ -1520,7 +1520,10 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
 // the per-64-bucket sums k_bk_sort accumulated before f's chunk + the buckets of f's chunk
 // before f (one load per lane of one wave); the centroids copied there (emit: through the
 // cloud's transform + colour as merged records); the cloud's last bucket writes its count.
-constexpr int kBkTE = 256;
+#ifndef PCP_BK_TE
+#define PCP_BK_TE 256
+#endif
+constexpr int kBkTE = PCP_BK_TE;          // k_bk_emit threads (build knob)
 __device__ __forceinline__ uint32_t bk_voxels_before(const uint2 *bkv, uint32_t f) {
     // wave 0 only (full wave): lanes sum chunk sums [0, f / 64) and buckets [f & ~63, f)
     const uint32_t lane = threadIdx.x & 63, nch = f >> 6, c0 = f & ~63u;
