@@ -78,6 +78,11 @@ def _self_launch(n: int) -> int:
 
 
 def _dist_init(n_gpus: int):
+    """torch.distributed as the host-side control plane only (gloo: barriers, the max-over-ranks
+    timing, the RCCL id hand-off).  The data-path collective (`backend`): "rccl" = libpcp's own
+    RCCL communicator (pcp_comm_init_rank), one process per GPU, so the only HIP runtime in the
+    process is libpcp's (torch never touches the GPU: its wheel bundles another runtime);
+    "gloo" = a rehearsal with more ranks than GPUs (ranks share devices, host vectors)."""
     import torch
     import torch.distributed as dist
 
@@ -89,14 +94,17 @@ def _dist_init(n_gpus: int):
     backend = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # one process per GPU over RCCL; with fewer GPUs than ranks (a rehearsal on a 1-GPU
-        # box) the ranks share devices and the collective runs over gloo
-        ndev = torch.cuda.device_count()
-        backend = os.environ.get("PCP_DIST_BACKEND", "nccl" if ndev >= world else "gloo")
+        try:
+            from pointcloud_processor_amd import _abi
+
+            ndev = _abi.device_count()
+        except OSError:          # no library (the CPU launch check)
+            ndev = 0
+        backend = os.environ.get("PCP_DIST_BACKEND", "rccl" if ndev >= world else "gloo")
+        backend = "rccl" if backend == "nccl" else backend
         if ndev:
             local = local % ndev
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+        dist.init_process_group(backend="gloo")
     return torch, (dist if world > 1 else None), world, rank, local, backend
 
 
@@ -275,16 +283,16 @@ def cpu_baseline_c3(clouds, box, leaf, tfs, budget_s: float = 4.0, threads: int 
                       f"{dt:.3f} s per frame ({how})"}
 
 
-def _timed(step, args, dist, on_gpu, dev):
-    """W untimed warmup steps, then exactly K steps between barrier + synchronize on both
-    sides; -> (max-over-ranks seconds, sum-over-ranks units, last step's result)."""
+def _timed(step, args, dist, sync):
+    """W untimed warmup steps, then exactly K steps between barrier + device synchronize on both
+    sides (sync: the library context's stream synchronisation -- all of a step's work is on that
+    stream); -> (max-over-ranks seconds, sum-over-ranks units, last step's result)."""
     import torch
 
     def barrier_sync():
         if dist is not None:
             dist.barrier()
-        if on_gpu:
-            torch.cuda.synchronize()
+        sync()
 
     for _ in range(args.warmup):
         step()
@@ -306,8 +314,7 @@ def _timed(step, args, dist, on_gpu, dev):
             gc.enable()
     t = torch.tensor([dt], dtype=torch.float64)
     uu = torch.tensor([units], dtype=torch.float64)
-    if dist is not None:
-        t, uu = t.to(dev), uu.to(dev)
+    if dist is not None:   # host-side (gloo)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(uu, op=dist.ReduceOp.SUM)
     return float(t.item()), float(uu.item()), res
@@ -423,9 +430,11 @@ def run_all(args, torch, dist, world, rank, local, backend):
     from pointcloud_processor_amd import _abi, synth
     from pointcloud_processor_amd import dist as pd
 
-    on_gpu = torch.cuda.is_available()
-    dev = torch.device("cuda", local) if (on_gpu and backend != "gloo") else torch.device("cpu")
     ctx = _abi.Context(local)
+    if backend == "rccl":   # libpcp's own communicator; the id travels over the gloo group
+        uid = [_abi.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init_rank(world, uid[0], rank)
     scene = synth.terrain_scene()
     ctx.set_terrain(scene.terrain, point_step=32)
     P_total = args.poses_per_gpu * world
@@ -439,59 +448,40 @@ def run_all(args, torch, dist, world, rank, local, backend):
 
     blocked_h = np.zeros(max(poses.shape[0], 1), np.uint32)
     units_h = np.zeros(max(poses.shape[0], 1), np.uint64)
-    # N > 1 over RCCL: the per-pose keys never leave the device before the collective --
-    # pcp_raycast_fan_keys writes (blocked << 32) | pose into a torch int64 vector (INT64_MAX
-    # in the other ranks' slots) on the library's stream and returns once they are written, one
-    # all_reduce(MIN) in place, and only the reduced vector comes back D2H.  The gloo
+    # N > 1 over RCCL: libpcp's own communicator -- the per-pose keys (blocked << 32) | pose
+    # are written into the context's device vector, ONE ncclAllReduce(MIN) runs on the library's
+    # stream, only the reduced vector comes back (pcp_raycast_fan_allreduce).  The gloo
     # rehearsal (ranks sharing one GPU) keeps the host-side vector of dist.reduce_fan.
-    dev_keys = dist is not None and on_gpu and backend == "nccl"
-    if dev_keys:
-        keys_t = torch.empty(P_total, dtype=torch.int64, device=dev)
-        units_t = torch.zeros(max(poses.shape[0], 1), dtype=torch.int64, device=dev)
-        # no stream handle: torch's wheel carries its own HIP runtime, whose hipStream_t means
-        # nothing to libpcp's (/opt/rocm) -- the call waits for its keys before it returns, and
-        # the keys stay on the device for the collective
-        stream_ptr = None
-        units_step = {}
+    own_comm = backend == "rccl"
+    if own_comm:
+        blocked_all = np.zeros(max(P_total, 1), np.uint32)
 
         def fan_step():
-            ctx.raycast_fan_keys(poses, fan, lo, P_total, keys_t.data_ptr(), units_t.data_ptr(),
-                                 stream_ptr)
-            dist.all_reduce(keys_t, op=dist.ReduceOp.MIN)   # the one collective
-            kh = keys_t.cpu().numpy()                        # the reduced vector, D2H once
-            best["fan"] = int(kh.min()) & 0xFFFFFFFF
-            if "u" not in units_step:   # constant per pose set; re-read after the timed loop
-                units_step["u"] = int(units_t[:poses.shape[0]].sum().item())
-            return units_step["u"], kh
+            best["fan"], _ = ctx.raycast_fan_allreduce(poses, fan, lo, P_total, blocked_all,
+                                                       units_h)
+            return int(units_h[:poses.shape[0]].sum()), blocked_all
     else:
         def fan_step():
             b = ctx.raycast_fan_into(poses, fan, blocked_h, units_h)   # argmin of its poses
             if dist is None:   # one rank: the library's argmin is the node's answer
                 keys = blocked_h
             else:
-                keys, b = pd.reduce_fan(blocked_h[:poses.shape[0]], lo, hi, P_total, dist, dev)
+                keys, b = pd.reduce_fan(blocked_h[:poses.shape[0]], lo, hi, P_total, dist)
             best["fan"] = b   # ^ the one collective
             return int(units_h[:poses.shape[0]].sum()), keys
 
-    dt, units_all, _ = _timed(fan_step, args, dist, on_gpu, dev)
+    dt, units_all, _ = _timed(fan_step, args, dist, ctx.synchronize)
     collective = None
-    if dev_keys:
-        # the count the timed steps used is the kernel's (same poses, same work every step)
-        if int(units_t[:poses.shape[0]].sum().item()) != units_step["u"]:
-            raise SystemExit("bench.py: ray-hit tests changed between steps")
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if own_comm:
         ms = []
         for _ in range(max(args.steps, 3)):   # after the timed loop: events around the collective
-            ctx.raycast_fan_keys(poses, fan, lo, P_total, keys_t.data_ptr(), units_t.data_ptr(),
-                                 stream_ptr)
-            e0.record()
-            dist.all_reduce(keys_t, op=dist.ReduceOp.MIN)
-            e1.record()
-            e1.synchronize()
-            ms.append(e0.elapsed_time(e1))
-        collective = {"op": "all_reduce(MIN) int64", "backend": backend,
+            ms.append(ctx.raycast_fan_allreduce(poses, fan, lo, P_total, blocked_all, units_h,
+                                                timed=True)[1])
+        collective = {"op": "ncclAllReduce(ncclUint64, ncclMin)", "backend": "rccl (libpcp)",
                       "bytes": 8 * P_total, "collective_ms": float(np.median(ms)),
-                      "path": "device keys (pcp_raycast_fan_keys), reduced vector D2H once"}
+                      "path": "device keys in libpcp's vector, libpcp's own RCCL communicator on "
+                              "its stream (pcp_raycast_fan_allreduce), reduced vector D2H once; "
+                              "torch.distributed (gloo) only for the id hand-off and barriers"}
     elif dist is not None:
         collective = {"op": "all_reduce(MIN) int64", "backend": backend, "bytes": 8 * P_total,
                       "path": "host vector (gloo rehearsal: ranks share devices)"}
@@ -521,7 +511,7 @@ def run_all(args, torch, dist, world, rank, local, backend):
                    "terrain_points": int(scene.terrain.shape[0]),
                    "poses_total": P_total, "fan": [args.n_az, args.n_el],
                    "num_candidates_lattice": nc, "parallelism": f"pose-shard x{world}",
-                   "collective": None if dist is None else f"all_reduce(MIN) over {backend}"},
+                   "collective": None if dist is None else f"all-reduce(MIN) over {backend}"},
         "collective": collective,
         "poses_per_s": P_total * args.steps / dt,
         "best_pose": best["fan"],
@@ -530,8 +520,8 @@ def run_all(args, torch, dist, world, rank, local, backend):
     out["roofline"]["kernel_time_source"] = ("HIP events around 20 back-to-back launches "
                                              "(pcp_raycast_fan_burst)")
     out["roofline"]["event_avg_ms_in_loop"] = k_avg
-    if dist is not None and backend == "gloo" and on_gpu:
-        out["rehearsal"] = (f"{world} ranks on {torch.cuda.device_count()} GPU(s): collective "
+    if dist is not None and backend == "gloo":
+        out["rehearsal"] = (f"{world} ranks on {_abi.device_count()} GPU(s): collective "
                             "over gloo, ranks share devices")
     host = _host_cpu()
     cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
@@ -567,11 +557,11 @@ def run_all(args, torch, dist, world, rank, local, backend):
             if dist is None:   # one rank: the library's strict-'>' argmax (rep.best_idx)
                 b = rep.best_idx
             else:
-                _, b, _ = pd.reduce_scores(tot[:cposes.shape[0]], lo, hi, P_total, dist, dev)
+                _, b, _ = pd.reduce_scores(tot[:cposes.shape[0]], lo, hi, P_total, dist)
             best["cells"] = b
             return cposes.shape[0], tot
 
-        cdt, cunits, _ = _timed(cells_step, args, dist, on_gpu, dev)
+        cdt, cunits, _ = _timed(cells_step, args, dist, ctx.synchronize)
         kern = _profiled(ctx, cells_step, max(args.steps, 3),
                          ("score_cells", "pose_sum", "cell_flags"))
         out["poses_per_s_reference_mode"] = cunits / cdt
@@ -649,8 +639,6 @@ def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=Fal
 
     from pointcloud_processor_amd import _abi, synth
 
-    on_gpu = torch.cuda.is_available()
-    dev = torch.device("cuda", local) if (on_gpu and backend != "gloo") else torch.device("cpu")
     ctx = _abi.Context(local)
     n_each = args.filter_points // 2
     clouds = [synth.lidar_cloud(n_each, sensor_height=2.0, seed=1 + 2 * rank),
@@ -679,7 +667,7 @@ def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=Fal
         last["n_out"], last["per"] = n_out, per
         return n_in, n_out
 
-    dt, units_all, _ = _timed(step, args, dist, on_gpu, dev)
+    dt, units_all, _ = _timed(step, args, dist, ctx.synchronize)
     step_dev_ms = _profiled(ctx, step, max(args.steps, 3), ["filter_merge"])["filter_merge"]
     n_out = last["n_out"]
     stages = None
@@ -876,7 +864,9 @@ def run_c5(args, torch, dist, world, rank, local, backend=None):
     bb = ",".join(repr(float(v)) for v in cells.grid_bbox)
     cli = Path(__file__).resolve().parent / "pointcloud_processor_amd" / "_lib" / "pcp_nodes_cli"
     env = dict(os.environ)
-    ndev = torch.cuda.device_count()
+    from pointcloud_processor_amd import _abi
+
+    ndev = _abi.device_count()
     if ndev:   # the replica's own GPU (device 0 of the child)
         env["HIP_VISIBLE_DEVICES"] = str(local % ndev)
     frames = max(args.steps, 20)
@@ -892,8 +882,7 @@ def run_c5(args, torch, dist, world, rank, local, backend=None):
     lat = np.array(res["lat_ms"])
     vals = [1e3 / float(lat.mean()), res["p50_ms"], res["p99_ms"]]
     if dist is not None:
-        t = torch.tensor(vals, dtype=torch.float64,
-                         device=f"cuda:{local}" if backend == "nccl" else "cpu")
+        t = torch.tensor(vals, dtype=torch.float64)   # host-side (gloo)
         s = t.clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         m = t.clone()

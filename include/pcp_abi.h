@@ -60,6 +60,11 @@ void pcp_destroy(pcp_ctx *ctx);
 const char *pcp_last_error(const pcp_ctx *ctx);
 int pcp_synchronize(pcp_ctx *ctx);
 
+/* a second HIP stream of libpcp's own runtime on the context's device (e.g. the wait_stream of
+ * pcp_raycast_fan_keys); the caller destroys it before the context */
+int pcp_stream_create(pcp_ctx *ctx, void **stream);
+int pcp_stream_destroy(pcp_ctx *ctx, void *stream);
+
 /* device buffers owned by the caller (for inputs resident in HBM, e.g. benchmarks) */
 int pcp_dev_alloc(pcp_ctx *ctx, uint64_t bytes, void **dptr);
 int pcp_dev_free(pcp_ctx *ctx, void *dptr);
@@ -336,6 +341,34 @@ int pcp_raycast_fan_stamps(pcp_ctx *ctx, const double *poses5, uint64_t n,
 int pcp_raycast_fan_keys(pcp_ctx *ctx, const double *poses5, uint64_t n,
                          const pcp_fan_params *fan, uint64_t lo, uint64_t p_total,
                          int64_t *keys_dev, uint64_t *units_dev, void *wait_stream);
+
+/* ---- one process per GPU: libpcp's own RCCL communicator (bench.py --gpus N) ------------ */
+/* The caller's framework only carries the 128-byte id from rank 0 to the others (and its own
+ * host-side barriers); the collective runs in this library's HIP runtime on the context's
+ * stream, so no stream or device pointer ever crosses into another runtime (a PyTorch wheel
+ * bundles its own).  pcp_comm_unique_id: rank 0, before the others' pcp_comm_init_rank
+ * (ncclGetUniqueId); pcp_comm_init_rank: ncclCommInitRank on the context's device, collective
+ * over all ranks (each rank's context on a distinct device).  The communicator lives until
+ * pcp_destroy. */
+#define PCP_COMM_ID_BYTES 128
+int pcp_comm_unique_id(uint8_t id[PCP_COMM_ID_BYTES]);
+int pcp_comm_init_rank(pcp_ctx *ctx, int nranks, const uint8_t id[PCP_COMM_ID_BYTES], int rank);
+int pcp_comm_info(const pcp_ctx *ctx, int *nranks, int *rank);   /* 0 ranks: none */
+/* One rank's shard of a pose-sharded fan query, collective included (every rank calls it with
+ * the same p_total and fan): the fans of poses5[0 .. n) -- global poses [lo, lo + n) -- cast as
+ * pcp_raycast_fan does, their keys (blocked << 32) | global pose written into the context's
+ * device vector of p_total uint64 (UINT64_MAX elsewhere), ONE ncclAllReduce(ncclUint64,
+ * ncclMin) over it on the context's stream, the reduced vector copied back once.
+ * blocked_all (host, p_total entries, nullable): every pose's blocked count on every rank;
+ * units (host, n entries, nullable): this shard's ray-hit tests per pose; best_idx: the argmin
+ * (ties: lowest index; virtual_lidar.cpp:467-475); collective_ms (nullable): the all-reduce's
+ * time between two events on the stream.  PCP_E_STATE without a communicator, or when a pose
+ * of [0, p_total) was written by no rank.  Replaces the pose loop of runOptimization
+ * (virtual_lidar.cpp:467-475) for N processes. */
+int pcp_raycast_fan_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                              const pcp_fan_params *fan, uint64_t lo, uint64_t p_total,
+                              uint32_t *blocked_all, uint64_t *units, int64_t *best_idx,
+                              double *collective_ms);
 
 /* ---- one process, n GPUs: the pose search sharded over devices ------ */
 /* pcp_multi_create(n_dev, devices, &m): one context per device (devices NULL: 0 .. n_dev-1)

@@ -138,6 +138,14 @@ _SIGS = [
                                         C.POINTER(C.c_double)]),
     ("pcp_raycast_fan_keys", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), C.c_uint64,
                                        C.c_uint64, _P, _P, _P]),
+    ("pcp_comm_unique_id", C.c_int, [_P]),
+    ("pcp_comm_init_rank", C.c_int, [_P, C.c_int, _P, C.c_int]),
+    ("pcp_comm_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("pcp_raycast_fan_allreduce", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), C.c_uint64,
+                                            C.c_uint64, _P, _P, C.POINTER(C.c_int64),
+                                            C.POINTER(C.c_double)]),
+    ("pcp_stream_create", C.c_int, [_P, C.POINTER(_P)]),
+    ("pcp_stream_destroy", C.c_int, [_P, _P]),
     ("pcp_step_table", C.c_int, [C.c_double, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("pcp_terrain_info", C.c_int, [_P, C.POINTER(IndexInfo)]),
     ("pcp_multi_create", C.c_int, [C.c_int, _P, C.POINTER(_P)]),
@@ -186,6 +194,16 @@ def device_count() -> int:
     n = C.c_int(0)
     rc = load_library().pcp_device_count(C.byref(n))
     return n.value if rc == PCP_OK else 0
+
+
+def comm_unique_id() -> bytes:
+    """pcp_comm_unique_id: rank 0's 128-byte RCCL id, to be shared with the other ranks out
+    of band (bench.py: torch.distributed over gloo) before their comm_init_rank."""
+    buf = (C.c_uint8 * 128)()
+    rc = load_library().pcp_comm_unique_id(buf)
+    if rc != PCP_OK:
+        raise PcpError(rc, "pcp_comm_unique_id failed (ncclGetUniqueId)")
+    return bytes(buf)
 
 
 def _ptr(a: np.ndarray | None):
@@ -631,6 +649,52 @@ class Context:
         self._check(self.lib.pcp_raycast_fan_keys(self.h, poses5.ctypes.data, P, C.byref(fan),
                                                   lo, p_total, keys_dev_ptr, units_dev_ptr,
                                                   wait_stream), "pcp_raycast_fan_keys")
+
+    def stream_create(self) -> int:
+        """A second HIP stream of libpcp's own runtime on this context's device (a wait_stream
+        for raycast_fan_keys); release with stream_destroy."""
+        h = C.c_void_p()
+        self._check(self.lib.pcp_stream_create(self.h, C.byref(h)), "pcp_stream_create")
+        return h.value
+
+    def stream_destroy(self, stream: int):
+        self._check(self.lib.pcp_stream_destroy(self.h, stream), "pcp_stream_destroy")
+
+    def comm_init_rank(self, nranks: int, uid: bytes, rank: int):
+        """pcp_comm_init_rank: this context's own RCCL communicator (one process per GPU)."""
+        if len(uid) != 128:
+            raise ValueError("comm_init_rank: the id is 128 bytes (comm_unique_id)")
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.lib.pcp_comm_init_rank(self.h, nranks, buf, rank), "pcp_comm_init_rank")
+
+    def comm_info(self):
+        n, r = C.c_int(), C.c_int()
+        self._check(self.lib.pcp_comm_info(self.h, C.byref(n), C.byref(r)), "pcp_comm_info")
+        return n.value, r.value
+
+    def raycast_fan_allreduce(self, poses5: np.ndarray, fan: FanParams, lo: int, p_total: int,
+                              blocked_all: np.ndarray | None = None,
+                              units: np.ndarray | None = None, timed: bool = False):
+        """pcp_raycast_fan_allreduce: this rank's poses [lo, lo + P) of p_total, the keys
+        reduced by libpcp's own RCCL communicator (comm_init_rank).  blocked_all (uint32
+        [p_total]) / units (uint64 [P]) are filled when given.  -> (best index, collective ms
+        or None)."""
+        P = poses5.shape[0]
+        if (poses5.dtype != np.float64 or not poses5.flags.c_contiguous or poses5.ndim != 2
+                or poses5.shape[1] != 5):
+            raise ValueError("raycast_fan_allreduce: poses float64 [P, 5]")
+        if blocked_all is not None and (blocked_all.dtype != np.uint32 or
+                                        blocked_all.shape[0] < p_total):
+            raise ValueError("raycast_fan_allreduce: blocked_all uint32 [>= p_total]")
+        if units is not None and (units.dtype != np.uint64 or units.shape[0] < P):
+            raise ValueError("raycast_fan_allreduce: units uint64 [>= P]")
+        best = C.c_int64()
+        ms = C.c_double()
+        self._check(self.lib.pcp_raycast_fan_allreduce(
+            self.h, poses5.ctypes.data if P else None, P, C.byref(fan), lo, p_total,
+            _ptr(blocked_all), _ptr(units), C.byref(best), C.byref(ms) if timed else None),
+            "pcp_raycast_fan_allreduce")
+        return best.value, (ms.value if timed else None)
 
     def raycast_fan(self, poses5: np.ndarray, fan: FanParams, want_first_hit=False):
         poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)

@@ -456,6 +456,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     prof_resolve(ctx);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->keys_ev) (void)hipEventDestroy(ctx->keys_ev);
+    comm_release(ctx);
     for (int k = 0; k < pcp_ctx::kUpRing; ++k) {
         if (ctx->up_ev[k]) (void)hipEventDestroy(ctx->up_ev[k]);
         ctx->up_buf[k].release();
@@ -495,6 +496,23 @@ int pcp_synchronize(pcp_ctx *ctx) {
     if (!ctx) return PCP_E_INVALID;
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     prof_resolve(ctx);
+    return PCP_OK;
+}
+
+int pcp_stream_create(pcp_ctx *ctx, void **stream) {
+    if (!ctx || !stream) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = nullptr;
+    PCP_HIP(ctx, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return PCP_OK;
+}
+
+int pcp_stream_destroy(pcp_ctx *ctx, void *stream) {
+    if (!ctx || !stream) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    PCP_HIP(ctx, hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    PCP_HIP(ctx, hipStreamDestroy(static_cast<hipStream_t>(stream)));
     return PCP_OK;
 }
 

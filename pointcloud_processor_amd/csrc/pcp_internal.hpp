@@ -268,6 +268,13 @@ struct pcp_ctx {
     // query waits for it before it reuses the pinned pose staging
     hipEvent_t keys_ev = nullptr;
     bool keys_pending = false;
+    // one process per GPU (pcp_comm_init_rank): this rank's RCCL communicator (an ncclComm_t),
+    // the key vector its collective reduces and the pinned landing of the reduced vector
+    void *comm = nullptr;
+    int comm_nranks = 0, comm_rank = 0;
+    pcp::DevBuf comm_keys;
+    pcp::PinnedBuf comm_host;
+    hipEvent_t comm_ev[2] = {};
     // pinned upload ring (upload_async): host bytes copied here, then a stream-ordered DMA
     static constexpr int kUpRing = 4;
     pcp::PinnedBuf up_buf[kUpRing];
@@ -452,6 +459,9 @@ void launch_keys_combine(hipStream_t st, unsigned long long *a, const unsigned l
 // the colour-statistics slots (k_cell_flags order) -> pcp_vl_report
 void fill_report(const int32_t *st_h, double zx_total, int64_t best_idx, double best,
                  pcp_vl_report *rep);
+
+// the context's RCCL communicator and its buffers (pcp_comm.hip), at pcp_destroy
+void comm_release(pcp_ctx *ctx);
 
 // validate a cloud view
 int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what);

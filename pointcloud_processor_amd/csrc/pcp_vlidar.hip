@@ -1843,6 +1843,11 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
     int K = 0;
     int rc = ensure_steps(ctx, fan->max_distance - kVisRadius, &K);
     if (rc) return rc;
+    // a keys query handed to a wait_stream may not have uploaded its poses yet: its copy reads
+    // the pinned staging below, so that copy must be done before the staging is rewritten (or
+    // regrown) by this query, whichever entry point enqueues it
+    if (ctx->keys_pending) PCP_HIP(ctx, hipEventSynchronize(ctx->keys_ev));
+    ctx->keys_pending = false;
     // pinned staging: poses in (P x 8 doubles), then {units u64[P], blocked u32[P]} out
     PCP_HIP(ctx, ctx->fan_host.ensure((size_t)P * (8 * sizeof(double) + 12) + 64));
     double *pose8 = ctx->fan_host.as<double>();
@@ -2133,9 +2138,8 @@ int pcp_raycast_fan_keys(pcp_ctx *ctx, const double *poses5, uint64_t n,
                        (unsigned long long)p_total);
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    // the previous query's pose upload must be done before the pinned staging is rewritten
-    if (ctx->keys_pending) PCP_HIP(ctx, hipEventSynchronize(ctx->keys_ev));
-    ctx->keys_pending = false;
+    // (fan_enqueue waits for a previous keys query's pose upload before it rewrites the
+    // pinned staging; an n == 0 shard touches no staging)
     const uint32_t *blocked_d = nullptr;
     if (n) {
         FanEnq o;

@@ -1337,6 +1337,82 @@ def test_fan_device_keys_match_reduce_fan():
     assert "device keys ok" in r.stdout
 
 
+def test_fan_allreduce_own_communicator(gpu, loaded, scene):
+    """bench.py --gpus N with libpcp's OWN RCCL communicator (one HIP runtime in the process):
+    pcp_comm_init_rank over one rank, then pcp_raycast_fan_allreduce -- keys on the context's
+    device vector, ncclAllReduce(MIN) on its stream, the reduced vector back once -- bit-identical
+    to the host path (raycast_fan -> dist.reduce_fan): every blocked count, the units, the argmin.
+    A shard that leaves poses unwritten is refused (PCP_E_STATE), an empty shard is not."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    from pointcloud_processor_amd import dist as pd
+
+    poses, _ = bench._poses_for(gpu, bench._grid_bbox(scene.area), scene.zx120_pose5, 96)
+    fan = _abi.fan_params(n_az=256, n_el=64)
+    b1, u1, _, _ = gpu.raycast_fan(poses, fan)
+    P = poses.shape[0]
+    ref_keys, ref_best = pd.reduce_fan(b1, 0, P, P)
+    with _abi.Context(0) as ctx:
+        assert ctx.comm_info() == (0, 0)
+        with pytest.raises(_abi.PcpError):          # no communicator yet
+            ctx.raycast_fan_allreduce(poses, fan, 0, P)
+        ctx.comm_init_rank(1, _abi.comm_unique_id(), 0)
+        assert ctx.comm_info() == (1, 0)
+        ctx.set_terrain(scene.terrain, point_step=32)
+        for rep in range(3):                         # steady state: same answer every query
+            blocked = np.zeros(P, np.uint32)
+            units = np.zeros(P, np.uint64)
+            best, ms = ctx.raycast_fan_allreduce(poses, fan, 0, P, blocked, units, timed=rep == 2)
+            np.testing.assert_array_equal(blocked, ref_keys)
+            np.testing.assert_array_equal(units, u1)
+            assert best == ref_best == int(np.argmin(b1))
+        assert ms is not None and ms >= 0.0
+        with pytest.raises(_abi.PcpError):           # poses [P/2, P) written by no rank
+            ctx.raycast_fan_allreduce(np.ascontiguousarray(poses[:P // 2]), fan, 0, P)
+        best, _ = ctx.raycast_fan_allreduce(poses[:0].copy(), fan, 0, 0)
+        assert best == -1
+
+
+def test_fan_keys_wait_stream_then_fan(gpu, loaded, scene, oracle):
+    """a keys query handed to a libpcp wait_stream returns before its pose upload
+    has read the pinned staging; the next fan query on the context (other poses) must not
+    overwrite that staging first.  Keys of the first query == the oracle's blocked counts of its
+    poses, the second query's counts == its own."""
+    fan = _abi.fan_params(n_az=128, n_el=32)
+    sc = scene
+    rng = np.random.default_rng(7)
+    a = np.column_stack([rng.uniform(-5, 5, 48), rng.uniform(-5, 5, 48), rng.uniform(0.5, 2.0, 48),
+                         rng.uniform(-0.6, 0.0, 48), rng.uniform(-3, 3, 48)])
+    b = a.copy()
+    b[:, 4] += 1.0
+    b[:, 2] += 0.7
+    T = oracle.Cloud(sc.terrain)
+    ra, _, _ = oracle.raycast_fan(T, a, 128, 32, fan.el_min, fan.el_max, fan.max_distance,
+                                  want_first_hit=False)
+    rb, _, _ = oracle.raycast_fan(T, b, 128, 32, fan.el_min, fan.el_max, fan.max_distance,
+                                  want_first_hit=False)
+    assert not np.array_equal(ra, rb)
+    with _abi.Context(0) as ctx:
+        ctx.set_terrain(sc.terrain, point_step=32)
+        st = ctx.stream_create()
+        try:
+            keys = ctx.dev_alloc(8 * a.shape[0])
+            for _ in range(3):
+                ctx.raycast_fan_keys(np.ascontiguousarray(a), fan, 0, a.shape[0], keys, None, st)
+                got_b, _, _, _ = ctx.raycast_fan(b, fan)      # rewrites the pinned pose staging
+                kh = np.zeros(a.shape[0], np.int64)
+                ctx.synchronize()
+                ctx.d2h(kh, keys)
+                np.testing.assert_array_equal((kh >> 32).astype(np.uint32), ra)
+                np.testing.assert_array_equal(got_b, rb)
+            ctx.dev_free(keys)
+        finally:
+            ctx.stream_destroy(st)
+
+
 def _need_devices(devices):
     if len(set(devices)) > 1 and _abi.device_count() < len(set(devices)):
         pytest.skip(f"needs {len(set(devices))} GPUs (RCCL over distinct devices); "
