@@ -831,16 +831,23 @@ def run_c1(args, local, cpu: bool):
                                "sample": f"{frames} frames of the same scans through the oracle "
                                          "chain (crop_box, voxel_grid, transform_rgb, excavate, "
                                          "area_normals + excavation_grid, score_poses), 1 thread"}
-        # the same candidate pose (x, y, z exact, angles 1e-12) and cell grid; the score within
-        # 1e-3 relative: the oracle's cell normals follow PCL's float sums in FLANN order, the
-        # GPU's are order-free (normals within 2e-3 / 1e-4)
+        # the oracle chain on its own (its own normals and cells): the same
+        # candidate pose (x, y, z exact, angles 1e-12), the same cells, the same best index; the
+        # totals within 1e-12 relative (glibc vs ocml acos in the score, the normals are
+        # bit-identical)
         out["matches_oracle"] = bool(
             ref[0] == res[0] and ref[1] == res[1] and ref[4] == res[4] and
             np.array_equal(ref[3][:, :3], res[3][:, :3]) and
             np.allclose(ref[3][:, 3:], res[3][:, 3:], rtol=0, atol=1e-12) and
-            np.allclose(ref[2], res[2], rtol=1e-3, atol=0))
+            np.allclose(ref[2], res[2], rtol=1e-12, atol=0))
+        out["best_idx_matches_oracle"] = bool(ref[1] == res[1])
         out["score_rel_diff"] = (float(np.max(np.abs(ref[2] - res[2]) / np.abs(ref[2])))
                                  if len(ref[2]) and len(res[2]) else None)
+        # the margin of the argmax: (best - second) / |best| over the oracle's totals (None with
+        # one candidate: C1 scores ONE pose)
+        srt = np.sort(np.asarray(ref[2], np.float64))[::-1]
+        out["top2_gap"] = (float((srt[0] - srt[1]) / abs(srt[0])) if srt.size >= 2 and srt[0]
+                           else None)
     return out
 
 

@@ -426,6 +426,7 @@ int pcp_create(int device, pcp_ctx **out) {
         ctx->fan_npw = (v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 1;
     }
     if (const char *ho = std::getenv("PCP_FAN_HOST_OUT")) ctx->fan_host_out = std::atoi(ho) != 0;
+    if (const char *ne = std::getenv("PCP_NORMALS_EXACT")) ctx->normals_exact = std::atoi(ne) != 0;
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
     if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff);
     if (const char *bg = std::getenv("PCP_BK_GT")) ctx->bk_gt = std::atoi(bg);
@@ -469,6 +470,9 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->exc_norm.release();
     ctx->exc_near.release();
     ctx->area_nrm.release();
+    ctx->nb_list.release();
+    ctx->nb_meta.release();
+    ctx->nb_ctl.release();
     ctx->carve.release();
     ctx->carve_buf.release();
     ctx->cell_cnt.release();

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "pcp_internal.hpp"
+#include "pcp_libm.h"
 #include "pcp_stencil.hpp"
 
 namespace pcp {
@@ -44,11 +45,14 @@ __device__ __forceinline__ bool stencil_ranges(const GridView &g, float qx, floa
 }
 
 // ---- pcl::eigen33, smallest eigenvalue's eigenvector (float, as PCL's Scalar) ---------------
+// Every libm call and every float division / square root as the reference's platform computes
+// them (pcp_libm.h: glibc 2.35's atan2f / cosf / sinf restated, correctly rounded sqrt and
+// division), so the same covariance gives the same normal bits as the oracle (glibc)
 __device__ __forceinline__ void roots2(float b, float c, float r[3]) {
     r[0] = 0.0f;
     float d = (float)(b * b - 4.0 * c);
     if (d < 0.0f) d = 0.0f;
-    const float sd = sqrtf(d);
+    const float sd = pcp_lm_sqrt(d);
     r[2] = 0.5f * (b + sd);
     r[1] = 0.5f * (b - sd);
 }
@@ -65,16 +69,16 @@ __device__ __forceinline__ void roots3(const float m[3][3], float r[3]) {
         return;
     }
     const float s_inv3 = (float)(1.0 / 3.0);
-    const float s_sqrt3 = sqrtf(3.0f);
+    const float s_sqrt3 = pcp_lm_sqrt(3.0f);
     const float c2_over_3 = c2 * s_inv3;
     float a_over_3 = (c1 - c2 * c2_over_3) * s_inv3;
     if (a_over_3 > 0.0f) a_over_3 = 0.0f;
     const float half_b = 0.5f * (c0 + c2_over_3 * (2.0f * c2_over_3 * c2_over_3 - c1));
     float q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
     if (q > 0.0f) q = 0.0f;
-    const float rho = sqrtf(-a_over_3);
-    const float theta = atan2f(sqrtf(-q), half_b) * s_inv3;
-    const float ct = cosf(theta), st = sinf(theta);
+    const float rho = pcp_lm_sqrt(-a_over_3);
+    const float theta = pcp_atan2f(pcp_lm_sqrt(-q), half_b) * s_inv3;
+    const float ct = pcp_cosf(theta), st = pcp_sinf(theta);
     r[0] = c2_over_3 + 2.0f * rho * ct;
     r[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);
     r[2] = c2_over_3 - rho * (ct - s_sqrt3 * st);
@@ -104,7 +108,7 @@ __device__ __forceinline__ void eigen33_min(const float cov[3][3], float ev[3]) 
     if (scale <= FLT_MIN) scale = 1.0f;
     float m[3][3];
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) m[i][j] = cov[i][j] / scale;
+        for (int j = 0; j < 3; ++j) m[i][j] = pcp_lm_div(cov[i][j], scale);
     float r[3];
     roots3(m, r);
     for (int i = 0; i < 3; ++i) m[i][i] -= r[0];
@@ -124,8 +128,25 @@ __device__ __forceinline__ void eigen33_min(const float cov[3][3], float ev[3]) 
         v = v2;
         l = l2;
     }
-    const float s = sqrtf(l);
-    for (int a = 0; a < 3; ++a) ev[a] = v[a] / s;
+    const float s = pcp_lm_sqrt(l);
+    for (int a = 0; a < 3; ++a) ev[a] = pcp_lm_div(v[a], s);
+}
+
+// the normal of one area point from its covariance: eigen33, flipNormalTowardsViewpoint with
+// the viewpoint (0, 0, 0) (scalar PCL overload: ((vx nx + vy ny) + vz nz)), then the
+// reference's flip to normal_z >= 0 (virtual_lidar.cpp:223-229)
+__device__ __forceinline__ void normal_from_cov(const float cov[3][3], float qx, float qy,
+                                                float qz, float *o) {
+    float ev[3];
+    eigen33_min(cov, ev);
+    const float ct = (0.0f - qx) * ev[0] + (0.0f - qy) * ev[1] + (0.0f - qz) * ev[2];
+    if (ct < 0.0f)
+        for (int a = 0; a < 3; ++a) ev[a] = -ev[a];
+    if (ev[2] < 0.0f)
+        for (int a = 0; a < 3; ++a) ev[a] = -ev[a];
+    o[0] = ev[0];
+    o[1] = ev[1];
+    o[2] = ev[2];
 }
 
 // double-double accumulation (TwoSum): exact sums of these float addends
@@ -245,16 +266,367 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
     cov[1][0] = cov[0][1];
     cov[2][0] = cov[0][2];
     cov[2][1] = cov[1][2];
-    float ev[3];
-    eigen33_min(cov, ev);
-    const float ct = (0.0f - q.x) * ev[0] + (0.0f - q.y) * ev[1] + (0.0f - q.z) * ev[2];
-    if (ct < 0.0f)
-        for (int a = 0; a < 3; ++a) ev[a] = -ev[a];
-    if (ev[2] < 0.0f)
-        for (int a = 0; a < 3; ++a) ev[a] = -ev[a];
-    o[0] = ev[0];
-    o[1] = ev[1];
-    o[2] = ev[2];
+    normal_from_cov(cov, q.x, q.y, q.z, o);
+}
+
+// ---- the reference's neighbour order (the default path) --------------------------------------
+// PCL sums each covariance in float, and each cell normal in double, over the radius search's
+// result in FLANN's order: ascending (float distance, index) (RadiusResultSet, sorted = true;
+// the oracle's radius_search).  Float sums depend on that order, so the default path builds the
+// sorted neighbour list of every query and then sums it sequentially:
+//  k_nb_lists : one block per query: the stencil's points within r (FLANN predicate) counted
+//               into 2,048 distance buckets of LDS (bucket = (uint)(d * 2048 / r2): monotone in
+//               d, so buckets are ordered), scanned, scattered by bucket, each bucket's few
+//               entries put in (d, index) order by an insertion sort; the list (positions in the
+//               index's point array) goes to global memory at an atomically allocated base
+//  k_nb_sums  : a block per QB queries; waves 1-3 gather the listed points 64 steps at a time
+//               and form the summands (lane-parallel), wave 0 adds them in list order, one lane
+//               per (query, summand) -- the only sequential part, ~1 add per step
+constexpr int kNbBuckets = 2048;
+constexpr int kNbLds = 6144;   // list entries sorted in LDS; longer lists sort in global memory
+constexpr int kNbT = 256;
+
+__device__ __forceinline__ uint32_t nb_wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+
+__device__ __forceinline__ float flann_d2(float qx, float qy, float qz, const float4 &p) {
+    const float d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
+    float acc = 0.0f;
+    acc = acc + d0 * d0;
+    acc = acc + d1 * d1;
+    acc = acc + d2 * d2;
+    return acc;
+}
+
+struct NbLists {
+    uint32_t *list;                 // entries: positions in the index's point array
+    uint2 *meta;                    // per query: {base, m}
+    uint32_t *cursor;               // allocation cursor (zero before the launch)
+    uint32_t *overflow;             // set when the entries exceed cap (host regrows, reruns)
+    uint32_t cap;
+};
+
+// queries: the index's own points (CELLS false: area normals, nq = g.n_pts) or the cells
+// (double xyz rounded to float, nq = *n_dev)
+template <bool CELLS>
+__global__ void __launch_bounds__(kNbT)
+k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
+           const uint32_t *__restrict__ n_dev, NbLists L) {
+    __shared__ uint32_t cnt[kNbBuckets];
+    __shared__ uint32_t lst[kNbLds];
+    __shared__ uint32_t wsum[kNbT / 64];
+    __shared__ uint32_t sh_base, sh_ok;
+    const uint32_t nq = CELLS ? *n_dev : g.n_pts;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+        float qx, qy, qz;
+        if (CELLS) {
+            qx = (float)cells[3 * (size_t)qi];
+            qy = (float)cells[3 * (size_t)qi + 1];
+            qz = (float)cells[3 * (size_t)qi + 2];
+        } else {
+            const float4 q = g.pts[qi];
+            qx = q.x;
+            qy = q.y;
+            qz = q.z;
+        }
+        for (int b = threadIdx.x; b < kNbBuckets; b += kNbT) cnt[b] = 0;
+        __syncthreads();
+        uint32_t lo[4], hi[4];
+        const bool any = stencil_ranges(g, qx, qy, qz, lo, hi);
+        if (any) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                for (uint32_t k = lo[r] + threadIdx.x; k < hi[r]; k += kNbT) {
+                    const float d = flann_d2(qx, qy, qz, g.pts[k]);
+                    if (d < r2) atomicAdd(&cnt[min((uint32_t)(d * bscale), kNbBuckets - 1u)], 1u);
+                }
+        }
+        __syncthreads();
+        // exclusive scan of the buckets: thread t owns buckets [8 t, 8 t + 8)
+        constexpr int kPer = kNbBuckets / kNbT;
+        uint32_t v[kPer], run = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            v[j] = cnt[kPer * threadIdx.x + j];
+            run += v[j];
+        }
+        const uint32_t incl = nb_wave_incl_scan(run);
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        uint32_t ex = incl - run, m = 0;
+#pragma unroll
+        for (int w = 0; w < kNbT / 64; ++w) {
+            ex += w < wid ? wsum[w] : 0u;
+            m += wsum[w];
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            cnt[kPer * threadIdx.x + j] = ex;   // bucket start
+            ex += v[j];
+        }
+        if (threadIdx.x == 0) {
+            uint32_t base = m ? atomicAdd(L.cursor, m) : 0u;
+            uint32_t ok = 1;
+            if ((uint64_t)base + m > L.cap) {   // no room: the host regrows and runs again
+                atomicOr(L.overflow, 1u);
+                ok = 0;
+            }
+            sh_base = base;
+            sh_ok = ok;
+            L.meta[qi] = make_uint2(base, ok ? m : 0u);
+        }
+        __syncthreads();
+        const uint32_t base = sh_base;
+        if (sh_ok && m) {
+            uint32_t *Lp = m <= (uint32_t)kNbLds ? lst : L.list + base;
+            // scatter by bucket (cnt[b] becomes the bucket's end)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                for (uint32_t k = lo[r] + threadIdx.x; k < hi[r]; k += kNbT) {
+                    const float d = flann_d2(qx, qy, qz, g.pts[k]);
+                    if (d < r2)
+                        Lp[atomicAdd(&cnt[min((uint32_t)(d * bscale), kNbBuckets - 1u)], 1u)] = k;
+                }
+            __threadfence_block();
+            __syncthreads();
+            // each bucket's entries in (distance, index) order
+            for (int b = threadIdx.x; b < kNbBuckets; b += kNbT) {
+                const uint32_t e = cnt[b], s0 = b ? cnt[b - 1] : 0u;
+                if (e - s0 < 2) continue;
+                for (uint32_t i = s0 + 1; i < e; ++i) {
+                    const uint32_t ki = Lp[i];
+                    const float4 pi = g.pts[ki];
+                    const unsigned long long key =
+                        ((unsigned long long)__float_as_uint(flann_d2(qx, qy, qz, pi)) << 32) |
+                        __float_as_uint(pi.w);
+                    uint32_t j = i;
+                    while (j > s0) {
+                        const uint32_t kj = Lp[j - 1];
+                        const float4 pj = g.pts[kj];
+                        const unsigned long long kk =
+                            ((unsigned long long)__float_as_uint(flann_d2(qx, qy, qz, pj)) << 32) |
+                            __float_as_uint(pj.w);
+                        if (kk <= key) break;
+                        Lp[j] = kj;
+                        --j;
+                    }
+                    Lp[j] = ki;
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+            if (Lp == lst)
+                for (uint32_t i = threadIdx.x; i < m; i += kNbT) L.list[base + i] = lst[i];
+        }
+        __syncthreads();   // the LDS is reused by the next query
+    }
+}
+
+// sequential sums over the sorted lists.  CELLS false: the 9 float moments of
+// computeMeanAndCovarianceMatrix (shifted by K = the first listed point: xx xy xz yy yz zz x y
+// z), then the covariance and the normal; CELLS true: the 3 double sums of the finite
+// neighbours' normals (computeCellSurfaceNormal :301-340), then the cell normal.
+template <bool CELLS> struct NbCfg;
+template <> struct NbCfg<false> {
+    using T = float;
+    static constexpr int NT = 9, QB = 7;
+};
+template <> struct NbCfg<true> {
+    using T = double;
+    static constexpr int NT = 3, QB = 14;
+};
+constexpr int kNbSteps = 64;   // list entries per chunk
+
+template <bool CELLS>
+__global__ void __launch_bounds__(kNbT)
+k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict__ list,
+          const uint32_t *__restrict__ n_dev, const float *__restrict__ area_nrm,
+          float *__restrict__ out, const uint32_t *__restrict__ ctl, uint32_t *__restrict__ ctl_host) {
+    // the lists' cursors and overflow word (final: every k_nb_lists ran before this launch)
+    // to the caller's pinned landing, one plain store each
+    if (ctl_host && blockIdx.x == 0 && threadIdx.x < 3) ctl_host[threadIdx.x] = ctl[threadIdx.x];
+    using Cfg = NbCfg<CELLS>;
+    using T = typename Cfg::T;
+    constexpr int NT = Cfg::NT, QB = Cfg::QB, S = kNbSteps;
+    constexpr int PER = (QB * S + kNbT - 64 - 1) / (kNbT - 64);   // elements per producer lane
+    // rows of S summands padded by 16 bytes: the consumer lanes' 16-byte reads start 4 banks
+    // apart (conflict-free per 16 lanes)
+    constexpr int SP = S + 16 / (int)sizeof(T);
+    __shared__ __attribute__((aligned(16))) T buf[2][QB][NT][SP];
+    __shared__ uint2 qm[QB];
+    __shared__ float4 qk[QB];          // K (area) per query
+    __shared__ uint32_t valid[QB];     // finite neighbour normals (cells)
+    __shared__ T accs[QB][NT];
+    const uint32_t nq = CELLS ? *n_dev : g.n_pts;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t q0 = blockIdx.x * QB; q0 < nq; q0 += gridDim.x * QB) {
+        if (threadIdx.x < QB) {
+            const uint32_t qi = q0 + threadIdx.x;
+            const uint2 mt = qi < nq ? meta[qi] : make_uint2(0u, 0u);
+            qm[threadIdx.x] = mt;
+            valid[threadIdx.x] = 0;
+            if (!CELLS) qk[threadIdx.x] = mt.y ? g.pts[list[mt.x]] : make_float4(0, 0, 0, 0);
+        }
+        __syncthreads();
+        uint32_t maxm = 0;
+#pragma unroll
+        for (int q = 0; q < QB; ++q) maxm = max(maxm, qm[q].y);
+        const uint32_t nch = (maxm + S - 1) / S;
+        // producers: element e = (q, t) = (e / S, e % S) of each chunk, lane-parallel; the next
+        // chunk's list entries are loaded one chunk ahead
+        const int pl = (int)threadIdx.x - 64;
+        uint32_t kn[PER];
+        auto load_list = [&](uint32_t c, uint32_t (&kk)[PER]) {
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const int e = pl + j * (kNbT - 64);
+                kk[j] = 0xffffffffu;
+                if (e < QB * S) {
+                    const uint2 mt = qm[e / S];
+                    const uint32_t st = c * S + (uint32_t)(e % S);
+                    if (st < mt.y) kk[j] = list[mt.x + st];
+                }
+            }
+        };
+        if (wid > 0) load_list(0, kn);
+        T acc = 0;
+        const int cq = lane / NT, ca = lane % NT;   // the consumer lane's (query, summand)
+        for (uint32_t c = 0; c <= nch; ++c) {
+            if (wid > 0 && c < nch) {
+                uint32_t kc[PER];
+#pragma unroll
+                for (int j = 0; j < PER; ++j) kc[j] = kn[j];
+                if (c + 1 < nch) load_list(c + 1, kn);
+                T (*B)[NT][SP] = buf[c & 1];
+#pragma unroll
+                for (int j = 0; j < PER; ++j) {
+                    const int e = pl + j * (kNbT - 64);
+                    if (e >= QB * S) continue;
+                    const int q = e / S, t = e % S;
+                    T tv[NT];
+#pragma unroll
+                    for (int a = 0; a < NT; ++a) tv[a] = 0;
+                    if (kc[j] != 0xffffffffu) {
+                        const float4 p = g.pts[kc[j]];
+                        if (CELLS) {
+                            const float *n = area_nrm + 3 * (size_t)__float_as_uint(p.w);
+                            const float nx = n[0], ny = n[1], nz = n[2];
+                            if (isfinite(nx) && isfinite(ny) && isfinite(nz)) {
+                                tv[0] = (T)nx;
+                                tv[1] = (T)ny;
+                                tv[2 % NT] = (T)nz;
+                                atomicAdd(&valid[q], 1u);
+                            }
+                        } else {
+                            const float4 K = qk[q];
+                            const float x = p.x - K.x, y = p.y - K.y, z = p.z - K.z;
+                            tv[0] = (T)(x * x);
+                            tv[1] = (T)(x * y);
+                            tv[2 % NT] = (T)(x * z);
+                            tv[3 % NT] = (T)(y * y);
+                            tv[4 % NT] = (T)(y * z);
+                            tv[5 % NT] = (T)(z * z);
+                            tv[6 % NT] = (T)x;
+                            tv[7 % NT] = (T)y;
+                            tv[8 % NT] = (T)z;
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a < NT; ++a) B[q][a][t] = tv[a];
+                }
+            }
+            if (wid == 0 && c > 0 && cq < QB) {
+                // acc + 0 == acc for these sums (they start at +0 and never become -0): the
+                // zero padding past a query's list is exact
+                if (CELLS) {
+                    const double2 *v = reinterpret_cast<const double2 *>(&buf[(c - 1) & 1][cq][ca][0]);
+#pragma unroll 8
+                    for (int t = 0; t < S / 2; ++t) {
+                        const double2 w = v[t];
+                        acc = acc + (T)w.x;
+                        acc = acc + (T)w.y;
+                    }
+                } else {
+                    const float4 *v = reinterpret_cast<const float4 *>(&buf[(c - 1) & 1][cq][ca][0]);
+#pragma unroll 8
+                    for (int t = 0; t < S / 4; ++t) {
+                        const float4 w = v[t];
+                        acc = acc + (T)w.x;
+                        acc = acc + (T)w.y;
+                        acc = acc + (T)w.z;
+                        acc = acc + (T)w.w;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (wid == 0 && cq < QB) accs[cq][ca] = acc;
+        __syncthreads();
+        if (threadIdx.x < QB && q0 + threadIdx.x < nq) {
+            const int q = threadIdx.x;
+            const uint32_t qi = q0 + q;
+            const uint32_t m = qm[q].y;
+            if (CELLS) {
+                float *o = out + 3 * (size_t)qi;
+                o[0] = 0.0f;   // GridCell's default surface normal
+                o[1] = 0.0f;
+                o[2] = 1.0f;
+                if (valid[q] != 0) {
+                    const double sx = (double)accs[q][0], sy = (double)accs[q][1],
+                                 sz = (double)accs[q][2 % NT];
+                    const double norm = sqrt(sx * sx + sy * sy + sz * sz);
+                    if (norm > 1e-6) {
+                        o[0] = (float)(sx / norm);
+                        o[1] = (float)(sy / norm);
+                        o[2] = (float)(sz / norm);
+                    }
+                }
+            } else {
+                const float4 qp = g.pts[qi];
+                float *o = out + 3 * (size_t)__float_as_uint(qp.w);
+                if (m < 3) {   // computePointNormal: < 3 neighbours -> NaN
+                    o[0] = o[1] = o[2] = NAN;
+                } else {
+                    float a[9];
+                    const float fm = (float)m;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) a[k] = pcp_lm_div((float)accs[q][k % NT], fm);
+                    float cov[3][3];
+                    cov[0][0] = a[0] - a[6] * a[6];
+                    cov[0][1] = a[1] - a[6] * a[7];
+                    cov[0][2] = a[2] - a[6] * a[8];
+                    cov[1][1] = a[3] - a[7] * a[7];
+                    cov[1][2] = a[4] - a[7] * a[8];
+                    cov[2][2] = a[5] - a[8] * a[8];
+                    cov[1][0] = cov[0][1];
+                    cov[2][0] = cov[0][2];
+                    cov[2][1] = cov[1][2];
+                    normal_from_cov(cov, qp.x, qp.y, qp.z, o);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// the non-finite input points (not in the index) get their NaN normal (blocks per 256 points)
+__global__ void __launch_bounds__(kXT) k_area_nan(RawIn in, float *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kXT + threadIdx.x;
+    if (i >= in.n) return;
+    const unsigned char *p = in.raw + i * in.step;
+    const float x = *reinterpret_cast<const float *>(p + in.ox),
+                y = *reinterpret_cast<const float *>(p + in.oy),
+                z = *reinterpret_cast<const float *>(p + in.oz);
+    if (!(isfinite(x) && isfinite(y) && isfinite(z)))
+        out[3 * i] = out[3 * i + 1] = out[3 * i + 2] = NAN;
 }
 
 struct Lattice {
@@ -466,14 +838,52 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     }
     const GridView gn = ctx->exc_norm.view(), gq = ctx->exc_near.view();
     const float r2n = (float)(kNormalRadius * kNormalRadius), r2q = (float)(r_near * r_near);
-    // non-finite points are not in the index: PCL gives them a NaN normal (the kernel's blocks
-    // past the index's points)
+    // non-finite points are not in the index: PCL gives them a NaN normal
     const RawIn rin{raw, n, area->point_step, area->off_x, area->off_y, area->off_z};
-    hipLaunchKernelGGL(k_area_normals,
-                       dim3((unsigned)(ctx->exc_norm.n_pts + (n + kXT - 1) / kXT)), dim3(kXT), 0,
-                       ctx->stream, gn, r2n, ctx->area_nrm.as<float>(), rin);
-    PCP_CHECK_LAUNCH(ctx);
-    pin_release(ctx, ctx->stream);   // k_area_normals read the raw records last
+    const uint32_t npts = (uint32_t)ctx->exc_norm.n_pts;
+    const bool exact = ctx->normals_exact;
+    // the sorted neighbour lists (exact path): one buffer for the area's lists, then the cells'
+    // (the cells' lists overwrite the area's after k_nb_sums<false> consumed them); entries as
+    // needed by the previous call, first guess n x min(n, 4096), regrown on overflow
+    const float bscale = (float)kNbBuckets / r2n;
+    if (exact) {
+        const uint64_t guess = std::min<uint64_t>((uint64_t)npts * std::min<uint64_t>(npts, 4096),
+                                                  64ull << 20);
+        PCP_HIP(ctx, ctx->nb_list.ensure(std::max<uint64_t>(guess, ctx->nb_need) * 4 + 64));
+        PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
+    }
+    auto area_normals = [&]() -> int {
+        if (!exact) {
+            // order-free fixed-point moments (A/B: PCP_NORMALS_EXACT=0), NaN for the non-finite
+            // points by the blocks past the index's points
+            hipLaunchKernelGGL(k_area_normals, dim3((unsigned)(npts + (n + kXT - 1) / kXT)),
+                               dim3(kXT), 0, ctx->stream, gn, r2n, ctx->area_nrm.as<float>(), rin);
+            PCP_CHECK_LAUNCH(ctx);
+            return PCP_OK;
+        }
+        PCP_HIP(ctx, hipMemsetAsync(ctx->nb_ctl.p, 0, 16, ctx->stream));
+        uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
+        const NbLists L{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
+                        (uint32_t)std::min<size_t>(ctx->nb_list.cap / 4, 0xffffffffu)};
+        hipLaunchKernelGGL(k_nb_lists<false>, dim3(npts), dim3(kNbT), 0, ctx->stream, gn, r2n,
+                           bscale, (const double *)nullptr, (const uint32_t *)nullptr, L);
+        PCP_CHECK_LAUNCH(ctx);
+        hipLaunchKernelGGL(k_nb_sums<false>, dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB),
+                           dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)L.meta,
+                           (const uint32_t *)L.list, (const uint32_t *)nullptr,
+                           (const float *)nullptr, ctx->area_nrm.as<float>(),
+                           (const uint32_t *)ctl, (uint32_t *)nullptr);
+        PCP_CHECK_LAUNCH(ctx);
+        if (npts < n) {
+            hipLaunchKernelGGL(k_area_nan, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0,
+                               ctx->stream, rin, ctx->area_nrm.as<float>());
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        return PCP_OK;
+    };
+    if (exact) PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)npts * sizeof(uint2) + 64));
+    if (int rc0 = area_normals()) return rc0;
+    pin_release(ctx, ctx->stream);   // the normals read the raw records last
     // grid bounds (:239-256): min/max of the float coordinates as doubles, then the margin
     const double *bmin = ctx->exc_norm.bmin, *bmax = ctx->exc_norm.bmax;
     Lattice L;
@@ -509,21 +919,65 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     }
     PCP_HIP(ctx, ctx->small_host.ensure(4096));
     uint32_t *n_h = ctx->small_host.as<uint32_t>();
+    n_h[1] = n_h[2] = n_h[3] = 0;   // the lists' cursors + overflow (exact path, below)
     hipLaunchKernelGGL(k_lattice_compact, dim3(1), dim3(1024), 0, ctx->stream,
                        (const uint8_t *)ctx->stage.as<uint8_t>(), L, ctx->cells_xyz.as<double>(),
                        (uint32_t)total, n_d, n_h);
     PCP_CHECK_LAUNCH(ctx);
     // the cell normals read the lattice count on the device; the count comes back once, at
     // the end (one synchronisation for the whole call)
-    if (total) {
-        hipLaunchKernelGGL(k_cell_normals, dim3((unsigned)std::min<uint64_t>(total, 8192)),
-                           dim3(kXT), 0, ctx->stream, gn, r2n,
-                           (const double *)ctx->cells_xyz.as<double>(),
-                           (const float *)ctx->area_nrm.as<float>(), (const uint32_t *)n_d,
-                           ctx->cells_nrm.as<float>());
+    auto cell_normals = [&]() -> int {
+        if (!total && !exact) return PCP_OK;
+        if (!exact) {
+            hipLaunchKernelGGL(k_cell_normals, dim3((unsigned)std::min<uint64_t>(total, 8192)),
+                               dim3(kXT), 0, ctx->stream, gn, r2n,
+                               (const double *)ctx->cells_xyz.as<double>(),
+                               (const float *)ctx->area_nrm.as<float>(), (const uint32_t *)n_d,
+                               ctx->cells_nrm.as<float>());
+            PCP_CHECK_LAUNCH(ctx);
+            return PCP_OK;
+        }
+        uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
+        const NbLists Lc{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl + 1, ctl + 2,
+                         (uint32_t)std::min<size_t>(ctx->nb_list.cap / 4, 0xffffffffu)};
+        if (total) {
+            hipLaunchKernelGGL(k_nb_lists<true>, dim3((unsigned)std::min<uint64_t>(total, 16384)),
+                               dim3(kNbT), 0, ctx->stream, gn, r2n, bscale,
+                               (const double *)ctx->cells_xyz.as<double>(), (const uint32_t *)n_d,
+                               Lc);
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        // (launched for an empty lattice too: it lands the area lists' cursor and overflow)
+        constexpr int QB = NbCfg<true>::QB;
+        hipLaunchKernelGGL(k_nb_sums<true>,
+                           dim3((unsigned)std::max<uint64_t>(
+                               1, std::min<uint64_t>((total + QB - 1) / QB, 4096))),
+                           dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)Lc.meta,
+                           (const uint32_t *)Lc.list, (const uint32_t *)n_d,
+                           (const float *)ctx->area_nrm.as<float>(), ctx->cells_nrm.as<float>(),
+                           (const uint32_t *)ctl, n_h + 1);
         PCP_CHECK_LAUNCH(ctx);
-    }
+        return PCP_OK;
+    };
+    if (exact) PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)std::max<uint64_t>(npts, total) *
+                                                sizeof(uint2) + 64));
+    if (int rc1 = cell_normals()) return rc1;
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (exact && n_h[3]) {
+        // a list buffer too small (first frames, or a denser area): regrow to the entries both
+        // passes asked for and run the normals again (the lattice stands)
+        ctx->nb_need = std::max<uint64_t>(n_h[1], n_h[2]);
+        PCP_HIP(ctx, ctx->nb_list.ensure(ctx->nb_need * 4 + 64));
+        ctx->normals_regrown++;
+        n_h[1] = n_h[2] = n_h[3] = 0;
+        if (int rc2 = area_normals()) return rc2;
+        if (int rc3 = cell_normals()) return rc3;
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (n_h[3])
+            return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: neighbour lists "
+                                                   "overflowed after regrowing");
+    }
+    if (exact) ctx->nb_need = std::max<uint64_t>(ctx->nb_need, std::max<uint64_t>(n_h[1], n_h[2]));
     const uint32_t nc = *n_h;
     ctx->n_cells = nc;
     if (n_cells) *n_cells = nc;

@@ -239,6 +239,13 @@ struct pcp_ctx {
     pcp::GridIndex exc_norm, exc_near;
     pcp::DevBuf area_nrm;
     uint64_t area_n = 0;
+    // the normals in the reference's summation order (PCP_NORMALS_EXACT, default 1; 0: the
+    // order-free fixed-point kernels, A/B only): sorted neighbour lists, their per-query
+    // {base, count}, cursors + overflow word; list entries the last call needed
+    bool normals_exact = true;
+    pcp::DevBuf nb_list, nb_meta, nb_ctl;
+    uint64_t nb_need = 0;
+    uint64_t normals_regrown = 0;
     // excavated-terrain carve (pcp_excavate): index of the input cloud + scratch
     pcp::GridIndex carve;
     pcp::DevBuf carve_buf;

@@ -1058,11 +1058,22 @@ def test_score_poses_edge_states(oracle, scene, cells, aux):
 
 
 # ---------------------------------------------------------------- excavation-area setup
-def test_excavation_area_setup(oracle, scene):
+def _normals_equal(got, ref):
+    """Bit-identical normals, NaN where the reference has NaN (< 3 neighbours, non-finite)."""
+    fin = np.isfinite(ref).all(1)
+    assert np.array_equal(np.isfinite(got).all(1), fin)
+    np.testing.assert_array_equal(got[fin].view(np.uint32), ref[fin].view(np.uint32))
+
+
+@pytest.mark.parametrize("exact", ["1", "0"])
+def test_excavation_area_setup(oracle, scene, exact, monkeypatch):
     """pcp_set_excavation_area against the oracle: grid bounds and the valid cells (positions,
-    reference loop order) bit-exact; point normals within 2e-3 and cell normals within 1e-4
-    (PCL's float covariance sums, see test_oracle.test_excavation_vs_numpy); an empty area
-    keeps the previous cells (virtual_lidar.cpp:168)."""
+    reference loop order) bit-exact.  Default path (PCP_NORMALS_EXACT=1): point normals and cell
+    normals BIT-IDENTICAL -- PCL's float covariance sums in FLANN's (distance, index) order,
+    eigen33 with glibc's float libm restated (pcp_libm.h), the cells' double sums in the same
+    order.  The order-free A/B kernels (0): point normals within 2e-3, cells within 1e-4.  An
+    empty area keeps the previous cells (virtual_lidar.cpp:168)."""
+    monkeypatch.setenv("PCP_NORMALS_EXACT", exact)
     d = np.load(GOLD / "excavation.npz")
     ctx = _abi.Context(0)
     try:
@@ -1077,15 +1088,46 @@ def test_excavation_area_setup(oracle, scene):
             assert n == r_xyz.shape[0]
             xyz, cn = ctx.get_cells()
             np.testing.assert_array_equal(xyz, r_xyz)
-            np.testing.assert_allclose(cn, r_cn, atol=1e-4)
             an = ctx.get_area_normals()
-            fin = np.isfinite(r_n).all(1)
-            assert np.array_equal(np.isfinite(an).all(1), fin)
-            np.testing.assert_allclose(an[fin], r_n[fin], atol=2e-3)
+            if exact == "1":
+                _normals_equal(an, r_n)
+                np.testing.assert_array_equal(cn.view(np.uint32), r_cn.view(np.uint32))
+            else:
+                fin = np.isfinite(r_n).all(1)
+                assert np.array_equal(np.isfinite(an).all(1), fin)
+                np.testing.assert_allclose(an[fin], r_n[fin], atol=2e-3)
+                np.testing.assert_allclose(cn, r_cn, atol=1e-4)
         bb, n2 = ctx.set_excavation_area(np.zeros((0, 4), np.float32), 0.1, 10)
         assert n2 == n and np.array_equal(ctx.get_cells()[0], xyz)
     finally:
         ctx.close()
+
+
+def test_excavation_area_normals_long_lists_and_ties(oracle):
+    """The exact normals where the neighbour lists pass the LDS sort (> 6,144 neighbours within
+    1.5 m: sorted in global memory), with exact distance ties (a lattice, duplicated points: the
+    reference's order breaks them by index), non-finite points (NaN normals, absent from every
+    list) and isolated points (< 3 neighbours: NaN).  Point and cell normals bit-identical."""
+    rng = np.random.default_rng(11)
+    g = np.arange(90) * 0.025
+    X, Y = np.meshgrid(g, g)
+    P = np.stack([X.ravel(), Y.ravel(), 0.3 * np.sin(X.ravel()) + rng.normal(0, 0.002, X.size)], 1)
+    P[::7, 2] = np.round(P[::7, 2], 2)                        # many exact-distance ties
+    P = np.concatenate([P, P[100:140], [[9.0, 9.0, 0.0], [9.5, 9.0, 0.1]]])   # dups, isolated
+    a = np.zeros((P.shape[0], 4), np.float32)
+    a[:, :3] = P
+    a[rng.integers(0, a.shape[0], 6), 1] = np.nan
+    r_n = oracle.area_normals(a, 1.5)
+    r_xyz, r_cn, r_bb, _ = oracle.excavation_grid(a, 0.1, 4, r_n)
+    with _abi.Context(0) as ctx:
+        for _ in range(2):                                   # the regrown list buffer, reused
+            bb, n = ctx.set_excavation_area(a, 0.1, 4)
+            np.testing.assert_array_equal(bb, r_bb)
+            assert n == r_xyz.shape[0]
+            _normals_equal(ctx.get_area_normals(), r_n)
+            xyz, cn = ctx.get_cells()
+            np.testing.assert_array_equal(xyz, r_xyz)
+            np.testing.assert_array_equal(cn.view(np.uint32), r_cn.view(np.uint32))
 
 
 # ---------------------------------------------------------------- excavated-terrain carve
