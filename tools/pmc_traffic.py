@@ -6,9 +6,14 @@ wide coalesced streaming reads (doubled below, flagged as such: the fan kernel's
 an uncalibrated access width, so both the raw and the corrected read bytes are recorded).
 
     python tools/pmc_traffic.py KEY KERNEL_SUBSTR FETCH_DIR WRITE_DIR [per_dispatch|steps=N] [OUT]
+        [FACTOR_SOURCE]
 
-OUT (default profiles/pmc_traffic.json): the JSON file the entry is merged into (round 3 writes
-profiles/r03_pmc_traffic.json, which bench.py reads first).
+OUT (default profiles/pmc_traffic.json): the JSON file the entry is merged into (round 4 writes
+profiles/r04_pmc_traffic.json, which bench.py reads first).  The entry carries the source stamp
+of KEY's kernels (pointcloud_processor_amd/_stamps.py): bench.py reports it stale when the tree
+differs.  FACTOR_SOURCE: "stream" (the guide's x2 for 16-B/lane streaming reads, default) or a
+calibration file (profiles/r04_fetch_calibration.json, tools/gather_cal.sh) whose gather rows at
+the Infinity-Cache resident table size give the factor for divergent gathers (the fan).
 
 per_dispatch (default): average over the matching dispatches (one kernel per launch);
 steps=N: sum of every matching dispatch / N (a multi-kernel pipeline run N times).
@@ -32,10 +37,27 @@ def per_dispatch(d: Path, counter: str, substr: str):
     return list(vals.values())
 
 
+def gather_factor(cal_file: Path):
+    """FETCH_SIZE -> bytes factor of divergent gathers: 128 / the FETCH_SIZE bytes per line the
+    calibration measured for 2-, 4- and 12-byte lane gathers on the resident table (their mean;
+    the spread is recorded)."""
+    doc = json.loads(cal_file.read_text())
+    rows = doc["rows"]
+    small = min(r["table_bytes"] for r in rows)
+    g = [r for r in rows if r["table_bytes"] == small and r["kernel"] in
+         ("k_gather<2>", "k_gather<4>", "k_gather<12>")]
+    f = [r["factor_to_128B_lines"] for r in g]
+    return sum(f) / len(f), {r["kernel"]: r["factor_to_128B_lines"] for r in g}
+
+
 def main():
+    sys.path.insert(0, str(ROOT))
+    from pointcloud_processor_amd._stamps import workload_stamp
+
     key, substr, fdir, wdir = sys.argv[1:5]
     mode = sys.argv[5] if len(sys.argv) > 5 else "per_dispatch"
     out_name = sys.argv[6] if len(sys.argv) > 6 else "pmc_traffic.json"
+    fsrc = sys.argv[7] if len(sys.argv) > 7 else "stream"
     fetch = per_dispatch(Path(fdir), "FETCH_SIZE", substr)
     write = per_dispatch(Path(wdir), "WRITE_SIZE", substr)
     if not fetch or not write:
@@ -45,6 +67,11 @@ def main():
         fk, wk = sum(fetch) / n, sum(write) / n
     else:
         fk, wk = sum(fetch) / len(fetch), sum(write) / len(write)
+    if fsrc == "stream":
+        factor, detail = 2.0, "MI355X_MICROARCH.md HBM section: x2 for 16-B/lane streaming reads"
+    else:
+        factor, per = gather_factor(ROOT / fsrc)
+        detail = f"{fsrc}: mean of the 2/4/12-B gather factors {per}"
     out_f = ROOT / "profiles" / out_name
     data = json.loads(out_f.read_text()) if out_f.exists() else {}
     data[key] = {
@@ -52,11 +79,13 @@ def main():
         "fetch_kib_per_launch": fk,
         "write_kib_per_launch": wk,
         "bytes_per_launch_raw": (fk + wk) * 1024.0,
-        "bytes_per_launch": (2.0 * fk + wk) * 1024.0,
+        "fetch_factor": factor,
+        "fetch_factor_source": detail,
+        "bytes_per_launch": (factor * fk + wk) * 1024.0,
         "dispatches_sampled": [len(fetch), len(write)],
-        "note": "HBM-side bytes from TCC EA requests (Infinity-Cache hits included); "
-                "FETCH_SIZE doubled per the gfx950 correction for wide reads (uncalibrated for "
-                "gathers: bytes_per_launch_raw is the uncorrected figure)",
+        "source_stamp": workload_stamp(key),
+        "note": "HBM-side bytes from TCC EA requests (Infinity-Cache hits included): "
+                "fetch_factor x FETCH_SIZE + WRITE_SIZE",
     }
     out_f.write_text(json.dumps(data, indent=2) + "\n")
     print(json.dumps(data[key]))
