@@ -251,6 +251,68 @@ static void appendf(std::string &s, const char *fmt, ...) {
     s += '\n';
 }
 
+// the two RCLCPP_INFO tables of runOptimization, line for line: evaluateZX120Only (:419-451)
+// and the dual configuration (:522-543)
+std::string optimization_log(const SimplifiedDualLidarOptimizer::LidarPosition &zx120,
+                             const SimplifiedDualLidarOptimizer::LidarPosition &best,
+                             double best_score, const pcp_vl_report &q, size_t zx120_size) {
+    std::string log;
+    const int tc = q.total_cells;
+    // the colour lines divide first (static_cast<double>(n) / total_cells * 100.0, :401-416,
+    // :504-519); the Debug Info lines multiply first (n * 100.0 / total_cells, :427-432): the
+    // two can differ by an ulp, which can move a %.1f tie
+    auto pct = [tc](int v) { return tc > 0 ? (double)v / tc * 100.0 : 0.0; };
+    auto pct_mul = [tc](int v) { return tc > 0 ? v * 100.0 / tc : 0.0; };
+    auto ratio = [](int red, int green) {
+        return green > 0 ? (double)red / green
+                         : (red > 0 ? std::numeric_limits<double>::infinity() : 0.0);
+    };
+    const char *rule = "========================================";
+    const char *thin = "----------------------------------------";
+    appendf(log, "%s", rule);
+    appendf(log, "ZX120 LiDAR Only Evaluation");
+    appendf(log, "%s", rule);
+    appendf(log, "ZX120 Position: (%.2f, %.2f, %.2f)", zx120.x, zx120.y, zx120.z);
+    appendf(log, "Total Score (ZX120 only): %.2f", q.zx120_total_score);
+    appendf(log, "%s", thin);
+    appendf(log, "Debug Info:");
+    appendf(log, "  Cells in range: %d (%.1f%%)", q.zx120_range_ok, pct_mul(q.zx120_range_ok));
+    appendf(log, "  Cells in FOV: %d (%.1f%%)", q.zx120_fov_ok, pct_mul(q.zx120_fov_ok));
+    appendf(log, "  Cells visible: %d (%.1f%%)", q.zx120_visible_ok, pct_mul(q.zx120_visible_ok));
+    appendf(log, "  ZX120 point cloud size: %zu", zx120_size);
+    appendf(log, "%s", thin);
+    appendf(log, "Color-based Area Analysis (ZX120 only):");
+    appendf(log, "  Total cells: %d", tc);
+    appendf(log, "  Green (Observable): %d cells (%.1f%%)", q.zx120_green, pct(q.zx120_green));
+    appendf(log, "  Red (Occluded): %d cells (%.1f%%)", q.zx120_red, pct(q.zx120_red));
+    appendf(log, "  Blue (Out of range): %d cells (%.1f%%)", q.zx120_blue, pct(q.zx120_blue));
+    appendf(log, "  Yellow (Out of FOV): %d cells (%.1f%%)", q.zx120_yellow, pct(q.zx120_yellow));
+    appendf(log, "  ---");
+    appendf(log, "  Red/Green Ratio: %.3f", ratio(q.zx120_red, q.zx120_green));
+    const int unobs_z = q.zx120_red + q.zx120_blue + q.zx120_yellow;
+    appendf(log, "  Total Unobservable: %d cells (%.1f%%)", unobs_z, pct(unobs_z));
+    appendf(log, "%s", rule);
+    appendf(log, "%s", "");
+    appendf(log, "%s", rule);
+    appendf(log, "Dual LiDAR Configuration (ZX120 + Mobile)");
+    appendf(log, "%s", rule);
+    appendf(log, "Best Mobile LiDAR Position: (%.2f, %.2f, %.2f)", best.x, best.y, best.z);
+    appendf(log, "Total Score: %.2f", best_score);
+    appendf(log, "%s", rule);
+    appendf(log, "Color-based Area Analysis:");
+    appendf(log, "  Total cells: %d", tc);
+    appendf(log, "  Green (Observable): %d cells (%.1f%%)", q.green, pct(q.green));
+    appendf(log, "  Red (Occluded): %d cells (%.1f%%)", q.red, pct(q.red));
+    appendf(log, "  Blue (Out of range): %d cells (%.1f%%)", q.blue, pct(q.blue));
+    appendf(log, "  Yellow (Out of FOV): %d cells (%.1f%%)", q.yellow, pct(q.yellow));
+    appendf(log, "  ---");
+    appendf(log, "  Red/Green Ratio: %.3f", ratio(q.red, q.green));
+    const int unobs = q.red + q.blue + q.yellow;
+    appendf(log, "  Total Unobservable: %d cells (%.1f%%)", unobs, pct(unobs));
+    appendf(log, "%s", rule);
+    return log;
+}
+
 SimplifiedDualLidarOptimizer::Result SimplifiedDualLidarOptimizer::runOptimization(
     const Transform *zx120_base) {
     Result r;
@@ -302,58 +364,7 @@ SimplifiedDualLidarOptimizer::Result SimplifiedDualLidarOptimizer::runOptimizati
     }
     r.best_score = r.report.best_score;
     if (r.report.best_idx >= 0) r.best = r.candidates[r.report.best_idx];   // else default (:465)
-    // the two RCLCPP_INFO tables, line for line: evaluateZX120Only (:419-451) and the dual
-    // configuration (:522-543)
-    const pcp_vl_report &q = r.report;
-    const int tc = q.total_cells;
-    auto pct = [tc](int v) { return tc > 0 ? (double)v / tc * 100.0 : 0.0; };
-    auto ratio = [](int red, int green) {
-        return green > 0 ? (double)red / green
-                         : (red > 0 ? std::numeric_limits<double>::infinity() : 0.0);
-    };
-    const char *rule = "========================================";
-    const char *thin = "----------------------------------------";
-    appendf(r.log, "%s", rule);
-    appendf(r.log, "ZX120 LiDAR Only Evaluation");
-    appendf(r.log, "%s", rule);
-    appendf(r.log, "ZX120 Position: (%.2f, %.2f, %.2f)", r.zx120.x, r.zx120.y, r.zx120.z);
-    appendf(r.log, "Total Score (ZX120 only): %.2f", q.zx120_total_score);
-    appendf(r.log, "%s", thin);
-    appendf(r.log, "Debug Info:");
-    appendf(r.log, "  Cells in range: %d (%.1f%%)", q.zx120_range_ok, pct(q.zx120_range_ok));
-    appendf(r.log, "  Cells in FOV: %d (%.1f%%)", q.zx120_fov_ok, pct(q.zx120_fov_ok));
-    appendf(r.log, "  Cells visible: %d (%.1f%%)", q.zx120_visible_ok, pct(q.zx120_visible_ok));
-    appendf(r.log, "  ZX120 point cloud size: %zu", zx120_size_);
-    appendf(r.log, "%s", thin);
-    appendf(r.log, "Color-based Area Analysis (ZX120 only):");
-    appendf(r.log, "  Total cells: %d", tc);
-    appendf(r.log, "  Green (Observable): %d cells (%.1f%%)", q.zx120_green, pct(q.zx120_green));
-    appendf(r.log, "  Red (Occluded): %d cells (%.1f%%)", q.zx120_red, pct(q.zx120_red));
-    appendf(r.log, "  Blue (Out of range): %d cells (%.1f%%)", q.zx120_blue, pct(q.zx120_blue));
-    appendf(r.log, "  Yellow (Out of FOV): %d cells (%.1f%%)", q.zx120_yellow, pct(q.zx120_yellow));
-    appendf(r.log, "  ---");
-    appendf(r.log, "  Red/Green Ratio: %.3f", ratio(q.zx120_red, q.zx120_green));
-    const int unobs_z = q.zx120_red + q.zx120_blue + q.zx120_yellow;
-    appendf(r.log, "  Total Unobservable: %d cells (%.1f%%)", unobs_z, pct(unobs_z));
-    appendf(r.log, "%s", rule);
-    appendf(r.log, "%s", "");
-    appendf(r.log, "%s", rule);
-    appendf(r.log, "Dual LiDAR Configuration (ZX120 + Mobile)");
-    appendf(r.log, "%s", rule);
-    appendf(r.log, "Best Mobile LiDAR Position: (%.2f, %.2f, %.2f)", r.best.x, r.best.y, r.best.z);
-    appendf(r.log, "Total Score: %.2f", r.best_score);
-    appendf(r.log, "%s", rule);
-    appendf(r.log, "Color-based Area Analysis:");
-    appendf(r.log, "  Total cells: %d", tc);
-    appendf(r.log, "  Green (Observable): %d cells (%.1f%%)", q.green, pct(q.green));
-    appendf(r.log, "  Red (Occluded): %d cells (%.1f%%)", q.red, pct(q.red));
-    appendf(r.log, "  Blue (Out of range): %d cells (%.1f%%)", q.blue, pct(q.blue));
-    appendf(r.log, "  Yellow (Out of FOV): %d cells (%.1f%%)", q.yellow, pct(q.yellow));
-    appendf(r.log, "  ---");
-    appendf(r.log, "  Red/Green Ratio: %.3f", ratio(q.red, q.green));
-    const int unobs = q.red + q.blue + q.yellow;
-    appendf(r.log, "  Total Unobservable: %d cells (%.1f%%)", unobs, pct(unobs));
-    appendf(r.log, "%s", rule);
+    r.log = optimization_log(r.zx120, r.best, r.best_score, r.report, zx120_size_);
     return r;
 }
 

@@ -255,4 +255,10 @@ class SimplifiedDualLidarOptimizer {
     std::string err_;
 };
 
+// runOptimization's two RCLCPP_INFO tables (virtual_lidar.cpp:419-451, :522-543) from a report:
+// host arithmetic only (the percentages in the reference's expression order, line by line)
+std::string optimization_log(const SimplifiedDualLidarOptimizer::LidarPosition &zx120,
+                             const SimplifiedDualLidarOptimizer::LidarPosition &best,
+                             double best_score, const pcp_vl_report &q, size_t zx120_size);
+
 }  // namespace pcp

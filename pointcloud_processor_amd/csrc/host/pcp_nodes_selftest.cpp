@@ -67,6 +67,22 @@ int main() {
         }
         CHECK(threw);
     }
+    {   // runOptimization's log tables: the Debug Info lines multiply first (n * 100.0 /
+        // total_cells, virtual_lidar.cpp:427-432), the colour lines divide first (:401-416):
+        // 23 of 80 cells print 28.8 and 28.7 (the double of 23 / 80 lies below .2875)
+        pcp_vl_report q{};
+        q.total_cells = 80;
+        q.zx120_range_ok = q.zx120_fov_ok = q.zx120_visible_ok = 23;
+        q.zx120_green = 23;
+        q.green = 49;
+        SimplifiedDualLidarOptimizer::LidarPosition zx, best;
+        const std::string log = optimization_log(zx, best, 1.0, q, 7);
+        CHECK(log.find("  Cells in range: 23 (28.8%)") != std::string::npos);
+        CHECK(log.find("  Cells visible: 23 (28.8%)") != std::string::npos);
+        CHECK(log.find("  Green (Observable): 23 cells (28.7%)") != std::string::npos);
+        CHECK(log.find("  Green (Observable): 49 cells (61.3%)") != std::string::npos);
+        CHECK(log.find("  ZX120 point cloud size: 7") != std::string::npos);
+    }
     if (g_fail) return 1;
     std::printf("nodes selftest ok\n");
     return 0;

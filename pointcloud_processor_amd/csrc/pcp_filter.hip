@@ -1085,6 +1085,10 @@ constexpr int kBkMax = 4096;              // buckets per cloud at most
 #define PCP_BK_CAP 4096
 #endif
 constexpr int kBkCap = PCP_BK_CAP;        // points per bucket at most (LDS of k_bk_sort)
+#ifndef PCP_BK_DENSE
+#define PCP_BK_DENSE 512
+#endif
+constexpr int kBkDense = PCP_BK_DENSE;    // points per voxel ranked in k_bk_sort at most
 // bkv layout: [0, kBkChunkOff) per-bucket (voxels, item offset), then per-64-bucket voxel sums
 constexpr uint32_t kBkChunkOff = kBatch * kBkMax;
 constexpr int kBkGt = 15;                 // crop tiles per group at most
@@ -1458,7 +1462,9 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
     }
     __syncthreads();
     FLT_STAMP(1, f, 4);
-    // input order inside each voxel: rank by crop-slot position among the voxel's points
+    // input order inside each voxel: rank by crop-slot position among the voxel's points.  A
+    // voxel past kBkDense points would cost cnt^2 LDS reads in this one block (4,096 points: ~16 M,
+    // more than the whole frame): such a frame is redone on the LSD chain instead
     uint32_t head = 0, fin[kBkItems3];
 #pragma unroll
     for (int j = 0; j < kBkItems3; ++j) {
@@ -1467,7 +1473,9 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
             const uint32_t st = tab[sub[j]] & 0xffffu;
             const uint32_t cnt = (tab[sub[j] + 1] & 0xffffu) - st;
             uint32_t r = 0;
-            for (uint32_t u = st; cnt > 1 && u < st + cnt; ++u) r += p1[u] < pos[j] ? 1u : 0u;
+            if (cnt > (uint32_t)kBkDense) bk_redo(res);
+            else
+                for (uint32_t u = st; cnt > 1 && u < st + cnt; ++u) r += p1[u] < pos[j] ? 1u : 0u;
             fin[j] = st + r;
             head |= (r == 0 ? 1u : 0u) << j;
         }
@@ -2175,7 +2183,8 @@ static int crop_voxel_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b,
         return set_err(ctx, PCP_E_CAPACITY, "voxel output needs %u points, cap %llu", ri.n,
                        (unsigned long long)cap);
     }
-    if (J.fast) {   // the voxels already sit in pinned memory (synchronised by read_results)
+    if (J.fast || J.bk) {   // the fast chains (LSD or bucket) stored the voxels straight into
+                            // pinned memory (synchronised by read_results): a host copy only
         if (ri.n) std::memcpy(out_xyz16, J.out4, (size_t)ri.n * 16);
         prof_resolve(ctx);
         return PCP_OK;

@@ -282,7 +282,7 @@ def test_filter_merge_fast_chain(gpu, oracle, case, monkeypatch):
 
 
 @pytest.mark.parametrize("case", ["lidar", "three_clouds", "tiny", "one_bucket", "dense_redo",
-                                  "near_cap"])
+                                  "near_cap", "dense_voxel"])
 def test_filter_merge_bucket_chain(oracle, case, monkeypatch):
     """The bucket chain (PCP_FM_FAST=2, the default: crop -> per-group counting sort by bucket ->
     per-bucket LDS sort + input-order sums + look-back offsets) against the oracle and the LSD
@@ -290,7 +290,9 @@ def test_filter_merge_bucket_chain(oracle, case, monkeypatch):
     nothing cropped (no buckets) between two that voxelise; tiny: 5 points; one_bucket: a box of
     < 2^11 voxels (one bucket, bs = 0); dense_redo: one voxel of 60 k points (its bucket passes
     the LDS capacity, the frame is redone on the LSD chain: voxel_redo counts it); near_cap: a
-    dense cluster whose bucket stays just under the capacity."""
+    dense cluster whose bucket stays just under the capacity, but whose ONE voxel of ~3,500
+    points passes kBkDense (512: the in-voxel rank is quadratic) -- redone too (ADVICE r3);
+    dense_voxel: 400 points in one voxel, ranked in the bucket chain."""
     rng = np.random.default_rng(50 + len(case))
     tfs = _tfs()
     rgbs = [(255, 0, 0), (0, 0, 255)]
@@ -317,10 +319,15 @@ def test_filter_merge_bucket_chain(oracle, case, monkeypatch):
         a[100_000:160_000, :3] = [3.01, 2.02, 0.33]
         clouds = [a, synth.lidar_cloud(100_000, seed=37)]
         redo = 1
-    else:   # near_cap: ~3,500 points in one voxel of an otherwise sparse cloud
+    elif case == "near_cap":   # ~3,500 points in one voxel of an otherwise sparse cloud
         a = synth.lidar_cloud(200_000, seed=38)
         a[50_000:53_500, :3] = [7.51, -1.02, 0.43]
         clouds = [a, synth.lidar_cloud(100_000, seed=39)]
+        redo = 1
+    else:   # dense_voxel: 400 points in one voxel (under kBkDense), spread over the input
+        a = synth.lidar_cloud(200_000, seed=40)
+        a[7:200_000:500, :3] = [4.26, 3.17, 0.12]
+        clouds = [a, synth.lidar_cloud(100_000, seed=41)]
     parts = []
     for c, tf, rgb in zip(clouds, tfs, rgbs):
         k = oracle.crop_box(c, box)
