@@ -841,49 +841,6 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     // non-finite points are not in the index: PCL gives them a NaN normal
     const RawIn rin{raw, n, area->point_step, area->off_x, area->off_y, area->off_z};
     const uint32_t npts = (uint32_t)ctx->exc_norm.n_pts;
-    const bool exact = ctx->normals_exact;
-    // the sorted neighbour lists (exact path): one buffer for the area's lists, then the cells'
-    // (the cells' lists overwrite the area's after k_nb_sums<false> consumed them); entries as
-    // needed by the previous call, first guess n x min(n, 4096), regrown on overflow
-    const float bscale = (float)kNbBuckets / r2n;
-    if (exact) {
-        const uint64_t guess = std::min<uint64_t>((uint64_t)npts * std::min<uint64_t>(npts, 4096),
-                                                  64ull << 20);
-        PCP_HIP(ctx, ctx->nb_list.ensure(std::max<uint64_t>(guess, ctx->nb_need) * 4 + 64));
-        PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
-    }
-    auto area_normals = [&]() -> int {
-        if (!exact) {
-            // order-free fixed-point moments (A/B: PCP_NORMALS_EXACT=0), NaN for the non-finite
-            // points by the blocks past the index's points
-            hipLaunchKernelGGL(k_area_normals, dim3((unsigned)(npts + (n + kXT - 1) / kXT)),
-                               dim3(kXT), 0, ctx->stream, gn, r2n, ctx->area_nrm.as<float>(), rin);
-            PCP_CHECK_LAUNCH(ctx);
-            return PCP_OK;
-        }
-        PCP_HIP(ctx, hipMemsetAsync(ctx->nb_ctl.p, 0, 16, ctx->stream));
-        uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
-        const NbLists L{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
-                        (uint32_t)std::min<size_t>(ctx->nb_list.cap / 4, 0xffffffffu)};
-        hipLaunchKernelGGL(k_nb_lists<false>, dim3(npts), dim3(kNbT), 0, ctx->stream, gn, r2n,
-                           bscale, (const double *)nullptr, (const uint32_t *)nullptr, L);
-        PCP_CHECK_LAUNCH(ctx);
-        hipLaunchKernelGGL(k_nb_sums<false>, dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB),
-                           dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)L.meta,
-                           (const uint32_t *)L.list, (const uint32_t *)nullptr,
-                           (const float *)nullptr, ctx->area_nrm.as<float>(),
-                           (const uint32_t *)ctl, (uint32_t *)nullptr);
-        PCP_CHECK_LAUNCH(ctx);
-        if (npts < n) {
-            hipLaunchKernelGGL(k_area_nan, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0,
-                               ctx->stream, rin, ctx->area_nrm.as<float>());
-            PCP_CHECK_LAUNCH(ctx);
-        }
-        return PCP_OK;
-    };
-    if (exact) PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)npts * sizeof(uint2) + 64));
-    if (int rc0 = area_normals()) return rc0;
-    pin_release(ctx, ctx->stream);   // the normals read the raw records last
     // grid bounds (:239-256): min/max of the float coordinates as doubles, then the margin
     const double *bmin = ctx->exc_norm.bmin, *bmax = ctx->exc_norm.bmax;
     Lattice L;
@@ -907,6 +864,58 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: %llu lattice points",
                        (unsigned long long)total);
     L.total = (uint32_t)total;
+    const bool exact = ctx->normals_exact;
+    // the sorted neighbour lists (exact path): one buffer for the area's lists, then the cells'
+    // (the cells' lists overwrite the area's after k_nb_sums<false> consumed them); entries as
+    // needed by the previous call, first guess n x min(n, 4096), regrown on overflow
+    const float bscale = (float)kNbBuckets / r2n;
+    if (exact) {
+        const uint64_t guess = std::min<uint64_t>((uint64_t)npts * std::min<uint64_t>(npts, 4096),
+                                                  64ull << 20);
+        PCP_HIP(ctx, ctx->nb_list.ensure(std::max<uint64_t>(guess, ctx->nb_need) * 4 + 64));
+        PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
+    }
+    // nan_pass: the non-finite input points' NaN normals (k_area_nan reads the raw records:
+    // only before pin_release / the lattice flags reuse ctx->stage; the exact kernels never write
+    // those entries, so a rerun keeps them)
+    auto area_normals = [&](bool nan_pass) -> int {
+        if (!exact) {
+            // order-free fixed-point moments (A/B: PCP_NORMALS_EXACT=0), NaN for the non-finite
+            // points by the blocks past the index's points
+            hipLaunchKernelGGL(k_area_normals, dim3((unsigned)(npts + (n + kXT - 1) / kXT)),
+                               dim3(kXT), 0, ctx->stream, gn, r2n, ctx->area_nrm.as<float>(), rin);
+            PCP_CHECK_LAUNCH(ctx);
+            return PCP_OK;
+        }
+        PCP_HIP(ctx, hipMemsetAsync(ctx->nb_ctl.p, 0, 16, ctx->stream));
+        uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
+        const NbLists L{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
+                        (uint32_t)std::min<size_t>(ctx->nb_list.cap / 4, 0xffffffffu)};
+        hipLaunchKernelGGL(k_nb_lists<false>, dim3(npts), dim3(kNbT), 0, ctx->stream, gn, r2n,
+                           bscale, (const double *)nullptr, (const uint32_t *)nullptr, L);
+        PCP_CHECK_LAUNCH(ctx);
+        hipLaunchKernelGGL(k_nb_sums<false>, dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB),
+                           dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)L.meta,
+                           (const uint32_t *)L.list, (const uint32_t *)nullptr,
+                           (const float *)nullptr, ctx->area_nrm.as<float>(),
+                           (const uint32_t *)ctl, (uint32_t *)nullptr);
+        PCP_CHECK_LAUNCH(ctx);
+        if (nan_pass && npts < n) {
+            hipLaunchKernelGGL(k_area_nan, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0,
+                               ctx->stream, rin, ctx->area_nrm.as<float>());
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        return PCP_OK;
+    };
+    // one {base, count} per query: the area's points, later the lattice's cells (sized once,
+    // before any launch: a reallocation would free a buffer in flight)
+    if (exact)
+        PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)std::max<uint64_t>(npts, total) * sizeof(uint2) +
+                                         64));
+    if (int rc0 = area_normals(true)) return rc0;
+    pin_release(ctx, ctx->stream);   // the normals read the raw records last
+    // (after the normals' launches: a large area's raw records may sit in ctx->stage, which the
+    // lattice flags reuse -- a reallocation here frees it only after the device drained)
     PCP_HIP(ctx, ctx->stage.ensure(total + 64));
     PCP_HIP(ctx, ctx->cells_xyz.ensure(total * 3 * sizeof(double) + 16));
     PCP_HIP(ctx, ctx->cells_nrm.ensure(total * 3 * sizeof(float) + 16));
@@ -959,8 +968,6 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         PCP_CHECK_LAUNCH(ctx);
         return PCP_OK;
     };
-    if (exact) PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)std::max<uint64_t>(npts, total) *
-                                                sizeof(uint2) + 64));
     if (int rc1 = cell_normals()) return rc1;
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (exact && n_h[3]) {
@@ -970,7 +977,7 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         PCP_HIP(ctx, ctx->nb_list.ensure(ctx->nb_need * 4 + 64));
         ctx->normals_regrown++;
         n_h[1] = n_h[2] = n_h[3] = 0;
-        if (int rc2 = area_normals()) return rc2;
+        if (int rc2 = area_normals(false)) return rc2;
         if (int rc3 = cell_normals()) return rc3;
         PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
         if (n_h[3])
