@@ -451,8 +451,12 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
           const uint32_t *__restrict__ n_dev, const float *__restrict__ area_nrm,
           float *__restrict__ out, const uint32_t *__restrict__ ctl, uint32_t *__restrict__ ctl_host) {
     // the lists' cursors and overflow word (final: every k_nb_lists ran before this launch)
-    // to the caller's pinned landing, one plain store each
-    if (ctl_host && blockIdx.x == 0 && threadIdx.x < 3) ctl_host[threadIdx.x] = ctl[threadIdx.x];
+    // to the caller's pinned landing, one plain store each, then cleared for the next call (no
+    // memset launch in front of its k_nb_lists)
+    if (ctl_host && blockIdx.x == 0 && threadIdx.x < 3) {
+        ctl_host[threadIdx.x] = ctl[threadIdx.x];
+        const_cast<uint32_t *>(ctl)[threadIdx.x] = 0;
+    }
     using Cfg = NbCfg<CELLS>;
     using T = typename Cfg::T;
     constexpr int NT = Cfg::NT, QB = Cfg::QB, S = kNbSteps;
@@ -869,11 +873,14 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
     // (the cells' lists overwrite the area's after k_nb_sums<false> consumed them); entries as
     // needed by the previous call, first guess n x min(n, 4096), regrown on overflow
     const float bscale = (float)kNbBuckets / r2n;
+    bool ctl_dirty = !ctx->nb_ctl_zero;   // the cursors' word not known to be zero
     if (exact) {
         const uint64_t guess = std::min<uint64_t>((uint64_t)npts * std::min<uint64_t>(npts, 4096),
                                                   64ull << 20);
         PCP_HIP(ctx, ctx->nb_list.ensure(std::max<uint64_t>(guess, ctx->nb_need) * 4 + 64));
+        if (!ctx->nb_ctl.p) ctl_dirty = true;
         PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
+        ctx->nb_ctl_zero = false;   // set again once k_nb_sums<true> has cleared it
     }
     // nan_pass: the non-finite input points' NaN normals (k_area_nan reads the raw records:
     // only before pin_release / the lattice flags reuse ctx->stage; the exact kernels never write
@@ -887,7 +894,10 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
             PCP_CHECK_LAUNCH(ctx);
             return PCP_OK;
         }
-        PCP_HIP(ctx, hipMemsetAsync(ctx->nb_ctl.p, 0, 16, ctx->stream));
+        // the cursors are zero: cleared by the previous call's last k_nb_sums<true> (or, on a
+        // fresh buffer / a rerun, by the memset below)
+        if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctx->nb_ctl.p, 0, 16, ctx->stream));
+        ctl_dirty = false;
         uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
         const NbLists L{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
                         (uint32_t)std::min<size_t>(ctx->nb_list.cap / 4, 0xffffffffu)};
@@ -977,6 +987,7 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         PCP_HIP(ctx, ctx->nb_list.ensure(ctx->nb_need * 4 + 64));
         ctx->normals_regrown++;
         n_h[1] = n_h[2] = n_h[3] = 0;
+        ctl_dirty = false;   // (cleared by the first pass's k_nb_sums<true>)
         if (int rc2 = area_normals(false)) return rc2;
         if (int rc3 = cell_normals()) return rc3;
         PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -984,7 +995,10 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
             return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: neighbour lists "
                                                    "overflowed after regrowing");
     }
-    if (exact) ctx->nb_need = std::max<uint64_t>(ctx->nb_need, std::max<uint64_t>(n_h[1], n_h[2]));
+    if (exact) {
+        ctx->nb_need = std::max<uint64_t>(ctx->nb_need, std::max<uint64_t>(n_h[1], n_h[2]));
+        ctx->nb_ctl_zero = true;   // k_nb_sums<true> (always launched on this path) cleared it
+    }
     const uint32_t nc = *n_h;
     ctx->n_cells = nc;
     if (n_cells) *n_cells = nc;

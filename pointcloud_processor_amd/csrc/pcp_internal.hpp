@@ -244,6 +244,7 @@ struct pcp_ctx {
     // {base, count}, cursors + overflow word; list entries the last call needed
     bool normals_exact = true;
     pcp::DevBuf nb_list, nb_meta, nb_ctl;
+    bool nb_ctl_zero = false;                // nb_ctl's cursors known zero (cleared by the last call)
     uint64_t nb_need = 0;
     uint64_t normals_regrown = 0;
     // excavated-terrain carve (pcp_excavate): index of the input cloud + scratch
