@@ -691,8 +691,8 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     if ((*n_terrain && !terrain_out) || (*n_area && !area_out))
         return set_err(ctx, PCP_E_INVALID, "pcp_excavate: null output");
     if (land) {   // the records sit in pinned memory already
-        if (*n_terrain) std::memcpy(terrain_out, kept, *n_terrain * 32);
-        if (narea) std::memcpy(area_out, area_d, narea * 32);
+        if (*n_terrain) host_copy(ctx, terrain_out, kept, *n_terrain * 32);
+        if (narea) host_copy(ctx, area_out, area_d, narea * 32);
     } else if (!one_trip) {   // exact-size buffers: the records follow the sizes
         if (*n_terrain)
             PCP_HIP(ctx, hipMemcpyAsync(terrain_out, kept, *n_terrain * 32, hipMemcpyDeviceToHost,

@@ -113,7 +113,7 @@ int upload_async(pcp_ctx *ctx, void *dst_d, const void *src_h, size_t bytes, hip
     if (ctx->up_used[k]) PCP_HIP(ctx, hipEventSynchronize(ctx->up_ev[k]));   // its last DMA
     if (!ctx->up_ev[k]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[k], hipEventDisableTiming));
     if (int rc = ring_ensure(ctx, k, bytes)) return rc;
-    std::memcpy(ctx->up_buf[k].p, src_h, bytes);
+    host_copy(ctx, ctx->up_buf[k].p, src_h, bytes);
     if (int rc = copy_pinned_async(ctx, dst_d, ctx->up_buf[k].p, bytes, st)) return rc;
     PCP_HIP(ctx, hipEventRecord(ctx->up_ev[k], st));
     ctx->up_used[k] = true;
@@ -135,8 +135,8 @@ int upload_pieces(pcp_ctx *ctx, void *dst_d, const HostPiece *pc, int k, size_t 
     if (!ctx->up_ev[s]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[s], hipEventDisableTiming));
     if (int rc = ring_ensure(ctx, s, bytes)) return rc;
     for (int i = 0; i < k; ++i)
-        if (pc[i].bytes) std::memcpy(static_cast<char *>(ctx->up_buf[s].p) + pc[i].off, pc[i].src,
-                                     pc[i].bytes);
+        if (pc[i].bytes) host_copy(ctx, static_cast<char *>(ctx->up_buf[s].p) + pc[i].off,
+                                   pc[i].src, pc[i].bytes);
     if (int rc = copy_pinned_async(ctx, dst_d, ctx->up_buf[s].p, bytes, st)) return rc;
     PCP_HIP(ctx, hipEventRecord(ctx->up_ev[s], st));
     ctx->up_used[s] = true;
@@ -154,8 +154,8 @@ int pin_stage(pcp_ctx *ctx, const HostPiece *pc, int k, size_t bytes, const void
     if (!ctx->up_ev[s]) PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->up_ev[s], hipEventDisableTiming));
     if (int rc = ring_ensure(ctx, s, bytes + 256)) return rc;
     for (int i = 0; i < k; ++i)
-        if (pc[i].bytes) std::memcpy(static_cast<char *>(ctx->up_buf[s].p) + pc[i].off, pc[i].src,
-                                     pc[i].bytes);
+        if (pc[i].bytes) host_copy(ctx, static_cast<char *>(ctx->up_buf[s].p) + pc[i].off,
+                                   pc[i].src, pc[i].bytes);
     ctx->pin_held = s;
     *dev = ctx->up_buf[s].p;
     return PCP_OK;
@@ -427,6 +427,7 @@ int pcp_create(int device, pcp_ctx **out) {
     }
     if (const char *ho = std::getenv("PCP_FAN_HOST_OUT")) ctx->fan_host_out = std::atoi(ho) != 0;
     if (const char *ne = std::getenv("PCP_NORMALS_EXACT")) ctx->normals_exact = std::atoi(ne) != 0;
+    if (const char *ct = std::getenv("PCP_COPY_THREADS")) ctx->copy_threads = std::atoi(ct);
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
     if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff);
     if (const char *bg = std::getenv("PCP_BK_GT")) ctx->bk_gt = std::atoi(bg);
@@ -458,6 +459,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->keys_ev) (void)hipEventDestroy(ctx->keys_ev);
     comm_release(ctx);
+    host_copy_release(ctx);
     for (int k = 0; k < pcp_ctx::kUpRing; ++k) {
         if (ctx->up_ev[k]) (void)hipEventDestroy(ctx->up_ev[k]);
         ctx->up_buf[k].release();

@@ -2185,7 +2185,7 @@ static int crop_voxel_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const Box &b,
     }
     if (J.fast || J.bk) {   // the fast chains (LSD or bucket) stored the voxels straight into
                             // pinned memory (synchronised by read_results): a host copy only
-        if (ri.n) std::memcpy(out_xyz16, J.out4, (size_t)ri.n * 16);
+        if (ri.n) host_copy(ctx, out_xyz16, J.out4, (size_t)ri.n * 16);
         prof_resolve(ctx);
         return PCP_OK;
     }
@@ -2296,7 +2296,7 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, cons
         }
         pin_release(ctx, ctx->stream);
         PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        std::memcpy(out, o, total * 32);
+        host_copy(ctx, out, o, total * 32);
         prof_resolve(ctx);
         return PCP_OK;
     }

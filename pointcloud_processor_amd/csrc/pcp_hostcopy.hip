@@ -1,0 +1,129 @@
+// pcp_hostcopy.hip -- host-side copies of message-sized buffers into and out of libpcp's pinned
+// memory, split over a few helper threads (host code only).
+//
+// Every C5 frame moves ~3 MB through host memcpy: each callback's message into the pinned ring
+// (the kernels read it there, pin_stage / upload_*), and each result out of its pinned landing
+// into the caller's array.  One core copies ~25 GB/s, so a 60k-point scan (960 KB) costs ~40 us
+// on the critical path between callbacks.  Copies of at least kSplitMin bytes are split into
+// kParts parts: the calling thread copies the first, helper threads the others.  Helpers spin on
+// a job generation for a short while after each job (a streaming chain's next copy is ~100 us
+// away) and then sleep on a condition variable (a 10 Hz node's helpers sleep between frames).
+// PCP_COPY_THREADS=0 turns the helpers off (plain memcpy), N sets their count (default 3).
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "pcp_internal.hpp"
+
+namespace pcp {
+
+namespace {
+constexpr size_t kSplitMin = 256u << 10;
+constexpr int kMaxHelpers = 7;
+constexpr auto kSpin = std::chrono::microseconds(300);
+// every part of a split copy is non-empty, so every helper takes part in every job exactly once
+// (its one decrement of `pending` per job generation is what the caller waits for)
+static_assert(kSplitMin >= (size_t)(kMaxHelpers + 1) * 4096 * 2, "parts must be non-empty");
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+}  // namespace
+
+struct CopyPool {
+    struct Part {
+        char *d = nullptr;
+        const char *s = nullptr;
+        size_t n = 0;
+    };
+    explicit CopyPool(int helpers) {
+        for (int i = 0; i < helpers; ++i) th_.emplace_back([this, i] { run(i + 1); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            stop_.store(true, std::memory_order_release);
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int parts() const { return (int)th_.size() + 1; }
+    void copy(void *dst, const void *src, size_t n) {
+        const int k = parts();
+        // parts on 4 KiB boundaries (whole pages per thread)
+        const size_t per = ((n + k - 1) / k + 4095) & ~(size_t)4095;
+        int used = 0;
+        for (int i = 0; i < k; ++i) {
+            const size_t o = std::min(n, (size_t)i * per), e = std::min(n, o + per);
+            part_[i] = Part{static_cast<char *>(dst) + o, static_cast<const char *>(src) + o, e - o};
+            if (e > o) used = i + 1;
+        }
+        pending_.store(used - 1, std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        std::memcpy(part_[0].d, part_[0].s, part_[0].n);
+        while (pending_.load(std::memory_order_acquire) > 0) cpu_relax();
+    }
+
+   private:
+    void run(int id) {
+        uint64_t seen = 0;
+        for (;;) {
+            auto t0 = std::chrono::steady_clock::now();
+            uint64_t g;
+            for (int it = 0;; ++it) {
+                g = gen_.load(std::memory_order_acquire);
+                if (g != seen || stop_.load(std::memory_order_acquire)) break;
+                if ((it & 255) == 255 && std::chrono::steady_clock::now() - t0 > kSpin) {
+                    std::unique_lock<std::mutex> l(mu_);
+                    cv_.wait(l, [&] {
+                        return gen_.load(std::memory_order_acquire) != seen ||
+                               stop_.load(std::memory_order_acquire);
+                    });
+                    t0 = std::chrono::steady_clock::now();
+                }
+                cpu_relax();
+            }
+            if (stop_.load(std::memory_order_acquire)) return;
+            seen = g;
+            const Part p = part_[id];
+            if (p.n) {
+                std::memcpy(p.d, p.s, p.n);
+                pending_.fetch_sub(1, std::memory_order_acq_rel);
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> pending_{0};
+    std::atomic<bool> stop_{false};
+    Part part_[kMaxHelpers + 1];
+};
+
+void host_copy(pcp_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    if (bytes < kSplitMin || ctx->copy_threads <= 0) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    if (!ctx->copy_pool) ctx->copy_pool = new (std::nothrow) CopyPool(std::min(ctx->copy_threads, kMaxHelpers));
+    if (!ctx->copy_pool) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    ctx->copy_pool->copy(dst, src, bytes);
+}
+
+void host_copy_release(pcp_ctx *ctx) {
+    delete ctx->copy_pool;
+    ctx->copy_pool = nullptr;
+}
+
+}  // namespace pcp

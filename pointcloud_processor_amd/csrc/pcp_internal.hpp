@@ -13,6 +13,7 @@
 #include "pcp_abi.h"
 
 namespace pcp {
+struct CopyPool;
 
 // ---------------------------------------------------------------------------------------
 // reference constants (virtual_lidar.cpp:100-114)
@@ -297,6 +298,10 @@ struct pcp_ctx {
     pcp::PinnedBuf tc_host;                  // transform_concat / carve: records stored by the
                                              // kernels straight into pinned memory
     pcp::PinnedBuf cand_host;                // generate_candidates: poses + count in one readback
+    // host copies of message-sized buffers split over helper threads (pcp_hostcopy.hip,
+    // PCP_COPY_THREADS, default 3; 0: plain memcpy)
+    int copy_threads = 3;
+    pcp::CopyPool *copy_pool = nullptr;
     pcp::PinnedBuf cv_host;                  // pcp_crop_voxel's fast chain: centroids + result
                                              // sizes stored by the kernels (one round trip)
     int32_t fan_naz = -1, fan_nel = -1;      // cached fan direction tables
@@ -470,6 +475,10 @@ void fill_report(const int32_t *st_h, double zx_total, int64_t best_idx, double 
 
 // the context's RCCL communicator and its buffers (pcp_comm.hip), at pcp_destroy
 void comm_release(pcp_ctx *ctx);
+// memcpy for host buffers, split over the context's helper threads from 256 KiB on
+// (pcp_hostcopy.hip); host_copy_release stops the helpers (pcp_destroy)
+void host_copy(pcp_ctx *ctx, void *dst, const void *src, size_t bytes);
+void host_copy_release(pcp_ctx *ctx);
 
 // validate a cloud view
 int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what);
