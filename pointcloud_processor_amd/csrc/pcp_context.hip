@@ -475,6 +475,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->nb_list.release();
     ctx->nb_meta.release();
     ctx->nb_ctl.release();
+    ctx->nb_pts.release();
     ctx->carve.release();
     ctx->carve_buf.release();
     ctx->cell_cnt.release();

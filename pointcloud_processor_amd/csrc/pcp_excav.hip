@@ -276,15 +276,20 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
 // sorted neighbour list of every query and then sums it sequentially:
 //  k_nb_lists : one block per query: the stencil's points within r (FLANN predicate) counted
 //               into 2,048 distance buckets of LDS (bucket = (uint)(d * 2048 / r2): monotone in
-//               d, so buckets are ordered), scanned, scattered by bucket, each bucket's few
-//               entries put in (d, index) order by an insertion sort; the list (positions in the
-//               index's point array) goes to global memory at an atomically allocated base
-//  k_nb_sums  : a block per QB queries; waves 1-3 gather the listed points 64 steps at a time
-//               and form the summands (lane-parallel), wave 0 adds them in list order, one lane
-//               per (query, summand) -- the only sequential part, ~1 add per step
+//               d, so buckets are ordered), scanned, the 64-bit keys (distance bits << 32 |
+//               input index) scattered by bucket into LDS, each bucket's few keys put in order by
+//               an insertion sort in LDS; the list (input indices) goes to global memory at an
+//               atomically allocated base
+//  k_nb_sums  : a block per QB queries; waves 1-3 gather the listed points (by input index)
+//               64 steps at a time and form the summands (lane-parallel), wave 0 adds them in
+//               list order, one lane per (query, summand) -- the only sequential part, ~1 add
+//               per step.  The gathers of a chunk are issued one chunk ahead, its list entries
+//               two chunks ahead.
 constexpr int kNbBuckets = 2048;
-constexpr int kNbLds = 6144;   // list entries sorted in LDS; longer lists sort in global memory
+constexpr int kNbLds = 4096;   // keys sorted in LDS (32 KB); longer lists sort in global memory
 constexpr int kNbT = 256;
+constexpr uint32_t kNbChunk = 1024;    // least list words a block takes from the cursor at a time
+constexpr int kNbBlocks = 2048;        // k_nb_lists grid (blocks loop over the queries)
 
 __device__ __forceinline__ uint32_t nb_wave_incl_scan(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
@@ -306,12 +311,36 @@ __device__ __forceinline__ float flann_d2(float qx, float qy, float qz, const fl
 }
 
 struct NbLists {
-    uint32_t *list;                 // entries: positions in the index's point array
+    uint32_t *list;                 // entries: input indices of the neighbours, sorted
     uint2 *meta;                    // per query: {base, m}
     uint32_t *cursor;               // allocation cursor (zero before the launch)
     uint32_t *overflow;             // set when the entries exceed cap (host regrows, reruns)
     uint32_t cap;
 };
+
+// the stencil's points of query q within r2, 4 loads in flight per thread: f(k, p, d)
+template <class F>
+__device__ __forceinline__ void nb_for_within(const GridView &g, const uint32_t (&lo)[4],
+                                              const uint32_t (&hi)[4], float qx, float qy,
+                                              float qz, float r2, F f) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        for (uint32_t k0 = lo[r] + threadIdx.x; k0 < hi[r]; k0 += 4 * kNbT) {
+            float4 p[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + (uint32_t)u * kNbT;
+                p[u] = g.pts[k < hi[r] ? k : hi[r] - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + (uint32_t)u * kNbT;
+                if (k >= hi[r]) break;
+                const float d = flann_d2(qx, qy, qz, p[u]);
+                if (d < r2) f(p[u], d);
+            }
+        }
+}
 
 // queries: the index's own points (CELLS false: area normals, nq = g.n_pts) or the cells
 // (double xyz rounded to float, nq = *n_dev)
@@ -320,10 +349,11 @@ __global__ void __launch_bounds__(kNbT)
 k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
            const uint32_t *__restrict__ n_dev, NbLists L) {
     __shared__ uint32_t cnt[kNbBuckets];
-    __shared__ uint32_t lst[kNbLds];
+    __shared__ unsigned long long key[kNbLds];
     __shared__ uint32_t wsum[kNbT / 64];
-    __shared__ uint32_t sh_base, sh_ok;
+    __shared__ uint32_t sh_base, sh_ok, sh_pos, sh_end;
     const uint32_t nq = CELLS ? *n_dev : g.n_pts;
+    if (threadIdx.x == 0) sh_pos = sh_end = 0;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
         float qx, qy, qz;
@@ -339,16 +369,11 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
         }
         for (int b = threadIdx.x; b < kNbBuckets; b += kNbT) cnt[b] = 0;
         __syncthreads();
-        uint32_t lo[4], hi[4];
-        const bool any = stencil_ranges(g, qx, qy, qz, lo, hi);
-        if (any) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                for (uint32_t k = lo[r] + threadIdx.x; k < hi[r]; k += kNbT) {
-                    const float d = flann_d2(qx, qy, qz, g.pts[k]);
-                    if (d < r2) atomicAdd(&cnt[min((uint32_t)(d * bscale), kNbBuckets - 1u)], 1u);
-                }
-        }
+        uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
+        stencil_ranges(g, qx, qy, qz, lo, hi);   // (false: empty ranges)
+        nb_for_within(g, lo, hi, qx, qy, qz, r2, [&](const float4 &, float d) {
+            atomicAdd(&cnt[min((uint32_t)(d * bscale), kNbBuckets - 1u)], 1u);
+        });
         __syncthreads();
         // exclusive scan of the buckets: thread t owns buckets [8 t, 8 t + 8)
         constexpr int kPer = kNbBuckets / kNbT;
@@ -372,59 +397,51 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
             cnt[kPer * threadIdx.x + j] = ex;   // bucket start
             ex += v[j];
         }
+        const bool big = m > (uint32_t)kNbLds;
         if (threadIdx.x == 0) {
-            uint32_t base = m ? atomicAdd(L.cursor, m) : 0u;
-            uint32_t ok = 1;
-            if ((uint64_t)base + m > L.cap) {   // no room: the host regrows and runs again
-                atomicOr(L.overflow, 1u);
-                ok = 0;
+            // the list's words from the block's chunk (one device atomic per chunk, not per
+            // query: the cursor's atomics serialise across the XCDs).  A list past the LDS sorts
+            // its 64-bit keys in global memory, after its entries: m + 1 + 2 m words.
+            const uint32_t words = big ? 3 * m + 1 : m;
+            if ((uint64_t)sh_pos + words > sh_end) {
+                // room for this block's remaining queries at this one's size (up to 8)
+                const uint32_t rem = (nq - 1 - qi) / gridDim.x + 1;
+                const uint64_t want = std::max<uint64_t>((uint64_t)words * min(rem, 8u), kNbChunk);
+                const uint32_t grab = (uint32_t)std::min<uint64_t>(want, 1u << 30);
+                sh_pos = atomicAdd(L.cursor, grab);
+                sh_end = sh_pos + grab;
+                if ((uint64_t)sh_end > L.cap) atomicOr(L.overflow, 1u);   // the host regrows, reruns
             }
-            sh_base = base;
+            const uint32_t ok = (uint64_t)sh_end <= L.cap;
+            sh_base = sh_pos;
             sh_ok = ok;
-            L.meta[qi] = make_uint2(base, ok ? m : 0u);
+            sh_pos += words;
+            L.meta[qi] = make_uint2(sh_base, ok ? m : 0u);
         }
         __syncthreads();
         const uint32_t base = sh_base;
         if (sh_ok && m) {
-            uint32_t *Lp = m <= (uint32_t)kNbLds ? lst : L.list + base;
-            // scatter by bucket (cnt[b] becomes the bucket's end)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                for (uint32_t k = lo[r] + threadIdx.x; k < hi[r]; k += kNbT) {
-                    const float d = flann_d2(qx, qy, qz, g.pts[k]);
-                    if (d < r2)
-                        Lp[atomicAdd(&cnt[min((uint32_t)(d * bscale), kNbBuckets - 1u)], 1u)] = k;
-                }
+            uint32_t *out = L.list + base;
+            unsigned long long *K =
+                big ? reinterpret_cast<unsigned long long *>(L.list + ((base + m + 1) & ~1u)) : key;
+            // scatter the keys by bucket (cnt[b] becomes the bucket's end)
+            nb_for_within(g, lo, hi, qx, qy, qz, r2, [&](const float4 &p, float d) {
+                K[atomicAdd(&cnt[min((uint32_t)(d * bscale), kNbBuckets - 1u)], 1u)] =
+                    ((unsigned long long)__float_as_uint(d) << 32) | __float_as_uint(p.w);
+            });
             __threadfence_block();
             __syncthreads();
-            // each bucket's entries in (distance, index) order
-            for (int b = threadIdx.x; b < kNbBuckets; b += kNbT) {
-                const uint32_t e = cnt[b], s0 = b ? cnt[b - 1] : 0u;
-                if (e - s0 < 2) continue;
-                for (uint32_t i = s0 + 1; i < e; ++i) {
-                    const uint32_t ki = Lp[i];
-                    const float4 pi = g.pts[ki];
-                    const unsigned long long key =
-                        ((unsigned long long)__float_as_uint(flann_d2(qx, qy, qz, pi)) << 32) |
-                        __float_as_uint(pi.w);
-                    uint32_t j = i;
-                    while (j > s0) {
-                        const uint32_t kj = Lp[j - 1];
-                        const float4 pj = g.pts[kj];
-                        const unsigned long long kk =
-                            ((unsigned long long)__float_as_uint(flann_d2(qx, qy, qz, pj)) << 32) |
-                            __float_as_uint(pj.w);
-                        if (kk <= key) break;
-                        Lp[j] = kj;
-                        --j;
-                    }
-                    Lp[j] = ki;
-                }
+            // each key's place = its bucket's start + its rank among the bucket's keys (the
+            // keys are distinct: distinct indices); straight to the list, no in-place sort
+            for (uint32_t i = threadIdx.x; i < m; i += kNbT) {
+                const unsigned long long ki = K[i];
+                const uint32_t b =
+                    min((uint32_t)(__uint_as_float((uint32_t)(ki >> 32)) * bscale), kNbBuckets - 1u);
+                const uint32_t s0 = b ? cnt[b - 1] : 0u, e = cnt[b];
+                uint32_t rank = 0;
+                for (uint32_t j = s0; j < e; ++j) rank += K[j] < ki;
+                out[s0 + rank] = (uint32_t)ki;
             }
-            __threadfence_block();
-            __syncthreads();
-            if (Lp == lst)
-                for (uint32_t i = threadIdx.x; i < m; i += kNbT) L.list[base + i] = lst[i];
         }
         __syncthreads();   // the LDS is reused by the next query
     }
@@ -434,6 +451,13 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
 // computeMeanAndCovarianceMatrix (shifted by K = the first listed point: xx xy xz yy yz zz x y
 // z), then the covariance and the normal; CELLS true: the 3 double sums of the finite
 // neighbours' normals (computeCellSurfaceNormal :301-340), then the cell normal.
+//
+// A block takes QB queries; its lists are cut into chunks of 64 steps.  Wave 0 adds the
+// chunks' summands in list order, one lane per (query, summand) -- the only sequential part,
+// ~1 add per step.  Waves 1-3 feed it, each element (query, step) of a chunk on one producer
+// lane: chunk c + 2's list entries and chunk c + 1's records are loaded while chunk c's
+// summands are formed (LDS, double-buffered).  The kernel is bound by the VALU work per
+// element (producers) and the consumer's dependent adds, not by the loads.
 template <bool CELLS> struct NbCfg;
 template <> struct NbCfg<false> {
     using T = float;
@@ -441,15 +465,25 @@ template <> struct NbCfg<false> {
 };
 template <> struct NbCfg<true> {
     using T = double;
-    static constexpr int NT = 3, QB = 14;
+    static constexpr int NT = 3, QB = 7;
 };
 constexpr int kNbSteps = 64;   // list entries per chunk
+
+// a workgroup barrier ordering the LDS only: __syncthreads() also fences global memory, which
+// waits for every load in flight -- the prefetched gathers included
+__device__ __forceinline__ void nb_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// one neighbour's gathered record: its point (area moments) or its normal (cells), 16 bytes
+using NbRec = float4;
 
 template <bool CELLS>
 __global__ void __launch_bounds__(kNbT)
 k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict__ list,
-          const uint32_t *__restrict__ n_dev, const float *__restrict__ area_nrm,
-          float *__restrict__ out, const uint32_t *__restrict__ ctl, uint32_t *__restrict__ ctl_host) {
+          const uint32_t *__restrict__ n_dev, const float4 *__restrict__ recs,
+          float *__restrict__ out, float4 *__restrict__ out4, const uint32_t *__restrict__ ctl,
+          uint32_t *__restrict__ ctl_host) {
     // the lists' cursors and overflow word (final: every k_nb_lists ran before this launch)
     // to the caller's pinned landing, one plain store each, then cleared for the next call (no
     // memset launch in front of its k_nb_lists)
@@ -460,7 +494,9 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
     using Cfg = NbCfg<CELLS>;
     using T = typename Cfg::T;
     constexpr int NT = Cfg::NT, QB = Cfg::QB, S = kNbSteps;
-    constexpr int PER = (QB * S + kNbT - 64 - 1) / (kNbT - 64);   // elements per producer lane
+    static_assert(S == 64, "one wave's 64 lanes per query row");
+    constexpr int PW = kNbT / 64 - 1;            // producer waves
+    constexpr int PER = (QB + PW - 1) / PW;      // query rows per producer wave
     // rows of S summands padded by 16 bytes: the consumer lanes' 16-byte reads start 4 banks
     // apart (conflict-free per 16 lanes)
     constexpr int SP = S + 16 / (int)sizeof(T);
@@ -477,81 +513,99 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
             const uint2 mt = qi < nq ? meta[qi] : make_uint2(0u, 0u);
             qm[threadIdx.x] = mt;
             valid[threadIdx.x] = 0;
-            if (!CELLS) qk[threadIdx.x] = mt.y ? g.pts[list[mt.x]] : make_float4(0, 0, 0, 0);
+            if (!CELLS) qk[threadIdx.x] = mt.y ? recs[list[mt.x]] : make_float4(0, 0, 0, 0);
         }
         __syncthreads();
         uint32_t maxm = 0;
 #pragma unroll
         for (int q = 0; q < QB; ++q) maxm = max(maxm, qm[q].y);
         const uint32_t nch = (maxm + S - 1) / S;
-        // producers: element e = (q, t) = (e / S, e % S) of each chunk, lane-parallel; the next
-        // chunk's list entries are loaded one chunk ahead
-        const int pl = (int)threadIdx.x - 64;
-        uint32_t kn[PER];
+        // producer wave w (1..3) owns the query rows j = w - 1 + PW * i (i < PER): element
+        // (row j, step c * S + lane).  Every load unconditional (clamped to entry 0, the value
+        // discarded under the mask): a load under a branch, or a select right after it, waits
+        auto row = [&](int i) { return min(wid - 1 + PW * i, QB - 1); };
+        auto row_ok = [&](int i) { return wid > 0 && wid - 1 + PW * i < QB; };
         auto load_list = [&](uint32_t c, uint32_t (&kk)[PER]) {
+            uint32_t mk = 0;
 #pragma unroll
-            for (int j = 0; j < PER; ++j) {
-                const int e = pl + j * (kNbT - 64);
-                kk[j] = 0xffffffffu;
-                if (e < QB * S) {
-                    const uint2 mt = qm[e / S];
-                    const uint32_t st = c * S + (uint32_t)(e % S);
-                    if (st < mt.y) kk[j] = list[mt.x + st];
-                }
+            for (int i = 0; i < PER; ++i) {
+                const uint2 mt = qm[max(row(i), 0)];
+                const uint32_t st = c * S + (uint32_t)lane;
+                const bool ok = row_ok(i) && st < mt.y;
+                kk[i] = list[ok ? mt.x + st : 0u];
+                mk |= (ok ? 1u : 0u) << i;
             }
+            return mk;
         };
-        if (wid > 0) load_list(0, kn);
+        auto gather = [&](const uint32_t (&kk)[PER], uint32_t mk, NbRec (&rr)[PER]) {
+#pragma unroll
+            for (int i = 0; i < PER; ++i) rr[i] = recs[(mk >> i & 1u) ? kk[i] : 0u];
+        };
+        uint32_t K1[PER], K2[PER], M1 = 0, M2 = 0;   // list entries of chunks c + 1, c + 2
+        NbRec R0[PER];                               // records of chunk c
+        uint32_t M0 = 0;
+        if (wid > 0) {
+            M0 = load_list(0, K1);
+            gather(K1, M0, R0);
+            M1 = load_list(1, K1);
+        }
         T acc = 0;
         const int cq = lane / NT, ca = lane % NT;   // the consumer lane's (query, summand)
         for (uint32_t c = 0; c <= nch; ++c) {
             if (wid > 0 && c < nch) {
-                uint32_t kc[PER];
+                NbRec rc[PER];
+                const uint32_t mc = M0;
 #pragma unroll
-                for (int j = 0; j < PER; ++j) kc[j] = kn[j];
-                if (c + 1 < nch) load_list(c + 1, kn);
+                for (int i = 0; i < PER; ++i) rc[i] = R0[i];
+                // prefetch: chunk c + 2's list entries, chunk c + 1's records
+                M2 = load_list(c + 2, K2);
+                gather(K1, M1, R0);
+                M0 = M1;
+                M1 = M2;
+#pragma unroll
+                for (int i = 0; i < PER; ++i) K1[i] = K2[i];
                 T (*B)[NT][SP] = buf[c & 1];
 #pragma unroll
-                for (int j = 0; j < PER; ++j) {
-                    const int e = pl + j * (kNbT - 64);
-                    if (e >= QB * S) continue;
-                    const int q = e / S, t = e % S;
+                for (int i = 0; i < PER; ++i) {
+                    if (!row_ok(i)) continue;   // (uniform per wave)
+                    const int j = row(i);
                     T tv[NT];
 #pragma unroll
                     for (int a = 0; a < NT; ++a) tv[a] = 0;
-                    if (kc[j] != 0xffffffffu) {
-                        const float4 p = g.pts[kc[j]];
-                        if (CELLS) {
-                            const float *n = area_nrm + 3 * (size_t)__float_as_uint(p.w);
-                            const float nx = n[0], ny = n[1], nz = n[2];
-                            if (isfinite(nx) && isfinite(ny) && isfinite(nz)) {
-                                tv[0] = (T)nx;
-                                tv[1] = (T)ny;
-                                tv[2 % NT] = (T)nz;
-                                atomicAdd(&valid[q], 1u);
-                            }
-                        } else {
-                            const float4 K = qk[q];
-                            const float x = p.x - K.x, y = p.y - K.y, z = p.z - K.z;
-                            tv[0] = (T)(x * x);
-                            tv[1] = (T)(x * y);
-                            tv[2 % NT] = (T)(x * z);
-                            tv[3 % NT] = (T)(y * y);
-                            tv[4 % NT] = (T)(y * z);
-                            tv[5 % NT] = (T)(z * z);
-                            tv[6 % NT] = (T)x;
-                            tv[7 % NT] = (T)y;
-                            tv[8 % NT] = (T)z;
+                    const NbRec r = rc[i];
+                    if (CELLS) {
+                        const bool fin = (mc >> i & 1u) && isfinite(r.x) && isfinite(r.y) &&
+                                         isfinite(r.z);
+                        if (fin) {
+                            tv[0] = (T)r.x;
+                            tv[1] = (T)r.y;
+                            tv[2 % NT] = (T)r.z;
                         }
+                        const uint32_t nv = (uint32_t)__popcll(__ballot(fin));
+                        if (lane == 0) valid[j] += nv;
+                    } else if (mc >> i & 1u) {
+                        const float4 K = qk[j];
+                        const float x = r.x - K.x, y = r.y - K.y, z = r.z - K.z;
+                        tv[0] = (T)(x * x);
+                        tv[1] = (T)(x * y);
+                        tv[2 % NT] = (T)(x * z);
+                        tv[3 % NT] = (T)(y * y);
+                        tv[4 % NT] = (T)(y * z);
+                        tv[5 % NT] = (T)(z * z);
+                        tv[6 % NT] = (T)x;
+                        tv[7 % NT] = (T)y;
+                        tv[8 % NT] = (T)z;
                     }
 #pragma unroll
-                    for (int a = 0; a < NT; ++a) B[q][a][t] = tv[a];
+                    for (int a = 0; a < NT; ++a) B[j][a][lane] = tv[a];
                 }
             }
             if (wid == 0 && c > 0 && cq < QB) {
                 // acc + 0 == acc for these sums (they start at +0 and never become -0): the
                 // zero padding past a query's list is exact
                 if (CELLS) {
-                    const double2 *v = reinterpret_cast<const double2 *>(&buf[(c - 1) & 1][cq][ca][0]);
+                    const double2 *v =
+                        reinterpret_cast<const double2 *>(&buf[(c - 1) & 1][cq][ca][0]);
 #pragma unroll 8
                     for (int t = 0; t < S / 2; ++t) {
                         const double2 w = v[t];
@@ -559,7 +613,8 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
                         acc = acc + (T)w.y;
                     }
                 } else {
-                    const float4 *v = reinterpret_cast<const float4 *>(&buf[(c - 1) & 1][cq][ca][0]);
+                    const float4 *v =
+                        reinterpret_cast<const float4 *>(&buf[(c - 1) & 1][cq][ca][0]);
 #pragma unroll 8
                     for (int t = 0; t < S / 4; ++t) {
                         const float4 w = v[t];
@@ -570,7 +625,7 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
                     }
                 }
             }
-            __syncthreads();
+            nb_lds_barrier();
         }
         if (wid == 0 && cq < QB) accs[cq][ca] = acc;
         __syncthreads();
@@ -615,23 +670,29 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
                     cov[2][1] = cov[1][2];
                     normal_from_cov(cov, qp.x, qp.y, qp.z, o);
                 }
+                // (the cells' sums gather the normals as 16-byte records)
+                out4[__float_as_uint(qp.w)] = make_float4(o[0], o[1], o[2], 0.0f);
             }
         }
         __syncthreads();
     }
 }
 
-// the non-finite input points (not in the index) get their NaN normal (blocks per 256 points)
-__global__ void __launch_bounds__(kXT) k_area_nan(RawIn in, float *__restrict__ out) {
+// the raw input's points by input index (the sums gather them by the lists' indices) and the
+// non-finite points' NaN normals (they are in no list), one thread per input point
+__global__ void __launch_bounds__(kXT) k_area_prep(RawIn in, float4 *__restrict__ pts_in,
+                                                   float *__restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * kXT + threadIdx.x;
     if (i >= in.n) return;
     const unsigned char *p = in.raw + i * in.step;
     const float x = *reinterpret_cast<const float *>(p + in.ox),
                 y = *reinterpret_cast<const float *>(p + in.oy),
                 z = *reinterpret_cast<const float *>(p + in.oz);
+    pts_in[i] = make_float4(x, y, z, 0.0f);
     if (!(isfinite(x) && isfinite(y) && isfinite(z)))
         out[3 * i] = out[3 * i + 1] = out[3 * i + 2] = NAN;
 }
+
 
 struct Lattice {
     double x0, y0, z0, res, z_step;
@@ -882,10 +943,12 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
         ctx->nb_ctl_zero = false;   // set again once k_nb_sums<true> has cleared it
     }
-    // nan_pass: the non-finite input points' NaN normals (k_area_nan reads the raw records:
-    // only before pin_release / the lattice flags reuse ctx->stage; the exact kernels never write
-    // those entries, so a rerun keeps them)
-    auto area_normals = [&](bool nan_pass) -> int {
+    // first: the input points by input index for the sums' gathers, and the non-finite points'
+    // NaN normals (k_area_prep reads the raw records: only before pin_release / the lattice flags
+    // reuse ctx->stage; the exact kernels never write those entries, so a rerun keeps them)
+    // (nb_pts: the points by input index, then their normals as float4: the sums' records)
+    if (exact) PCP_HIP(ctx, ctx->nb_pts.ensure(2 * n * sizeof(float4) + 64));
+    auto area_normals = [&](bool first) -> int {
         if (!exact) {
             // order-free fixed-point moments (A/B: PCP_NORMALS_EXACT=0), NaN for the non-finite
             // points by the blocks past the index's points
@@ -901,20 +964,22 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
         const NbLists L{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
                         (uint32_t)std::min<size_t>(ctx->nb_list.cap / 4, 0xffffffffu)};
-        hipLaunchKernelGGL(k_nb_lists<false>, dim3(npts), dim3(kNbT), 0, ctx->stream, gn, r2n,
+        if (first) {
+            hipLaunchKernelGGL(k_area_prep, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0,
+                               ctx->stream, rin, ctx->nb_pts.as<float4>(),
+                               ctx->area_nrm.as<float>());
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        hipLaunchKernelGGL(k_nb_lists<false>, dim3(std::min<uint32_t>(npts, kNbBlocks)), dim3(kNbT), 0, ctx->stream, gn, r2n,
                            bscale, (const double *)nullptr, (const uint32_t *)nullptr, L);
         PCP_CHECK_LAUNCH(ctx);
         hipLaunchKernelGGL(k_nb_sums<false>, dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB),
                            dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)L.meta,
                            (const uint32_t *)L.list, (const uint32_t *)nullptr,
-                           (const float *)nullptr, ctx->area_nrm.as<float>(),
-                           (const uint32_t *)ctl, (uint32_t *)nullptr);
+                           (const float4 *)ctx->nb_pts.as<float4>(), ctx->area_nrm.as<float>(),
+                           ctx->nb_pts.as<float4>() + n, (const uint32_t *)ctl,
+                           (uint32_t *)nullptr);
         PCP_CHECK_LAUNCH(ctx);
-        if (nan_pass && npts < n) {
-            hipLaunchKernelGGL(k_area_nan, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0,
-                               ctx->stream, rin, ctx->area_nrm.as<float>());
-            PCP_CHECK_LAUNCH(ctx);
-        }
         return PCP_OK;
     };
     // one {base, count} per query: the area's points, later the lattice's cells (sized once,
@@ -960,7 +1025,7 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         const NbLists Lc{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl + 1, ctl + 2,
                          (uint32_t)std::min<size_t>(ctx->nb_list.cap / 4, 0xffffffffu)};
         if (total) {
-            hipLaunchKernelGGL(k_nb_lists<true>, dim3((unsigned)std::min<uint64_t>(total, 16384)),
+            hipLaunchKernelGGL(k_nb_lists<true>, dim3((unsigned)std::min<uint64_t>(total, kNbBlocks)),
                                dim3(kNbT), 0, ctx->stream, gn, r2n, bscale,
                                (const double *)ctx->cells_xyz.as<double>(), (const uint32_t *)n_d,
                                Lc);
@@ -973,7 +1038,8 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
                                1, std::min<uint64_t>((total + QB - 1) / QB, 4096))),
                            dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)Lc.meta,
                            (const uint32_t *)Lc.list, (const uint32_t *)n_d,
-                           (const float *)ctx->area_nrm.as<float>(), ctx->cells_nrm.as<float>(),
+                           (const float4 *)(ctx->nb_pts.as<float4>() + n),
+                           ctx->cells_nrm.as<float>(), (float4 *)nullptr,
                            (const uint32_t *)ctl, n_h + 1);
         PCP_CHECK_LAUNCH(ctx);
         return PCP_OK;

@@ -244,7 +244,7 @@ struct pcp_ctx {
     // order-free fixed-point kernels, A/B only): sorted neighbour lists, their per-query
     // {base, count}, cursors + overflow word; list entries the last call needed
     bool normals_exact = true;
-    pcp::DevBuf nb_list, nb_meta, nb_ctl;
+    pcp::DevBuf nb_list, nb_meta, nb_ctl, nb_pts;   // nb_pts: input points by index
     bool nb_ctl_zero = false;                // nb_ctl's cursors known zero (cleared by the last call)
     uint64_t nb_need = 0;
     uint64_t normals_regrown = 0;
