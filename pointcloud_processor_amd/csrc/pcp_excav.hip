@@ -288,8 +288,8 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
 constexpr int kNbBuckets = 2048;
 constexpr int kNbLds = 4096;   // keys sorted in LDS (32 KB); longer lists sort in global memory
 constexpr int kNbT = 256;
-constexpr uint32_t kNbChunk = 1024;    // least list words a block takes from the cursor at a time
 constexpr int kNbBlocks = 2048;        // k_nb_lists grid (blocks loop over the queries)
+constexpr int kNbU = 8;                // k_nb_lists candidates in flight per thread
 
 __device__ __forceinline__ uint32_t nb_wave_incl_scan(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
@@ -301,11 +301,16 @@ __device__ __forceinline__ uint32_t nb_wave_incl_scan(uint32_t x) {
     return x;
 }
 
+// FLANN's L2 (acc = 0; acc += d0 d0; acc += d1 d1; acc += d2 d2, each op rounded; 0 + d0 d0
+// is d0 d0 exactly).  x and y as one packed pair: v_pk_add / v_pk_mul round each half like the
+// scalar ops, one instruction for two
+typedef float nb_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float flann_d2(float qx, float qy, float qz, const float4 &p) {
-    const float d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
-    float acc = 0.0f;
-    acc = acc + d0 * d0;
-    acc = acc + d1 * d1;
+    const nb_f2 q2 = {qx, qy}, p2 = {p.x, p.y};
+    const nb_f2 d01 = q2 - p2;
+    const nb_f2 s01 = d01 * d01;
+    const float d2 = qz - p.z;
+    float acc = s01.x + s01.y;
     acc = acc + d2 * d2;
     return acc;
 }
@@ -313,9 +318,9 @@ __device__ __forceinline__ float flann_d2(float qx, float qy, float qz, const fl
 struct NbLists {
     uint32_t *list;                 // entries: input indices of the neighbours, sorted
     uint2 *meta;                    // per query: {base, m}
-    uint32_t *cursor;               // allocation cursor (zero before the launch)
-    uint32_t *overflow;             // set when the entries exceed cap (host regrows, reruns)
-    uint32_t cap;
+    uint32_t *need;                 // the largest words one block needed (zero before the launch)
+    uint32_t *overflow;             // set when a block's region was too small (host regrows)
+    uint32_t per_block;             // words of each block's region (block b: [b pb, (b + 1) pb))
 };
 
 // the stencil's points of query q within r2, 4 loads in flight per thread: f(k, p, d)
@@ -342,19 +347,32 @@ __device__ __forceinline__ void nb_for_within(const GridView &g, const uint32_t 
         }
 }
 
+// a workgroup barrier ordering the LDS only.  __syncthreads() also fences global memory: it
+// waits for every load in flight (the sums' prefetched gathers) and for every store's
+// acknowledgement (the lists' entries) -- microseconds per barrier
+__device__ __forceinline__ void nb_lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // queries: the index's own points (CELLS false: area normals, nq = g.n_pts) or the cells
-// (double xyz rounded to float, nq = *n_dev)
+// (double xyz rounded to float, nq = *n_dev).  One pass over the stencil counts the neighbours
+// into the distance buckets and appends their 64-bit keys (distance bits << 32 | input index)
+// to LDS in any order; the keys are then grouped by bucket (indices into the appended array)
+// and each key's rank among its bucket's keys places it in the list.  A query with more than
+// kNbLds neighbours takes a second stencil pass that scatters its keys into global memory.
 template <bool CELLS>
 __global__ void __launch_bounds__(kNbT)
 k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
            const uint32_t *__restrict__ n_dev, NbLists L) {
     __shared__ uint32_t cnt[kNbBuckets];
-    __shared__ unsigned long long key[kNbLds];
+    __shared__ unsigned long long key[kNbLds];   // appended keys
+    __shared__ unsigned long long grp[kNbLds];   // the keys grouped by bucket
     __shared__ uint32_t wsum[kNbT / 64];
-    __shared__ uint32_t sh_base, sh_ok, sh_pos, sh_end;
+    __shared__ uint32_t sh_base, sh_ok, sh_pos, sh_m;
     const uint32_t nq = CELLS ? *n_dev : g.n_pts;
-    if (threadIdx.x == 0) sh_pos = sh_end = 0;
+    if (threadIdx.x == 0) sh_pos = 0;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    auto bucket_of = [&](float d) { return min((uint32_t)(d * bscale), kNbBuckets - 1u); };
     for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
         float qx, qy, qz;
         if (CELLS) {
@@ -368,13 +386,53 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
             qz = q.z;
         }
         for (int b = threadIdx.x; b < kNbBuckets; b += kNbT) cnt[b] = 0;
-        __syncthreads();
+        if (threadIdx.x == 0) sh_m = 0;
+        nb_lds_barrier();
         uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
         stencil_ranges(g, qx, qy, qz, lo, hi);   // (false: empty ranges)
-        nb_for_within(g, lo, hi, qx, qy, qz, r2, [&](const float4 &, float d) {
-            atomicAdd(&cnt[min((uint32_t)(d * bscale), kNbBuckets - 1u)], 1u);
-        });
-        __syncthreads();
+        // the one pass over the stencil's four row ranges as one flat index space (no partial
+        // round per range), kNbU candidates in flight per thread -- the pass is bound by the
+        // load latency of its rounds -- and one LDS append per wave and round
+        const uint32_t c1 = hi[0] - lo[0], c2 = c1 + (hi[1] - lo[1]), c3 = c2 + (hi[2] - lo[2]);
+        const uint32_t ntot = c3 + (hi[3] - lo[3]);
+        auto cand = [&](uint32_t f) {
+            return f < c1 ? lo[0] + f : f < c2 ? lo[1] + (f - c1) : f < c3 ? lo[2] + (f - c2)
+                                                                           : lo[3] + (f - c3);
+        };
+        for (uint32_t f0 = threadIdx.x; f0 < ntot; f0 += kNbU * kNbT) {
+            float4 p[kNbU];
+#pragma unroll
+            for (int u = 0; u < kNbU; ++u) p[u] = g.pts[cand(min(f0 + (uint32_t)u * kNbT, ntot - 1))];
+            bool in[kNbU];
+            float dd[kNbU];
+            uint64_t bal[kNbU];
+            uint32_t tot = 0;
+#pragma unroll
+            for (int u = 0; u < kNbU; ++u) {
+                dd[u] = flann_d2(qx, qy, qz, p[u]);
+                in[u] = f0 + (uint32_t)u * kNbT < ntot && dd[u] < r2;
+                if (in[u]) atomicAdd(&cnt[bucket_of(dd[u])], 1u);
+                bal[u] = __ballot(in[u]);
+                tot += (uint32_t)__popcll(bal[u]);
+            }
+            if (tot) {   // (uniform)
+                const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&sh_m, tot);
+                base = (uint32_t)__shfl((int)base, leader);
+#pragma unroll
+                for (int u = 0; u < kNbU; ++u) {
+                    const uint32_t pos =
+                        base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[u] >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
+                    if (in[u] && pos < (uint32_t)kNbLds)
+                        key[pos] = ((unsigned long long)__float_as_uint(dd[u]) << 32) |
+                                   __float_as_uint(p[u].w);
+                    base += (uint32_t)__popcll(bal[u]);
+                }
+            }
+        }
+        nb_lds_barrier();
         // exclusive scan of the buckets: thread t owns buckets [8 t, 8 t + 8)
         constexpr int kPer = kNbBuckets / kNbT;
         uint32_t v[kPer], run = 0;
@@ -385,7 +443,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
         }
         const uint32_t incl = nb_wave_incl_scan(run);
         if (lane == 63) wsum[wid] = incl;
-        __syncthreads();
+        nb_lds_barrier();
         uint32_t ex = incl - run, m = 0;
 #pragma unroll
         for (int w = 0; w < kNbT / 64; ++w) {
@@ -399,52 +457,72 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
         }
         const bool big = m > (uint32_t)kNbLds;
         if (threadIdx.x == 0) {
-            // the list's words from the block's chunk (one device atomic per chunk, not per
-            // query: the cursor's atomics serialise across the XCDs).  A list past the LDS sorts
-            // its 64-bit keys in global memory, after its entries: m + 1 + 2 m words.
+            // the list's words from the block's own region of the list buffer (no device
+            // atomics: those on one shared cursor serialise across the XCDs).  A list past the LDS sorts its 64-bit
+            // keys in global memory, after its entries: m + 1 + 2 m words.  A region too small
+            // marks the list empty and the overflow; the block's use goes to the host, which
+            // regrows the buffer to the largest use x the grid and runs the normals again.
             const uint32_t words = big ? 3 * m + 1 : m;
-            if ((uint64_t)sh_pos + words > sh_end) {
-                // room for this block's remaining queries at this one's size (up to 8)
-                const uint32_t rem = (nq - 1 - qi) / gridDim.x + 1;
-                const uint64_t want = std::max<uint64_t>((uint64_t)words * min(rem, 8u), kNbChunk);
-                const uint32_t grab = (uint32_t)std::min<uint64_t>(want, 1u << 30);
-                sh_pos = atomicAdd(L.cursor, grab);
-                sh_end = sh_pos + grab;
-                if ((uint64_t)sh_end > L.cap) atomicOr(L.overflow, 1u);   // the host regrows, reruns
-            }
-            const uint32_t ok = (uint64_t)sh_end <= L.cap;
-            sh_base = sh_pos;
+            const uint32_t ok = (uint64_t)sh_pos + words <= L.per_block;
+            if (!ok) atomicOr(L.overflow, 1u);
+            sh_base = L.per_block * blockIdx.x + sh_pos;
             sh_ok = ok;
-            sh_pos += words;
+            sh_pos += words;   // (the need, counted on: the host's regrow size)
             L.meta[qi] = make_uint2(sh_base, ok ? m : 0u);
         }
-        __syncthreads();
+        nb_lds_barrier();
         const uint32_t base = sh_base;
         if (sh_ok && m) {
             uint32_t *out = L.list + base;
-            unsigned long long *K =
-                big ? reinterpret_cast<unsigned long long *>(L.list + ((base + m + 1) & ~1u)) : key;
-            // scatter the keys by bucket (cnt[b] becomes the bucket's end)
-            nb_for_within(g, lo, hi, qx, qy, qz, r2, [&](const float4 &p, float d) {
-                K[atomicAdd(&cnt[min((uint32_t)(d * bscale), kNbBuckets - 1u)], 1u)] =
-                    ((unsigned long long)__float_as_uint(d) << 32) | __float_as_uint(p.w);
-            });
-            __threadfence_block();
-            __syncthreads();
-            // each key's place = its bucket's start + its rank among the bucket's keys (the
-            // keys are distinct: distinct indices); straight to the list, no in-place sort
-            for (uint32_t i = threadIdx.x; i < m; i += kNbT) {
-                const unsigned long long ki = K[i];
-                const uint32_t b =
-                    min((uint32_t)(__uint_as_float((uint32_t)(ki >> 32)) * bscale), kNbBuckets - 1u);
-                const uint32_t s0 = b ? cnt[b - 1] : 0u, e = cnt[b];
-                uint32_t rank = 0;
-                for (uint32_t j = s0; j < e; ++j) rank += K[j] < ki;
-                out[s0 + rank] = (uint32_t)ki;
+            if (!big) {
+                // group the appended keys by bucket (cnt[b] becomes the bucket's end)
+                for (uint32_t i = threadIdx.x; i < m; i += kNbT) {
+                    const unsigned long long ki = key[i];
+                    grp[atomicAdd(&cnt[bucket_of(__uint_as_float((uint32_t)(ki >> 32)))], 1u)] = ki;
+                }
+                nb_lds_barrier();
+                // each key's place = its bucket's start + its rank among the bucket's keys (the
+                // keys are distinct: distinct indices).  Lanes take consecutive grouped keys: a
+                // wave mostly reads one bucket's keys (broadcast LDS reads); the bucket holds the
+                // distance's exact ties, a handful on a lattice
+                for (uint32_t i = threadIdx.x; i < m; i += kNbT) {
+                    const unsigned long long ki = grp[i];
+                    const uint32_t b = bucket_of(__uint_as_float((uint32_t)(ki >> 32)));
+                    const uint32_t s0 = b ? cnt[b - 1] : 0u, e = cnt[b];
+                    // four independent reads per round (a loop of single reads waits on each)
+                    uint32_t rank = 0, j = s0;
+                    for (; j + 4 <= e; j += 4) {
+                        const unsigned long long a0 = grp[j], a1 = grp[j + 1], a2 = grp[j + 2],
+                                                 a3 = grp[j + 3];
+                        rank += (uint32_t)(a0 < ki) + (uint32_t)(a1 < ki) + (uint32_t)(a2 < ki) +
+                                (uint32_t)(a3 < ki);
+                    }
+                    for (; j < e; ++j) rank += grp[j] < ki;
+                    out[s0 + rank] = (uint32_t)ki;
+                }
+            } else {
+                unsigned long long *K =
+                    reinterpret_cast<unsigned long long *>(L.list + ((base + m + 1) & ~1u));
+                // a second stencil pass scatters the keys by bucket into global memory
+                nb_for_within(g, lo, hi, qx, qy, qz, r2, [&](const float4 &p, float d) {
+                    K[atomicAdd(&cnt[bucket_of(d)], 1u)] =
+                        ((unsigned long long)__float_as_uint(d) << 32) | __float_as_uint(p.w);
+                });
+                __threadfence_block();
+                __syncthreads();   // (global memory: the keys)
+                for (uint32_t i = threadIdx.x; i < m; i += kNbT) {
+                    const unsigned long long ki = K[i];
+                    const uint32_t b = bucket_of(__uint_as_float((uint32_t)(ki >> 32)));
+                    const uint32_t s0 = b ? cnt[b - 1] : 0u, e = cnt[b];
+                    uint32_t rank = 0;
+                    for (uint32_t j = s0; j < e; ++j) rank += K[j] < ki;
+                    out[s0 + rank] = (uint32_t)ki;
+                }
             }
         }
-        __syncthreads();   // the LDS is reused by the next query
+        nb_lds_barrier();   // the LDS is reused by the next query
     }
+    if (threadIdx.x == 0 && sh_pos) atomicMax(L.need, sh_pos);   // (no return value awaited)
 }
 
 // sequential sums over the sorted lists.  CELLS false: the 9 float moments of
@@ -469,11 +547,6 @@ template <> struct NbCfg<true> {
 };
 constexpr int kNbSteps = 64;   // list entries per chunk
 
-// a workgroup barrier ordering the LDS only: __syncthreads() also fences global memory, which
-// waits for every load in flight -- the prefetched gathers included
-__device__ __forceinline__ void nb_lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 // one neighbour's gathered record: its point (area moments) or its normal (cells), 16 bytes
 using NbRec = float4;
@@ -484,7 +557,7 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
           const uint32_t *__restrict__ n_dev, const float4 *__restrict__ recs,
           float *__restrict__ out, float4 *__restrict__ out4, const uint32_t *__restrict__ ctl,
           uint32_t *__restrict__ ctl_host) {
-    // the lists' cursors and overflow word (final: every k_nb_lists ran before this launch)
+    // the lists' largest block uses and overflow word (final: every k_nb_lists ran before this launch)
     // to the caller's pinned landing, one plain store each, then cleared for the next call (no
     // memset launch in front of its k_nb_lists)
     if (ctl_host && blockIdx.x == 0 && threadIdx.x < 3) {
@@ -515,7 +588,7 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
             valid[threadIdx.x] = 0;
             if (!CELLS) qk[threadIdx.x] = mt.y ? recs[list[mt.x]] : make_float4(0, 0, 0, 0);
         }
-        __syncthreads();
+        nb_lds_barrier();
         uint32_t maxm = 0;
 #pragma unroll
         for (int q = 0; q < QB; ++q) maxm = max(maxm, qm[q].y);
@@ -674,7 +747,7 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
                 out4[__float_as_uint(qp.w)] = make_float4(o[0], o[1], o[2], 0.0f);
             }
         }
-        __syncthreads();
+        nb_lds_barrier();   // (LDS reuse; the stores need no acknowledgement here)
     }
 }
 
@@ -930,140 +1003,168 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
                        (unsigned long long)total);
     L.total = (uint32_t)total;
     const bool exact = ctx->normals_exact;
-    // the sorted neighbour lists (exact path): one buffer for the area's lists, then the cells'
-    // (the cells' lists overwrite the area's after k_nb_sums<false> consumed them); entries as
-    // needed by the previous call, first guess n x min(n, 4096), regrown on overflow
-    const float bscale = (float)kNbBuckets / r2n;
-    bool ctl_dirty = !ctx->nb_ctl_zero;   // the cursors' word not known to be zero
-    if (exact) {
-        const uint64_t guess = std::min<uint64_t>((uint64_t)npts * std::min<uint64_t>(npts, 4096),
-                                                  64ull << 20);
-        PCP_HIP(ctx, ctx->nb_list.ensure(std::max<uint64_t>(guess, ctx->nb_need) * 4 + 64));
-        if (!ctx->nb_ctl.p) ctl_dirty = true;
-        PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
-        ctx->nb_ctl_zero = false;   // set again once k_nb_sums<true> has cleared it
-    }
-    // first: the input points by input index for the sums' gathers, and the non-finite points'
-    // NaN normals (k_area_prep reads the raw records: only before pin_release / the lattice flags
-    // reuse ctx->stage; the exact kernels never write those entries, so a rerun keeps them)
-    // (nb_pts: the points by input index, then their normals as float4: the sums' records)
-    if (exact) PCP_HIP(ctx, ctx->nb_pts.ensure(2 * n * sizeof(float4) + 64));
-    auto area_normals = [&](bool first) -> int {
-        if (!exact) {
-            // order-free fixed-point moments (A/B: PCP_NORMALS_EXACT=0), NaN for the non-finite
-            // points by the blocks past the index's points
-            hipLaunchKernelGGL(k_area_normals, dim3((unsigned)(npts + (n + kXT - 1) / kXT)),
-                               dim3(kXT), 0, ctx->stream, gn, r2n, ctx->area_nrm.as<float>(), rin);
-            PCP_CHECK_LAUNCH(ctx);
-            return PCP_OK;
-        }
-        // the cursors are zero: cleared by the previous call's last k_nb_sums<true> (or, on a
-        // fresh buffer / a rerun, by the memset below)
-        if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctx->nb_ctl.p, 0, 16, ctx->stream));
-        ctl_dirty = false;
-        uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
-        const NbLists L{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
-                        (uint32_t)std::min<size_t>(ctx->nb_list.cap / 4, 0xffffffffu)};
-        if (first) {
-            hipLaunchKernelGGL(k_area_prep, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0,
-                               ctx->stream, rin, ctx->nb_pts.as<float4>(),
-                               ctx->area_nrm.as<float>());
+    PCP_HIP(ctx, ctx->small_host.ensure(4096));
+    uint32_t *n_h = ctx->small_host.as<uint32_t>();
+    n_h[1] = n_h[2] = n_h[3] = 0;   // the lists' largest block uses + overflow (exact path)
+    PCP_HIP(ctx, ctx->out_c.ensure(64));
+    uint32_t *n_d = ctx->out_c.as<uint32_t>();
+    // the lattice of candidate cells (:258-298) on stream st.  Its buffers are sized after the
+    // raw records' last reader was launched: a large area's raw records may sit in ctx->stage,
+    // which the lattice flags reuse (a reallocation frees it only after the device drained)
+    auto lattice = [&](hipStream_t st) -> int {
+        PCP_HIP(ctx, ctx->stage.ensure(total + 64));
+        PCP_HIP(ctx, ctx->cells_xyz.ensure(total * 3 * sizeof(double) + 16));
+        PCP_HIP(ctx, ctx->cells_nrm.ensure(total * 3 * sizeof(float) + 16));
+        if (total) {
+            hipLaunchKernelGGL(k_lattice_flags,
+                               dim3((unsigned)((total + kLatWaves - 1) / kLatWaves)), dim3(kXT), 0,
+                               st, gq, r2q, L, ctx->stage.as<uint8_t>());
             PCP_CHECK_LAUNCH(ctx);
         }
-        hipLaunchKernelGGL(k_nb_lists<false>, dim3(std::min<uint32_t>(npts, kNbBlocks)), dim3(kNbT), 0, ctx->stream, gn, r2n,
-                           bscale, (const double *)nullptr, (const uint32_t *)nullptr, L);
-        PCP_CHECK_LAUNCH(ctx);
-        hipLaunchKernelGGL(k_nb_sums<false>, dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB),
-                           dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)L.meta,
-                           (const uint32_t *)L.list, (const uint32_t *)nullptr,
-                           (const float4 *)ctx->nb_pts.as<float4>(), ctx->area_nrm.as<float>(),
-                           ctx->nb_pts.as<float4>() + n, (const uint32_t *)ctl,
-                           (uint32_t *)nullptr);
+        hipLaunchKernelGGL(k_lattice_compact, dim3(1), dim3(1024), 0, st,
+                           (const uint8_t *)ctx->stage.as<uint8_t>(), L,
+                           ctx->cells_xyz.as<double>(), (uint32_t)total, n_d, n_h);
         PCP_CHECK_LAUNCH(ctx);
         return PCP_OK;
     };
-    // one {base, count} per query: the area's points, later the lattice's cells (sized once,
-    // before any launch: a reallocation would free a buffer in flight)
-    if (exact)
-        PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)std::max<uint64_t>(npts, total) * sizeof(uint2) +
-                                         64));
-    if (int rc0 = area_normals(true)) return rc0;
-    pin_release(ctx, ctx->stream);   // the normals read the raw records last
-    // (after the normals' launches: a large area's raw records may sit in ctx->stage, which the
-    // lattice flags reuse -- a reallocation here frees it only after the device drained)
-    PCP_HIP(ctx, ctx->stage.ensure(total + 64));
-    PCP_HIP(ctx, ctx->cells_xyz.ensure(total * 3 * sizeof(double) + 16));
-    PCP_HIP(ctx, ctx->cells_nrm.ensure(total * 3 * sizeof(float) + 16));
-    PCP_HIP(ctx, ctx->out_c.ensure(64));
-    uint32_t *n_d = ctx->out_c.as<uint32_t>();
-    if (total) {
-        hipLaunchKernelGGL(k_lattice_flags, dim3((unsigned)((total + kLatWaves - 1) / kLatWaves)), dim3(kXT),
-                           0, ctx->stream, gq, r2q, L, ctx->stage.as<uint8_t>());
+    if (!exact) {
+        // order-free fixed-point moments (A/B: PCP_NORMALS_EXACT=0), NaN for the non-finite
+        // points by the blocks past the index's points; one stream
+        hipLaunchKernelGGL(k_area_normals, dim3((unsigned)(npts + (n + kXT - 1) / kXT)), dim3(kXT),
+                           0, ctx->stream, gn, r2n, ctx->area_nrm.as<float>(), rin);
         PCP_CHECK_LAUNCH(ctx);
-    }
-    PCP_HIP(ctx, ctx->small_host.ensure(4096));
-    uint32_t *n_h = ctx->small_host.as<uint32_t>();
-    n_h[1] = n_h[2] = n_h[3] = 0;   // the lists' cursors + overflow (exact path, below)
-    hipLaunchKernelGGL(k_lattice_compact, dim3(1), dim3(1024), 0, ctx->stream,
-                       (const uint8_t *)ctx->stage.as<uint8_t>(), L, ctx->cells_xyz.as<double>(),
-                       (uint32_t)total, n_d, n_h);
-    PCP_CHECK_LAUNCH(ctx);
-    // the cell normals read the lattice count on the device; the count comes back once, at
-    // the end (one synchronisation for the whole call)
-    auto cell_normals = [&]() -> int {
-        if (!total && !exact) return PCP_OK;
-        if (!exact) {
+        pin_release(ctx, ctx->stream);   // the normals read the raw records last
+        if (int rcl = lattice(ctx->stream)) return rcl;
+        if (total) {
             hipLaunchKernelGGL(k_cell_normals, dim3((unsigned)std::min<uint64_t>(total, 8192)),
                                dim3(kXT), 0, ctx->stream, gn, r2n,
                                (const double *)ctx->cells_xyz.as<double>(),
                                (const float *)ctx->area_nrm.as<float>(), (const uint32_t *)n_d,
                                ctx->cells_nrm.as<float>());
             PCP_CHECK_LAUNCH(ctx);
-            return PCP_OK;
         }
-        uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
-        const NbLists Lc{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl + 1, ctl + 2,
-                         (uint32_t)std::min<size_t>(ctx->nb_list.cap / 4, 0xffffffffu)};
-        if (total) {
-            hipLaunchKernelGGL(k_nb_lists<true>, dim3((unsigned)std::min<uint64_t>(total, kNbBlocks)),
-                               dim3(kNbT), 0, ctx->stream, gn, r2n, bscale,
-                               (const double *)ctx->cells_xyz.as<double>(), (const uint32_t *)n_d,
-                               Lc);
-            PCP_CHECK_LAUNCH(ctx);
-        }
-        // (launched for an empty lattice too: it lands the area lists' cursor and overflow)
-        constexpr int QB = NbCfg<true>::QB;
-        hipLaunchKernelGGL(k_nb_sums<true>,
-                           dim3((unsigned)std::max<uint64_t>(
-                               1, std::min<uint64_t>((total + QB - 1) / QB, 4096))),
-                           dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)Lc.meta,
-                           (const uint32_t *)Lc.list, (const uint32_t *)n_d,
-                           (const float4 *)(ctx->nb_pts.as<float4>() + n),
-                           ctx->cells_nrm.as<float>(), (float4 *)nullptr,
-                           (const uint32_t *)ctl, n_h + 1);
-        PCP_CHECK_LAUNCH(ctx);
-        return PCP_OK;
-    };
-    if (int rc1 = cell_normals()) return rc1;
-    PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (exact && n_h[3]) {
-        // a list buffer too small (first frames, or a denser area): regrow to the entries both
-        // passes asked for and run the normals again (the lattice stands)
-        ctx->nb_need = std::max<uint64_t>(n_h[1], n_h[2]);
-        PCP_HIP(ctx, ctx->nb_list.ensure(ctx->nb_need * 4 + 64));
-        ctx->normals_regrown++;
-        n_h[1] = n_h[2] = n_h[3] = 0;
-        ctl_dirty = false;   // (cleared by the first pass's k_nb_sums<true>)
-        if (int rc2 = area_normals(false)) return rc2;
-        if (int rc3 = cell_normals()) return rc3;
         PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        if (n_h[3])
-            return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: neighbour lists "
-                                                   "overflowed after regrowing");
-    }
-    if (exact) {
-        ctx->nb_need = std::max<uint64_t>(ctx->nb_need, std::max<uint64_t>(n_h[1], n_h[2]));
-        ctx->nb_ctl_zero = true;   // k_nb_sums<true> (always launched on this path) cleared it
+    } else {
+        // The sorted neighbour lists: the area's (nb_list / nb_meta) and the cells' (nb_list_c /
+        // nb_meta_c), one region per k_nb_lists block, words as the previous call needed (first
+        // guess n x min(n, 4096)), regrown on overflow to the largest block's use x the grid.
+        // Two streams: the cells' lists need the lattice and the area index, not the area
+        // normals, so the lattice and k_nb_lists<true> run on the side stream beside the area's
+        // lists and sums; k_nb_sums<true> joins them.  Every buffer is sized before the launches.
+        const float bscale = (float)kNbBuckets / r2n;
+        const uint32_t grid_a = std::min<uint32_t>(npts, kNbBlocks);
+        const uint32_t grid_c =
+            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(total, kNbBlocks));
+        const uint64_t per_pt = std::min<uint64_t>(npts, 4096);
+        const uint64_t guess_a = std::min<uint64_t>((uint64_t)npts * per_pt, 64ull << 20);
+        const uint64_t guess_c = std::min<uint64_t>(std::max<uint64_t>(total, 1) * per_pt, 64ull << 20);
+        PCP_HIP(ctx, ctx->nb_list.ensure(std::max<uint64_t>(guess_a, ctx->nb_need) * 4 + 64));
+        PCP_HIP(ctx, ctx->nb_list_c.ensure(std::max<uint64_t>(guess_c, ctx->nb_need_c) * 4 + 64));
+        PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)npts * sizeof(uint2) + 64));
+        PCP_HIP(ctx, ctx->nb_meta_c.ensure((size_t)total * sizeof(uint2) + 64));
+        bool ctl_dirty = !ctx->nb_ctl_zero || !ctx->nb_ctl.p;   // control words not known zero
+        PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
+        ctx->nb_ctl_zero = false;   // set again once k_nb_sums<true> has cleared them
+        // nb_pts: the points by input index, then their normals as float4 (the sums' records)
+        PCP_HIP(ctx, ctx->nb_pts.ensure(2 * n * sizeof(float4) + 64));
+        if (ctx->normals_overlap && !ctx->side_stream) {
+            PCP_HIP(ctx, hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
+            for (auto &e : ctx->side_ev) PCP_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        // (PCP_NORMALS_OVERLAP=1: the side stream.  Measured slower -- both list kernels are
+        // throughput-bound and share the same CUs -- so one stream by default)
+        const hipStream_t side = ctx->normals_overlap ? ctx->side_stream : ctx->stream;
+        uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
+        auto per_block = [](const DevBuf &b, uint32_t grid) {
+            return (uint32_t)(std::min<uint64_t>(b.cap / 4, 0xffffffffull) / grid);
+        };
+        auto area_lists_sums = [&](hipStream_t st) -> int {
+            const NbLists La{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
+                             per_block(ctx->nb_list, grid_a)};
+            hipLaunchKernelGGL(k_nb_lists<false>, dim3(grid_a), dim3(kNbT), 0, st, gn, r2n, bscale,
+                               (const double *)nullptr, (const uint32_t *)nullptr, La);
+            PCP_CHECK_LAUNCH(ctx);
+            hipLaunchKernelGGL(k_nb_sums<false>,
+                               dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB), dim3(kNbT),
+                               0, st, gn, (const uint2 *)La.meta, (const uint32_t *)La.list,
+                               (const uint32_t *)nullptr, (const float4 *)ctx->nb_pts.as<float4>(),
+                               ctx->area_nrm.as<float>(), ctx->nb_pts.as<float4>() + n,
+                               (const uint32_t *)ctl, (uint32_t *)nullptr);
+            PCP_CHECK_LAUNCH(ctx);
+            return PCP_OK;
+        };
+        const NbLists Lc{ctx->nb_list_c.as<uint32_t>(), ctx->nb_meta_c.as<uint2>(), ctl + 1,
+                         ctl + 2, per_block(ctx->nb_list_c, grid_c)};
+        auto cell_lists = [&](hipStream_t st, const NbLists &lc) -> int {
+            if (!total) return PCP_OK;
+            hipLaunchKernelGGL(k_nb_lists<true>, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n, bscale,
+                               (const double *)ctx->cells_xyz.as<double>(), (const uint32_t *)n_d,
+                               lc);
+            PCP_CHECK_LAUNCH(ctx);
+            return PCP_OK;
+        };
+        // (launched for an empty lattice too: it lands both lists' uses and the overflow)
+        auto cell_sums = [&](const NbLists &lc) -> int {
+            constexpr int QB = NbCfg<true>::QB;
+            hipLaunchKernelGGL(k_nb_sums<true>,
+                               dim3((unsigned)std::max<uint64_t>(
+                                   1, std::min<uint64_t>((total + QB - 1) / QB, 4096))),
+                               dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)lc.meta,
+                               (const uint32_t *)lc.list, (const uint32_t *)n_d,
+                               (const float4 *)(ctx->nb_pts.as<float4>() + n),
+                               ctx->cells_nrm.as<float>(), (float4 *)nullptr,
+                               (const uint32_t *)ctl, n_h + 1);
+            PCP_CHECK_LAUNCH(ctx);
+            return PCP_OK;
+        };
+        // the control words are zero: cleared by the previous call's last k_nb_sums<true> (or,
+        // on a fresh buffer, by this memset)
+        if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctl, 0, 16, ctx->stream));
+        // first: the input points by input index for the sums' gathers, and the non-finite
+        // points' NaN normals (k_area_prep is the raw records' last reader; the exact kernels
+        // never write those entries, so a rerun keeps them)
+        hipLaunchKernelGGL(k_area_prep, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0,
+                           ctx->stream, rin, ctx->nb_pts.as<float4>(), ctx->area_nrm.as<float>());
+        PCP_CHECK_LAUNCH(ctx);
+        pin_release(ctx, ctx->stream);
+        if (side != ctx->stream) {
+            PCP_HIP(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
+            PCP_HIP(ctx, hipStreamWaitEvent(side, ctx->side_ev[0], 0));
+        }
+        if (int rcl = lattice(side)) return rcl;
+        if (int rcc = cell_lists(side, Lc)) return rcc;
+        if (side != ctx->stream) PCP_HIP(ctx, hipEventRecord(ctx->side_ev[1], side));
+        if (int rca = area_lists_sums(ctx->stream)) return rca;
+        if (side != ctx->stream) PCP_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[1], 0));
+        if (int rcs = cell_sums(Lc)) return rcs;
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (n_h[3]) {
+            // a list buffer too small (first frames, or a denser area): regrow both to their
+            // largest block's use x the grid and run the lists and sums again on one stream (the
+            // lattice and the records stand)
+            ctx->nb_need = std::max<uint64_t>(ctx->nb_need, (uint64_t)n_h[1] * grid_a);
+            ctx->nb_need_c = std::max<uint64_t>(ctx->nb_need_c, (uint64_t)n_h[2] * grid_c);
+            if (std::max(ctx->nb_need, ctx->nb_need_c) > 0xffffffffull)
+                return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: %llu neighbour "
+                               "list words (32-bit list offsets)",
+                               (unsigned long long)std::max(ctx->nb_need, ctx->nb_need_c));
+            PCP_HIP(ctx, ctx->nb_list.ensure(ctx->nb_need * 4 + 64));
+            PCP_HIP(ctx, ctx->nb_list_c.ensure(ctx->nb_need_c * 4 + 64));
+            ctx->normals_regrown++;
+            n_h[1] = n_h[2] = n_h[3] = 0;   // (the control words: cleared by k_nb_sums<true>)
+            const NbLists Lc2{ctx->nb_list_c.as<uint32_t>(), ctx->nb_meta_c.as<uint2>(), ctl + 1,
+                              ctl + 2, per_block(ctx->nb_list_c, grid_c)};
+            if (int rc2 = area_lists_sums(ctx->stream)) return rc2;
+            if (int rc3 = cell_lists(ctx->stream, Lc2)) return rc3;
+            if (int rc4 = cell_sums(Lc2)) return rc4;
+            PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            if (n_h[3])
+                return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: neighbour lists "
+                                                       "overflowed after regrowing");
+        }
+        ctx->nb_need = std::max<uint64_t>(ctx->nb_need, (uint64_t)n_h[1] * grid_a);
+        ctx->nb_need_c = std::max<uint64_t>(ctx->nb_need_c, (uint64_t)n_h[2] * grid_c);
+        ctx->nb_ctl_zero = true;   // k_nb_sums<true> (always launched on this path) cleared them
     }
     const uint32_t nc = *n_h;
     ctx->n_cells = nc;

@@ -244,7 +244,13 @@ struct pcp_ctx {
     // order-free fixed-point kernels, A/B only): sorted neighbour lists, their per-query
     // {base, count}, cursors + overflow word; list entries the last call needed
     bool normals_exact = true;
+    bool score_wide = true;
+    bool normals_overlap = false;   // PCP_NORMALS_OVERLAP=1: cells' lists on a side stream (A/B)   // k_score_cells_wide for few-ray launches (PCP_SCORE_WIDE=0: A/B)
     pcp::DevBuf nb_list, nb_meta, nb_ctl, nb_pts;   // nb_pts: input points by index
+    pcp::DevBuf nb_list_c, nb_meta_c;                // the cells' lists
+    uint64_t nb_need_c = 0;
+    hipStream_t side_stream = nullptr;               // (the cells' lists beside the area's)
+    hipEvent_t side_ev[2] = {};
     bool nb_ctl_zero = false;                // nb_ctl's cursors known zero (cleared by the last call)
     uint64_t nb_need = 0;
     uint64_t normals_regrown = 0;

@@ -249,22 +249,27 @@ __device__ __forceinline__ void clip_kf(const GridView &g, double px, double py,
 //    approximate corner's window holds every point within r of q_k (the same margin argument as
 //    the block's), so no exact corner and no directory load are needed.  FN = 2 decides at run
 //    time (g.frec null or not).
+//  * koff, kstr: a lane of a group of kstr lanes marching one ray takes the samples
+//    k = klo + koff (mod kstr) (NB-sample rounds: the rounds koff (mod kstr)); the ray is blocked
+//    iff some lane finds a blocked sample -- the group's answer to "march < 0" is the same
 template <bool STATS, bool ZB = true, int NB = 1, int FN = 0>
 __device__ __forceinline__ int march(const GridView &g, double px, double py, double pz,
                                      double dx, double dy, double dz,
                                      const double *__restrict__ steps, int K, double end,
-                                     float r2, float rexit, uint32_t *cnt = nullptr) {
+                                     float r2, float rexit, uint32_t *cnt = nullptr,
+                                     int koff = 0, int kstr = 1) {
     if (FN == 2) {
         if (g.frec && g.ftile == 2)
             return march<STATS, ZB, NB, 8>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, rexit,
-                                           cnt);
+                                           cnt, koff, kstr);
         if (g.frec && g.ftile)
             return march<STATS, ZB, NB, 4>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, rexit,
-                                           cnt);
+                                           cnt, koff, kstr);
         if (g.frec)
             return march<STATS, ZB, NB, 1>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, rexit,
-                                           cnt);
-        return march<STATS, ZB, NB, 0>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, rexit, cnt);
+                                           cnt, koff, kstr);
+        return march<STATS, ZB, NB, 0>(g, px, py, pz, dx, dy, dz, steps, K, end, r2, rexit, cnt,
+                                       koff, kstr);
     }
     int klo, khi;
     clip_kf(g, px, py, pz, dx, dy, dz, K, klo, khi);
@@ -291,7 +296,7 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
         const uint32_t mx = g.frx - 1, my = g.fry - 1, mz = g.frz - 1;
         const uint32_t rx = FN == 4 ? (g.frx + 3) >> 2 : FN == 8 ? (g.frx + 7) >> 3 : g.frx;
         const uint32_t ry = FN == 4 ? (g.fry + 3) >> 2 : FN == 8 ? (g.fry + 7) >> 3 : g.fry;
-        for (int k = klo; k <= khi; ++k) {
+        for (int k = klo + koff; k <= khi; k += kstr) {
             const float kf = (float)k;
             const float fx = __builtin_fmaf(D2x, kf, A2x);
             const float fy = __builtin_fmaf(D2y, kf, A2y);
@@ -357,7 +362,7 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
     if (NB > 1 && ZB) {
         // latency-bound callers (few rays in flight): NB probes per round as independent loads,
         // then taken in sample order -- the same samples, candidates and scans as below
-        for (int k0 = klo; k0 <= khi; k0 += NB) {
+        for (int k0 = klo + NB * koff; k0 <= khi; k0 += NB * kstr) {
             uint32_t zz[NB], izs[NB];
             float fzs[NB];
 #pragma unroll
@@ -397,7 +402,7 @@ __device__ __forceinline__ int march(const GridView &g, double px, double py, do
         }
         return -1;
     }
-    for (int k = klo; k <= khi; ++k) {
+    for (int k = klo + koff; k <= khi; k += kstr) {
         const float kf = (float)k;
         const float fx = __builtin_fmaf(Dx, kf, Ax);
         const float fy = __builtin_fmaf(Dy, kf, Ay);
@@ -449,6 +454,9 @@ struct VisEnv {
 };
 
 // result bits: 1 = in_range, 2 = in_fov (valid if in_range), 4 = visible (valid if both)
+// G > 1: the G lanes of an aligned lane group evaluate the same (pose, cell), each marching the
+// samples koff (mod G) (march's koff / kstr); every lane returns the same result
+template <int G = 1>
 __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double py, double pz,
                                             double pitch, double cx, double cy, double cz,
                                             float nx, float ny, float nz, bool is_zx120,
@@ -487,9 +495,16 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
         visible = march<false, true, PCP_CELL_PROBES>(E.terrain, px, py, pz, ndx, ndy, ndz,
                                                       steps, E.K, end, 1e30f, 1e15f) < 0;
 #else
-        visible = march<false, true, PCP_CELL_PROBES, 2>(E.terrain, px, py, pz, ndx, ndy, ndz,
-                                                         steps, E.K, end, E.r2_ray,
-                                                         E.rexit_ray) < 0;
+        const int lane = threadIdx.x & 63;
+        const bool clear = march<false, true, PCP_CELL_PROBES, 2>(
+                               E.terrain, px, py, pz, ndx, ndy, ndz, steps, E.K, end, E.r2_ray,
+                               E.rexit_ray, nullptr, G > 1 ? lane % G : 0, G) < 0;
+        if (G > 1) {   // the group's lanes all reach here (same inputs, same branches)
+            const uint64_t blocked = __ballot(!clear);
+            visible = ((blocked >> (lane & ~(G - 1))) & ((1ull << G) - 1)) == 0;
+        } else {
+            visible = clear;
+        }
 #endif
     }
     if (!visible) return 0.0;
@@ -544,6 +559,48 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
         mbits[(size_t)p * C + c] = (uint8_t)bits;
     }
 }
+
+// The same rows with G lanes per (cell, row): for launches with few rays (one candidate pose,
+// C1 / C5), where one lane per ray leaves the GPU nearly empty and each ray's march is a long
+// chain of dependent probes.  The G lanes split the ray's samples (march koff / kstr) and AND
+// their verdicts; lane 0 of the group writes.
+template <bool SL, int G>
+__global__ void __launch_bounds__(kT)
+k_score_cells_wide(VisEnv E, const double *__restrict__ cxyz, const float *__restrict__ cn,
+                   int C, const double *__restrict__ poses5, int P,
+                   const double *__restrict__ zx5, double *__restrict__ sm_out,
+                   uint8_t *__restrict__ mbits, double *__restrict__ score_z,
+                   uint8_t *__restrict__ zbits, int32_t *__restrict__ stats,
+                   const uint32_t *__restrict__ P_dev) {
+    static_assert(G > 1 && G <= 64 && (G & (G - 1)) == 0, "lane groups within a wave");
+    const int c = (int)((blockIdx.x * kT + threadIdx.x) / G);
+    if (stats && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) stats[threadIdx.x] = 0;
+    __shared__ double s_steps[SL ? kStepLds : 1];
+    if (SL) {
+        for (int q = threadIdx.x; q < E.K; q += kT) s_steps[q] = E.steps[q];
+        __syncthreads();
+    }
+    const double *steps = SL ? s_steps : E.steps;
+    if (c >= C) return;   // (whole groups: C * G threads, groups aligned)
+    const int p = blockIdx.y;
+    const bool zrow = p == P;
+    if (P_dev && !zrow && p >= (int)*P_dev) return;
+    const double *Q = zrow ? zx5 : poses5 + 5 * (size_t)p;
+    uint32_t bits;
+    const double s = eval_cell<G>(E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1],
+                                  cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], zrow,
+                                  bits, steps);
+    if ((threadIdx.x & (G - 1)) != 0) return;
+    if (zrow) {
+        score_z[c] = s;
+        zbits[c] = (uint8_t)bits;
+    } else {
+        sm_out[(size_t)p * C + c] = s;
+        mbits[(size_t)p * C + c] = (uint8_t)bits;
+    }
+}
+constexpr int kWideG = 16;               // lanes per ray of k_score_cells_wide
+constexpr int kWideMaxRays = 1 << 15;    // (rows x cells) up to which the wide kernel runs
 
 // ordered sequential sum per row (evaluatePosition :634-645): total_score += s for s > 0 in cell
 // order, s = std::max(score_zx120, score_mobile) = (sz < sm) ? sm : sz for a pose row, sz for
@@ -1615,7 +1672,20 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
         {
             ProfScope ps(ctx, PCP_K_SCORE_CELLS);
             const dim3 g(cb, (unsigned)(P + 1));
-            if (E.K <= kStepLds)
+            const bool wide = (uint64_t)(P + 1) * (uint64_t)C <= (uint64_t)kWideMaxRays &&
+                              ctx->score_wide;
+            const dim3 gw((unsigned)(((uint64_t)C * kWideG + kT - 1) / kT), (unsigned)(P + 1));
+            if (wide && E.K <= kStepLds)
+                hipLaunchKernelGGL((k_score_cells_wide<true, kWideG>), gw, dim3(kT), 0, st, E,
+                                   ctx->cells_xyz.as<const double>(),
+                                   ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
+                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev);
+            else if (wide)
+                hipLaunchKernelGGL((k_score_cells_wide<false, kWideG>), gw, dim3(kT), 0, st, E,
+                                   ctx->cells_xyz.as<const double>(),
+                                   ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
+                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev);
+            else if (E.K <= kStepLds)
                 hipLaunchKernelGGL(k_score_cells<true>, g, dim3(kT), 0, st, E,
                                    ctx->cells_xyz.as<const double>(),
                                    ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,

@@ -883,6 +883,33 @@ def test_score_poses_matches_reference_loop(gpu, oracle, loaded, scene, cells):
     assert rep2.best_idx == r_rep2.best_idx
 
 
+@pytest.mark.parametrize("wide", ["1", "0"])
+@pytest.mark.parametrize("npose", [1, 3])
+def test_score_few_poses_wide_lanes(oracle, scene, cells, aux, wide, npose, monkeypatch):
+    """Few rays (C1 / C5 score one candidate): k_score_cells_wide splits each ray's samples
+    over 16 lanes and ANDs their verdicts.  Same flags, coverage, totals and best pose as the
+    reference loop, with the wide kernel on (default) and off (PCP_SCORE_WIDE=0)."""
+    monkeypatch.setenv("PCP_SCORE_WIDE", wide)
+    params = _abi.default_vl_params()
+    T, A = oracle.Cloud(scene.terrain), oracle.Cloud(aux)
+    with _abi.Context(0) as ctx:
+        ctx.set_terrain(scene.terrain, point_step=32)
+        ctx.set_aux_cloud(aux, point_step=32)
+        ctx.set_cells(cells.xyz, cells.normals)
+        poses = ctx.generate_candidates(cells.grid_bbox, params, scene.zx120_pose5)[:npose]
+        assert (npose + 1) * cells.xyz.shape[0] <= 1 << 15   # the wide kernel's range
+        fg = np.zeros(cells.xyz.shape[0], np.uint8)
+        fr = fg.copy()
+        tot, cov, rep = ctx.score_poses(poses, scene.zx120_pose5, params, fg)
+        r_tot, r_cov, r_rep = oracle.score_poses(T, A, cells.xyz, cells.normals, poses,
+                                                 scene.zx120_pose5, oracle.vl_params(), fr)
+        np.testing.assert_array_equal(fg, fr)
+        np.testing.assert_array_equal(cov, r_cov)
+        assert _rel_close(tot, r_tot), np.max(np.abs(tot - r_tot))
+        assert rep.best_idx == r_rep.best_idx
+        assert rep.as_dict()["total_cells"] == r_rep.as_dict()["total_cells"]
+
+
 def test_generate_and_score_matches_two_calls(gpu, loaded, scene, cells):
     """pcp_generate_and_score (one round trip: the scoring reads the candidates and their count
     where the generation left them) against pcp_generate_candidates + pcp_score_poses on the
