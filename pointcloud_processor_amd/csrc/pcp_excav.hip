@@ -289,7 +289,7 @@ constexpr int kNbBuckets = 2048;
 constexpr int kNbLds = 4096;   // keys sorted in LDS (32 KB); longer lists sort in global memory
 constexpr int kNbT = 256;
 constexpr int kNbBlocks = 2048;        // k_nb_lists grid (blocks loop over the queries)
-constexpr int kNbU = 8;                // k_nb_lists candidates in flight per thread
+constexpr int kNbU = 4;                // k_nb_lists candidates in flight per thread
 
 __device__ __forceinline__ uint32_t nb_wave_incl_scan(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
@@ -366,7 +366,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
            const uint32_t *__restrict__ n_dev, NbLists L) {
     __shared__ uint32_t cnt[kNbBuckets];
     __shared__ unsigned long long key[kNbLds];   // appended keys
-    __shared__ unsigned long long grp[kNbLds];   // the keys grouped by bucket
+    __shared__ uint16_t grp[kNbLds];             // the keys' indices grouped by bucket
     __shared__ uint32_t wsum[kNbT / 64];
     __shared__ uint32_t sh_base, sh_ok, sh_pos, sh_m;
     const uint32_t nq = CELLS ? *n_dev : g.n_pts;
@@ -390,48 +390,48 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
         nb_lds_barrier();
         uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
         stencil_ranges(g, qx, qy, qz, lo, hi);   // (false: empty ranges)
-        // the one pass over the stencil's four row ranges as one flat index space (no partial
-        // round per range), kNbU candidates in flight per thread -- the pass is bound by the
-        // load latency of its rounds -- and one LDS append per wave and round
-        const uint32_t c1 = hi[0] - lo[0], c2 = c1 + (hi[1] - lo[1]), c3 = c2 + (hi[2] - lo[2]);
-        const uint32_t ntot = c3 + (hi[3] - lo[3]);
-        auto cand = [&](uint32_t f) {
-            return f < c1 ? lo[0] + f : f < c2 ? lo[1] + (f - c1) : f < c3 ? lo[2] + (f - c2)
-                                                                           : lo[3] + (f - c3);
-        };
-        for (uint32_t f0 = threadIdx.x; f0 < ntot; f0 += kNbU * kNbT) {
-            float4 p[kNbU];
+        // the one pass over the stencil's four row ranges, kNbU candidates in flight per thread,
+        // one LDS append per wave and round.  (The ranges as one flat index space with 8 in
+        // flight measured slower: 66 vs 45 us per C1 frame -- the range selects cost more VALU
+        // than the partial rounds cost latency)
 #pragma unroll
-            for (int u = 0; u < kNbU; ++u) p[u] = g.pts[cand(min(f0 + (uint32_t)u * kNbT, ntot - 1))];
-            bool in[kNbU];
-            float dd[kNbU];
-            uint64_t bal[kNbU];
-            uint32_t tot = 0;
-#pragma unroll
-            for (int u = 0; u < kNbU; ++u) {
-                dd[u] = flann_d2(qx, qy, qz, p[u]);
-                in[u] = f0 + (uint32_t)u * kNbT < ntot && dd[u] < r2;
-                if (in[u]) atomicAdd(&cnt[bucket_of(dd[u])], 1u);
-                bal[u] = __ballot(in[u]);
-                tot += (uint32_t)__popcll(bal[u]);
-            }
-            if (tot) {   // (uniform)
-                const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(&sh_m, tot);
-                base = (uint32_t)__shfl((int)base, leader);
+        for (int r = 0; r < 4; ++r)
+            for (uint32_t k0 = lo[r] + threadIdx.x; k0 < hi[r]; k0 += kNbU * kNbT) {
+                float4 p[kNbU];
 #pragma unroll
                 for (int u = 0; u < kNbU; ++u) {
-                    const uint32_t pos =
-                        base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[u] >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
-                    if (in[u] && pos < (uint32_t)kNbLds)
-                        key[pos] = ((unsigned long long)__float_as_uint(dd[u]) << 32) |
-                                   __float_as_uint(p[u].w);
-                    base += (uint32_t)__popcll(bal[u]);
+                    const uint32_t k = k0 + (uint32_t)u * kNbT;
+                    p[u] = g.pts[k < hi[r] ? k : hi[r] - 1];
+                }
+                bool in[kNbU];
+                float dd[kNbU];
+                uint64_t bal[kNbU];
+                uint32_t tot = 0;
+#pragma unroll
+                for (int u = 0; u < kNbU; ++u) {
+                    dd[u] = flann_d2(qx, qy, qz, p[u]);
+                    in[u] = k0 + (uint32_t)u * kNbT < hi[r] && dd[u] < r2;
+                    if (in[u]) atomicAdd(&cnt[bucket_of(dd[u])], 1u);
+                    bal[u] = __ballot(in[u]);
+                    tot += (uint32_t)__popcll(bal[u]);
+                }
+                if (tot) {   // (uniform)
+                    const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+                    uint32_t base = 0;
+                    if (lane == leader) base = atomicAdd(&sh_m, tot);
+                    base = (uint32_t)__shfl((int)base, leader);
+#pragma unroll
+                    for (int u = 0; u < kNbU; ++u) {
+                        const uint32_t pos =
+                            base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[u] >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
+                        if (in[u] && pos < (uint32_t)kNbLds)
+                            key[pos] = ((unsigned long long)__float_as_uint(dd[u]) << 32) |
+                                       __float_as_uint(p[u].w);
+                        base += (uint32_t)__popcll(bal[u]);
+                    }
                 }
             }
-        }
         nb_lds_barrier();
         // exclusive scan of the buckets: thread t owns buckets [8 t, 8 t + 8)
         constexpr int kPer = kNbBuckets / kNbT;
@@ -475,30 +475,54 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
         if (sh_ok && m) {
             uint32_t *out = L.list + base;
             if (!big) {
-                // group the appended keys by bucket (cnt[b] becomes the bucket's end)
-                for (uint32_t i = threadIdx.x; i < m; i += kNbT) {
-                    const unsigned long long ki = key[i];
-                    grp[atomicAdd(&cnt[bucket_of(__uint_as_float((uint32_t)(ki >> 32)))], 1u)] = ki;
+                // group the appended keys by bucket (cnt[b] becomes the bucket's end).  Four keys
+                // per thread at a time: the loops are chains of LDS round trips, and few waves
+                // share a CU (48 KB of LDS per block)
+                constexpr int G4 = 4;
+                for (uint32_t i0 = threadIdx.x; i0 < m; i0 += G4 * kNbT) {
+                    uint32_t bk[G4];
+#pragma unroll
+                    for (int u = 0; u < G4; ++u) {
+                        const uint32_t i = min(i0 + (uint32_t)u * kNbT, m - 1);
+                        bk[u] = bucket_of(__uint_as_float((uint32_t)(key[i] >> 32)));
+                    }
+                    uint32_t pos[G4];
+#pragma unroll
+                    for (int u = 0; u < G4; ++u)
+                        if (i0 + (uint32_t)u * kNbT < m) pos[u] = atomicAdd(&cnt[bk[u]], 1u);
+#pragma unroll
+                    for (int u = 0; u < G4; ++u)
+                        if (i0 + (uint32_t)u * kNbT < m) grp[pos[u]] = (uint16_t)(i0 + (uint32_t)u * kNbT);
                 }
                 nb_lds_barrier();
                 // each key's place = its bucket's start + its rank among the bucket's keys (the
-                // keys are distinct: distinct indices).  Lanes take consecutive grouped keys: a
-                // wave mostly reads one bucket's keys (broadcast LDS reads); the bucket holds the
-                // distance's exact ties, a handful on a lattice
-                for (uint32_t i = threadIdx.x; i < m; i += kNbT) {
-                    const unsigned long long ki = grp[i];
-                    const uint32_t b = bucket_of(__uint_as_float((uint32_t)(ki >> 32)));
-                    const uint32_t s0 = b ? cnt[b - 1] : 0u, e = cnt[b];
-                    // four independent reads per round (a loop of single reads waits on each)
-                    uint32_t rank = 0, j = s0;
-                    for (; j + 4 <= e; j += 4) {
-                        const unsigned long long a0 = grp[j], a1 = grp[j + 1], a2 = grp[j + 2],
-                                                 a3 = grp[j + 3];
-                        rank += (uint32_t)(a0 < ki) + (uint32_t)(a1 < ki) + (uint32_t)(a2 < ki) +
-                                (uint32_t)(a3 < ki);
+                // keys are distinct: distinct indices; a bucket holds a distance's exact ties, 2.4
+                // keys on average in C1).  Four grouped positions per thread, in lockstep
+                for (uint32_t i0 = threadIdx.x; i0 < m; i0 += G4 * kNbT) {
+                    unsigned long long kv[G4];
+                    uint32_t s0[G4], len[G4], rank[G4], lmax = 0;
+#pragma unroll
+                    for (int u = 0; u < G4; ++u) kv[u] = key[grp[min(i0 + (uint32_t)u * kNbT, m - 1)]];
+#pragma unroll
+                    for (int u = 0; u < G4; ++u) {
+                        const uint32_t b = bucket_of(__uint_as_float((uint32_t)(kv[u] >> 32)));
+                        s0[u] = b ? cnt[b - 1] : 0u;
+                        len[u] = i0 + (uint32_t)u * kNbT < m ? cnt[b] - s0[u] : 0u;
+                        rank[u] = 0;
                     }
-                    for (; j < e; ++j) rank += grp[j] < ki;
-                    out[s0 + rank] = (uint32_t)ki;
+#pragma unroll
+                    for (int u = 0; u < G4; ++u) lmax = max(lmax, len[u]);
+                    for (uint32_t jj = 0; jj < lmax; ++jj) {
+                        unsigned long long o[G4];
+#pragma unroll
+                        for (int u = 0; u < G4; ++u)
+                            o[u] = key[grp[jj < len[u] ? s0[u] + jj : s0[u]]];
+#pragma unroll
+                        for (int u = 0; u < G4; ++u) rank[u] += (jj < len[u]) & (o[u] < kv[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < G4; ++u)
+                        if (i0 + (uint32_t)u * kNbT < m) out[s0[u] + rank[u]] = (uint32_t)kv[u];
                 }
             } else {
                 unsigned long long *K =
