@@ -459,6 +459,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *ne = std::getenv("PCP_NORMALS_EXACT")) ctx->normals_exact = std::atoi(ne) != 0;
     if (const char *sw = std::getenv("PCP_SCORE_WIDE")) ctx->score_wide = std::atoi(sw) != 0;
     if (const char *no = std::getenv("PCP_NORMALS_OVERLAP")) ctx->normals_overlap = std::atoi(no) != 0;
+    if (const char *nbk = std::getenv("PCP_NB_BLOCKS")) ctx->nb_blocks = std::atoi(nbk);
     if (const char *ct = std::getenv("PCP_COPY_THREADS")) ctx->copy_threads = std::atoi(ct);
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
     if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff);

@@ -289,7 +289,7 @@ constexpr int kNbBuckets = 2048;
 constexpr int kNbLds = 4096;   // keys sorted in LDS (32 KB); longer lists sort in global memory
 constexpr int kNbT = 256;
 constexpr int kNbBlocks = 2048;        // k_nb_lists grid (blocks loop over the queries)
-constexpr int kNbU = 4;                // k_nb_lists candidates in flight per thread
+constexpr int kNbU = 8;                // k_nb_lists candidates in flight per thread
 
 __device__ __forceinline__ uint32_t nb_wave_incl_scan(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
@@ -1072,13 +1072,15 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         // The sorted neighbour lists: the area's (nb_list / nb_meta) and the cells' (nb_list_c /
         // nb_meta_c), one region per k_nb_lists block, words as the previous call needed (first
         // guess n x min(n, 4096)), regrown on overflow to the largest block's use x the grid.
-        // Two streams: the cells' lists need the lattice and the area index, not the area
-        // normals, so the lattice and k_nb_lists<true> run on the side stream beside the area's
-        // lists and sums; k_nb_sums<true> joins them.  Every buffer is sized before the launches.
+        // The cells' lists need the lattice and the area index, not the area normals: with
+        // PCP_NORMALS_OVERLAP=1 the lattice and k_nb_lists<true> run on a side stream beside the
+        // area's lists and sums, k_nb_sums<true> joining them (measured slower: one stream by
+        // default).  Every buffer is sized before the launches.
         const float bscale = (float)kNbBuckets / r2n;
-        const uint32_t grid_a = std::min<uint32_t>(npts, kNbBlocks);
+        const uint32_t nbb = ctx->nb_blocks > 0 ? (uint32_t)ctx->nb_blocks : (uint32_t)kNbBlocks;
+        const uint32_t grid_a = std::min<uint32_t>(npts, nbb);
         const uint32_t grid_c =
-            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(total, kNbBlocks));
+            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(total, nbb));
         const uint64_t per_pt = std::min<uint64_t>(npts, 4096);
         const uint64_t guess_a = std::min<uint64_t>((uint64_t)npts * per_pt, 64ull << 20);
         const uint64_t guess_c = std::min<uint64_t>(std::max<uint64_t>(total, 1) * per_pt, 64ull << 20);

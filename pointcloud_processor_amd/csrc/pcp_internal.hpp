@@ -245,7 +245,8 @@ struct pcp_ctx {
     // {base, count}, cursors + overflow word; list entries the last call needed
     bool normals_exact = true;
     bool score_wide = true;
-    bool normals_overlap = false;   // PCP_NORMALS_OVERLAP=1: cells' lists on a side stream (A/B)   // k_score_cells_wide for few-ray launches (PCP_SCORE_WIDE=0: A/B)
+    bool normals_overlap = false;
+    int nb_blocks = 0;              // PCP_NB_BLOCKS: k_nb_lists grid (A/B; 0 = kNbBlocks)   // PCP_NORMALS_OVERLAP=1: cells' lists on a side stream (A/B)   // k_score_cells_wide for few-ray launches (PCP_SCORE_WIDE=0: A/B)
     pcp::DevBuf nb_list, nb_meta, nb_ctl, nb_pts;   // nb_pts: input points by index
     pcp::DevBuf nb_list_c, nb_meta_c;                // the cells' lists
     uint64_t nb_need_c = 0;
