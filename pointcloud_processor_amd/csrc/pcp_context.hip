@@ -458,7 +458,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *ho = std::getenv("PCP_FAN_HOST_OUT")) ctx->fan_host_out = std::atoi(ho) != 0;
     if (const char *ne = std::getenv("PCP_NORMALS_EXACT")) ctx->normals_exact = std::atoi(ne) != 0;
     if (const char *sw = std::getenv("PCP_SCORE_WIDE")) ctx->score_wide = std::atoi(sw) != 0;
-    if (const char *no = std::getenv("PCP_NORMALS_OVERLAP")) ctx->normals_overlap = std::atoi(no) != 0;
+    if (const char *co = std::getenv("PCP_CELLS_ORDER_FREE")) ctx->cells_all_ordered = std::atoi(co) == 0;
     if (const char *nbk = std::getenv("PCP_NB_BLOCKS")) ctx->nb_blocks = std::atoi(nbk);
     if (const char *ct = std::getenv("PCP_COPY_THREADS")) ctx->copy_threads = std::atoi(ct);
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
@@ -511,9 +511,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->nb_pts.release();
     ctx->nb_list_c.release();
     ctx->nb_meta_c.release();
-    for (auto &e : ctx->side_ev)
-        if (e) (void)hipEventDestroy(e);
-    if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
+    ctx->nb_sel.release();
     ctx->carve.release();
     ctx->carve_buf.release();
     ctx->cell_cnt.release();

@@ -363,22 +363,25 @@ __device__ __forceinline__ void nb_lds_barrier() {
 template <bool CELLS>
 __global__ void __launch_bounds__(kNbT)
 k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
-           const uint32_t *__restrict__ n_dev, NbLists L) {
+           const uint32_t *__restrict__ n_dev, NbLists L, const uint32_t *__restrict__ sel) {
     __shared__ uint32_t cnt[kNbBuckets];
     __shared__ unsigned long long key[kNbLds];   // appended keys
     __shared__ uint16_t grp[kNbLds];             // the keys' indices grouped by bucket
     __shared__ uint32_t wsum[kNbT / 64];
     __shared__ uint32_t sh_base, sh_ok, sh_pos, sh_m;
-    const uint32_t nq = CELLS ? *n_dev : g.n_pts;
+    // CELLS with sel: only the cells sel[1 ..= sel[0]] (those k_cell_sums_exact left to the
+    // ordered path), their lists at the compact positions
+    const uint32_t nq = CELLS ? (sel ? *sel : *n_dev) : g.n_pts;
     if (threadIdx.x == 0) sh_pos = 0;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     auto bucket_of = [&](float d) { return min((uint32_t)(d * bscale), kNbBuckets - 1u); };
     for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
         float qx, qy, qz;
         if (CELLS) {
-            qx = (float)cells[3 * (size_t)qi];
-            qy = (float)cells[3 * (size_t)qi + 1];
-            qz = (float)cells[3 * (size_t)qi + 2];
+            const uint32_t ci = sel ? sel[1 + qi] : qi;
+            qx = (float)cells[3 * (size_t)ci];
+            qy = (float)cells[3 * (size_t)ci + 1];
+            qz = (float)cells[3 * (size_t)ci + 2];
         } else {
             const float4 q = g.pts[qi];
             qx = q.x;
@@ -549,6 +552,23 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
     if (threadIdx.x == 0 && sh_pos) atomicMax(L.need, sh_pos);   // (no return value awaited)
 }
 
+// computeCellSurfaceNormal's tail (:301-340): the normalised sum of the finite neighbours'
+// normals, GridCell's default (0, 0, 1) without any or below 1e-6
+__device__ __forceinline__ void cell_normal_out(float *o, double sx, double sy, double sz,
+                                                uint32_t nvalid) {
+    o[0] = 0.0f;
+    o[1] = 0.0f;
+    o[2] = 1.0f;
+    if (nvalid != 0) {
+        const double norm = sqrt(sx * sx + sy * sy + sz * sz);
+        if (norm > 1e-6) {
+            o[0] = (float)(sx / norm);
+            o[1] = (float)(sy / norm);
+            o[2] = (float)(sz / norm);
+        }
+    }
+}
+
 // sequential sums over the sorted lists.  CELLS false: the 9 float moments of
 // computeMeanAndCovarianceMatrix (shifted by K = the first listed point: xx xy xz yy yz zz x y
 // z), then the covariance and the normal; CELLS true: the 3 double sums of the finite
@@ -580,7 +600,7 @@ __global__ void __launch_bounds__(kNbT)
 k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict__ list,
           const uint32_t *__restrict__ n_dev, const float4 *__restrict__ recs,
           float *__restrict__ out, float4 *__restrict__ out4, const uint32_t *__restrict__ ctl,
-          uint32_t *__restrict__ ctl_host) {
+          uint32_t *__restrict__ ctl_host, const uint32_t *__restrict__ sel) {
     // the lists' largest block uses and overflow word (final: every k_nb_lists ran before this launch)
     // to the caller's pinned landing, one plain store each, then cleared for the next call (no
     // memset launch in front of its k_nb_lists)
@@ -602,7 +622,7 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
     __shared__ float4 qk[QB];          // K (area) per query
     __shared__ uint32_t valid[QB];     // finite neighbour normals (cells)
     __shared__ T accs[QB][NT];
-    const uint32_t nq = CELLS ? *n_dev : g.n_pts;
+    const uint32_t nq = CELLS ? (sel ? *sel : *n_dev) : g.n_pts;   // (sel: as k_nb_lists)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (uint32_t q0 = blockIdx.x * QB; q0 < nq; q0 += gridDim.x * QB) {
         if (threadIdx.x < QB) {
@@ -731,20 +751,8 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
             const uint32_t qi = q0 + q;
             const uint32_t m = qm[q].y;
             if (CELLS) {
-                float *o = out + 3 * (size_t)qi;
-                o[0] = 0.0f;   // GridCell's default surface normal
-                o[1] = 0.0f;
-                o[2] = 1.0f;
-                if (valid[q] != 0) {
-                    const double sx = (double)accs[q][0], sy = (double)accs[q][1],
-                                 sz = (double)accs[q][2 % NT];
-                    const double norm = sqrt(sx * sx + sy * sy + sz * sz);
-                    if (norm > 1e-6) {
-                        o[0] = (float)(sx / norm);
-                        o[1] = (float)(sy / norm);
-                        o[2] = (float)(sz / norm);
-                    }
-                }
+                cell_normal_out(out + 3 * (size_t)(sel ? sel[1 + qi] : qi), (double)accs[q][0],
+                                (double)accs[q][1], (double)accs[q][2 % NT], valid[q]);
             } else {
                 const float4 qp = g.pts[qi];
                 float *o = out + 3 * (size_t)__float_as_uint(qp.w);
@@ -775,10 +783,113 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
     }
 }
 
+// The cells' sums where their order cannot matter.  computeCellSurfaceNormal adds the finite
+// neighbours' float normals as doubles.  Let E_min / E_max be the smallest / largest exponent
+// of their nonzero components and n their count: every component is a multiple of
+// U = 2^(E_min - 23), every partial sum -- of any subset, in any order -- a multiple of U below
+// n 2^(E_max + 1) in magnitude, so when n 2^(E_max + 1) <= 2^53 U, i.e.
+// E_min - E_max >= ceil(log2 n) - 29, every addition is exact and the sum is the same in every
+// order: FLANN's included.  One block per cell sums its stencil's neighbours in any order (no
+// list, no sort) and checks the bound; a cell that fails it (a component below ~2^-17 of the
+// largest, a subnormal) goes to sel for the ordered path (k_nb_lists / k_nb_sums over sel).
+__global__ void __launch_bounds__(kNbT)
+k_cell_sums_exact(GridView g, float r2, const double *__restrict__ cells,
+                  const uint32_t *__restrict__ n_dev, const float4 *__restrict__ nrm4,
+                  float *__restrict__ out, uint32_t *__restrict__ sel, int all_ordered) {
+    __shared__ double rs[3][kNbT / 64];
+    __shared__ uint32_t rc[kNbT / 64], rmin[kNbT / 64], rmax[kNbT / 64];
+    const uint32_t nq = *n_dev;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+        const float qx = (float)cells[3 * (size_t)qi], qy = (float)cells[3 * (size_t)qi + 1],
+                    qz = (float)cells[3 * (size_t)qi + 2];
+        uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
+        stencil_ranges(g, qx, qy, qz, lo, hi);   // (false: empty ranges)
+        double sx = 0.0, sy = 0.0, sz = 0.0;
+        uint32_t cnt = 0, emin = 255, emax = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            for (uint32_t k0 = lo[r] + threadIdx.x; k0 < hi[r]; k0 += kNbU * kNbT) {
+                float4 p[kNbU];
+#pragma unroll
+                for (int u = 0; u < kNbU; ++u) {
+                    const uint32_t k = k0 + (uint32_t)u * kNbT;
+                    p[u] = g.pts[k < hi[r] ? k : hi[r] - 1];
+                }
+                bool in[kNbU];
+                float4 v[kNbU];
+#pragma unroll
+                for (int u = 0; u < kNbU; ++u) {
+                    in[u] = k0 + (uint32_t)u * kNbT < hi[r] && flann_d2(qx, qy, qz, p[u]) < r2;
+                    v[u] = nrm4[in[u] ? __float_as_uint(p[u].w) : 0u];   // (unconditional)
+                }
+#pragma unroll
+                for (int u = 0; u < kNbU; ++u) {
+                    if (!(in[u] && isfinite(v[u].x) && isfinite(v[u].y) && isfinite(v[u].z)))
+                        continue;
+                    sx += (double)v[u].x;
+                    sy += (double)v[u].y;
+                    sz += (double)v[u].z;
+                    ++cnt;
+                    const uint32_t b[3] = {__float_as_uint(v[u].x) & 0x7fffffffu,
+                                           __float_as_uint(v[u].y) & 0x7fffffffu,
+                                           __float_as_uint(v[u].z) & 0x7fffffffu};
+#pragma unroll
+                    for (int a = 0; a < 3; ++a)
+                        if (b[a]) {   // (a subnormal has exponent field 0: emin 0 fails the bound)
+                            emin = min(emin, b[a] >> 23);
+                            emax = max(emax, b[a] >> 23);
+                        }
+                }
+            }
+        // any-order reduction (exact whenever the bound holds; discarded otherwise)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            sx += __shfl_xor(sx, o);
+            sy += __shfl_xor(sy, o);
+            sz += __shfl_xor(sz, o);
+            cnt += (uint32_t)__shfl_xor((int)cnt, o);
+            emin = min(emin, (uint32_t)__shfl_xor((int)emin, o));
+            emax = max(emax, (uint32_t)__shfl_xor((int)emax, o));
+        }
+        if (lane == 0) {
+            rs[0][wid] = sx;
+            rs[1][wid] = sy;
+            rs[2][wid] = sz;
+            rc[wid] = cnt;
+            rmin[wid] = emin;
+            rmax[wid] = emax;
+        }
+        nb_lds_barrier();
+        if (threadIdx.x == 0) {
+            double tx = 0.0, ty = 0.0, tz = 0.0;
+            uint32_t n = 0, e0 = 255, e1 = 0;
+            for (int w = 0; w < kNbT / 64; ++w) {
+                tx += rs[0][w];
+                ty += rs[1][w];
+                tz += rs[2][w];
+                n += rc[w];
+                e0 = min(e0, rmin[w]);
+                e1 = max(e1, rmax[w]);
+            }
+            const int lg = n <= 1 ? 0 : 32 - __clz((int)(n - 1));   // ceil(log2 n)
+            const bool exact = n == 0 || (e0 > 0 && (e0 == 255 || (int)e0 - (int)e1 >= lg - 29));
+            if (exact && !all_ordered) {   // (all_ordered: PCP_CELLS_ORDER_FREE=0, A/B)
+                cell_normal_out(out + 3 * (size_t)qi, tx, ty, tz, n);
+            } else {   // sel[0]: the count (zeroed by k_area_prep), sel[1 + i]: the cells
+                const uint32_t pos = atomicAdd(&sel[0], 1u);
+                sel[1 + pos] = qi;
+            }
+        }
+        nb_lds_barrier();   // (the LDS is reused by the next cell)
+    }
+}
+
 // the raw input's points by input index (the sums gather them by the lists' indices) and the
 // non-finite points' NaN normals (they are in no list), one thread per input point
 __global__ void __launch_bounds__(kXT) k_area_prep(RawIn in, float4 *__restrict__ pts_in,
-                                                   float *__restrict__ out) {
+                                                   float *__restrict__ out, uint32_t *sel) {
+    if (sel && blockIdx.x == 0 && threadIdx.x == 0) sel[0] = 0;   // (k_cell_sums_exact's count)
     const uint64_t i = (uint64_t)blockIdx.x * kXT + threadIdx.x;
     if (i >= in.n) return;
     const unsigned char *p = in.raw + i * in.step;
@@ -1072,10 +1183,9 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         // The sorted neighbour lists: the area's (nb_list / nb_meta) and the cells' (nb_list_c /
         // nb_meta_c), one region per k_nb_lists block, words as the previous call needed (first
         // guess n x min(n, 4096)), regrown on overflow to the largest block's use x the grid.
-        // The cells' lists need the lattice and the area index, not the area normals: with
-        // PCP_NORMALS_OVERLAP=1 the lattice and k_nb_lists<true> run on a side stream beside the
-        // area's lists and sums, k_nb_sums<true> joining them (measured slower: one stream by
-        // default).  Every buffer is sized before the launches.
+        // The cells go through k_cell_sums_exact first (any order where no order can change
+        // the sums); only those it leaves in nb_sel take the ordered lists.  Every buffer is
+        // sized before the launches.
         const float bscale = (float)kNbBuckets / r2n;
         const uint32_t nbb = ctx->nb_blocks > 0 ? (uint32_t)ctx->nb_blocks : (uint32_t)kNbBlocks;
         const uint32_t grid_a = std::min<uint32_t>(npts, nbb);
@@ -1088,86 +1198,83 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         PCP_HIP(ctx, ctx->nb_list_c.ensure(std::max<uint64_t>(guess_c, ctx->nb_need_c) * 4 + 64));
         PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)npts * sizeof(uint2) + 64));
         PCP_HIP(ctx, ctx->nb_meta_c.ensure((size_t)total * sizeof(uint2) + 64));
+        PCP_HIP(ctx, ctx->nb_sel.ensure(((size_t)total + 2) * sizeof(uint32_t)));
         bool ctl_dirty = !ctx->nb_ctl_zero || !ctx->nb_ctl.p;   // control words not known zero
         PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
         ctx->nb_ctl_zero = false;   // set again once k_nb_sums<true> has cleared them
         // nb_pts: the points by input index, then their normals as float4 (the sums' records)
         PCP_HIP(ctx, ctx->nb_pts.ensure(2 * n * sizeof(float4) + 64));
-        if (ctx->normals_overlap && !ctx->side_stream) {
-            PCP_HIP(ctx, hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking));
-            for (auto &e : ctx->side_ev) PCP_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
-        // (PCP_NORMALS_OVERLAP=1: the side stream.  Measured slower -- both list kernels are
-        // throughput-bound and share the same CUs -- so one stream by default)
-        const hipStream_t side = ctx->normals_overlap ? ctx->side_stream : ctx->stream;
         uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
+        uint32_t *sel = ctx->nb_sel.as<uint32_t>();
+        const float4 *nrm4 = ctx->nb_pts.as<float4>() + n;
         auto per_block = [](const DevBuf &b, uint32_t grid) {
             return (uint32_t)(std::min<uint64_t>(b.cap / 4, 0xffffffffull) / grid);
         };
-        auto area_lists_sums = [&](hipStream_t st) -> int {
+        hipStream_t st = ctx->stream;
+        auto area_lists_sums = [&]() -> int {
             const NbLists La{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
                              per_block(ctx->nb_list, grid_a)};
             hipLaunchKernelGGL(k_nb_lists<false>, dim3(grid_a), dim3(kNbT), 0, st, gn, r2n, bscale,
-                               (const double *)nullptr, (const uint32_t *)nullptr, La);
+                               (const double *)nullptr, (const uint32_t *)nullptr, La,
+                               (const uint32_t *)nullptr);
             PCP_CHECK_LAUNCH(ctx);
             hipLaunchKernelGGL(k_nb_sums<false>,
                                dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB), dim3(kNbT),
                                0, st, gn, (const uint2 *)La.meta, (const uint32_t *)La.list,
                                (const uint32_t *)nullptr, (const float4 *)ctx->nb_pts.as<float4>(),
                                ctx->area_nrm.as<float>(), ctx->nb_pts.as<float4>() + n,
-                               (const uint32_t *)ctl, (uint32_t *)nullptr);
+                               (const uint32_t *)ctl, (uint32_t *)nullptr,
+                               (const uint32_t *)nullptr);
             PCP_CHECK_LAUNCH(ctx);
             return PCP_OK;
         };
-        const NbLists Lc{ctx->nb_list_c.as<uint32_t>(), ctx->nb_meta_c.as<uint2>(), ctl + 1,
-                         ctl + 2, per_block(ctx->nb_list_c, grid_c)};
-        auto cell_lists = [&](hipStream_t st, const NbLists &lc) -> int {
-            if (!total) return PCP_OK;
-            hipLaunchKernelGGL(k_nb_lists<true>, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n, bscale,
-                               (const double *)ctx->cells_xyz.as<double>(), (const uint32_t *)n_d,
-                               lc);
-            PCP_CHECK_LAUNCH(ctx);
-            return PCP_OK;
-        };
-        // (launched for an empty lattice too: it lands both lists' uses and the overflow)
-        auto cell_sums = [&](const NbLists &lc) -> int {
+        // the cells: the order-free exact sums, then the ordered lists and sums of the cells
+        // left in sel (k_nb_sums<true> launched for an empty selection too: it lands both
+        // lists' uses and the overflow, and clears the control words)
+        auto cells = [&]() -> int {
+            const NbLists Lc{ctx->nb_list_c.as<uint32_t>(), ctx->nb_meta_c.as<uint2>(), ctl + 1,
+                             ctl + 2, per_block(ctx->nb_list_c, grid_c)};
+            if (total) {
+                hipLaunchKernelGGL(k_cell_sums_exact, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n,
+                                   (const double *)ctx->cells_xyz.as<double>(),
+                                   (const uint32_t *)n_d, nrm4, ctx->cells_nrm.as<float>(), sel,
+                                   ctx->cells_all_ordered ? 1 : 0);
+                PCP_CHECK_LAUNCH(ctx);
+                hipLaunchKernelGGL(k_nb_lists<true>, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n,
+                                   bscale, (const double *)ctx->cells_xyz.as<double>(),
+                                   (const uint32_t *)n_d, Lc, (const uint32_t *)sel);
+                PCP_CHECK_LAUNCH(ctx);
+            }
             constexpr int QB = NbCfg<true>::QB;
             hipLaunchKernelGGL(k_nb_sums<true>,
                                dim3((unsigned)std::max<uint64_t>(
                                    1, std::min<uint64_t>((total + QB - 1) / QB, 4096))),
-                               dim3(kNbT), 0, ctx->stream, gn, (const uint2 *)lc.meta,
-                               (const uint32_t *)lc.list, (const uint32_t *)n_d,
-                               (const float4 *)(ctx->nb_pts.as<float4>() + n),
+                               dim3(kNbT), 0, st, gn, (const uint2 *)Lc.meta,
+                               (const uint32_t *)Lc.list, (const uint32_t *)n_d, nrm4,
                                ctx->cells_nrm.as<float>(), (float4 *)nullptr,
-                               (const uint32_t *)ctl, n_h + 1);
+                               (const uint32_t *)ctl, n_h + 1,
+                               (const uint32_t *)(total ? sel : nullptr));
             PCP_CHECK_LAUNCH(ctx);
             return PCP_OK;
         };
         // the control words are zero: cleared by the previous call's last k_nb_sums<true> (or,
         // on a fresh buffer, by this memset)
-        if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctl, 0, 16, ctx->stream));
-        // first: the input points by input index for the sums' gathers, and the non-finite
-        // points' NaN normals (k_area_prep is the raw records' last reader; the exact kernels
-        // never write those entries, so a rerun keeps them)
-        hipLaunchKernelGGL(k_area_prep, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0,
-                           ctx->stream, rin, ctx->nb_pts.as<float4>(), ctx->area_nrm.as<float>());
+        if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctl, 0, 16, st));
+        // first: the input points by input index for the sums' gathers, the non-finite points'
+        // NaN normals (k_area_prep is the raw records' last reader; the exact kernels never
+        // write those entries, so a rerun keeps them), and sel's count cleared
+        hipLaunchKernelGGL(k_area_prep, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0, st,
+                           rin, ctx->nb_pts.as<float4>(), ctx->area_nrm.as<float>(), sel);
         PCP_CHECK_LAUNCH(ctx);
-        pin_release(ctx, ctx->stream);
-        if (side != ctx->stream) {
-            PCP_HIP(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
-            PCP_HIP(ctx, hipStreamWaitEvent(side, ctx->side_ev[0], 0));
-        }
-        if (int rcl = lattice(side)) return rcl;
-        if (int rcc = cell_lists(side, Lc)) return rcc;
-        if (side != ctx->stream) PCP_HIP(ctx, hipEventRecord(ctx->side_ev[1], side));
-        if (int rca = area_lists_sums(ctx->stream)) return rca;
-        if (side != ctx->stream) PCP_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[1], 0));
-        if (int rcs = cell_sums(Lc)) return rcs;
-        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        pin_release(ctx, st);
+        if (int rca = area_lists_sums()) return rca;
+        if (int rcl = lattice(st)) return rcl;
+        if (int rcs = cells()) return rcs;
+        PCP_HIP(ctx, hipStreamSynchronize(st));
         if (n_h[3]) {
             // a list buffer too small (first frames, or a denser area): regrow both to their
-            // largest block's use x the grid and run the lists and sums again on one stream (the
-            // lattice and the records stand)
+            // largest block's use x the grid and run the normals again (the lattice and the
+            // records stand; the cells' order-free pass too, over the new area normals)
             ctx->nb_need = std::max<uint64_t>(ctx->nb_need, (uint64_t)n_h[1] * grid_a);
             ctx->nb_need_c = std::max<uint64_t>(ctx->nb_need_c, (uint64_t)n_h[2] * grid_c);
             if (std::max(ctx->nb_need, ctx->nb_need_c) > 0xffffffffull)
@@ -1178,12 +1285,10 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
             PCP_HIP(ctx, ctx->nb_list_c.ensure(ctx->nb_need_c * 4 + 64));
             ctx->normals_regrown++;
             n_h[1] = n_h[2] = n_h[3] = 0;   // (the control words: cleared by k_nb_sums<true>)
-            const NbLists Lc2{ctx->nb_list_c.as<uint32_t>(), ctx->nb_meta_c.as<uint2>(), ctl + 1,
-                              ctl + 2, per_block(ctx->nb_list_c, grid_c)};
-            if (int rc2 = area_lists_sums(ctx->stream)) return rc2;
-            if (int rc3 = cell_lists(ctx->stream, Lc2)) return rc3;
-            if (int rc4 = cell_sums(Lc2)) return rc4;
-            PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            PCP_HIP(ctx, hipMemsetAsync(sel, 0, sizeof(uint32_t), st));
+            if (int rc2 = area_lists_sums()) return rc2;
+            if (int rc3 = cells()) return rc3;
+            PCP_HIP(ctx, hipStreamSynchronize(st));
             if (n_h[3])
                 return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: neighbour lists "
                                                        "overflowed after regrowing");

@@ -243,15 +243,14 @@ struct pcp_ctx {
     // the normals in the reference's summation order (PCP_NORMALS_EXACT, default 1; 0: the
     // order-free fixed-point kernels, A/B only): sorted neighbour lists, their per-query
     // {base, count}, cursors + overflow word; list entries the last call needed
-    bool normals_exact = true;
-    bool score_wide = true;
-    bool normals_overlap = false;
-    int nb_blocks = 0;              // PCP_NB_BLOCKS: k_nb_lists grid (A/B; 0 = kNbBlocks)   // PCP_NORMALS_OVERLAP=1: cells' lists on a side stream (A/B)   // k_score_cells_wide for few-ray launches (PCP_SCORE_WIDE=0: A/B)
+    bool normals_exact = true;       // PCP_NORMALS_EXACT=0: round 3's order-free normals (A/B)
+    bool score_wide = true;          // k_score_cells_wide for few-ray launches (PCP_SCORE_WIDE=0: A/B)
+    bool cells_all_ordered = false;  // PCP_CELLS_ORDER_FREE=0: every cell through the lists (A/B)
+    int nb_blocks = 0;               // PCP_NB_BLOCKS: k_nb_lists grid (A/B; 0 = kNbBlocks)
     pcp::DevBuf nb_list, nb_meta, nb_ctl, nb_pts;   // nb_pts: input points by index
     pcp::DevBuf nb_list_c, nb_meta_c;                // the cells' lists
+    pcp::DevBuf nb_sel;                              // cells left to the ordered path
     uint64_t nb_need_c = 0;
-    hipStream_t side_stream = nullptr;               // (the cells' lists beside the area's)
-    hipEvent_t side_ev[2] = {};
     bool nb_ctl_zero = false;                // nb_ctl's cursors known zero (cleared by the last call)
     uint64_t nb_need = 0;
     uint64_t normals_regrown = 0;

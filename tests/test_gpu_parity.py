@@ -1095,15 +1095,19 @@ def _normals_equal(got, ref):
     np.testing.assert_array_equal(got[fin].view(np.uint32), ref[fin].view(np.uint32))
 
 
-@pytest.mark.parametrize("exact", ["1", "0"])
-def test_excavation_area_setup(oracle, scene, exact, monkeypatch):
+@pytest.mark.parametrize("mode", ["exact", "exact_ordered", "fixed"])
+def test_excavation_area_setup(oracle, scene, mode, monkeypatch):
     """pcp_set_excavation_area against the oracle: grid bounds and the valid cells (positions,
     reference loop order) bit-exact.  Default path (PCP_NORMALS_EXACT=1): point normals and cell
     normals BIT-IDENTICAL -- PCL's float covariance sums in FLANN's (distance, index) order,
-    eigen33 with glibc's float libm restated (pcp_libm.h), the cells' double sums in the same
-    order.  The order-free A/B kernels (0): point normals within 2e-3, cells within 1e-4.  An
-    empty area keeps the previous cells (virtual_lidar.cpp:168)."""
+    eigen33 with glibc's float libm restated (pcp_libm.h), the cells' double sums where their
+    order cannot change them in any order (k_cell_sums_exact), the others in FLANN's order;
+    exact_ordered (PCP_CELLS_ORDER_FREE=0) sends every cell through the ordered lists.  The
+    order-free fixed-point A/B kernels (PCP_NORMALS_EXACT=0): point normals within 2e-3, cells
+    within 1e-4.  An empty area keeps the previous cells (virtual_lidar.cpp:168)."""
+    exact = "0" if mode == "fixed" else "1"
     monkeypatch.setenv("PCP_NORMALS_EXACT", exact)
+    monkeypatch.setenv("PCP_CELLS_ORDER_FREE", "0" if mode == "exact_ordered" else "1")
     d = np.load(GOLD / "excavation.npz")
     ctx = _abi.Context(0)
     try:
@@ -1133,17 +1137,26 @@ def test_excavation_area_setup(oracle, scene, exact, monkeypatch):
         ctx.close()
 
 
-def test_excavation_area_normals_long_lists_and_ties(oracle):
-    """The exact normals where the neighbour lists pass the LDS sort (> 6,144 neighbours within
+@pytest.mark.parametrize("order_free", ["1", "0"])
+def test_excavation_area_normals_long_lists_and_ties(oracle, order_free, monkeypatch):
+    """The exact normals where the neighbour lists pass the LDS sort (> 4,096 neighbours within
     1.5 m: sorted in global memory), with exact distance ties (a lattice, duplicated points: the
     reference's order breaks them by index), non-finite points (NaN normals, absent from every
-    list) and isolated points (< 3 neighbours: NaN).  Point and cell normals bit-identical."""
+    list) and isolated points (< 3 neighbours: NaN).  A plane tilted by 1e-6 beside it gives
+    normals with components ~2^-20 of their largest: the cells near it fail
+    k_cell_sums_exact's bound and take the ordered path in the same frame as the others.
+    Point and cell normals bit-identical, cells order-free where exact (default) and all
+    ordered (PCP_CELLS_ORDER_FREE=0)."""
+    monkeypatch.setenv("PCP_CELLS_ORDER_FREE", order_free)
     rng = np.random.default_rng(11)
     g = np.arange(90) * 0.025
     X, Y = np.meshgrid(g, g)
     P = np.stack([X.ravel(), Y.ravel(), 0.3 * np.sin(X.ravel()) + rng.normal(0, 0.002, X.size)], 1)
     P[::7, 2] = np.round(P[::7, 2], 2)                        # many exact-distance ties
-    P = np.concatenate([P, P[100:140], [[9.0, 9.0, 0.0], [9.5, 9.0, 0.1]]])   # dups, isolated
+    t = np.arange(30) * 0.05
+    TX, TY = np.meshgrid(4.0 + t, t)
+    tilt = np.stack([TX.ravel(), TY.ravel(), 1e-6 * TX.ravel()], 1)   # tiny normal components
+    P = np.concatenate([P, P[100:140], tilt, [[9.0, 9.0, 0.0], [9.5, 9.0, 0.1]]])   # dups, isolated
     a = np.zeros((P.shape[0], 4), np.float32)
     a[:, :3] = P
     a[rng.integers(0, a.shape[0], 6), 1] = np.nan
