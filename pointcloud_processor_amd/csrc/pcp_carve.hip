@@ -26,8 +26,15 @@
 namespace pcp {
 
 constexpr int kCT = 256;
-constexpr int kKeepItems = 16;
-constexpr int kKeepTile = kCT * kKeepItems;
+constexpr int kKeepItems = 16;   // most points per thread of a keep tile (large clouds)
+// points per thread of the keep tiles for n points: message-sized clouds (C5: ~10 k) get at
+// least kKeepMinTiles tiles -- the emit is a chain of per-item load rounds, and 3 tiles of 16
+// items left it latency-bound (21 us)
+constexpr int kKeepMinTiles = 64;
+static inline int keep_items(uint64_t n) {
+    const uint64_t per = (n + (uint64_t)kCT * kKeepMinTiles - 1) / ((uint64_t)kCT * kKeepMinTiles);
+    return (int)std::min<uint64_t>(std::max<uint64_t>(per, 1), kKeepItems);
+}
 
 struct ExcBox {
     double cx, cy, len, wid, min_x, max_x, min_y, max_y;
@@ -169,9 +176,9 @@ k_nearest(GridView g, const double2 *__restrict__ qxy, const uint32_t *__restric
         const float qx = (float)xy.x, qy = (float)xy.y, qz = 0.0f;
         float bd = INFINITY;
         uint32_t bi = UINT32_MAX, bk = 0;
-        // four independent loads in flight per step (the minimum of (distance, index) does not
+        // sixteen independent loads in flight per step (the minimum of (distance, index) does not
         // depend on the order the points are taken in)
-        constexpr int kU = 4;
+        constexpr int kU = 16;
         for (uint32_t k0 = threadIdx.x; k0 < g.n_pts; k0 += kU * kCT) {
             float4 pu[kU];
 #pragma unroll
@@ -255,11 +262,12 @@ k_carve_decide(CarveArgs a, const uint32_t *__restrict__ qidx, const uint32_t *_
 
 // kept points per 4096-point tile
 __global__ void __launch_bounds__(kCT)
-k_keep_count(uint64_t n, const uint8_t *__restrict__ removed, uint32_t *__restrict__ counts) {
-    const uint64_t base = (uint64_t)blockIdx.x * kKeepTile;
+k_keep_count(uint64_t n, const uint8_t *__restrict__ removed, uint32_t *__restrict__ counts,
+             int items) {
+    const uint64_t base = (uint64_t)blockIdx.x * kCT * items;
     uint32_t c = 0;
 #pragma unroll 4
-    for (int j = 0; j < kKeepItems; ++j) {
+    for (int j = 0; j < items; ++j) {
         const uint64_t i = base + (uint64_t)j * kCT + threadIdx.x;
         c += (i < n && !removed[i]) ? 1u : 0u;
     }
@@ -305,8 +313,8 @@ k_gen_emit(const GenPoint *__restrict__ gp, uint32_t ng, const double *__restric
 // kept points in input order as PointXYZRGB records (x, y, z, 1, rgb, 0, 0, 0)
 __global__ void __launch_bounds__(kCT)
 k_keep_emit(CarveArgs a, const uint8_t *__restrict__ removed, const uint32_t *__restrict__ counts,
-            float4 *__restrict__ out, uint32_t *__restrict__ n_out) {
-    const uint64_t base = (uint64_t)blockIdx.x * kKeepTile;
+            float4 *__restrict__ out, uint32_t *__restrict__ n_out, int items) {
+    const uint64_t base = (uint64_t)blockIdx.x * kCT * items;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     __shared__ uint32_t wc[kCT / 64];
     uint32_t pre_t = 0;
@@ -318,7 +326,7 @@ k_keep_emit(CarveArgs a, const uint8_t *__restrict__ removed, const uint32_t *__
     uint32_t run = wc[0] + wc[1] + wc[2] + wc[3];
     __syncthreads();
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_out = run + counts[blockIdx.x];
-    for (int j = 0; j < kKeepItems; ++j) {
+    for (int j = 0; j < items; ++j) {
         const uint64_t i = base + (uint64_t)j * kCT + threadIdx.x;
         const bool keep = i < a.n && !removed[i];
         const uint64_t bal = __ballot(keep);
@@ -560,7 +568,8 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     // device scratch: candidate indices (n), heights, fallback list, removed flags, tile
     // counts, kept records (the queries live in carve_gen)
     const uint64_t nq_max = G + n;
-    const uint32_t nb = (uint32_t)((n + kKeepTile - 1) / kKeepTile);
+    const int kitems = keep_items(n);
+    const uint32_t nb = (uint32_t)((n + (uint64_t)kCT * kitems - 1) / ((uint64_t)kCT * kitems));
     const size_t qb = 0;
     const size_t ib = (n * 4 + 256) & ~(size_t)255;
     const size_t hb = (nq_max * 8 + 255) & ~(size_t)255;
@@ -617,7 +626,10 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     hipLaunchKernelGGL(k_heights, dim3(gq), dim3(kCT), 0, st, g, r2, p->terrain_search_radius,
                        (const double2 *)qxy, (const uint32_t *)ctr, G, h, fb_list, ctr + 1);
     PCP_CHECK_LAUNCH(ctx);
-    hipLaunchKernelGGL(k_nearest, dim3(256), dim3(kCT), 0, st, g, (const double2 *)qxy,
+    // (one block per fallback query, up to 4,096 at once: the count is on the device, the
+    // blocks past it return at once)
+    hipLaunchKernelGGL(k_nearest, dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nq_max, 4096))),
+                       dim3(kCT), 0, st, g, (const double2 *)qxy,
                        (const uint32_t *)fb_list, (const uint32_t *)(ctr + 1), h);
     PCP_CHECK_LAUNCH(ctx);
     if (n) {
@@ -625,10 +637,10 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
                            (const uint32_t *)ctr, (const double *)(h + G), removed);
         PCP_CHECK_LAUNCH(ctx);
         hipLaunchKernelGGL(k_keep_count, dim3(nb), dim3(kCT), 0, st, n, (const uint8_t *)removed,
-                           tcount);
+                           tcount, kitems);
         PCP_CHECK_LAUNCH(ctx);
         hipLaunchKernelGGL(k_keep_emit, dim3(nb), dim3(kCT), 0, st, a, (const uint8_t *)removed,
-                           (const uint32_t *)tcount, kept, ctr + 2);
+                           (const uint32_t *)tcount, kept, ctr + 2, kitems);
         PCP_CHECK_LAUNCH(ctx);
     }
     pin_release(ctx, st);   // k_keep_emit was the raw records' last reader
