@@ -1130,11 +1130,19 @@ __global__ void __launch_bounds__(kCandT) k_candidates(CandArgs a) {
                 const int iy = y0 + r % ny_r, iz = z0 + r / ny_r;
                 const size_t row = (size_t)g.nx * ((size_t)iy + (size_t)g.ny * iz);
                 const uint32_t s = g.start[row + x0], e = g.start[row + x1 + 1];
-                for (uint32_t k = s; k < e; ++k) {
-                    const float4 p = g.pts[k];
-                    if (!flann_within(qx, qy, qz, p, r2)) continue;
-                    const double dx = (double)p.x - x, dy = (double)p.y - y;
-                    if (sqrt(dx * dx + dy * dy) < 1.0) mz = fmax(mz, (double)p.z);
+                // four independent loads per step: a row's walk is a chain of load latencies,
+                // and the maximum does not depend on the order the points come in
+                for (uint32_t k0 = s; k0 < e; k0 += 4) {
+                    float4 p4[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) p4[u] = g.pts[min(k0 + (uint32_t)u, e - 1)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float4 p = p4[u];
+                        if (k0 + (uint32_t)u >= e || !flann_within(qx, qy, qz, p, r2)) continue;
+                        const double dx = (double)p.x - x, dy = (double)p.y - y;
+                        if (sqrt(dx * dx + dy * dy) < 1.0) mz = fmax(mz, (double)p.z);
+                    }
                 }
             }
         }
