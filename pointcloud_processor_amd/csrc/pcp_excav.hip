@@ -274,17 +274,20 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
 // result in FLANN's order: ascending (float distance, index) (RadiusResultSet, sorted = true;
 // the oracle's radius_search).  Float sums depend on that order, so the default path builds the
 // sorted neighbour list of every query and then sums it sequentially:
-//  k_nb_lists : one block per query: the stencil's points within r (FLANN predicate) counted
-//               into 2,048 distance buckets of LDS (bucket = (uint)(d * 2048 / r2): monotone in
-//               d, so buckets are ordered), scanned, the 64-bit keys (distance bits << 32 |
-//               input index) scattered by bucket into LDS, each bucket's few keys put in order by
-//               an insertion sort in LDS; the list (input indices) goes to global memory at an
-//               atomically allocated base
+//  k_nb_lists : blocks loop over the queries: one pass over the stencil counts the points
+//               within r (FLANN predicate) into 2,048 distance buckets of LDS (bucket =
+//               (uint)(d * 2048 / r2): monotone in d, so buckets are ordered) and appends their
+//               64-bit keys (distance bits << 32 | input index) to LDS; a block scan, the keys
+//               grouped by bucket, each key placed at its bucket's start + its rank among the
+//               bucket's keys; the list (input indices) goes to the block's own region of the
+//               list buffer
 //  k_nb_sums  : a block per QB queries; waves 1-3 gather the listed points (by input index)
 //               64 steps at a time and form the summands (lane-parallel), wave 0 adds them in
 //               list order, one lane per (query, summand) -- the only sequential part, ~1 add
 //               per step.  The gathers of a chunk are issued one chunk ahead, its list entries
 //               two chunks ahead.
+//  k_cell_sums_exact : the cells' double sums in any order where an exponent bound makes
+//               every order equal; the cells it leaves take k_nb_lists / k_nb_sums in order
 constexpr int kNbBuckets = 2048;
 constexpr int kNbLds = 4096;   // keys sorted in LDS (32 KB); longer lists sort in global memory
 constexpr int kNbT = 256;
