@@ -288,8 +288,14 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
 //               two chunks ahead.
 //  k_cell_sums_exact : the cells' double sums in any order where an exponent bound makes
 //               every order equal; the cells it leaves take k_nb_lists / k_nb_sums in order
-constexpr int kNbBuckets = 2048;
-constexpr int kNbLds = 4096;   // keys sorted in LDS (32 KB); longer lists sort in global memory
+#ifndef PCP_NB_BUCKETS
+#define PCP_NB_BUCKETS 2048   // distance buckets of k_nb_lists (build knob, A/B)
+#endif
+#ifndef PCP_NB_LDS
+#define PCP_NB_LDS 4096       // keys sorted in LDS (build knob, A/B)
+#endif
+constexpr int kNbBuckets = PCP_NB_BUCKETS;
+constexpr int kNbLds = PCP_NB_LDS;   // keys sorted in LDS (32 KB); longer lists sort in global memory
 constexpr int kNbT = 256;
 constexpr int kNbBlocks = 2048;        // k_nb_lists grid (blocks loop over the queries)
 constexpr int kNbU = 8;                // k_nb_lists candidates in flight per thread
