@@ -1173,6 +1173,44 @@ def test_excavation_area_normals_long_lists_and_ties(oracle, order_free, monkeyp
             np.testing.assert_array_equal(cn.view(np.uint32), r_cn.view(np.uint32))
 
 
+def _degenerate_areas():
+    rng = np.random.default_rng(23)
+    out = {}
+    out["three_points"] = np.array([[0.0, 0.0, 0.0], [0.1, 0.0, 0.0], [0.0, 0.1, 0.01]])
+    out["identical"] = np.concatenate([np.tile([[1.0, 2.0, 0.5]], (50, 1)),
+                                       rng.uniform(0, 0.4, (30, 3)) + [1.0, 2.0, 0.3]])
+    t = np.arange(200) * 0.01
+    out["collinear"] = np.stack([t, 0.5 * t, 0.1 * t], 1)                 # rank-1 covariance
+    g = np.arange(40) * 0.05
+    X, Y = np.meshgrid(g, g)
+    plane = np.stack([X.ravel(), Y.ravel(), 0.2 * X.ravel() + rng.normal(0, 0.003, X.size)], 1)
+    out["far_from_origin"] = plane + [2000.0, -1500.0, 300.0]            # float spacing ~1e-4 m
+    return out
+
+
+@pytest.mark.parametrize("case", ["three_points", "identical", "collinear", "far_from_origin"])
+def test_excavation_area_normals_degenerate(oracle, case):
+    """Degenerate areas through the exact normals: three points (lists below PCL's minimum),
+    50 identical points beside a few others (zero distances: the order is the index order, zero
+    covariance), a line (rank-1 covariance: eigen33's degenerate branches), and a plane
+    kilometres from the origin (coarse float spacing in the distances and the sums).  Point and
+    cell normals and the cells bit-identical to the oracle."""
+    P = _degenerate_areas()[case]
+    a = np.zeros((P.shape[0], 4), np.float32)
+    a[:, :3] = P
+    r_n = oracle.area_normals(a, 1.5)
+    r_xyz, r_cn, r_bb, _ = oracle.excavation_grid(a, 0.1, 4, r_n)
+    with _abi.Context(0) as ctx:
+        bb, n = ctx.set_excavation_area(a, 0.1, 4)
+        np.testing.assert_array_equal(bb, r_bb)
+        assert n == r_xyz.shape[0]
+        _normals_equal(ctx.get_area_normals(), r_n)
+        if n:
+            xyz, cn = ctx.get_cells()
+            np.testing.assert_array_equal(xyz, r_xyz)
+            np.testing.assert_array_equal(cn.view(np.uint32), r_cn.view(np.uint32))
+
+
 # ---------------------------------------------------------------- excavated-terrain carve
 def _matched_cloud(seed=3):
     """A /matched_point_cloud stand-in: a noisy 0.05 m lattice (PointXYZRGB, 32 B), a raised
