@@ -1256,6 +1256,39 @@ def test_excavate_matches_oracle(gpu, oracle):
         np.testing.assert_array_equal(area[:, [0, 1, 2, 4]].view(np.uint32), r_area.view(np.uint32))
 
 
+@pytest.mark.parametrize("case", ["empty", "all_nan", "far", "rect", "dense_deep"])
+def test_excavate_edge_cases(gpu, oracle, case):
+    """pcp_excavate against the CPU restatement on the edges: an empty cloud, an all-NaN cloud,
+    a cloud 200 m away from the pit (every height from the nearest-point fallback), the
+    rectangle mode (l_shape_enabled 0) and a denser, deeper surface (point_density 0.1, depth
+    0.5).  Kept points, generated surface, /excavation_area records and the marker pose
+    bit-exact."""
+    c = _matched_cloud(6)
+    kw = {}
+    if case == "empty":
+        c = np.zeros((0, 8), np.float32)
+    elif case == "all_nan":
+        c[:, 0] = np.nan
+    elif case == "far":
+        c[:, 0] += 200.0
+    elif case == "rect":
+        kw = {"l_shape_enabled": 0}
+    else:
+        kw = {"point_density": 0.1, "depth": 0.5}
+    yaw = math.radians(15.0)
+    t, q = (0.3, -0.2, 0.1), (0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2))
+    terr, area, pose = gpu.excavate(c, (t, q), _abi.excavation_params(**kw))
+    keep, surf, r_area, r_pose = oracle.excavate(c, t, q, oracle.exc_params(**kw))
+    np.testing.assert_array_equal(pose, r_pose)
+    nk = int(keep.sum())
+    assert terr.shape[0] == nk + surf.shape[0]
+    kept = c[keep]
+    np.testing.assert_array_equal(terr[:nk, :3].view(np.uint32), kept[:, :3].view(np.uint32))
+    np.testing.assert_array_equal(terr[:nk, 4].view(np.uint32), kept[:, 4].view(np.uint32))
+    np.testing.assert_array_equal(terr[nk:, [0, 1, 2, 4]].view(np.uint32), surf.view(np.uint32))
+    np.testing.assert_array_equal(area[:, [0, 1, 2, 4]].view(np.uint32), r_area.view(np.uint32))
+
+
 def test_excavate_bounds_hold(gpu):
     """pcp_excavate_bounds caps every output the carve can produce (rectangle and L modes)."""
     c = _matched_cloud(5)
@@ -1292,6 +1325,39 @@ def test_drivable_area_matches_oracle(gpu, oracle, kw):
     np.testing.assert_array_equal(origin, r_origin)
     np.testing.assert_array_equal(grid, ref)
     assert {-1, 0, 100} <= set(np.unique(grid).tolist())
+
+
+@pytest.mark.parametrize("case", ["empty", "all_nan", "outside_map", "one_cell"])
+def test_drivable_area_edge_cases(gpu, oracle, case):
+    """calc_drivable_area on the edges: an empty cloud and an all-NaN one (only the start-clear
+    disc is free; an empty cloud leaves the whole grid free, as the reference's), every point
+    outside the map, and one column of points (a single cell, an obstacle by its z spread).
+    Grid and origin bit-exact against the CPU restatement."""
+    rng = np.random.default_rng(5)
+    if case == "empty":
+        c = np.zeros((0, 4), np.float32)
+    else:
+        n = 5_000
+        c = np.zeros((n, 4), np.float32)
+        c[:, 0] = rng.uniform(-2, 2, n)
+        c[:, 1] = rng.uniform(-2, 2, n)
+        c[:, 2] = rng.normal(-1.5, 0.05, n)
+        if case == "all_nan":
+            c[:, 0] = np.nan
+        elif case == "outside_map":
+            c[:, 0] += 500.0
+        else:
+            c[:, 0] = 4.0
+            c[:, 1] = 6.0
+    yaw = math.radians(-40.0)
+    t, q = (1.0, 2.0, 1.8), (0.0, 0.0, math.sin(yaw / 2), math.cos(yaw / 2))
+    p = _abi.drivable_params(min_points_per_cell=3)
+    grid, origin = gpu.drivable_area(c, (t, q), (1.0, 2.0), (0.0, 0.0), p)
+    ref, r_origin = oracle.drivable_area(c, t, q, (1.0, 2.0), (0.0, 0.0), p.grid_resolution,
+                                         p.map_width, p.map_height, p.max_gradient,
+                                         p.min_points_per_cell, p.start_clear_radius)
+    np.testing.assert_array_equal(origin, r_origin)
+    np.testing.assert_array_equal(grid, ref)
 
 
 # (PCP_TERRAIN_BLOCKS, PCP_TERRAIN_FINE) -> the layout the scans walk from the first query
