@@ -4,6 +4,9 @@
 # (PCP_LIB), interleaved, then the exact-normals parity tests on each variant.
 #   libraries: pointcloud_processor_amd/_lib (default 4096 / 2048), _lib_nbA (2048 / 2048),
 #   _lib_nbB (1024 / 1024)
+# build the variants on the CPU first (from pointcloud_processor_amd/csrc):
+#   make -j8 OUTDIR=../_lib_nbA EXTRA="-DPCP_NB_LDS=2048" ../_lib_nbA/libpcp.so
+#   make -j8 OUTDIR=../_lib_nbB EXTRA="-DPCP_NB_LDS=1024 -DPCP_NB_BUCKETS=1024" ../_lib_nbB/libpcp.so
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
