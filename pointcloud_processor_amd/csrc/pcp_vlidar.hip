@@ -14,6 +14,7 @@
 
 #include <hip/hip_ext.h>
 
+#include "pcp_crmath.h"
 #include "pcp_internal.hpp"
 #include "pcp_stencil.hpp"
 
@@ -1163,14 +1164,16 @@ __global__ void __launch_bounds__(kCandT) k_candidates(CandArgs a) {
         out[0] = 0.0;
         return;
     }
-    const double elev = atan2(-dz, hd);
+    // glibc's atan2 (the reference's) rounds correctly but for rare near-ties; ocml's is within
+    // an ulp: pcp_cr_atan2_fix rounds it correctly (pcp_crmath.h, tests/test_crmath.py)
+    const double elev = pcp_cr_atan2_fix(-dz, hd, atan2(-dz, hd));
     if (elev >= kMinElevation && elev <= kMaxElevation) {
         out[0] = 1.0;
         out[1] = x;
         out[2] = y;
         out[3] = z;
         out[4] = -kPi / 2 + elev;
-        out[5] = atan2(dy, dx);
+        out[5] = pcp_cr_atan2_fix(dy, dx, atan2(dy, dx));
     } else {
         out[0] = 0.0;
     }
