@@ -515,6 +515,9 @@ def test_terrain_index_info(gpu, loaded, scene):
 
 
 def test_candidates_match(gpu, oracle, loaded, scene, cells):
+    """generateCandidatePositions: positions bit-exact; pitch and yaw (atan2, correctly rounded
+    on the device, pcp_crmath.h) bit-identical to glibc's but for its rare near-tie misroundings
+    (< 1 % of the angles here; ocml's own atan2 left ~8 % one ulp off), always within 1e-12."""
     T, _ = loaded
     for nc in (100, 400, 1000):
         p = _abi.default_vl_params(num_candidates=nc)
@@ -524,6 +527,8 @@ def test_candidates_match(gpu, oracle, loaded, scene, cells):
         assert g.shape == r.shape
         np.testing.assert_array_equal(g[:, :3], r[:, :3])
         np.testing.assert_allclose(g[:, 3:], r[:, 3:], rtol=0, atol=1e-12)
+        differ = int((g[:, 3:].view(np.uint64) != r[:, 3:].view(np.uint64)).sum())
+        assert differ <= max(1, g[:, 3:].size // 100), differ
 
 
 def test_step_table():
