@@ -3,7 +3,8 @@
  * upper neighbour} (a faithful device result), and pcp_cr_atan2_fix(y, x, r0) must give g.
  * Half the pairs span the candidate generator's magnitudes (metres), a quarter tiny / huge
  * ratios, a quarter arbitrary finite bit patterns (those whose angle is below 2^-900 are
- * outside the fix's domain and skipped).  Prints "atan2 checked mismatches skipped". */
+ * outside the fix's domain and skipped); then acos and sin the same way.  Prints one
+ * "<fn> checked mismatches skipped" line per function. */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -58,5 +59,21 @@ int main(int argc, char **argv) {
         }
     }
     printf("atan2 %ld %ld %ld\n", n - skipped, bad, skipped);
+    /* acos over (0, 1) and sin over the scoring's pi / 2 - acos(..) in [0, pi / 2] */
+    long bad_acos = 0, bad_sin = 0;
+    for (long i = 0; i < n; ++i) {
+        const double d = uni(0.0, 1.0);
+        if (d == 0.0) continue;
+        const double g = acos(d);
+        const int pick = (int)(rnd() % 3);
+        const double r0 = pick == 0 ? nextafter(g, -INFINITY) : pick == 1 ? g : nextafter(g, INFINITY);
+        const double r = pcp_cr_acos_fix(d, r0);
+        if (memcmp(&r, &g, 8) != 0) ++bad_acos;
+        const double a = uni(0x1p-20, 1.5707963267948966);
+        const double gs = sin(a), rs = pcp_cr_sin(a);
+        if (memcmp(&rs, &gs, 8) != 0) ++bad_sin;
+    }
+    printf("acos %ld %ld 0\n", n, bad_acos);
+    printf("sin %ld %ld 0\n", n, bad_sin);
     return 0;
 }
