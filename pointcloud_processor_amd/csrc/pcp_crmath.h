@@ -10,7 +10,8 @@
  * series to t^31 for |t| <= pi / 4), so the sign is decided unless t lies within ~2^-100 of a
  * midpoint.  Zeros, infinities, NaNs and |r| < 2^-900 return r unchanged.
  * pcp_cr_acos_fix(d, r) and pcp_cr_sin(a): the same for the scoring's acos and sin
- * (virtual_lidar.cpp:700-705); checked on the CPU, not yet used by a kernel.
+ * (virtual_lidar.cpp:700-705); checked on the CPU and not used by a kernel: glibc misrounds
+ * those near ties more often than ocml disagrees with it.
  * Compile with -ffp-contract=off: the error-free transformations need every operation rounded
  * on its own (fma() is called explicitly where one is meant).
  */
