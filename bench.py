@@ -2,8 +2,7 @@
 """Benchmark of the virtual-LiDAR pose search (BASELINE.json metric, configs[1]).
 
 A step = one pass of the hot path over one batch: the candidate poses of this rank (256 per
-GPU: BASELINE configs[1] at N=1; --poses-per-gpu 512 on 8 GPUs = configs[3]'s 4096) each cast the dense
-1024 x 256 azimuth x elevation fan against the 1M-point excavation terrain with the
+GPU: BASELINE configs[1] at N=1, weak-scaled) each cast the dense 1024 x 256 azimuth x elevation fan against the 1M-point excavation terrain with the
 reference's march rule (virtual_lidar.cpp:765-797), plus ONE collective: all-reduce(MIN)
 of the per-pose blocked-ray counts (RCCL over xGMI when N > 1), then the argmin.
 
@@ -14,11 +13,15 @@ The same line carries the rest of the metric ("+ candidate poses/sec (whole node
 poses_per_s_reference_mode (runOptimization over the excavation cells, virtual_lidar.cpp:
 454-548) and c3 (crop + voxel + transform frame, BASELINE configs[2]), each its own timed loop
 of K steps, and CPU baselines (the oracle restatement, 1 thread and the host's CPU share) for
-all three on rank 0 at N = 1.
+all three on rank 0 at N = 1.  With N > 1 the line also carries c4 (BASELINE configs[3]: 4096
+poses strong-scaled over the N ranks, oracle-checked on a sample); at N = 1 it carries c1 and
+c5 (configs[0] / configs[4]: the per-frame chain through the C++ node cores).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode all|fan|filter|cells|c1|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode all|fan|filter|cells|c1|c4|c5]
 
---gpus N without WORLD_SIZE starts N ranks itself (one process per GPU).
+--gpus N without WORLD_SIZE starts N ranks itself (one process per GPU).  The rank processes
+never import torch (their control plane is hostgroup.py's helper), so libpcp runs on the HIP
+runtime and RCCL of /opt/rocm (the line's "runtime").
 """
 from __future__ import annotations
 
@@ -54,8 +57,9 @@ def _self_launch(n: int) -> int:
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # own process group: a rank's control-plane helper (hostgroup.py) goes with it
         procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] +
-                                      sys.argv[1:], env=env))
+                                      sys.argv[1:], env=env, start_new_session=True))
     rc = 0
     try:
         # any rank may die first: poll them all, and a non-zero exit ends the others (they
@@ -70,42 +74,61 @@ def _self_launch(n: int) -> int:
             if live and not rc:
                 time.sleep(0.05)
     finally:
+        import signal
+
         for p in procs:
-            if p.poll() is None:
-                p.kill()
-                p.wait()
+            try:
+                os.killpg(p.pid, signal.SIGKILL)   # the rank and its helper, if still there
+            except (ProcessLookupError, PermissionError):
+                pass
+            p.wait()
     return rc
 
 
 def _dist_init(n_gpus: int):
-    """torch.distributed as the host-side control plane only (gloo: barriers, the max-over-ranks
-    timing, the RCCL id hand-off).  The data-path collective (`backend`): "rccl" = libpcp's own
-    RCCL communicator (pcp_comm_init_rank), one process per GPU, so the only HIP runtime in the
-    process is libpcp's (torch never touches the GPU: its wheel bundles another runtime);
-    "gloo" = a rehearsal with more ranks than GPUs (ranks share devices, host vectors)."""
-    import torch
-    import torch.distributed as dist
-
+    """The host-side control plane (barriers, the max-over-ranks timing, the RCCL id hand-off):
+    a hostgroup.HostGroup, i.e. torch.distributed over gloo in a helper child process, so that
+    THIS process never imports torch and libpcp runs on the HIP runtime and RCCL its RUNPATH
+    names (/opt/rocm/lib) -- a PyTorch wheel bundles its own copies under the same SONAMEs
+    (pcp_get_runtime_info reports which ones ran: the line's "runtime").  The data-path
+    collective (`backend`): "rccl" = libpcp's own RCCL communicator (pcp_comm_init_rank), one
+    process per GPU; "gloo" = a rehearsal with more ranks than GPUs (ranks share devices, the
+    keys go through the host group)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n_gpus:
         raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}")
+    # libpcp first (RTLD_GLOBAL): its NEEDED libamdhip64.so.7 / librccl.so.1 resolve to /opt/rocm
+    try:
+        from pointcloud_processor_amd import _abi
+
+        _abi.load_library()
+        ndev = _abi.device_count()
+    except OSError:          # no library (the CPU launch check)
+        ndev = 0
     backend = None
+    group = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        try:
-            from pointcloud_processor_amd import _abi
-
-            ndev = _abi.device_count()
-        except OSError:          # no library (the CPU launch check)
-            ndev = 0
         backend = os.environ.get("PCP_DIST_BACKEND", "rccl" if ndev >= world else "gloo")
         backend = "rccl" if backend == "nccl" else backend
         if ndev:
             local = local % ndev
-        dist.init_process_group(backend="gloo")
-    return torch, (dist if world > 1 else None), world, rank, local, backend
+        from pointcloud_processor_amd.hostgroup import HostGroup
+
+        group = HostGroup()
+    return group, world, rank, local, backend
+
+
+def _runtime():
+    """pcp_get_runtime_info: the HIP runtime and RCCL libpcp ran on in this process."""
+    try:
+        from pointcloud_processor_amd import _abi
+
+        return _abi.runtime_info()
+    except OSError:
+        return None
 
 
 def _poses_for(ctx, grid_bbox, zx, total: int):
@@ -300,7 +323,6 @@ def _timed(step, args, dist, sync):
     """W untimed warmup steps, then exactly K steps between barrier + device synchronize on both
     sides (sync: the library context's stream synchronisation -- all of a step's work is on that
     stream); -> (max-over-ranks seconds, sum-over-ranks units, last step's result)."""
-    import torch
 
     def barrier_sync():
         if dist is not None:
@@ -325,12 +347,10 @@ def _timed(step, args, dist, sync):
     finally:
         if gc_was:
             gc.enable()
-    t = torch.tensor([dt], dtype=torch.float64)
-    uu = torch.tensor([units], dtype=torch.float64)
-    if dist is not None:   # host-side (gloo)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(uu, op=dist.ReduceOp.SUM)
-    return float(t.item()), float(uu.item()), res
+    if dist is not None:   # host-side (the control plane)
+        dt = float(dist.allreduce(np.array([dt]), "max")[0])
+        units = float(dist.allreduce(np.array([units], np.float64), "sum")[0])
+    return dt, units, res
 
 
 def _profiled(ctx, step, reps, names):
@@ -439,41 +459,22 @@ def _fan_roofline(ctx, poses, fan, avg_kernel_s, units_per_launch):
     }
 
 
-def run_all(args, torch, dist, world, rank, local, backend):
-    """Default line: the C2 fan (value), reference-mode scoring of the same node
-    (runOptimization, poses/s) and the C3 filter frame, each timed as its own loop of K steps
-    with the barrier / max-over-ranks discipline; CPU baselines on rank 0 at N = 1."""
-    import numpy as np
-
-    from pointcloud_processor_amd import _abi, synth
+def _fan_stepper(ctx, poses, fan, lo, P_total, dist, backend):
+    """One step of the pose-sharded fan search for this rank's poses [lo, lo + len(poses)) of
+    P_total -> (step() -> (ray-hit tests of this rank, blocked counts), best {"fan": argmin},
+    the all-poses blocked vector the step fills).  N > 1 over RCCL: libpcp's own communicator --
+    the per-pose keys (blocked << 32) | pose are written into the context's device vector, ONE
+    ncclAllReduce(MIN) runs on the library's stream, only the reduced vector comes back
+    (pcp_raycast_fan_allreduce).  The gloo rehearsal (ranks sharing one GPU) reduces a host
+    vector through the control plane (dist.reduce_fan)."""
     from pointcloud_processor_amd import dist as pd
 
-    ctx = _abi.Context(local)
-    if backend == "rccl":   # libpcp's own communicator; the id travels over the gloo group
-        uid = [_abi.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init_rank(world, uid[0], rank)
-    scene = synth.terrain_scene()
-    ctx.set_terrain(scene.terrain, point_step=32)
-    P_total = args.poses_per_gpu * world
-    poses_all, nc = _poses_for(ctx, _grid_bbox(scene.area), scene.zx120_pose5, P_total)
-    lo, hi = pd.shard(P_total, world, rank)
-    poses = np.ascontiguousarray(poses_all[lo:hi])
-    fan = _abi.fan_params(n_az=args.n_az, n_el=args.n_el)
-
-    # ---- C2 / C4: the fan (the headline) -------------------------------------------------
     best = {}
-
     blocked_h = np.zeros(max(poses.shape[0], 1), np.uint32)
     units_h = np.zeros(max(poses.shape[0], 1), np.uint64)
-    # N > 1 over RCCL: libpcp's own communicator -- the per-pose keys (blocked << 32) | pose
-    # are written into the context's device vector, ONE ncclAllReduce(MIN) runs on the library's
-    # stream, only the reduced vector comes back (pcp_raycast_fan_allreduce).  The gloo
-    # rehearsal (ranks sharing one GPU) keeps the host-side vector of dist.reduce_fan.
-    own_comm = backend == "rccl"
-    if own_comm:
-        blocked_all = np.zeros(max(P_total, 1), np.uint32)
-
+    # one rank: its own blocked vector is the whole one (no copy inside the timed steps)
+    blocked_all = blocked_h if dist is None else np.zeros(max(P_total, 1), np.uint32)
+    if backend == "rccl":
         def fan_step():
             best["fan"], _ = ctx.raycast_fan_allreduce(poses, fan, lo, P_total, blocked_all,
                                                        units_h)
@@ -484,11 +485,96 @@ def run_all(args, torch, dist, world, rank, local, backend):
             if dist is None:   # one rank: the library's argmin is the node's answer
                 keys = blocked_h
             else:
-                keys, b = pd.reduce_fan(blocked_h[:poses.shape[0]], lo, hi, P_total, dist)
+                keys, b = pd.reduce_fan(blocked_h[:poses.shape[0]], lo, lo + poses.shape[0],
+                                        P_total, dist)
+            if dist is not None:
+                blocked_all[:P_total] = np.asarray(keys[:P_total], np.uint32)
             best["fan"] = b   # ^ the one collective
             return int(units_h[:poses.shape[0]].sum()), keys
+    return fan_step, best, blocked_all
 
+
+C4_POSES = 4096   # BASELINE configs[3]: 4096 candidate poses sharded over the GPUs
+
+
+def run_c4(args, dist, world, rank, local, backend, ctx=None, scene=None):
+    """BASELINE configs[3]: the 4,096-pose search STRONG-scaled over the N ranks (rank r casts
+    poses [r*4096/N, (r+1)*4096/N), the split of runOptimization's candidate loop,
+    virtual_lidar.cpp:467-475), one all-reduce(MIN) per step.  value = ray-hit tests of all
+    ranks / max-over-ranks time.  Rank 0 re-casts a sample of the poses on the oracle (the best
+    one among them) and compares their blocked counts with the reduced vector."""
+    from pointcloud_processor_amd import _abi, synth
+    from pointcloud_processor_amd import dist as pd
+
+    own = ctx is None
+    if own:
+        ctx = _abi.Context(local)
+        if backend == "rccl":
+            uid = dist.broadcast_bytes(_abi.comm_unique_id() if rank == 0 else None, src=0)
+            ctx.comm_init_rank(world, uid, rank)
+        scene = synth.terrain_scene()
+        ctx.set_terrain(scene.terrain, point_step=32)
+    fan = _abi.fan_params(n_az=args.n_az, n_el=args.n_el)
+    poses_all, nc = _poses_for(ctx, _grid_bbox(scene.area), scene.zx120_pose5, C4_POSES)
+    lo, hi = pd.shard(C4_POSES, world, rank)
+    poses = np.ascontiguousarray(poses_all[lo:hi])
+    step, best, blocked_all = _fan_stepper(ctx, poses, fan, lo, C4_POSES, dist, backend)
+    dt, units_all, _ = _timed(step, args, dist, ctx.synchronize)
+    shards = [pd.shard(C4_POSES, world, r) for r in range(world)]
+    res = {"workload": "C4 (configs[3]): 4096 candidate poses strong-scaled over the ranks, "
+                       f"1024x256 fan each, one all-reduce(MIN) per step ({backend or 'none'})",
+           "value": units_all / dt, "unit": "ray-hit tests/s", "n_gpus": world,
+           "scaling": "strong", "steps": args.steps, "ms_per_step": dt / args.steps * 1e3,
+           "poses_total": C4_POSES, "poses_per_rank": [h - l for l, h in shards],
+           "poses_per_s": C4_POSES * args.steps / dt, "best_pose": best["fan"],
+           "num_candidates_lattice": nc}
+    if rank == 0 and not args.no_cpu_baseline:
+        # oracle check: the argmin pose plus 7 poses spread over every rank's shard
+        pyoracle = _oracle()
+        pyoracle.set_threads(_host_cpu()["threads_used"])
+        pick = sorted({int(best["fan"])} | {int(i) for i in
+                                            np.linspace(0, C4_POSES - 1, 7).astype(int)})
+        rb, _, _ = pyoracle.raycast_fan(pyoracle.Cloud(scene.terrain), poses_all[pick], fan.n_az,
+                                        fan.n_el, fan.el_min, fan.el_max, fan.max_distance,
+                                        want_first_hit=False)
+        pyoracle.set_threads(1)
+        res["oracle_check"] = {"poses": pick,
+                               "blocked_equal": bool(np.array_equal(
+                                   np.asarray(rb, np.int64),
+                                   blocked_all[pick].astype(np.int64))),
+                               "best_blocked": int(blocked_all[best["fan"]]),
+                               "min_of_reduced_vector": int(blocked_all[:C4_POSES].min())}
+    if own:
+        ctx.close()
+    return res
+
+
+def run_all(args, dist, world, rank, local, backend):
+    """Default line: the C2 fan (value), reference-mode scoring of the same node
+    (runOptimization, poses/s) and the C3 filter frame, each timed as its own loop of K steps
+    with the barrier / max-over-ranks discipline; CPU baselines on rank 0 at N = 1."""
+    import numpy as np
+
+    from pointcloud_processor_amd import _abi, synth
+    from pointcloud_processor_amd import dist as pd
+
+    ctx = _abi.Context(local)
+    if backend == "rccl":   # libpcp's own communicator; the id travels over the gloo group
+        uid = dist.broadcast_bytes(_abi.comm_unique_id() if rank == 0 else None, src=0)
+        ctx.comm_init_rank(world, uid, rank)
+    scene = synth.terrain_scene()
+    ctx.set_terrain(scene.terrain, point_step=32)
+    P_total = args.poses_per_gpu * world
+    poses_all, nc = _poses_for(ctx, _grid_bbox(scene.area), scene.zx120_pose5, P_total)
+    lo, hi = pd.shard(P_total, world, rank)
+    poses = np.ascontiguousarray(poses_all[lo:hi])
+    fan = _abi.fan_params(n_az=args.n_az, n_el=args.n_el)
+
+    # ---- C2: the fan (the headline) --------------------------------------------------------
+    fan_step, best, blocked_all = _fan_stepper(ctx, poses, fan, lo, P_total, dist, backend)
+    own_comm = backend == "rccl"
     dt, units_all, _ = _timed(fan_step, args, dist, ctx.synchronize)
+    units_h = np.zeros(max(poses.shape[0], 1), np.uint64)
     collective = None
     if own_comm:
         ms = []
@@ -499,7 +585,11 @@ def run_all(args, torch, dist, world, rank, local, backend):
                       "bytes": 8 * P_total, "collective_ms": float(np.median(ms)),
                       "path": "device keys in libpcp's vector, libpcp's own RCCL communicator on "
                               "its stream (pcp_raycast_fan_allreduce), reduced vector D2H once; "
-                              "torch.distributed (gloo) only for the id hand-off and barriers"}
+                              "torch.distributed (gloo, in a helper process: hostgroup.py) only "
+                              "for the id hand-off and barriers"}
+        nr, rr = ctx.comm_info()
+        collective["rccl_nranks"] = nr   # the ranks RCCL's communicator saw (pcp_comm_info)
+        collective["runtime"] = _runtime()
     elif dist is not None:
         collective = {"op": "all_reduce(MIN) int64", "backend": backend, "bytes": 8 * P_total,
                       "path": "host vector (gloo rehearsal: ranks share devices)"}
@@ -524,8 +614,7 @@ def run_all(args, torch, dist, world, rank, local, backend):
         "dtype": "f64 march / f32 point test",
         "data": "synthetic (seeded T1M L-pit terrain, reference candidate lattice)",
         "config": {"workload": "C2: 1M-pt L-shape excavation terrain, 1024x256 ray fan, "
-                               f"{args.poses_per_gpu} candidate poses per GPU"
-                               + (" (C4 at 8 GPUs x 512)" if args.poses_per_gpu == 512 else ""),
+                               f"{args.poses_per_gpu} candidate poses per GPU",
                    "terrain_points": int(scene.terrain.shape[0]),
                    "poses_total": P_total, "fan": [args.n_az, args.n_el],
                    "num_candidates_lattice": nc, "parallelism": f"pose-shard x{world}",
@@ -541,6 +630,8 @@ def run_all(args, torch, dist, world, rank, local, backend):
     if dist is not None and backend == "gloo":
         out["rehearsal"] = (f"{world} ranks on {_abi.device_count()} GPU(s): collective "
                             "over gloo, ranks share devices")
+    if world > 1:   # configs[3]: the 4096-pose search strong-scaled over these ranks
+        out["c4"] = run_c4(args, dist, world, rank, local, backend, ctx=ctx, scene=scene)
     host = _host_cpu()
     cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     if cpu:
@@ -599,10 +690,13 @@ def run_all(args, torch, dist, world, rank, local, backend):
             out["reference_mode"]["cpu_baseline_kdtree"] = cpu_baseline_cells(
                 scene.terrain, aux, cells, cposes, scene.zx120_pose5, args.cpu_seconds / 2,
                 kdtree=True)
-        out["c3"] = run_filter(args, torch, dist, world, rank, local, backend, embedded=True,
+        out["c3"] = run_filter(args, dist, world, rank, local, backend, embedded=True,
                                cpu=cpu)
         if rank == 0 and world == 1:
             out["c1"] = run_c1(args, local, cpu)
+            # configs[4] on this GPU: 200 frames of the whole chain through the node cores,
+            # the first and last dumped frames re-run through the oracle chain
+            out["c5"] = run_c5(args, None, 1, 0, local, None, frames=200, check=cpu)
     ctx.close()
     return out
 
@@ -647,7 +741,7 @@ def _pcie_inclusive(ctx, clouds, box, tfs, n_in, cap, reps=5):
     return res
 
 
-def run_filter(args, torch, dist, world, rank, local, backend=None, embedded=False, cpu=False):
+def run_filter(args, dist, world, rank, local, backend=None, embedded=False, cpu=False):
     """C3: crop + voxel(0.05) + transform on a 10M-pt dual-LiDAR frame, inputs in HBM.  Every
     rank runs its own frame (replicas); value = input points of all ranks / max-over-ranks
     time."""
@@ -869,12 +963,75 @@ def run_c1(args, local, cpu: bool):
     return out
 
 
-def run_c5(args, torch, dist, world, rank, local, backend=None):
+C5_BOX = np.array([0.0, 15.0, -10.0, 10.0, -1.5, 10.0])       # pointcloud_filter.cpp:30-36
+C5_RT = ((8.0, -3.0, 2.0), (0.0, 0.0, 0.2588190451025208, 0.9659258262890683))   # replay's TFs
+C5_ZT = ((0.55, 0.4, 3.5), (0.0, 0.21633, 0.0, 0.97632))
+
+
+def c5_oracle_check(pyoracle, dump: Path, frame: int, best_idx: int) -> dict:
+    """One dumped frame of the streamed chain re-run through the oracle chain ON ITS OWN, from
+    the raw scans (every stage fed by the oracle's previous stage, never by a GPU output), and
+    compared with what the node cores published: filtered clouds, merged cloud, carved terrain,
+    excavation area, cells + cell normals (bits), candidate poses (xyz bits, angles 1e-12), the
+    per-candidate totals (largest relative difference) and the best index."""
+    pre = f"f{frame}_"
+
+    def ld(name, dt, cols):
+        return np.fromfile(dump / (pre + name), dt).reshape(-1, cols)
+
+    ok = {}
+    filt = []
+    for tag, k in (("rscan", "rf"), ("zscan", "zf")):
+        scan = ld(tag + ".f32", np.float32, 4)
+        vox, _, _, _ = pyoracle.voxel_grid(scan[pyoracle.crop_box(scan, C5_BOX)], 0.2)
+        ok[f"filtered_{k}"] = bool(np.array_equal(ld(k + ".bin", np.float32, 4)[:, :3], vox))
+        filt.append(vox)
+    ref = np.concatenate([pyoracle.transform_rgb(filt[0], C5_RT[0], C5_RT[1], (255, 0, 0)),
+                          pyoracle.transform_rgb(filt[1], C5_ZT[0], C5_ZT[1], (0, 0, 255))])
+    merged = ld("merged.bin", np.float32, 8)
+    ok["merged"] = bool(merged.shape[0] == ref.shape[0] and np.array_equal(
+        merged[:, :5].view(np.uint32), ref[:, :5].view(np.uint32)))
+    keep, surf, area, _ = pyoracle.excavate(ref, (0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))
+    r_terr = np.concatenate([ref[keep][:, [0, 1, 2, 4]], surf])
+    terr = ld("terrain.bin", np.float32, 8)
+    ok["terrain"] = bool(terr.shape[0] == r_terr.shape[0] and np.array_equal(
+        terr[:, [0, 1, 2, 4]].view(np.uint32), r_terr.view(np.uint32)))
+    got_area = ld("area.bin", np.float32, 8)
+    ok["area"] = bool(got_area.shape[0] == area.shape[0] and np.array_equal(
+        got_area[:, [0, 1, 2, 4]].view(np.uint32), area.view(np.uint32)))
+    r_xyz, r_cn, bb, _ = pyoracle.excavation_grid(area, 0.1, 10, pyoracle.area_normals(area, 1.5))
+    cx, cn = ld("cells.f64", np.float64, 3), ld("cnrm.f32", np.float32, 3)
+    ok["cells"] = bool(cx.shape == r_xyz.shape and np.array_equal(cx, r_xyz) and
+                       np.array_equal(cn.view(np.uint32), r_cn.view(np.uint32)))
+    T = pyoracle.Cloud(r_terr)
+    zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])     # getZX120Position on the origin
+    poses = ld("poses.f64", np.float64, 5)
+    r_poses = pyoracle.generate_candidates(T, bb, pyoracle.vl_params(), zx)
+    ok["candidates"] = bool(poses.shape == r_poses.shape and
+                            np.array_equal(poses[:, :3], r_poses[:, :3]) and
+                            np.allclose(poses[:, 3:], r_poses[:, 3:], rtol=0, atol=1e-12))
+    aux = np.zeros((filt[1].shape[0], 4), np.float32)
+    aux[:, :3] = filt[1]
+    tot, _, rep = pyoracle.score_poses(T, pyoracle.Cloud(aux), r_xyz, r_cn, r_poses, zx,
+                                       pyoracle.vl_params(), np.zeros(r_xyz.shape[0], np.uint8))
+    got = np.fromfile(dump / (pre + "tot.f64"), np.float64)
+    top = np.sort(np.asarray(tot))[::-1]
+    return {"frame": frame, **ok, "best_idx": best_idx, "oracle_best_idx": int(rep.best_idx),
+            "best_idx_matches": best_idx == int(rep.best_idx),
+            "totals_max_rel_diff": (float(np.max(np.abs(got - tot) / np.abs(tot)))
+                                    if got.shape == tot.shape and tot.size else None),
+            "top2_gap": float((top[0] - top[1]) / abs(top[0])) if top.size >= 2 and top[0]
+            else None}
+
+
+def run_c5(args, dist, world, rank, local, backend=None, frames=None, check=False):
     """BASELINE configs[4] (8 GPUs x 60k-pt streams): C5 is replicas only -- each
     rank streams its own frames through the C++ node cores (pcp_nodes_cli replay, full chain:
     filter x2 -> merge -> carve -> normals + grid -> terrain index -> pose search), nothing is
     exchanged on the data path.  value = frames/s of all replicas (each rank's frames over its
-    mean frame latency, summed by one reduction at the end); p50/p99 = the worst rank's."""
+    mean frame latency, summed by one reduction at the end); p50/p99 = the worst rank's.
+    check: rank 0 re-runs the first and the last dumped frame through the oracle chain on its
+    own (c5_oracle_check) -- after the timed frames, outside them."""
     import subprocess
     import tempfile
 
@@ -894,40 +1051,53 @@ def run_c5(args, torch, dist, world, rank, local, backend=None):
     ndev = _abi.device_count()
     if ndev:   # the replica's own GPU (device 0 of the child)
         env["HIP_VISIBLE_DEVICES"] = str(local % ndev)
-    frames = max(args.steps, 20)
+    frames = frames or max(args.steps, 20)
     if dist is not None:
         dist.barrier()
-    r = subprocess.run([str(cli), "replay", str(d / "t.f32"), str(sc.terrain.shape[0]),
-                        str(d / "c.f64"), str(d / "n.f32"), str(cells.xyz.shape[0]), bb,
-                        str(frames), "60032", "1"], env=env, capture_output=True, text=True,
-                       timeout=600)
+    cmd = [str(cli), "replay", str(d / "t.f32"), str(sc.terrain.shape[0]), str(d / "c.f64"),
+           str(d / "n.f32"), str(cells.xyz.shape[0]), bb, str(frames), "60032", "1"]
+    if check and rank == 0:
+        cmd.append(str(d))   # dump frames 0, 1, 2 and the last one
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         raise SystemExit(f"bench.py --mode c5: replay failed (rank {rank}): {r.stderr[-400:]}")
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     lat = np.array(res["lat_ms"])
     vals = [1e3 / float(lat.mean()), res["p50_ms"], res["p99_ms"]]
-    if dist is not None:
-        t = torch.tensor(vals, dtype=torch.float64)   # host-side (gloo)
-        s = t.clone()
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        m = t.clone()
-        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    if dist is not None:   # host-side (the control plane)
+        s = dist.allreduce(np.array(vals, np.float64), "sum")
+        m = dist.allreduce(np.array(vals, np.float64), "max")
         vals = [float(s[0]), float(m[1]), float(m[2])]
-    return {"metric": "C5 frames/s (full chain, replicas)", "value": vals[0], "unit": "frames/s",
-            "n_gpus": world, "steps": frames, "warmup": 2, "ms_per_step": vals[1],
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32 points / f64 scoring", "data": "synthetic 60,032-pt HDL-64-like scans",
-            "config": {"workload": "C5: 60k-pt stream per GPU, filter x2 -> merge -> carve -> "
-                                   "normals + grid -> terrain index -> pose search",
-                       "parallelism": f"replicas x{world}"},
-            "p50_ms_worst_rank": vals[1], "p99_ms_worst_rank": vals[2],
-            "stage_p50_ms_rank0": res.get("stage_p50_ms")}
+    out = {"metric": "C5 frames/s (full chain, replicas)", "value": vals[0], "unit": "frames/s",
+           "n_gpus": world, "steps": frames, "warmup": 2, "ms_per_step": vals[1],
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32 points / f64 scoring", "data": "synthetic 60,032-pt HDL-64-like scans",
+           "config": {"workload": "C5: 60k-pt stream per GPU, filter x2 -> merge -> carve -> "
+                                  "normals + grid -> terrain index -> pose search",
+                      "parallelism": f"replicas x{world}"},
+           "p50_ms": vals[1], "p99_ms": vals[2], "max_ms_rank0": res.get("max_ms"),
+           "p50_ms_worst_rank": vals[1], "p99_ms_worst_rank": vals[2],
+           "stage_p50_ms_rank0": res.get("stage_p50_ms"),
+           "reallocs_after_warmup": res.get("reallocs_after_warmup"),
+           "candidates_best_idx_last_frame": res.get("best_idx")}
+    if check and rank == 0 and res.get("dumped"):
+        pyoracle = _oracle()
+        pyoracle.set_threads(1)
+        dumped = res["dumped"]
+        out["oracle_check"] = [c5_oracle_check(pyoracle, d, fr["frame"], int(fr["best_idx"]))
+                               for fr in (dumped[0], dumped[-1])]
+        out["matches_oracle"] = all(all(v for k, v in c.items() if isinstance(v, bool))
+                                    for c in out["oracle_check"])
+    import shutil
+
+    shutil.rmtree(d, ignore_errors=True)
+    return out
 
 
-def run_cells(args, torch, dist, world, rank, local, backend=None):
+def run_cells(args, dist, world, rank, local, backend=None):
     """Reference-mode scoring (runOptimization) alone: poses/s."""
     a = argparse.Namespace(**vars(args))
-    out = run_all(a, torch, dist, world, rank, local, backend)
+    out = run_all(a, dist, world, rank, local, backend)
     rm = out["reference_mode"]
     return {"metric": "candidate poses/sec (reference cell scoring)", "value": rm["value"],
             "unit": "poses/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -942,13 +1112,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--mode", choices=["all", "fan", "filter", "cells", "c1", "c5",
+    ap.add_argument("--mode", choices=["all", "fan", "filter", "cells", "c1", "c4", "c5",
                                        "launch-check"],
                     default="all",
                     help="all (default): the fan line with reference-mode scoring and C3 as "
                          "extra keys; fan: the fan alone (profiling); filter: C3 with PCIe and "
-                         "stage breakdown; cells: reference mode alone; c1 / c5: the streaming "
-                         "chain (configs[0] / configs[4], replicas)")
+                         "stage breakdown; cells: reference mode alone; c4: 4096 poses strong-"
+                         "scaled over the ranks (configs[3]); c1 / c5: the streaming chain "
+                         "(configs[0] / configs[4], replicas)")
     ap.add_argument("--poses-per-gpu", type=int, default=256)
     ap.add_argument("--n-az", type=int, default=1024)
     ap.add_argument("--n-el", type=int, default=256)
@@ -961,26 +1132,40 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_self_launch(args.gpus))
     args.fan_only = args.mode == "fan"
-    torch, dist, world, rank, local, backend = _dist_init(args.gpus)
+    dist, world, rank, local, backend = _dist_init(args.gpus)
     if args.mode == "launch-check":   # the launch path alone (CPU test): ranks + one collective
-        t = torch.tensor([float(rank)])
+        t = np.array([float(rank)])
         if dist is not None:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        out = {"n_gpus": world, "backend": backend, "rank_sum": float(t.item())}
+            t = dist.allreduce(t, "sum")
+        from pointcloud_processor_amd import dist as pd
+
+        lo, hi = pd.shard(C4_POSES, world, rank)   # the C4 plan each rank would cast
+        c4 = np.array([hi - lo, lo], np.int64)
+        got = dist.allreduce(c4, "sum") if dist is not None else c4
+        out = {"n_gpus": world, "backend": backend, "rank_sum": float(t[0]),
+               "torch_in_rank_process": "torch" in sys.modules,
+               "c4": {"poses_total": int(got[0]), "scaling": "strong",
+                      "poses_per_rank": [h - l for l, h in
+                                         (pd.shard(C4_POSES, world, r) for r in range(world))]}}
     elif args.mode == "filter":
-        out = run_filter(args, torch, dist, world, rank, local, backend)
+        out = run_filter(args, dist, world, rank, local, backend)
     elif args.mode == "cells":
-        out = run_cells(args, torch, dist, world, rank, local, backend)
+        out = run_cells(args, dist, world, rank, local, backend)
     elif args.mode == "c1":
         out = run_c1(args, local, cpu=not args.no_cpu_baseline)
     elif args.mode == "c5":
-        out = run_c5(args, torch, dist, world, rank, local, backend)
+        out = run_c5(args, dist, world, rank, local, backend)
+    elif args.mode == "c4":
+        out = run_c4(args, dist, world, rank, local, backend)
     else:
-        out = run_all(args, torch, dist, world, rank, local, backend)
+        out = run_all(args, dist, world, rank, local, backend)
+    if rank == 0 and args.mode != "launch-check":
+        out["runtime"] = _runtime()
+        out["runtime"] = dict(out["runtime"] or {}, torch_in_process="torch" in sys.modules)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
-        dist.destroy_process_group()
+        dist.close()
 
 
 if __name__ == "__main__":

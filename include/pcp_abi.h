@@ -354,6 +354,18 @@ int pcp_raycast_fan_keys(pcp_ctx *ctx, const double *poses5, uint64_t n,
 int pcp_comm_unique_id(uint8_t id[PCP_COMM_ID_BYTES]);
 int pcp_comm_init_rank(pcp_ctx *ctx, int nranks, const uint8_t id[PCP_COMM_ID_BYTES], int rank);
 int pcp_comm_info(const pcp_ctx *ctx, int *nranks, int *rank);   /* 0 ranks: none */
+/* Which HIP runtime and RCCL this process's libpcp actually runs on (a PyTorch wheel ships both
+ * under the same SONAMEs; whichever was loaded first serves every later NEEDED entry): the
+ * versions the libraries report (hipRuntimeGetVersion, ncclGetVersion) and the files they were
+ * loaded from (dladdr of hipMalloc / ncclAllReduce).  Paths are NUL-terminated, truncated to
+ * cap bytes.  No device call: safe without a GPU. */
+typedef struct pcp_runtime_info {
+    int32_t hip_runtime_version;   /* HIP_VERSION encoding: major * 10^7 + minor * 10^5 + patch */
+    int32_t rccl_version;          /* NCCL_VERSION_CODE encoding: major * 10^4 + minor * 100 + patch */
+    char hip_path[512];
+    char rccl_path[512];
+} pcp_runtime_info;
+int pcp_get_runtime_info(pcp_runtime_info *info);
 /* One rank's shard of a pose-sharded fan query, collective included (every rank calls it with
  * the same p_total and fan): the fans of poses5[0 .. n) -- global poses [lo, lo + n) -- cast as
  * pcp_raycast_fan does, their keys (blocked << 32) | global pose written into the context's

@@ -81,6 +81,11 @@ class IndexInfo(C.Structure):
                 ("bmax", C.c_double * 3), ("scan_layout", C.c_int32), ("fine_tile", C.c_int32)]
 
 
+class RuntimeInfo(C.Structure):
+    _fields_ = [("hip_runtime_version", C.c_int32), ("rccl_version", C.c_int32),
+                ("hip_path", C.c_char * 512), ("rccl_path", C.c_char * 512)]
+
+
 # (name, restype, argtypes) for every entry point of include/pcp_abi.h
 _P = C.c_void_p
 _SIGS = [
@@ -141,6 +146,7 @@ _SIGS = [
     ("pcp_comm_unique_id", C.c_int, [_P]),
     ("pcp_comm_init_rank", C.c_int, [_P, C.c_int, _P, C.c_int]),
     ("pcp_comm_info", C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("pcp_get_runtime_info", C.c_int, [C.POINTER(RuntimeInfo)]),
     ("pcp_raycast_fan_allreduce", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), C.c_uint64,
                                             C.c_uint64, _P, _P, C.POINTER(C.c_int64),
                                             C.POINTER(C.c_double)]),
@@ -176,7 +182,11 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
     if not p.exists():
         raise OSError(f"libpcp.so not found at {p}: run __graft_entry__.build() "
                       f"(make -C pointcloud_processor_amd/csrc)")
-    lib = C.CDLL(str(p))
+    # RTLD_GLOBAL, and before torch: a PyTorch wheel ships its own libamdhip64.so.7 /
+    # librccl.so.1, and whichever copy is loaded first serves every later NEEDED entry of that
+    # SONAME.  Loaded first, libpcp runs on the runtime its RUNPATH names (/opt/rocm/lib);
+    # runtime_info() reports which one it got.
+    lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
     for name, res, args in _SIGS:
         fn = getattr(lib, name)
         fn.restype = res
@@ -187,6 +197,22 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
     if path is None:
         _lib = lib
     return lib
+
+
+def runtime_info() -> dict:
+    """pcp_get_runtime_info: the HIP runtime and RCCL this process's libpcp runs on (versions
+    and the files they were loaded from).  No device call."""
+    ri = RuntimeInfo()
+    rc = load_library().pcp_get_runtime_info(C.byref(ri))
+    if rc != PCP_OK:
+        raise PcpError(rc, "pcp_get_runtime_info failed")
+    hv, rv = ri.hip_runtime_version, ri.rccl_version
+    return {"hip_runtime_version": hv,
+            "hip_runtime": f"{hv // 10**7}.{hv // 10**5 % 100}.{hv % 10**5}",
+            "hip_path": os.path.realpath(ri.hip_path.decode()) if ri.hip_path else None,
+            "rccl_version": rv,
+            "rccl": f"{rv // 10**4}.{rv // 100 % 100}.{rv % 100}",
+            "rccl_path": os.path.realpath(ri.rccl_path.decode()) if ri.rccl_path else None}
 
 
 def device_count() -> int:

@@ -10,6 +10,9 @@
 // candidate loop (virtual_lidar.cpp:467-475): lowest blocked count, ties to the lowest index.
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
+#include <cstdio>
 #include <cstring>
 
 #include "pcp_internal.hpp"
@@ -40,6 +43,30 @@ void comm_release(pcp_ctx *ctx) {
     } while (0)
 
 static_assert(sizeof(ncclUniqueId) == PCP_COMM_ID_BYTES, "ncclUniqueId size");
+
+// the shard's fans and its keys on the context's stream, up to (not including) the collective
+static int fan_allreduce_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                                 const pcp_fan_params *fan, uint64_t lo, uint32_t P,
+                                 double *collective_ms, const unsigned long long **units_out) {
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    PCP_HIP(ctx, ctx->comm_keys.ensure((size_t)P * 8 + 64));
+    const uint32_t *blocked_d = nullptr;
+    if (n) {
+        FanEnq o;   // device results (no host landing): the keys kernel reads them
+        if (int rc = fan_enqueue(ctx, poses5, n, fan, false, false, false, o)) return rc;
+        blocked_d = o.blocked_d;
+        *units_out = o.units_d;
+    }
+    unsigned long long *keys = ctx->comm_keys.as<unsigned long long>();
+    launch_fan_keys(st, blocked_d, (uint32_t)lo, (uint32_t)n, P, keys);   // ~0 elsewhere
+    PCP_CHECK_LAUNCH(ctx);
+    if (collective_ms)
+        for (hipEvent_t &e : ctx->comm_ev)
+            if (!e) PCP_HIP(ctx, hipEventCreate(&e));
+    if (collective_ms) PCP_HIP(ctx, hipEventRecord(ctx->comm_ev[0], st));
+    return PCP_OK;
+}
 
 extern "C" {
 
@@ -74,6 +101,22 @@ int pcp_comm_info(const pcp_ctx *ctx, int *nranks, int *rank) {
     return PCP_OK;
 }
 
+int pcp_get_runtime_info(pcp_runtime_info *info) {
+    if (!info) return PCP_E_INVALID;
+    std::memset(info, 0, sizeof(*info));
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) == hipSuccess) info->hip_runtime_version = v;
+    v = 0;
+    if (ncclGetVersion(&v) == ncclSuccess) info->rccl_version = v;
+    Dl_info d;
+    hipError_t (*hip_malloc)(void **, size_t) = &hipMalloc;
+    if (dladdr(reinterpret_cast<const void *>(hip_malloc), &d) && d.dli_fname)
+        std::snprintf(info->hip_path, sizeof(info->hip_path), "%s", d.dli_fname);
+    if (dladdr(reinterpret_cast<const void *>(&ncclAllReduce), &d) && d.dli_fname)
+        std::snprintf(info->rccl_path, sizeof(info->rccl_path), "%s", d.dli_fname);
+    return PCP_OK;
+}
+
 int pcp_raycast_fan_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
                               const pcp_fan_params *fan, uint64_t lo, uint64_t p_total,
                               uint32_t *blocked_all, uint64_t *units, int64_t *best_idx,
@@ -91,25 +134,20 @@ int pcp_raycast_fan_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
                        (unsigned long long)lo, (unsigned long long)(lo + n),
                        (unsigned long long)p_total);
     if (p_total == 0) return PCP_OK;   // every rank sees the same p_total: no rank reduces
-    PCP_HIP(ctx, hipSetDevice(ctx->device));
-    hipStream_t st = ctx->stream;
     const uint32_t P = (uint32_t)p_total;
-    PCP_HIP(ctx, ctx->comm_keys.ensure((size_t)P * 8 + 64));
-    const uint32_t *blocked_d = nullptr;
     const unsigned long long *units_d = nullptr;
-    if (n) {
-        FanEnq o;   // device results (no host landing): the keys kernel reads them
-        if (int rc = fan_enqueue(ctx, poses5, n, fan, false, false, false, o)) return rc;
-        blocked_d = o.blocked_d;
-        units_d = o.units_d;
+    // everything before the collective: a failure here would leave the other ranks blocked in
+    // ncclAllReduce with no timeout, so it aborts the communicator (their collective then fails
+    // instead of hanging) and marks this context's communicator gone
+    if (int rc = fan_allreduce_enqueue(ctx, poses5, n, fan, lo, P, collective_ms, &units_d)) {
+        (void)ncclCommAbort(static_cast<ncclComm_t>(ctx->comm));
+        ctx->comm = nullptr;
+        ctx->comm_nranks = 0;
+        ctx->comm_rank = 0;
+        return rc;
     }
+    hipStream_t st = ctx->stream;
     unsigned long long *keys = ctx->comm_keys.as<unsigned long long>();
-    launch_fan_keys(st, blocked_d, (uint32_t)lo, (uint32_t)n, P, keys);   // ~0 elsewhere
-    PCP_CHECK_LAUNCH(ctx);
-    if (collective_ms)
-        for (hipEvent_t &e : ctx->comm_ev)
-            if (!e) PCP_HIP(ctx, hipEventCreate(&e));
-    if (collective_ms) PCP_HIP(ctx, hipEventRecord(ctx->comm_ev[0], st));
     PCP_NCCL(ctx, ncclAllReduce(keys, keys, P, ncclUint64, ncclMin,
                                 static_cast<ncclComm_t>(ctx->comm), st));   // the one collective
     if (collective_ms) PCP_HIP(ctx, hipEventRecord(ctx->comm_ev[1], st));

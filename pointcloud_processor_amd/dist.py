@@ -10,8 +10,9 @@ contiguously, terrain index replicated, and ONE collective per pose search:
                      identical on every rank.
 
 Each position of the vector is written by exactly one rank, so MIN/MAX reductions are exact
-(no arithmetic on the values).  With torch.distributed, backend "nccl" is RCCL over xGMI on
-the GPU nodes; "gloo" runs the same code on CPU for the tests.
+(no arithmetic on the values).  `dist_mod` is torch.distributed (gloo: the CPU tests) or a
+hostgroup.HostGroup (bench.py's ranks, whose processes never import torch); the GPU data path's
+collective is libpcp's own RCCL communicator (pcp_raycast_fan_allreduce).
 """
 from __future__ import annotations
 
@@ -30,6 +31,8 @@ def shard(total: int, world: int, rank: int) -> tuple[int, int]:
 def _reduce(vec: np.ndarray, op: str, dist_mod, device):
     if dist_mod is None:
         return vec
+    if hasattr(dist_mod, "allreduce_np"):   # hostgroup.HostGroup (bench.py's ranks)
+        return dist_mod.allreduce_np(vec, op)
     import torch
 
     t = torch.from_numpy(vec).to(device)

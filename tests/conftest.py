@@ -9,6 +9,17 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "oracle"))
 
+# libpcp before anything can import torch: a PyTorch wheel bundles its own HIP runtime and RCCL
+# under the SONAMEs libpcp links, and whichever copy is loaded first serves both.  Loaded here
+# (RTLD_GLOBAL), libpcp runs on /opt/rocm's, the runtime it ships with; no test module imports
+# torch in this process (torch-side checks run in their own processes).
+try:
+    from pointcloud_processor_amd import _abi as _pcp_abi
+
+    _pcp_abi.load_library()
+except OSError:   # not built yet: the ABI tests say so
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and libpcp.so")

@@ -74,3 +74,27 @@ def test_no_cpu_fallback_without_gpu():
         pytest.skip("a GPU is visible")
     with pytest.raises(_abi.PcpError):
         _abi.Context(0)
+
+
+def _assert_opt_rocm_runtime():
+    import sys
+
+    info = _abi.runtime_info()
+    print("libpcp runtime:", info)
+    assert info["hip_path"] and info["hip_path"].startswith("/opt/rocm"), info
+    assert info["rccl_path"] and info["rccl_path"].startswith("/opt/rocm"), info
+    assert info["hip_runtime_version"] >= 70200000, info   # the image's ROCm 7.2
+    assert "torch" not in sys.modules   # torch's bundled copies never joined this process
+
+
+def test_libpcp_runs_on_opt_rocm_runtime():
+    """libpcp is loaded before anything imports torch (conftest.py), so its NEEDED
+    libamdhip64.so.7 / librccl.so.1 are /opt/rocm's, not a PyTorch wheel's (pcp_get_runtime_info:
+    versions + dladdr paths; no device call)."""
+    _assert_opt_rocm_runtime()
+
+
+@pytest.mark.gpu
+def test_libpcp_runs_on_opt_rocm_runtime_gpu(gpu):
+    """The same on the GPU box, with a context created (the runtime initialised)."""
+    _assert_opt_rocm_runtime()
