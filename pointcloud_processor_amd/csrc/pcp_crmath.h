@@ -9,9 +9,9 @@
  * with cos m and sin m in double-double (Cody-Waite reduction by pi / 2 in three parts, Taylor
  * series to t^31 for |t| <= pi / 4), so the sign is decided unless t lies within ~2^-100 of a
  * midpoint.  Zeros, infinities, NaNs and |r| < 2^-900 return r unchanged.
- * pcp_cr_acos_fix(d, r) and pcp_cr_sin(a): the same for the scoring's acos and sin
- * (virtual_lidar.cpp:700-705); checked on the CPU and not used by a kernel: glibc misrounds
- * those near ties more often than ocml disagrees with it.
+ * (The same construction for the scoring's acos and sin, virtual_lidar.cpp:700-705, lives in
+ * tests/libm/crmath_extra.h: checked on the CPU, not used by a kernel, because glibc misrounds
+ * those near ties more often than ocml disagrees with it -- DESIGN.md §8.)
  * Compile with -ffp-contract=off: the error-free transformations need every operation rounded
  * on its own (fma() is called explicitly where one is meant).
  */
@@ -179,28 +179,6 @@ PCP_CR double pcp_cr_atan2_fix(double y, double x, double r) {
         if (side == 1 && v > 0.0) return hi;
     }
     return r;
-}
-
-/* acos(d) for 0 < d < 1 from a faithful first result r: acos is decreasing, so the true angle
- * lies below the midpoint m exactly when d > cos m (cos m in double-double) */
-PCP_CR double pcp_cr_acos_fix(double d, double r) {
-    if (!(d > 0.0 && d < 1.0) || !isfinite(r) || r == 0.0) return r;
-    const double lo = nextafter(r, -INFINITY), hi = nextafter(r, INFINITY);
-    pcp_dd s, c;
-    pcp_dd_sincos(pcp_fast_two_sum(r, 0.5 * (lo - r)), &s, &c);
-    if (pcp_dd_add(pcp_dd_make(d, 0.0), pcp_dd_neg(c)).hi > 0.0) return lo;
-    pcp_dd_sincos(pcp_fast_two_sum(r, 0.5 * (hi - r)), &s, &c);
-    if (pcp_dd_add(pcp_dd_make(d, 0.0), pcp_dd_neg(c)).hi < 0.0) return hi;
-    return r;
-}
-
-/* sin(a) for |a| <= 4, a >= 2^-500: the double-double value rounded once (its normalised high
- * part) -- correct unless sin(a) lies within ~2^-100 relative of a midpoint */
-PCP_CR double pcp_cr_sin(double a) {
-    if (!isfinite(a) || fabs(a) > 4.0 || fabs(a) < 0x1p-500) return sin(a);
-    pcp_dd s, c;
-    pcp_dd_sincos(pcp_dd_make(a, 0.0), &s, &c);
-    return s.hi + s.lo;
 }
 
 #endif /* PCP_CRMATH_H */

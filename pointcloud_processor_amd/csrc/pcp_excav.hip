@@ -608,14 +608,14 @@ template <bool CELLS>
 __global__ void __launch_bounds__(kNbT)
 k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict__ list,
           const uint32_t *__restrict__ n_dev, const float4 *__restrict__ recs,
-          float *__restrict__ out, float4 *__restrict__ out4, const uint32_t *__restrict__ ctl,
+          float *__restrict__ out, float4 *__restrict__ out4, uint32_t *ctl,
           uint32_t *__restrict__ ctl_host, const uint32_t *__restrict__ sel) {
     // the lists' largest block uses and overflow word (final: every k_nb_lists ran before this launch)
     // to the caller's pinned landing, one plain store each, then cleared for the next call (no
     // memset launch in front of its k_nb_lists)
     if (ctl_host && blockIdx.x == 0 && threadIdx.x < 3) {
         ctl_host[threadIdx.x] = ctl[threadIdx.x];
-        const_cast<uint32_t *>(ctl)[threadIdx.x] = 0;
+        ctl[threadIdx.x] = 0;   // (ctl is written: neither const nor restrict)
     }
     using Cfg = NbCfg<CELLS>;
     using T = typename Cfg::T;
@@ -1232,7 +1232,7 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
                                0, st, gn, (const uint2 *)La.meta, (const uint32_t *)La.list,
                                (const uint32_t *)nullptr, (const float4 *)ctx->nb_pts.as<float4>(),
                                ctx->area_nrm.as<float>(), ctx->nb_pts.as<float4>() + n,
-                               (const uint32_t *)ctl, (uint32_t *)nullptr,
+                               (uint32_t *)ctl, (uint32_t *)nullptr,
                                (const uint32_t *)nullptr);
             PCP_CHECK_LAUNCH(ctx);
             return PCP_OK;
@@ -1261,7 +1261,7 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
                                dim3(kNbT), 0, st, gn, (const uint2 *)Lc.meta,
                                (const uint32_t *)Lc.list, (const uint32_t *)n_d, nrm4,
                                ctx->cells_nrm.as<float>(), (float4 *)nullptr,
-                               (const uint32_t *)ctl, n_h + 1,
+                               (uint32_t *)ctl, n_h + 1,
                                (const uint32_t *)(total ? sel : nullptr));
             PCP_CHECK_LAUNCH(ctx);
             return PCP_OK;

@@ -1342,6 +1342,7 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
     __shared__ uint32_t p1[kBkCap];                  // slot -> crop-slot position, then
                                                      // input-order slot -> xyz index
     __shared__ uint32_t lsa[kBkT3 / 64], lsb[kBkT3 / 64];
+    __shared__ uint32_t sdense;   // a voxel of the bucket holds more than kBkDense points
     // the bucket's run in every group, and its item offset in the cloud (points of the earlier
     // buckets: sum over the groups of row[b] - row[0])
     uint32_t gc = 0, gsum = 0;
@@ -1358,6 +1359,7 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
     if (threadIdx.x < ng) og[threadIdx.x] = gex;
     if (threadIdx.x == kBkT3 - 1) og[ng] = gex + gc;
     for (uint32_t e = threadIdx.x; e <= nsub; e += kBkT3) tab[e] = 0;
+    if (threadIdx.x == 0) sdense = 0u;
     __syncthreads();
     uint32_t ioff = 0;
 #pragma unroll
@@ -1464,7 +1466,9 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
     FLT_STAMP(1, f, 4);
     // input order inside each voxel: rank by crop-slot position among the voxel's points.  A
     // voxel past kBkDense points would cost cnt^2 LDS reads in this one block (4,096 points: ~16 M,
-    // more than the whole frame): such a frame is redone on the LSD chain instead
+    // more than the whole frame): such a frame is redone on the LSD chain instead,
+    // and the block stops here -- no rank, no sums (dense points left r = 0, so every
+    // one of them summed the whole voxel)
     uint32_t head = 0, fin[kBkItems3];
 #pragma unroll
     for (int j = 0; j < kBkItems3; ++j) {
@@ -1473,7 +1477,7 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
             const uint32_t st = tab[sub[j]] & 0xffffu;
             const uint32_t cnt = (tab[sub[j] + 1] & 0xffffu) - st;
             uint32_t r = 0;
-            if (cnt > (uint32_t)kBkDense) bk_redo(res);
+            if (cnt > (uint32_t)kBkDense) sdense = 1u;
             else
                 for (uint32_t u = st; cnt > 1 && u < st + cnt; ++u) r += p1[u] < pos[j] ? 1u : 0u;
             fin[j] = st + r;
@@ -1481,6 +1485,13 @@ k_bk_sort(const JobBatch jobs, int k, uint32_t *__restrict__ res, uint2 *__restr
         }
     }
     __syncthreads();   // every rank read p1 before it holds xyz indices
+    if (sdense) {   // uniform: the host redoes the frame on the LSD chain
+        if (threadIdx.x == 0) {
+            bk_redo(res);
+            bkv[f] = make_uint2(0u, ioff);
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < kBkItems3; ++j) {
         const uint32_t q = (uint32_t)j * kBkT3 + threadIdx.x;

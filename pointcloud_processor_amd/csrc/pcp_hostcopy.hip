@@ -27,8 +27,10 @@ constexpr size_t kSplitMin = 256u << 10;
 constexpr int kMaxHelpers = 7;
 constexpr auto kSpin = std::chrono::microseconds(300);
 // every part of a split copy is non-empty, so every helper takes part in every job exactly once
-// (its one decrement of `pending` per job generation is what the caller waits for)
-static_assert(kSplitMin >= (size_t)(kMaxHelpers + 1) * 4096 * 2, "parts must be non-empty");
+// (its one decrement of `pending` per job generation is what the caller waits for).  With k
+// parts of per = ceil(n / k) rounded up to 4 KiB < n / k + 4096 bytes, the last part starts at
+// (k - 1) per < n whenever n > k (k - 1) 4096 (2 k 4096 did not imply it)
+static_assert(kSplitMin > (size_t)(kMaxHelpers + 1) * kMaxHelpers * 4096, "parts must be non-empty");
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
 }  // namespace

@@ -16,6 +16,19 @@
  *  - sqrtf and float division: correctly rounded on both sides (IEEE); written through double,
  *    which is exact-then-rounded-once for both operations at float precision.
  * Compile with -ffp-contract=off: every other operation must round on its own.
+ *
+ * Notices of the restated upstream code (its constants and control flow are reproduced here):
+ *
+ *   atanf / atan2f (fdlibm, as carried by glibc):
+ *   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+ *   Developed at SunPro, a Sun Microsystems, Inc. business.
+ *   Permission to use, copy, modify, and distribute this software is freely granted, provided
+ *   that this notice is preserved.
+ *
+ *   sinf / cosf / sincosf.h (Arm optimized-routines, as carried by glibc 2.35):
+ *   Copyright (c) 2018 Arm Ltd.  Contributed to the GNU C Library, which distributes it under
+ *   the GNU Lesser General Public License v2.1 or later; upstream Arm optimized-routines
+ *   license the same code under SPDX-License-Identifier: MIT OR Apache-2.0 WITH LLVM-exception.
  */
 #ifndef PCP_LIBM_H
 #define PCP_LIBM_H

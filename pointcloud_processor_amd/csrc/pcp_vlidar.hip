@@ -513,7 +513,11 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
     const double dot = ndx * (double)nx + ndy * (double)ny + ndz * (double)nz;
     const double theta = acos(fmax(0.0, fmin(1.0, fabs(dot))));
     const double score = 1.0 * sin(kPi / 2 - theta) + 1.0 * (1.0 / L);
+#if PCP_SCORE_ULP   // parity-bar check build only (make perturb): every cell score one ulp up
+    return fmax(0.0, nextafter(score, INFINITY));
+#else
     return fmax(0.0, score);
+#endif
 }
 
 // one thread per (cell c, row r): rows r < P are the candidate poses (evaluatePosition's

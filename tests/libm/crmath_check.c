@@ -10,7 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "pcp_crmath.h"
+#include "crmath_extra.h"
 
 static uint64_t s = 0x9E3779B97F4A7C15ull;
 static uint64_t rnd(void) {
