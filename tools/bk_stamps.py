@@ -10,11 +10,12 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
-import torch  # noqa: F401,E402  (torch's HIP runtime first, as bench.py does)
-
 from pointcloud_processor_amd import _abi, synth  # noqa: E402
 
-DIAG = ROOT / "pointcloud_processor_amd" / "_lib" / "diag" / "libpcp.so"
+import os  # noqa: E402
+
+DIAG = os.environ.get("PCP_DIAG_LIB", str(ROOT / "pointcloud_processor_amd" / "_lib" / "diag" /
+                                         "libpcp.so"))
 ctx = _abi.Context(0, lib_path=DIAG)
 lib = ctx.lib
 lib.pcp_diag_filter_stamps.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_size_t]
@@ -42,6 +43,22 @@ if len(e):
     print("k_bk_emit", f"blocks {len(e)}", f"span {(e[:, 2].max() - t0) * 10 / 1000:.2f} us",
           f"start spread {(e[:, 0].max() - t0) * 10 / 1000:.2f} us",
           f"prefix mean {d[:, 0].mean():.2f} max {d[:, 0].max():.2f} us, copy mean {d[:, 1].mean():.2f} max {d[:, 1].max():.2f} us")
+# the fused emit (PCP_BK_FUSE=1): phase 7 = after the look-back; rank + look-back = ph7 - ph4
+s1 = allst[1]
+m = (s1[:, 0] > 0) & (s1[:, 7] > 0)
+if m.any():
+    lb = (s1[m, 7] - s1[m, 4]) * 10 / 1000.0
+    pub = (s1[m, 3] - s1[m, 0]) * 10 / 1000.0
+    t0 = s1[m, 0].min()
+    print("k_bk_sort fused:", f"blocks {m.sum()}", f"rank+look-back mean {lb.mean():.2f} "
+          f"p50 {np.median(lb):.2f} p90 {np.percentile(lb, 90):.2f} max {lb.max():.2f} us",
+          f"publish at mean {pub.mean():.2f} us after start",
+          f"span {(s1[m, 6].max() - t0) * 10 / 1000:.2f} us")
+    idx = np.nonzero(m)[0]
+    for lo in range(0, len(idx), max(1, len(idx) // 8)):
+        sel = idx[lo:lo + max(1, len(idx) // 8)]
+        print(f"  buckets {sel[0]}-{sel[-1]}: start {(s1[sel, 0].mean() - t0) * 10 / 1000:.2f} us, "
+              f"look-back {((s1[sel, 7] - s1[sel, 4]) * 10 / 1000).mean():.2f} us")
 for which in (0, 1):
     st = np.zeros(4096 * 8, np.uint64)
     lib.pcp_diag_filter_stamps(ctx.h, which, st.ctypes.data, st.size)
