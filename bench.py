@@ -225,14 +225,14 @@ def _ulps(a, b) -> np.ndarray:
 
 
 def _totals_bar(got, ref) -> dict:
-    """tests/parity.py's bar for the per-pose totals: <= 4 ulps each, at most max(2, 10 %) not
+    """tests/parity.py's bar for the per-pose totals: <= 4 ulps each, at most max(2, 25 %) not
     bit-identical (the oracle scores with glibc's acos / sin, the kernels with ocml's)."""
     got, ref = np.asarray(got, np.float64).ravel(), np.asarray(ref, np.float64).ravel()
     if got.shape != ref.shape:
         return {"ok": False, "shape": [got.size, ref.size]}
     d = _ulps(got, ref) if got.size else np.zeros(0)
     n_diff = int((d != 0).sum())
-    return {"ok": bool(d.max(initial=0) <= 4 and n_diff <= max(2, math.ceil(0.1 * got.size))),
+    return {"ok": bool(d.max(initial=0) <= 4 and n_diff <= max(2, math.ceil(0.25 * got.size))),
             "max_ulps": float(d.max(initial=0)), "differ": n_diff, "n": int(got.size)}
 
 

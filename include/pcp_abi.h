@@ -153,6 +153,17 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds,
 int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const double *boxes,
                      float leaf, const pcp_rigid *tf, const uint8_t *rgb, void *out_xyzrgb32,
                      uint64_t cap, uint64_t *n_out, uint64_t *n_per_cloud, uint32_t flags);
+/* The launch file's filter node (both sensors) and merger node composed in one process (a
+ * component container; the C5 chain): per cloud i crop -> voxel(leaf), its centroids in its own
+ * frame into filtered[i] (host, clouds[i].n PointXYZ 16-B records at most: the node's
+ * /filtered_points message) AND all clouds transformed + coloured + concatenated into `out`
+ * (host, PointXYZRGB 32-B, cap records: pcp_filter_merge's output), ONE synchronisation.  Host
+ * memory in and out (message-sized clouds are read in place from pinned staging).
+ * n_per_cloud / n_cropped (nullable, k entries): centroids and cropped points of each cloud. */
+int pcp_filter_merge_nodes(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds,
+                           const double *boxes, float leaf, const pcp_rigid *tf,
+                           const uint8_t *rgb, void *out, uint64_t cap, uint64_t *n_out,
+                           uint64_t *n_per_cloud, float *const *filtered, uint64_t *n_cropped);
 
 /* ---- virtual_lidar (SimplifiedDualLidarOptimizer) -------------------------------------- */
 typedef struct pcp_vl_params {      /* virtual_lidar.cpp:66-71 */
@@ -203,6 +214,20 @@ int pcp_set_cells(pcp_ctx *ctx, const double *xyz, const float *normals, uint64_
  * `area` is host memory (the PointCloud2 data blob). */
 int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
                             int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells);
+/* The same setup, enqueued on the context's stream and NOT waited for (a composed chain: the
+ * terrain and zx120 indices and the tick are enqueued behind it while it runs).  grid_bbox as
+ * above (host arithmetic, exact at return); cells_cap: the lattice's points, an upper bound of
+ * the cell count.  The count is settled -- and the neighbour lists regrown and rerun, should
+ * they have overflowed -- by the next call that needs it: pcp_generate_and_score does so after
+ * its own synchronisation (ONE wait for both; its cell_flags must then hold cells_cap bytes,
+ * are taken as fresh GridCells -- all clear, :259 -- and come back for the settled count), every
+ * other call that reads the cells (pcp_score_poses, pcp_get_cells, pcp_set_cells, the multi
+ * calls, another setup) before it starts.  Results are identical to pcp_set_excavation_area's. */
+int pcp_set_excavation_area_async(pcp_ctx *ctx, const pcp_cloud_view *area,
+                                  double grid_resolution, int32_t vertical_layers,
+                                  double grid_bbox[6], uint64_t *cells_cap);
+/* the context's scoring cells (settles a pending setup: may wait for the stream) */
+int pcp_cells_count(pcp_ctx *ctx, uint64_t *n_cells);
 /* ---- excavated_surface_generator.cpp (ExcavationTerrainGenerator) ------------------------ */
 typedef struct pcp_excavation_params {   /* excavated_surface_generator.cpp:29-51 */
     double depth;                 /* excavation.depth 1.0 */

@@ -119,10 +119,15 @@ _SIGS = [
     ("pcp_filter_merge", C.c_int, [_P, C.c_int, C.POINTER(CloudView), _P, C.c_float,
                                    C.POINTER(Rigid), _P, _P, C.c_uint64, C.POINTER(C.c_uint64),
                                    _P, C.c_uint32]),
+    ("pcp_filter_merge_nodes", C.c_int, [_P, C.c_int, C.POINTER(CloudView), _P, C.c_float,
+                                         C.POINTER(Rigid), _P, _P, C.c_uint64,
+                                         C.POINTER(C.c_uint64), _P, _P, _P]),
     ("pcp_set_terrain", C.c_int, [_P, C.POINTER(CloudView)]),
     ("pcp_set_aux_cloud", C.c_int, [_P, C.POINTER(CloudView)]),
     ("pcp_set_cells", C.c_int, [_P, _P, _P, C.c_uint64]),
     ("pcp_set_excavation_area", C.c_int, [_P, _P, C.c_double, C.c_int32, _P, _P]),
+    ("pcp_set_excavation_area_async", C.c_int, [_P, _P, C.c_double, C.c_int32, _P, _P]),
+    ("pcp_cells_count", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("pcp_get_cells", C.c_int, [_P, _P, _P, C.c_uint64, _P]),
     ("pcp_get_area_normals", C.c_int, [_P, _P, C.c_uint64, _P]),
     ("pcp_excavate", C.c_int, [_P, _P, _P, _P, _P, C.c_uint64, _P, _P, C.c_uint64, _P, _P]),
@@ -433,6 +438,27 @@ class Context:
         res = out[: n.value].copy() if own else out[: n.value]
         return res, per[:k].copy()
 
+    def filter_merge_nodes(self, clouds, boxes, leaf, tfs, rgbs):
+        """pcp_filter_merge_nodes: the filter node (every cloud) and the merger node in one call
+        -> (merged float32 [n, 8], [each cloud's centroids float32 [n_i, 4]], n_cropped)."""
+        k = len(clouds)
+        views = (CloudView * max(k, 1))(*[cloud_view(c) for c in clouds])
+        total = sum(c.shape[0] for c in clouds)
+        out = np.empty((max(total, 1), 8), np.float32)
+        filt = [np.empty((max(c.shape[0], 1), 4), np.float32) for c in clouds]
+        fptr = (C.c_void_p * max(k, 1))(*[f.ctypes.data for f in filt])
+        rgb = np.ascontiguousarray(np.asarray(rgbs, np.uint8).reshape(-1))
+        bx = np.ascontiguousarray(np.asarray(boxes, np.float64).reshape(-1))
+        n = C.c_uint64()
+        per = np.zeros(max(k, 1), np.uint64)
+        crop = np.zeros(max(k, 1), np.uint64)
+        self._check(self.lib.pcp_filter_merge_nodes(self.h, k, views, _ptr(bx), C.c_float(leaf),
+                                                    self._rigids(tfs), _ptr(rgb), _ptr(out),
+                                                    total, C.byref(n), _ptr(per), fptr,
+                                                    _ptr(crop)), "pcp_filter_merge_nodes")
+        return (out[: n.value].copy(), [f[: int(p)].copy() for f, p in zip(filt, per[:k])],
+                crop[:k].copy())
+
     def filter_merge_device(self, views, boxes, leaf, tfs, rgbs, out_dev: int, cap: int):
         """Device-resident pipeline (benchmark): views hold device pointers."""
         k = len(views)
@@ -504,6 +530,25 @@ class Context:
                                                       C.byref(n)), "pcp_set_excavation_area")
         self.n_cells = n.value
         return bbox, n.value
+
+    def set_excavation_area_async(self, area: np.ndarray, grid_resolution: float = 0.1,
+                                  vertical_layers: int = 10, point_step=None, offs=(0, 4, 8)):
+        """pcp_set_excavation_area_async: the same setup enqueued, not waited for.  Returns
+        (grid_bbox (6,), cells_cap): the count is settled by the next call that needs it
+        (cells_count(), generate_and_score with a cells_cap-sized flag array, ...)."""
+        v = cloud_view(area, point_step, offs)
+        bbox = np.zeros(6, np.float64)
+        n = C.c_uint64()
+        self._check(self.lib.pcp_set_excavation_area_async(
+            self.h, C.byref(v), float(grid_resolution), int(vertical_layers), _ptr(bbox),
+            C.byref(n)), "pcp_set_excavation_area_async")
+        return bbox, n.value   # (the host bytes are copied or staged before the return)
+
+    def cells_count(self) -> int:
+        n = C.c_uint64()
+        self._check(self.lib.pcp_cells_count(self.h, C.byref(n)), "pcp_cells_count")
+        self.n_cells = n.value
+        return n.value
 
     def get_cells(self):
         n = C.c_uint64()

@@ -167,6 +167,72 @@ GnssGicpMatcher::Output GnssGicpMatcher::processPointClouds(bool origin_set,
     return o;
 }
 
+// ---- filter + merger composed ------------------------------------------------------------------
+ComposedFilterMerge::Output ComposedFilterMerge::frame(const PointCloud2 &robot,
+                                                       const PointCloud2 &backhoe, bool origin_set,
+                                                       const Transform *robot_tf,
+                                                       const Transform *zx120_tf) {
+    err_.clear();
+    Output o;
+    o.robot_filtered = make_xyz_cloud(nullptr, 0, robot.frame_id);
+    o.robot_filtered.stamp = robot.stamp;
+    o.backhoe_filtered = make_xyz_cloud(nullptr, 0, backhoe.frame_id);
+    o.backhoe_filtered.stamp = backhoe.stamp;
+    o.merge.merged = make_xyzrgb_cloud(nullptr, 0, "map");
+    o.merge.robot_colored = o.merge.merged;
+    o.merge.backhoe_colored = o.merge.merged;
+    pcp_cloud_view v[2];
+    if (!cloud_view(robot, v[0], &err_) || !cloud_view(backhoe, v[1], &err_)) return o;
+    // cropFrontArea's boxes (:93-101, :111-113), downsampleCloud's leaf
+    const double boxes[12] = {0.0, p_.robot_front_range, -p_.robot_side_range, p_.robot_side_range,
+                              -1.5, p_.robot_height_range,
+                              0.0, p_.backhoe_front_range, -p_.backhoe_side_range,
+                              p_.backhoe_side_range, -1.5, p_.backhoe_height_range};
+    // the merge's clouds: the TFs found (a missing one drops that cloud from the concatenation)
+    const Transform *tfs[2] = {robot_tf, zx120_tf};
+    pcp_rigid tf[2];
+    uint8_t rgb[6] = {255, 0, 0, 0, 0, 255};   // red robot, blue zx120 (:376-387)
+    for (int i = 0; i < 2; ++i) {
+        const Transform *t = tfs[i] ? tfs[i] : tfs[1 - i];   // (placeholder: the cloud is dropped)
+        if (t) {
+            std::memcpy(tf[i].t, t->t, sizeof(tf[i].t));
+            std::memcpy(tf[i].q, t->q, sizeof(tf[i].q));
+        } else {
+            tf[i] = pcp_rigid{{0, 0, 0}, {0, 0, 0, 1}};
+        }
+    }
+    float *outs[2] = {landing(rf_, 4 * (v[0].n ? v[0].n : 1)), landing(zf_, 4 * (v[1].n ? v[1].n : 1))};
+    const uint64_t cap = v[0].n + v[1].n;
+    uint8_t *mrg = landing(merged_, 32 * (cap ? cap : 1));
+    uint64_t n = 0, per[2] = {0, 0}, crop[2] = {0, 0};
+    if (pcp_filter_merge_nodes(dev_.ctx(), 2, v, boxes, (float)p_.voxel_leaf_size, tf, rgb, mrg,
+                               cap, &n, per, outs, crop) != PCP_OK) {
+        err_ = dev_.error();
+        return o;
+    }
+    o.robot_filtered = make_xyz_cloud(outs[0], per[0], robot.frame_id);
+    o.robot_filtered.stamp = robot.stamp;
+    o.backhoe_filtered = make_xyz_cloud(outs[1], per[1], backhoe.frame_id);
+    o.backhoe_filtered.stamp = backhoe.stamp;
+    if (!origin_set) return o;   // :309
+    // the concatenation of the clouds whose TF was found, robot first (:316-325)
+    uint64_t base = 0, keep_n = 0;
+    std::vector<uint8_t> cat;
+    const bool both = robot_tf && zx120_tf;
+    for (int i = 0; i < 2; ++i) {
+        PointCloud2 part = make_xyzrgb_cloud(mrg + 32 * base, per[i], "map");
+        if (tfs[i]) (i == 0 ? o.merge.robot_colored : o.merge.backhoe_colored) = part;
+        if (tfs[i] && !both) {
+            cat.assign(mrg + 32 * base, mrg + 32 * (base + per[i]));
+            keep_n = per[i];
+        }
+        base += per[i];
+    }
+    o.merge.merged = both ? make_xyzrgb_cloud(mrg, n, "map")
+                          : make_xyzrgb_cloud(cat.data(), keep_n, "map");
+    return o;
+}
+
 // ---- virtual_lidar ---------------------------------------------------------------------------
 void SimplifiedDualLidarOptimizer::terrainCallback(const PointCloud2 &msg) {
     err_.clear();
@@ -204,6 +270,18 @@ bool SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg
     if (msg.empty()) return false;   // :168
     double bb[6];
     uint64_t n = 0;
+    if (defer_grid_) {   // composed chain: enqueued, settled by the next tick
+        if (pcp_set_excavation_area_async(dev_.ctx(), &v, p_.grid_resolution, p_.vertical_layers,
+                                          bb, &n) != PCP_OK) {
+            err_ = dev_.error();
+            return false;
+        }
+        n_cells_ = n;                 // the capacity: the flags' bytes until settled
+        grid_pending_ = n != 0;
+        flags_.assign(n_cells_, 0);   // fresh GridCells (:259)
+        std::memcpy(bbox_, bb, sizeof(bbox_));
+        return true;
+    }
     if (pcp_set_excavation_area(dev_.ctx(), &v, p_.grid_resolution, p_.vertical_layers, bb, &n) !=
         PCP_OK) {
         err_ = dev_.error();   // "Failed to process excavation area" (:175-177)
@@ -225,10 +303,25 @@ bool SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg
     return true;
 }
 
+size_t SimplifiedDualLidarOptimizer::lastCells() {
+    if (grid_pending_) {
+        uint64_t n = 0;
+        if (pcp_cells_count(dev_.ctx(), &n) == PCP_OK) {
+            n_cells_ = n;
+            flags_.resize(n_cells_);
+        } else {
+            err_ = dev_.error();
+        }
+        grid_pending_ = false;
+    }
+    return n_cells_;
+}
+
 void SimplifiedDualLidarOptimizer::setExcavationGrid(const std::vector<double> &xyz,
                                                      const std::vector<float> &normals,
                                                      const double grid_bbox[6]) {
     err_.clear();
+    grid_pending_ = false;   // (pcp_set_cells settles a pending setup first)
     n_cells_ = xyz.size() / 3;
     flags_.assign(n_cells_, 0);   // fresh GridCells (:259, ctor :34-43)
     std::memcpy(bbox_, grid_bbox, sizeof(bbox_));
@@ -344,12 +437,20 @@ SimplifiedDualLidarOptimizer::Result SimplifiedDualLidarOptimizer::runOptimizati
         rc = pcp_multi_score_poses(multi_, poses.data(), n, zx, &p, flags_.data(), totals.data(),
                                    nullptr, &r.report);
     } else {   // generateCandidatePositions + the candidate loop, one round trip
+        // (a deferred grid: flags_ holds the capacity's fresh bytes, settled by this call)
         rc = pcp_generate_and_score(dev_.ctx(), bbox_, &p, zx, poses.data(), poses.size() / 5, &n,
                                     flags_.data(), totals.data(), nullptr, &r.report);
     }
     if (rc != PCP_OK) {
         err_ = multi_ ? pcp_multi_last_error(multi_) : dev_.error();
+        grid_pending_ = false;
         return r;
+    }
+    if (grid_pending_) {   // the tick settled the deferred grid: its count is final now
+        lastCells();
+        // :455 -- the reference never ticks over an empty grid (the results of the tick that
+        // settled it are discarded, as if it had returned early)
+        if (n_cells_ == 0) return Result{};
     }
     r.ran = true;
     r.candidates.resize(n);

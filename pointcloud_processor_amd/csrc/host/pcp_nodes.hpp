@@ -137,6 +137,32 @@ class GnssGicpMatcher {
     std::string err_;
 };
 
+// ---- the filter node (both sensors) + the merger node, composed in one process ----------------
+// (a component container / the C5 chain): per frame ONE call, pcp_filter_merge_nodes -- both
+// /filtered_points messages exactly as SimplifiedScanMatcher publishes them and the merged cloud
+// exactly as GnssGicpMatcher::processPointClouds publishes it, with one synchronisation instead
+// of three.  Transforms: nullptr = the TF lookup threw, that robot is skipped in the merge (its
+// filtered message is still produced), as the two nodes do.
+class ComposedFilterMerge {
+   public:
+    explicit ComposedFilterMerge(Device &dev) : dev_(dev) {}
+    ComposedFilterMerge(Device &dev, const SimplifiedScanMatcher::Params &p) : dev_(dev), p_(p) {}
+    struct Output {
+        PointCloud2 robot_filtered, backhoe_filtered;   // the filter node's two messages
+        GnssGicpMatcher::Output merge;                  // the merger node's outputs
+    };
+    Output frame(const PointCloud2 &robot, const PointCloud2 &backhoe, bool origin_set,
+                 const Transform *robot_tf, const Transform *zx120_tf);
+    const std::string &lastError() const { return err_; }
+
+   private:
+    Device &dev_;
+    SimplifiedScanMatcher::Params p_;
+    std::vector<uint8_t> merged_;
+    std::vector<float> rf_, zf_;
+    std::string err_;
+};
+
 // ---- excavated_surface_generator.cpp (ExcavationTerrainGenerator) --------------------------
 class ExcavationTerrainGenerator {
    public:
@@ -240,7 +266,13 @@ class SimplifiedDualLidarOptimizer {
     // runOptimization (:454-548); zx120_base = TF map -> zx120/base_link, nullptr = missing
     Result runOptimization(const Transform *zx120_base);
     const std::vector<uint8_t> &cellFlags() const { return flags_; }
-    size_t lastCells() const { return n_cells_; }
+    // settles a pending deferred grid first (may wait for the device)
+    size_t lastCells();
+    // composed chain (intra-process nodes, e.g. the C5 replay): excavationAreaCallback enqueues
+    // the grid setup and returns without waiting (pcp_set_excavation_area_async); the next
+    // runOptimization waits once for both.  Off by default: a ROS shell publishes the grid
+    // markers from the area callback, which needs the cells there
+    void setDeferredGrid(bool on) { defer_grid_ = on && !multi_; }
     const std::string &lastError() const { return err_; }
 
    private:
@@ -249,7 +281,9 @@ class SimplifiedDualLidarOptimizer {
     Params p_;
     bool terrain_cloud_ = false;   // terrain_cloud_ non-null (a message arrived)
     size_t zx120_size_ = 0;        // zx120_cloud_->size() (:433-434)
-    size_t n_cells_ = 0;
+    size_t n_cells_ = 0;           // deferred: the lattice's capacity until settled
+    bool defer_grid_ = false;
+    bool grid_pending_ = false;    // a deferred setup whose count is not settled yet
     double bbox_[6] = {0, 0, 0, 0, 0, 0};
     std::vector<uint8_t> flags_;   // GridCell flag state across ticks
     std::string err_;

@@ -212,8 +212,18 @@ static int cmd_replay(Device &dev, char **a) {
     const std::string dump = (a[8] && a[9]) ? a[9] : "";
     SimplifiedScanMatcher filt(dev);
     GnssGicpMatcher merger(dev);
+    ComposedFilterMerge front(dev);
+    bool front_fused = true;
+    if (const char *ff = std::getenv("PCP_FRONT_FUSED")) front_fused = std::atoi(ff) != 0;
     ExcavationTerrainGenerator gen(dev);
     SimplifiedDualLidarOptimizer vl(dev);
+    // the nodes composed in one process: the grid setup is enqueued by the area callback and
+    // waited for once by the tick (PCP_AREA_ASYNC=0: settled in the area callback, as a ROS shell
+    // that publishes the grid markers there)
+    {
+        const char *ea = std::getenv("PCP_AREA_ASYNC");
+        vl.setDeferredGrid(!ea || std::atoi(ea) != 0);
+    }
     vl.terrainCallback(cloud_from(t, tn, 32, "map"));
     std::vector<double> xyz(cn * 3);
     std::vector<float> nrm(cn * 3);
@@ -247,13 +257,30 @@ static int cmd_replay(Device &dev, char **a) {
             last = now;
         };
         // pointcloud_filter: both sensors; pointcloud_merger: 10 Hz tick; virtual_lidar: zx120
-        // filtered cloud + the pose search
-        PointCloud2 rf = filt.robotCloudCallback(rm), zf = filt.backhoeCloudCallback(zm);
-        lap(0);
-        merger.robotCloudCallback(rf);
-        merger.backhoeCloudCallback(zf);
-        auto o = merger.processPointClouds(true, &robot_tf, &zx_tf);
-        lap(1);
+        // filtered cloud + the pose search.  Composed (PCP_FRONT_FUSED, default): the filter
+        // and merger nodes in one call and one synchronisation (stage "filter" then holds both)
+        PointCloud2 rf, zf;
+        GnssGicpMatcher::Output o;
+        if (front_fused) {
+            auto fo = front.frame(rm, zm, true, &robot_tf, &zx_tf);
+            if (!front.lastError().empty()) {
+                std::fprintf(stderr, "replay: filter+merge failed: %s\n", front.lastError().c_str());
+                return 1;
+            }
+            rf = std::move(fo.robot_filtered);
+            zf = std::move(fo.backhoe_filtered);
+            o = std::move(fo.merge);
+            lap(0);
+            lap(1);
+        } else {
+            rf = filt.robotCloudCallback(rm);
+            zf = filt.backhoeCloudCallback(zm);
+            lap(0);
+            merger.robotCloudCallback(rf);
+            merger.backhoeCloudCallback(zf);
+            o = merger.processPointClouds(true, &robot_tf, &zx_tf);
+            lap(1);
+        }
         ExcavationTerrainGenerator::Output e;
         if (chain) {
             e = gen.matchedCloudCallback(o.merged, &zx_base);
@@ -266,12 +293,12 @@ static int cmd_replay(Device &dev, char **a) {
             lap(3);
             vl.terrainCallback(e.excavated_terrain);
             lap(4);
-            cells_n = vl.lastCells();
         }
         vl.zx120PointsCallback(zf);
         lap(5);
         auto r = vl.runOptimization(&zx_base);
         lap(6);
+        if (chain) cells_n = vl.lastCells();   // (settled by the tick)
         const auto t1 = std::chrono::steady_clock::now();
         if (f >= 2)
             for (int k = 0; k < kStages; ++k) {

@@ -520,7 +520,8 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->res_host.release();
     ctx->fm_res_host.release();
     ctx->small_host.release();
-    DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->stage, &ctx->fan_tab,
+    ctx->area_host.release();
+    DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->cells_n_d, &ctx->stage, &ctx->fan_tab,
                       &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,
                       &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->f_in,
                       &ctx->f_misc,    &ctx->bk_stat};

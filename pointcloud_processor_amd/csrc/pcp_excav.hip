@@ -1087,19 +1087,120 @@ k_cell_normals(GridView g, float r2, const double *__restrict__ cells,
 
 }  // namespace pcp
 
-using namespace pcp;
+namespace pcp {
 
-extern "C" {
+// the exact normals' two phases over the device-resident setup (pcp_set_excavation_area):
+// the area's sorted lists + ordered sums, and the cells' (order-free exact sums, then the lists
+// and sums of the cells they leave).  Everything they read is on the device: the indices
+// (exc_norm), the points by input index (nb_pts), the lattice and its count (cells_xyz,
+// cells_n_d), so an overflow can rerun them long after the raw records are gone.
+static void nb_area_launch(pcp_ctx *ctx, hipStream_t st) {
+    const GridView gn = ctx->exc_norm.view();
+    const float r2n = (float)(kNormalRadius * kNormalRadius), bscale = (float)kNbBuckets / r2n;
+    const uint32_t grid_a = ctx->area_grid_a, npts = ctx->area_npts;
+    const uint64_t n = ctx->area_n;
+    uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
+    const NbLists La{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
+                     (uint32_t)(std::min<uint64_t>(ctx->nb_list.cap / 4, 0xffffffffull) / grid_a)};
+    hipLaunchKernelGGL(k_nb_lists<false>, dim3(grid_a), dim3(kNbT), 0, st, gn, r2n, bscale,
+                       (const double *)nullptr, (const uint32_t *)nullptr, La,
+                       (const uint32_t *)nullptr);
+    hipLaunchKernelGGL(k_nb_sums<false>, dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB),
+                       dim3(kNbT), 0, st, gn, (const uint2 *)La.meta, (const uint32_t *)La.list,
+                       (const uint32_t *)nullptr, (const float4 *)ctx->nb_pts.as<float4>(),
+                       ctx->area_nrm.as<float>(), ctx->nb_pts.as<float4>() + n, ctl,
+                       (uint32_t *)nullptr, (const uint32_t *)nullptr);
+}
+static void nb_cells_launch(pcp_ctx *ctx, hipStream_t st) {
+    const GridView gn = ctx->exc_norm.view();
+    const float r2n = (float)(kNormalRadius * kNormalRadius), bscale = (float)kNbBuckets / r2n;
+    const uint32_t grid_c = ctx->area_grid_c;
+    const uint64_t total = ctx->area_total;
+    uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
+    uint32_t *sel = ctx->nb_sel.as<uint32_t>();
+    const uint32_t *n_d = ctx->cells_n_d.as<uint32_t>();
+    const float4 *nrm4 = ctx->nb_pts.as<float4>() + ctx->area_n;
+    uint32_t *n_h = ctx->area_host.as<uint32_t>();
+    const NbLists Lc{ctx->nb_list_c.as<uint32_t>(), ctx->nb_meta_c.as<uint2>(), ctl + 1, ctl + 2,
+                     (uint32_t)(std::min<uint64_t>(ctx->nb_list_c.cap / 4, 0xffffffffull) / grid_c)};
+    if (total) {
+        hipLaunchKernelGGL(k_cell_sums_exact, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n,
+                           (const double *)ctx->cells_xyz.as<double>(), n_d, nrm4,
+                           ctx->cells_nrm.as<float>(), sel, ctx->cells_all_ordered ? 1 : 0);
+        hipLaunchKernelGGL(k_nb_lists<true>, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n, bscale,
+                           (const double *)ctx->cells_xyz.as<double>(), n_d, Lc,
+                           (const uint32_t *)sel);
+    }
+    // launched for an empty selection too: it lands both lists' uses and the overflow word in
+    // area_host[1..3], and clears the control words
+    constexpr int QB = NbCfg<true>::QB;
+    hipLaunchKernelGGL(k_nb_sums<true>,
+                       dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>((total + QB - 1) / QB,
+                                                                                4096))),
+                       dim3(kNbT), 0, st, gn, (const uint2 *)Lc.meta, (const uint32_t *)Lc.list,
+                       n_d, nrm4, ctx->cells_nrm.as<float>(), (float4 *)nullptr, ctl, n_h + 1,
+                       (const uint32_t *)(total ? sel : nullptr));
+}
 
-int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
-                            int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells) {
+bool area_overflowed(const pcp_ctx *ctx) {
+    return ctx->area_host.p && ctx->area_host.as<const uint32_t>()[3] != 0u;
+}
+
+int area_finish(pcp_ctx *ctx) {
+    if (!ctx->area_pending) return PCP_OK;
+    hipStream_t st = ctx->stream;
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    uint32_t *n_h = ctx->area_host.as<uint32_t>();
+    if (n_h[3]) {
+        // a list buffer too small (first frames, or a denser area): regrow both to their largest
+        // block's use x the grid and run the normals again (the lattice and the records stand;
+        // the cells' order-free pass too, over the new area normals)
+        ctx->nb_need = std::max<uint64_t>(ctx->nb_need, (uint64_t)n_h[1] * ctx->area_grid_a);
+        ctx->nb_need_c = std::max<uint64_t>(ctx->nb_need_c, (uint64_t)n_h[2] * ctx->area_grid_c);
+        if (std::max(ctx->nb_need, ctx->nb_need_c) > 0xffffffffull) {
+            ctx->area_pending = false;
+            return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: %llu neighbour list "
+                           "words (32-bit list offsets)",
+                           (unsigned long long)std::max(ctx->nb_need, ctx->nb_need_c));
+        }
+        PCP_HIP(ctx, ctx->nb_list.ensure(ctx->nb_need * 4 + 64));
+        PCP_HIP(ctx, ctx->nb_list_c.ensure(ctx->nb_need_c * 4 + 64));
+        ctx->normals_regrown++;
+        n_h[1] = n_h[2] = n_h[3] = 0;   // (the control words: cleared by k_nb_sums<true>)
+        PCP_HIP(ctx, hipMemsetAsync(ctx->nb_sel.p, 0, sizeof(uint32_t), st));
+        nb_area_launch(ctx, st);
+        PCP_CHECK_LAUNCH(ctx);
+        nb_cells_launch(ctx, st);
+        PCP_CHECK_LAUNCH(ctx);
+        PCP_HIP(ctx, hipStreamSynchronize(st));
+        if (n_h[3]) {
+            ctx->area_pending = false;
+            return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: neighbour lists "
+                                                "overflowed after regrowing");
+        }
+    }
+    ctx->nb_need = std::max<uint64_t>(ctx->nb_need, (uint64_t)n_h[1] * ctx->area_grid_a);
+    ctx->nb_need_c = std::max<uint64_t>(ctx->nb_need_c, (uint64_t)n_h[2] * ctx->area_grid_c);
+    ctx->nb_ctl_zero = true;   // k_nb_sums<true> (always launched on this path) cleared them
+    ctx->n_cells = n_h[0];
+    ctx->area_pending = false;
+    prof_resolve(ctx);
+    return PCP_OK;
+}
+
+// pcp_set_excavation_area (defer = false: settled before the return) and its _async form
+static int area_setup(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
+                      int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells,
+                      bool defer) {
     if (!ctx) return PCP_E_INVALID;
     int rc = check_view(ctx, area, "pcp_set_excavation_area");
     if (rc) return rc;
     if (!(grid_resolution > 0.0))
         return set_err(ctx, PCP_E_INVALID, "pcp_set_excavation_area: grid_resolution must be > 0");
     PCP_HIP(ctx, hipSetDevice(ctx->device));
-    if (n_cells) *n_cells = ctx->n_cells;
+    // a setup still pending is settled first (its lists may need a rerun)
+    if ((rc = area_finish(ctx))) return rc;
+    if (n_cells) *n_cells = defer ? ctx->cells_cap : ctx->n_cells;
     if (area->n == 0) return PCP_OK;   // :168, nothing is rebuilt; the previous cells stay
     ProfScope prof(ctx, PCP_K_EXCAV_SETUP);
     const double r_near = grid_resolution * 1.5;
@@ -1115,6 +1216,7 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
         PCP_HIP(ctx, hipMemsetAsync(ctx->area_nrm.p, 0xff, n * 3 * sizeof(float), ctx->stream));
         pin_release(ctx, ctx->stream);
         ctx->n_cells = 0;
+        ctx->cells_cap = 0;
         if (n_cells) *n_cells = 0;
         return PCP_OK;
     }
@@ -1147,11 +1249,12 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
                        (unsigned long long)total);
     L.total = (uint32_t)total;
     const bool exact = ctx->normals_exact;
-    PCP_HIP(ctx, ctx->small_host.ensure(4096));
-    uint32_t *n_h = ctx->small_host.as<uint32_t>();
+    defer = defer && exact;   // (the order-free A/B kernels settle before the return)
+    PCP_HIP(ctx, ctx->area_host.ensure(64));
+    uint32_t *n_h = ctx->area_host.as<uint32_t>();
     n_h[1] = n_h[2] = n_h[3] = 0;   // the lists' largest block uses + overflow (exact path)
-    PCP_HIP(ctx, ctx->out_c.ensure(64));
-    uint32_t *n_d = ctx->out_c.as<uint32_t>();
+    PCP_HIP(ctx, ctx->cells_n_d.ensure(64));
+    uint32_t *n_d = ctx->cells_n_d.as<uint32_t>();
     // the lattice of candidate cells (:258-298) on stream st.  Its buffers are sized after the
     // raw records' last reader was launched: a large area's raw records may sit in ctx->stage,
     // which the lattice flags reuse (a reallocation frees it only after the device drained)
@@ -1188,134 +1291,95 @@ int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double gri
             PCP_CHECK_LAUNCH(ctx);
         }
         PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    } else {
-        // The sorted neighbour lists: the area's (nb_list / nb_meta) and the cells' (nb_list_c /
-        // nb_meta_c), one region per k_nb_lists block, words as the previous call needed (first
-        // guess n x min(n, 4096)), regrown on overflow to the largest block's use x the grid.
-        // The cells go through k_cell_sums_exact first (any order where no order can change
-        // the sums); only those it leaves in nb_sel take the ordered lists.  Every buffer is
-        // sized before the launches.
-        const float bscale = (float)kNbBuckets / r2n;
-        const uint32_t nbb = ctx->nb_blocks > 0 ? (uint32_t)ctx->nb_blocks : (uint32_t)kNbBlocks;
-        const uint32_t grid_a = std::min<uint32_t>(npts, nbb);
-        const uint32_t grid_c =
-            (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(total, nbb));
-        const uint64_t per_pt = std::min<uint64_t>(npts, 4096);
-        const uint64_t guess_a = std::min<uint64_t>((uint64_t)npts * per_pt, 64ull << 20);
-        const uint64_t guess_c = std::min<uint64_t>(std::max<uint64_t>(total, 1) * per_pt, 64ull << 20);
-        PCP_HIP(ctx, ctx->nb_list.ensure(std::max<uint64_t>(guess_a, ctx->nb_need) * 4 + 64));
-        PCP_HIP(ctx, ctx->nb_list_c.ensure(std::max<uint64_t>(guess_c, ctx->nb_need_c) * 4 + 64));
-        PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)npts * sizeof(uint2) + 64));
-        PCP_HIP(ctx, ctx->nb_meta_c.ensure((size_t)total * sizeof(uint2) + 64));
-        PCP_HIP(ctx, ctx->nb_sel.ensure(((size_t)total + 2) * sizeof(uint32_t)));
-        bool ctl_dirty = !ctx->nb_ctl_zero || !ctx->nb_ctl.p;   // control words not known zero
-        PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
-        ctx->nb_ctl_zero = false;   // set again once k_nb_sums<true> has cleared them
-        // nb_pts: the points by input index, then their normals as float4 (the sums' records)
-        PCP_HIP(ctx, ctx->nb_pts.ensure(2 * n * sizeof(float4) + 64));
-        uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
-        uint32_t *sel = ctx->nb_sel.as<uint32_t>();
-        const float4 *nrm4 = ctx->nb_pts.as<float4>() + n;
-        auto per_block = [](const DevBuf &b, uint32_t grid) {
-            return (uint32_t)(std::min<uint64_t>(b.cap / 4, 0xffffffffull) / grid);
-        };
-        hipStream_t st = ctx->stream;
-        auto area_lists_sums = [&]() -> int {
-            const NbLists La{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
-                             per_block(ctx->nb_list, grid_a)};
-            hipLaunchKernelGGL(k_nb_lists<false>, dim3(grid_a), dim3(kNbT), 0, st, gn, r2n, bscale,
-                               (const double *)nullptr, (const uint32_t *)nullptr, La,
-                               (const uint32_t *)nullptr);
-            PCP_CHECK_LAUNCH(ctx);
-            hipLaunchKernelGGL(k_nb_sums<false>,
-                               dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB), dim3(kNbT),
-                               0, st, gn, (const uint2 *)La.meta, (const uint32_t *)La.list,
-                               (const uint32_t *)nullptr, (const float4 *)ctx->nb_pts.as<float4>(),
-                               ctx->area_nrm.as<float>(), ctx->nb_pts.as<float4>() + n,
-                               (uint32_t *)ctl, (uint32_t *)nullptr,
-                               (const uint32_t *)nullptr);
-            PCP_CHECK_LAUNCH(ctx);
-            return PCP_OK;
-        };
-        // the cells: the order-free exact sums, then the ordered lists and sums of the cells
-        // left in sel (k_nb_sums<true> launched for an empty selection too: it lands both
-        // lists' uses and the overflow, and clears the control words)
-        auto cells = [&]() -> int {
-            const NbLists Lc{ctx->nb_list_c.as<uint32_t>(), ctx->nb_meta_c.as<uint2>(), ctl + 1,
-                             ctl + 2, per_block(ctx->nb_list_c, grid_c)};
-            if (total) {
-                hipLaunchKernelGGL(k_cell_sums_exact, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n,
-                                   (const double *)ctx->cells_xyz.as<double>(),
-                                   (const uint32_t *)n_d, nrm4, ctx->cells_nrm.as<float>(), sel,
-                                   ctx->cells_all_ordered ? 1 : 0);
-                PCP_CHECK_LAUNCH(ctx);
-                hipLaunchKernelGGL(k_nb_lists<true>, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n,
-                                   bscale, (const double *)ctx->cells_xyz.as<double>(),
-                                   (const uint32_t *)n_d, Lc, (const uint32_t *)sel);
-                PCP_CHECK_LAUNCH(ctx);
-            }
-            constexpr int QB = NbCfg<true>::QB;
-            hipLaunchKernelGGL(k_nb_sums<true>,
-                               dim3((unsigned)std::max<uint64_t>(
-                                   1, std::min<uint64_t>((total + QB - 1) / QB, 4096))),
-                               dim3(kNbT), 0, st, gn, (const uint2 *)Lc.meta,
-                               (const uint32_t *)Lc.list, (const uint32_t *)n_d, nrm4,
-                               ctx->cells_nrm.as<float>(), (float4 *)nullptr,
-                               (uint32_t *)ctl, n_h + 1,
-                               (const uint32_t *)(total ? sel : nullptr));
-            PCP_CHECK_LAUNCH(ctx);
-            return PCP_OK;
-        };
-        // the control words are zero: cleared by the previous call's last k_nb_sums<true> (or,
-        // on a fresh buffer, by this memset)
-        if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctl, 0, 16, st));
-        // first: the input points by input index for the sums' gathers, the non-finite points'
-        // NaN normals (k_area_prep is the raw records' last reader; the exact kernels never
-        // write those entries, so a rerun keeps them), and sel's count cleared
-        hipLaunchKernelGGL(k_area_prep, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0, st,
-                           rin, ctx->nb_pts.as<float4>(), ctx->area_nrm.as<float>(), sel);
-        PCP_CHECK_LAUNCH(ctx);
-        pin_release(ctx, st);
-        if (int rca = area_lists_sums()) return rca;
-        if (int rcl = lattice(st)) return rcl;
-        if (int rcs = cells()) return rcs;
-        PCP_HIP(ctx, hipStreamSynchronize(st));
-        if (n_h[3]) {
-            // a list buffer too small (first frames, or a denser area): regrow both to their
-            // largest block's use x the grid and run the normals again (the lattice and the
-            // records stand; the cells' order-free pass too, over the new area normals)
-            ctx->nb_need = std::max<uint64_t>(ctx->nb_need, (uint64_t)n_h[1] * grid_a);
-            ctx->nb_need_c = std::max<uint64_t>(ctx->nb_need_c, (uint64_t)n_h[2] * grid_c);
-            if (std::max(ctx->nb_need, ctx->nb_need_c) > 0xffffffffull)
-                return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: %llu neighbour "
-                               "list words (32-bit list offsets)",
-                               (unsigned long long)std::max(ctx->nb_need, ctx->nb_need_c));
-            PCP_HIP(ctx, ctx->nb_list.ensure(ctx->nb_need * 4 + 64));
-            PCP_HIP(ctx, ctx->nb_list_c.ensure(ctx->nb_need_c * 4 + 64));
-            ctx->normals_regrown++;
-            n_h[1] = n_h[2] = n_h[3] = 0;   // (the control words: cleared by k_nb_sums<true>)
-            PCP_HIP(ctx, hipMemsetAsync(sel, 0, sizeof(uint32_t), st));
-            if (int rc2 = area_lists_sums()) return rc2;
-            if (int rc3 = cells()) return rc3;
-            PCP_HIP(ctx, hipStreamSynchronize(st));
-            if (n_h[3])
-                return set_err(ctx, PCP_E_CAPACITY, "pcp_set_excavation_area: neighbour lists "
-                                                       "overflowed after regrowing");
-        }
-        ctx->nb_need = std::max<uint64_t>(ctx->nb_need, (uint64_t)n_h[1] * grid_a);
-        ctx->nb_need_c = std::max<uint64_t>(ctx->nb_need_c, (uint64_t)n_h[2] * grid_c);
-        ctx->nb_ctl_zero = true;   // k_nb_sums<true> (always launched on this path) cleared them
+        ctx->n_cells = n_h[0];
+        ctx->cells_cap = total;
+        if (n_cells) *n_cells = ctx->n_cells;
+        prof_resolve(ctx);
+        return PCP_OK;
     }
-    const uint32_t nc = *n_h;
-    ctx->n_cells = nc;
-    if (n_cells) *n_cells = nc;
-    prof_resolve(ctx);
+    // The sorted neighbour lists: the area's (nb_list / nb_meta) and the cells' (nb_list_c /
+    // nb_meta_c), one region per k_nb_lists block, words as the previous call needed (first
+    // guess n x min(n, 4096)), regrown on overflow to the largest block's use x the grid (by
+    // area_finish).  The cells go through k_cell_sums_exact first (any order where no order can
+    // change the sums); only those it leaves in nb_sel take the ordered lists.  Every buffer is
+    // sized before the launches.
+    const uint32_t nbb = ctx->nb_blocks > 0 ? (uint32_t)ctx->nb_blocks : (uint32_t)kNbBlocks;
+    ctx->area_grid_a = std::min<uint32_t>(npts, nbb);
+    ctx->area_grid_c = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(total, nbb));
+    ctx->area_npts = npts;
+    ctx->area_total = total;
+    const uint64_t per_pt = std::min<uint64_t>(npts, 4096);
+    const uint64_t guess_a = std::min<uint64_t>((uint64_t)npts * per_pt, 64ull << 20);
+    const uint64_t guess_c = std::min<uint64_t>(std::max<uint64_t>(total, 1) * per_pt, 64ull << 20);
+    PCP_HIP(ctx, ctx->nb_list.ensure(std::max<uint64_t>(guess_a, ctx->nb_need) * 4 + 64));
+    PCP_HIP(ctx, ctx->nb_list_c.ensure(std::max<uint64_t>(guess_c, ctx->nb_need_c) * 4 + 64));
+    PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)npts * sizeof(uint2) + 64));
+    PCP_HIP(ctx, ctx->nb_meta_c.ensure((size_t)total * sizeof(uint2) + 64));
+    PCP_HIP(ctx, ctx->nb_sel.ensure(((size_t)total + 2) * sizeof(uint32_t)));
+    bool ctl_dirty = !ctx->nb_ctl_zero || !ctx->nb_ctl.p;   // control words not known zero
+    PCP_HIP(ctx, ctx->nb_ctl.ensure(64));
+    ctx->nb_ctl_zero = false;   // set again once k_nb_sums<true> has cleared them
+    // nb_pts: the points by input index, then their normals as float4 (the sums' records)
+    PCP_HIP(ctx, ctx->nb_pts.ensure(2 * n * sizeof(float4) + 64));
+    uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
+    uint32_t *sel = ctx->nb_sel.as<uint32_t>();
+    hipStream_t st = ctx->stream;
+    // the control words are zero: cleared by the previous call's last k_nb_sums<true> (or, on a
+    // fresh buffer, by this memset)
+    if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctl, 0, 16, st));
+    // first: the input points by input index for the sums' gathers, the non-finite points' NaN
+    // normals (k_area_prep is the raw records' last reader; the exact kernels never write those
+    // entries, so a rerun keeps them), and sel's count cleared
+    hipLaunchKernelGGL(k_area_prep, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0, st, rin,
+                       ctx->nb_pts.as<float4>(), ctx->area_nrm.as<float>(), sel);
+    PCP_CHECK_LAUNCH(ctx);
+    pin_release(ctx, st);
+    nb_area_launch(ctx, st);
+    PCP_CHECK_LAUNCH(ctx);
+    if (int rcl = lattice(st)) return rcl;
+    nb_cells_launch(ctx, st);
+    PCP_CHECK_LAUNCH(ctx);
+    ctx->cells_cap = total;
+    ctx->area_pending = true;
+    if (defer) {   // the count (<= cells_cap) is settled by the next call that needs it
+        if (n_cells) *n_cells = total;
+        return PCP_OK;
+    }
+    if ((rc = area_finish(ctx))) return rc;
+    if (n_cells) *n_cells = ctx->n_cells;
+    return PCP_OK;
+}
+
+}  // namespace pcp
+
+using namespace pcp;
+
+extern "C" {
+
+int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
+                            int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells) {
+    return area_setup(ctx, area, grid_resolution, vertical_layers, grid_bbox, n_cells, false);
+}
+
+int pcp_set_excavation_area_async(pcp_ctx *ctx, const pcp_cloud_view *area,
+                                  double grid_resolution, int32_t vertical_layers,
+                                  double grid_bbox[6], uint64_t *cells_cap) {
+    return area_setup(ctx, area, grid_resolution, vertical_layers, grid_bbox, cells_cap, true);
+}
+
+int pcp_cells_count(pcp_ctx *ctx, uint64_t *n_cells) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!n_cells) return set_err(ctx, PCP_E_INVALID, "pcp_cells_count: null n_cells");
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    if (int rc = area_finish(ctx)) return rc;
+    *n_cells = ctx->n_cells;
     return PCP_OK;
 }
 
 int pcp_get_cells(pcp_ctx *ctx, double *xyz, float *normals, uint64_t cap, uint64_t *n_cells) {
     if (!ctx) return PCP_E_INVALID;
     if (!n_cells) return set_err(ctx, PCP_E_INVALID, "pcp_get_cells: null n_cells");
+    if (int rc = area_finish(ctx)) return rc;
     *n_cells = ctx->n_cells;
     if (ctx->n_cells > cap)
         return set_err(ctx, PCP_E_CAPACITY, "pcp_get_cells: %llu cells, cap %llu",
@@ -1335,6 +1399,7 @@ int pcp_get_cells(pcp_ctx *ctx, double *xyz, float *normals, uint64_t cap, uint6
 int pcp_get_area_normals(pcp_ctx *ctx, float *normals, uint64_t cap, uint64_t *n) {
     if (!ctx) return PCP_E_INVALID;
     if (!n) return set_err(ctx, PCP_E_INVALID, "pcp_get_area_normals: null n");
+    if (int rc = area_finish(ctx)) return rc;
     *n = ctx->area_n;
     if (ctx->area_n > cap)
         return set_err(ctx, PCP_E_CAPACITY, "pcp_get_area_normals: %llu points, cap %llu",

@@ -328,6 +328,9 @@ struct CloudJob {
     int32_t bk;
     uint32_t nbkcap;      // buckets the rows and the look-back words are sized for
     uint32_t *brows;      // [ng][nbk + 1] compact position of the group's first item of bucket b
+    // pcp_filter_merge_nodes: the cloud's centroids in its own frame beside the merged records
+    // (the filter node's message), written by k_bk_emit; null otherwise
+    float4 *keep16;
 };
 constexpr int kMaxGroupTiles = 32;   // crop tiles per pass-0 sort tile, at most
 constexpr int kS0Items = 10;         // pass-0 chunk: 5,120 items (a group of ~10 C3 crop tiles
@@ -1560,12 +1563,19 @@ k_bk_emit(const JobBatch jobs, int k, uint32_t *__restrict__ res, float4 *__rest
     if (c < 0) return;
     const CloudJob &J = jobs.j[c];
     __shared__ uint32_t sh[2];
+    // the cloud's own outputs (centroids, or keep16 beside the merged records) are indexed from
+    // the cloud's first voxel: eb = the voxels of the earlier clouds' buckets
+    const bool own = !emit || J.keep16;
     if (threadIdx.x < 64) {
         const uint32_t e = bk_voxels_before(bkv, f);
-        if (threadIdx.x == 0) sh[0] = e;
+        const uint32_t eb = own ? bk_voxels_before(bkv, b0) : 0u;
+        if (threadIdx.x == 0) {
+            sh[0] = e;
+            sh[1] = eb;
+        }
     }
     __syncthreads();
-    const uint32_t e = sh[0];
+    const uint32_t e = sh[0], eo = sh[0] - sh[1];
     const uint2 kv = bkv[f];
     const float4 *tmp = J.sparse + kv.y;
     for (uint32_t v0 = 0; v0 < kv.x; v0 += 4 * kBkTE) {
@@ -1588,10 +1598,11 @@ k_bk_emit(const JobBatch jobs, int k, uint32_t *__restrict__ res, float4 *__rest
             if (v >= kv.x) continue;
             if (emit) {
                 xform_store(J.rig, a[u].x, a[u].y, a[u].z, emit + 2 * ((size_t)e + v));
+                if (J.keep16) J.keep16[eo + v] = a[u];
             } else {
-                J.out4[e + v] = a[u];
-                J.vidx[e + v] = iv[u];
-                J.vcnt[e + v] = cv[u];
+                J.out4[eo + v] = a[u];
+                J.vidx[eo + v] = iv[u];
+                J.vcnt[eo + v] = cv[u];
             }
         }
     }
@@ -2494,6 +2505,139 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
         PCP_HIP(ctx, hipMemcpyAsync(out, obuf, total * 32, hipMemcpyDeviceToHost, ctx->stream));
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     prof_resolve(ctx);
+    return PCP_OK;
+}
+
+// The launch file's filter node (both sensors) and merger node composed in one process
+// (the C5 chain): each cloud cropped + voxelised, its centroids in its own frame
+// (the /filtered_points message, PointXYZ 16-B stride) AND the concatenated transformed + coloured
+// records (the merged PointXYZRGB message), one batch of launches and ONE synchronisation.  The
+// clouds are read in place from the pinned ring, the results are stored by the kernels into
+// pinned memory (host output only).
+int pcp_filter_merge_nodes(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds,
+                           const double *boxes, float leaf, const pcp_rigid *tf,
+                           const uint8_t *rgb, void *out, uint64_t cap, uint64_t *n_out,
+                           uint64_t *n_per_cloud, float *const *filtered, uint64_t *n_cropped) {
+    if (!ctx) return PCP_E_INVALID;
+    if (k < 0 || k > kBatch || (k && (!clouds || !boxes || !tf || !rgb || !filtered)) || !n_out)
+        return set_err(ctx, PCP_E_INVALID, "pcp_filter_merge_nodes: bad argument");
+    uint64_t upper = 0, in_bytes = 0;
+    for (int i = 0; i < k; ++i) {
+        int rc = check_view(ctx, &clouds[i], "pcp_filter_merge_nodes");
+        if (rc) return rc;
+        upper += clouds[i].n;
+        in_bytes += clouds[i].n * (uint64_t)clouds[i].point_step;
+    }
+    *n_out = 0;
+    if (k == 0) return PCP_OK;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    VoxParams *vp;
+    uint32_t *res;
+    int rc = ensure_misc(ctx, vp, res);
+    if (rc) return rc;
+    if ((int)ctx->fbuf.size() < k) ctx->fbuf.resize(k);
+    // inputs: one pinned-ring slot holding every cloud (message-sized), else DMA'd staging
+    const bool zc = ctx->zc_in && in_bytes <= kPinDirectMax;
+    std::vector<size_t> soff(k + 1, 0);
+    for (int i = 0; i < k; ++i)
+        soff[i + 1] = soff[i] + align256(clouds[i].n * clouds[i].point_step);
+    std::vector<CloudIn> cin(k);
+    if (zc) {
+        std::vector<HostPiece> pc;
+        for (int i = 0; i < k; ++i) {
+            if ((rc = stage_cloud(ctx, clouds[i], true, ctx->f_in, 0, cin[i]))) return rc;   // fields
+            if (clouds[i].n) pc.push_back(HostPiece{soff[i], clouds[i].data,
+                                                    clouds[i].n * (uint64_t)clouds[i].point_step});
+        }
+        const void *dv = nullptr;
+        if (!pc.empty()) {
+            if ((rc = pin_stage(ctx, pc.data(), (int)pc.size(), soff[k], &dv))) return rc;
+            for (int i = 0; i < k; ++i)
+                if (clouds[i].n) cin[i].raw = static_cast<const unsigned char *>(dv) + soff[i];
+        }
+    } else {
+        PCP_HIP(ctx, ctx->f_in.ensure(soff[k] + 256));
+        for (int i = 0; i < k; ++i)
+            if ((rc = stage_cloud(ctx, clouds[i], false, ctx->f_in, soff[i], cin[i]))) return rc;
+    }
+    std::vector<CloudJob> jobs(k);
+    for (int i = 0; i < k; ++i) {
+        const double *bx = boxes + 6 * i;
+        const Box b{bx[0], bx[1], bx[2], bx[3], bx[4], bx[5]};
+        if ((rc = make_job(ctx, i, cin[i], b, leaf, false, make_rigid(tf[i], rgb + 3 * i), vp,
+                           jobs[i])))
+            return rc;
+    }
+    // landing (pinned): [result words | merged records | each cloud's centroids]
+    const size_t res_b = align256(kResWords * sizeof(uint32_t));
+    const size_t mrg_b = align256((upper + 1) * 32);
+    std::vector<size_t> koff(k + 1, 0);
+    for (int i = 0; i < k; ++i) koff[i + 1] = koff[i] + align256((clouds[i].n + 1) * 16);
+    PCP_HIP(ctx, ctx->tc_host.ensure(res_b + mrg_b + koff[k] + 256));
+    char *land = ctx->tc_host.as<char>();
+    uint32_t *res_h = reinterpret_cast<uint32_t *>(land);
+    float4 *mrg = reinterpret_cast<float4 *>(land + res_b);
+    auto keep = [&](int i) { return reinterpret_cast<float4 *>(land + res_b + mrg_b + koff[i]); };
+    std::vector<ResultInfo> ri(k);
+    bool done = false;
+    // the bucket chain with the emit writing both outputs (every cloud certainly voxelises)
+    std::vector<Batch> bts = batches_of(jobs);
+    if (ctx->fm_fast == 2 && emit_in_centroid(bts)) {
+        std::vector<CloudJob> fj = jobs;
+        bool bucket = true;
+        for (int i = 0; i < k && bucket; ++i) bucket = bucket_geometry(ctx, i, fj[i], k);
+        if (bucket) {
+            for (int i = 0; i < k; ++i) fj[i].keep16 = keep(i);
+            {
+                ProfScope ps(ctx, PCP_K_FILTER_MERGE);
+                if ((rc = enqueue_all(ctx, batches_of(fj), res_h, mrg, ctx->stream))) return rc;
+            }
+            uint32_t redo = 0;
+            if ((rc = read_results(ctx, res_h, k, ri.data(), true, &redo))) return rc;
+            if (redo) prof_count(ctx, PCP_K_VOXEL_REDO);
+            done = !redo;
+        }
+    }
+    if (!done) {   // the general chain: each cloud's result, then the transform + concat
+        std::vector<CloudJob> gj = jobs;
+        for (int i = 0; i < k; ++i) gj[i].bk = 0;
+        bts = batches_of(gj);
+        {
+            ProfScope ps(ctx, PCP_K_FILTER_MERGE);
+            for (const Batch &bt : bts)
+                if ((rc = enqueue_chain(ctx, bt, res, ctx->stream))) return rc;
+            for (const Batch &bt : bts)
+                if ((rc = enqueue_emit(ctx, bt, res, mrg, ctx->stream))) return rc;
+        }
+        if ((rc = read_results(ctx, res, k, ri.data()))) return rc;
+        // each cloud's result (centroids, or the cropped points of a passthrough cloud) down
+        for (int i = 0; i < k; ++i) {
+            if (!ri[i].n) continue;
+            VoxParams v;
+            PCP_HIP(ctx, hipMemcpyAsync(&v, gj[i].vp, sizeof(v), hipMemcpyDeviceToHost, ctx->stream));
+            PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            const float4 *src = (v.do_voxel && !v.overflow) ? gj[i].out4 : gj[i].xyz;
+            PCP_HIP(ctx, hipMemcpyAsync(keep(i), src, (size_t)ri[i].n * 16, hipMemcpyDeviceToHost,
+                                        ctx->stream));
+        }
+        PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    if (zc) pin_release(ctx, ctx->stream);
+    uint64_t total = 0;
+    for (int i = 0; i < k; ++i) {
+        const uint64_t ni = clouds[i].n ? ri[i].n : 0;
+        if (n_per_cloud) n_per_cloud[i] = ni;
+        if (n_cropped) n_cropped[i] = clouds[i].n ? ri[i].m : 0;
+        total += ni;
+    }
+    *n_out = total;
+    prof_resolve(ctx);
+    if (total > cap)
+        return set_err(ctx, PCP_E_CAPACITY, "pcp_filter_merge_nodes: need %llu, cap %llu",
+                       (unsigned long long)total, (unsigned long long)cap);
+    if (total && out) host_copy(ctx, out, mrg, total * 32);
+    for (int i = 0; i < k; ++i)
+        if (clouds[i].n && ri[i].n && filtered[i]) host_copy(ctx, filtered[i], keep(i), (size_t)ri[i].n * 16);
     return PCP_OK;
 }
 

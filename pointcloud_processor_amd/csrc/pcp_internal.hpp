@@ -235,6 +235,16 @@ struct pcp_ctx {
     uint64_t aux_cloud_n = 0;
     uint64_t n_cells = 0;
     pcp::DevBuf cells_xyz, cells_nrm;
+    pcp::DevBuf cells_n_d;           // the lattice's cell count on the device (k_lattice_compact)
+    // pcp_set_excavation_area_async: the setup enqueued and not waited for; area_finish (the
+    // next call that needs the cells on the host, or the tick after its own synchronisation)
+    // settles the count and regrows + reruns the neighbour lists on an overflow
+    bool area_pending = false;
+    uint64_t cells_cap = 0;          // the lattice's points: an upper bound of n_cells
+    uint32_t area_npts = 0, area_grid_a = 0, area_grid_c = 0;
+    uint64_t area_total = 0;
+    pcp::PinnedBuf area_host;        // the setup's landing: [cells, area list use, cell list use,
+                                     // overflow]
     // excavation area (pcp_set_excavation_area): indices for the normal radius (1.5 m) and the
     // lattice test radius (1.5 * grid_resolution), and the per-point normals
     pcp::GridIndex exc_norm, exc_near;
@@ -448,6 +458,8 @@ struct ScoreEnq {
     int32_t *stats_host = nullptr; // zc: where the last flag block copies the finished stats
     bool zc = false;               // flags / totals / covered live in the pinned block itself
     const uint32_t *P_dev = nullptr;   // the device's pose count (rows P = capacity)
+    const uint32_t *C_dev = nullptr;   // the device's cell count (C = the lattice's capacity:
+                                       // a pcp_set_excavation_area_async still in flight)
     // the query's block (poses_d on the device, res_host pinned, same offsets): poses at 0,
     // cell flags at fl_off, totals + covered (tc_bytes) ending at most at st_off, stats at
     // st_off, blk_bytes in all
@@ -478,6 +490,13 @@ void launch_keys_combine(hipStream_t st, unsigned long long *a, const unsigned l
 // the colour-statistics slots (k_cell_flags order) -> pcp_vl_report
 void fill_report(const int32_t *st_h, double zx_total, int64_t best_idx, double best,
                  pcp_vl_report *rep);
+
+// pcp_set_excavation_area_async's settlement (pcp_excav.hip): waits for the stream, regrows and
+// reruns the neighbour lists on an overflow, sets ctx->n_cells; a no-op with nothing pending
+int area_finish(pcp_ctx *ctx);
+// after a stream synchronisation that followed the pending setup: did its lists overflow?  (the
+// count in ctx->area_host is then valid, the cells' normals are not)
+bool area_overflowed(const pcp_ctx *ctx);
 
 // the context's RCCL communicator and its buffers (pcp_comm.hip), at pcp_destroy
 void comm_release(pcp_ctx *ctx);

@@ -345,6 +345,9 @@ int pcp_multi_score_poses(pcp_multi *m, const double *poses5, uint64_t n,
                           uint8_t *cell_flags, double *total_score, int32_t *covered,
                           pcp_vl_report *rep) {
     if (!m) return PCP_E_INVALID;
+    for (int r = 0; r < m->n; ++r)   // (a setup still in flight on a rank: settled first)
+        if (area_finish(m->ctx[r]) != PCP_OK)
+            return merr(m, PCP_E_HIP, "pcp_multi_score_poses: %s", m->ctx[r]->err.c_str());
     const uint64_t C = m->ctx[0]->n_cells;
     if (!zx120_pose5 || !p || !rep || (n && !poses5) || (C && !cell_flags))
         return merr(m, PCP_E_INVALID, "pcp_multi_score_poses: null argument");

