@@ -219,8 +219,8 @@ def _host_cpu():
 def _ulps(a, b) -> np.ndarray:
     """Units in the last place between two float64 arrays (0: the same bits; +-0 equal)."""
     def key(x):
-        u = np.atleast_1d(np.asarray(x, np.float64)).view(np.int64).astype(object)
-        return np.array([v if v >= 0 else -(2**63) - v for v in u], dtype=object)
+        u = np.ascontiguousarray(np.asarray(x, np.float64)).ravel().view(np.int64)
+        return np.array([int(v) if v >= 0 else -(2**63) - int(v) for v in u], dtype=object)
     return np.abs(key(a) - key(b)).astype(np.float64)
 
 

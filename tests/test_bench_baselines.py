@@ -30,3 +30,26 @@ def test_fan_baseline_grid_and_kdtree_count_the_same_work():
         r = bench.cpu_baseline_fan(sc.terrain, poses, fan, 0.05, kdtree=kd)
         assert r["value"] > 0 and r["cores"] == 1 and r["kind"] == "port"
         assert ("KdTreeFLANN" in r["sample"]) == kd
+
+
+def test_bench_parity_helpers():
+    """bench.py's C1 / C5 oracle checks use the tests' totals bar (tests/parity.py) on 1-D
+    totals and 2-D candidate angles alike."""
+    import sys
+
+    import numpy as np
+
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1]))
+    import bench
+    import parity
+
+    a = np.array([[1.0, -2.0], [0.0, 3.0e-300]])
+    b = np.nextafter(a, np.inf)
+    assert bench._ulps(a, b).tolist() == [1.0] * 4
+    assert bench._ulps(-0.0, 0.0).tolist() == [0.0]
+    np.testing.assert_array_equal(bench._ulps(a, b), parity.ulps(a, b).ravel())
+    t = np.linspace(1.0, 2.0, 40)
+    assert bench._totals_bar(t, t)["ok"] and parity.totals_match(t, t)
+    t2 = t.copy()
+    t2[:12] = np.nextafter(t2[:12], 3.0)   # 12 of 40 differ: past max(2, 25 %)
+    assert not bench._totals_bar(t2, t)["ok"] and not parity.totals_match(t2, t)
