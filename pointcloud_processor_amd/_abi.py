@@ -220,6 +220,16 @@ def runtime_info() -> dict:
             "rccl_path": os.path.realpath(ri.rccl_path.decode()) if ri.rccl_path else None}
 
 
+def alloc_stats() -> dict:
+    """pcp_alloc_stats: the process's device / pinned (re)allocations and their bytes so far
+    (every growth of a grow-only buffer counts one)."""
+    d, p, b = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+    rc = load_library().pcp_alloc_stats(C.byref(d), C.byref(p), C.byref(b))
+    if rc != PCP_OK:
+        raise PcpError(rc, "pcp_alloc_stats failed")
+    return {"device": d.value, "pinned": p.value, "bytes": b.value}
+
+
 def device_count() -> int:
     """Visible gfx950 devices (pcp_device_count)."""
     n = C.c_int(0)

@@ -244,7 +244,9 @@ static int cmd_replay(Device &dev, char **a) {
     size_t merged_n = 0, best = 0, cells_n = cn;
     uint64_t realloc_after_warmup = 0, ra0 = 0;
     std::string dumped;
+    const bool alloc_trace = std::getenv("PCP_ALLOC_TRACE") != nullptr;
     for (int f = 0; f < frames + 2; ++f) {
+        if (alloc_trace) std::fprintf(stderr, "replay frame %d\n", f);
         if (f == 2) pcp_alloc_stats(&ra0, nullptr, nullptr);
         auto rs = synth_scan(npts, 2.0, rng), zs = synth_scan(npts, 3.5, rng);
         PointCloud2 rm = make_xyz_cloud(rs.data(), npts, "four_wheel_robot/velodyne_link");

@@ -1,5 +1,8 @@
 // pcp_context.hip -- context, errors, profiling, device helpers, prefix scan.
 #include <cmath>
+#include <cstdio>
+#include <dlfcn.h>
+#include <execinfo.h>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
@@ -44,9 +47,22 @@ int check_view(pcp_ctx *ctx, const pcp_cloud_view *v, const char *what) {
 }
 
 static std::atomic<uint64_t> g_reallocs{0}, g_pinned_reallocs{0}, g_alloc_bytes{0};
-void note_realloc(size_t bytes, bool pinned) {
+__attribute__((noinline)) void note_realloc(size_t bytes, bool pinned) {
     (pinned ? g_pinned_reallocs : g_reallocs).fetch_add(1, std::memory_order_relaxed);
     g_alloc_bytes.fetch_add(bytes, std::memory_order_relaxed);
+    // PCP_ALLOC_TRACE=1: the allocation site as an offset into libpcp (addr2line -e libpcp.so)
+    static const bool trace = std::getenv("PCP_ALLOC_TRACE") != nullptr;
+    if (trace) {
+        void *fr[6];
+        const int nf = backtrace(fr, 6);
+        std::fprintf(stderr, "pcp realloc %s %zu B at", pinned ? "pinned" : "device", bytes);
+        for (int i = 1; i < nf; ++i) {
+            Dl_info di{};
+            const uintptr_t base = dladdr(fr[i], &di) ? (uintptr_t)di.dli_fbase : 0;
+            std::fprintf(stderr, " +0x%zx", (size_t)((uintptr_t)fr[i] - base));
+        }
+        std::fprintf(stderr, "\n");
+    }
 }
 uint64_t alloc_count(int which) {
     return which == 0 ? g_reallocs.load() : which == 1 ? g_pinned_reallocs.load() : g_alloc_bytes.load();
@@ -460,6 +476,10 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *sw = std::getenv("PCP_SCORE_WIDE")) ctx->score_wide = std::atoi(sw) != 0;
     if (const char *co = std::getenv("PCP_CELLS_ORDER_FREE")) ctx->cells_all_ordered = std::atoi(co) == 0;
     if (const char *nbk = std::getenv("PCP_NB_BLOCKS")) ctx->nb_blocks = std::atoi(nbk);
+    if (const char *rp = std::getenv("PCP_NB_REGION_PCT"))
+        ctx->nb_region_pct = std::min(100, std::max(1, std::atoi(rp)));
+    if (const char *gw = std::getenv("PCP_NB_GUESS_WORDS"))
+        ctx->nb_guess_max = std::max<uint64_t>(1, std::strtoull(gw, nullptr, 10));
     if (const char *ct = std::getenv("PCP_COPY_THREADS")) ctx->copy_threads = std::atoi(ct);
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
     if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff);

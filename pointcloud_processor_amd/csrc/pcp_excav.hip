@@ -328,8 +328,10 @@ struct NbLists {
     uint32_t *list;                 // entries: input indices of the neighbours, sorted
     uint2 *meta;                    // per query: {base, m}
     uint32_t *need;                 // the largest words one block needed (zero before the launch)
-    uint32_t *overflow;             // set when a block's region was too small (host regrows)
+    uint32_t *overflow;             // set when a list fit neither its block's region nor the pool
     uint32_t per_block;             // words of each block's region (block b: [b pb, (b + 1) pb))
+    uint32_t *pool_cursor;          // the shared spill pool's cursor (zero before the launch)
+    uint64_t pool_base, pool_words; // the pool: words [pool_base, pool_base + pool_words)
 };
 
 // the stencil's points of query q within r2, 4 loads in flight per thread: f(k, p, d)
@@ -377,11 +379,11 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
     __shared__ unsigned long long key[kNbLds];   // appended keys
     __shared__ uint16_t grp[kNbLds];             // the keys' indices grouped by bucket
     __shared__ uint32_t wsum[kNbT / 64];
-    __shared__ uint32_t sh_base, sh_ok, sh_pos, sh_m;
+    __shared__ uint32_t sh_base, sh_ok, sh_pos, sh_m, sh_need;
     // CELLS with sel: only the cells sel[1 ..= sel[0]] (those k_cell_sums_exact left to the
     // ordered path), their lists at the compact positions
     const uint32_t nq = CELLS ? (sel ? *sel : *n_dev) : g.n_pts;
-    if (threadIdx.x == 0) sh_pos = 0;
+    if (threadIdx.x == 0) sh_pos = sh_need = 0;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     auto bucket_of = [&](float d) { return min((uint32_t)(d * bscale), kNbBuckets - 1u); };
     for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
@@ -471,15 +473,25 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
         if (threadIdx.x == 0) {
             // the list's words from the block's own region of the list buffer (no device
             // atomics: those on one shared cursor serialise across the XCDs).  A list past the LDS sorts its 64-bit
-            // keys in global memory, after its entries: m + 1 + 2 m words.  A region too small
-            // marks the list empty and the overflow; the block's use goes to the host, which
-            // regrows the buffer to the largest use x the grid and runs the normals again.
+            // keys in global memory, after its entries: m + 1 + 2 m words.  A list its region
+            // cannot hold spills to the shared pool behind the regions (one device atomic per
+            // spilled list: the dense blocks of a streamed area, not every block); one that
+            // fits neither marks the list empty and the overflow.  The block's use (region +
+            // spills) goes to the host, which then regrows the buffer and runs the normals again.
             const uint32_t words = big ? 3 * m + 1 : m;
-            const uint32_t ok = (uint64_t)sh_pos + words <= L.per_block;
-            if (!ok) atomicOr(L.overflow, 1u);
-            sh_base = L.per_block * blockIdx.x + sh_pos;
+            uint32_t ok = (uint64_t)sh_pos + words <= L.per_block;
+            uint64_t b = (uint64_t)L.per_block * blockIdx.x + sh_pos;
+            if (ok) {
+                sh_pos += words;
+            } else {
+                const uint32_t at = atomicAdd(L.pool_cursor, words);
+                ok = (uint64_t)at + words <= L.pool_words;
+                b = L.pool_base + at;
+                if (!ok) atomicOr(L.overflow, 1u);
+            }
+            sh_base = (uint32_t)b;
             sh_ok = ok;
-            sh_pos += words;   // (the need, counted on: the host's regrow size)
+            sh_need += words;   // (counted on: the host's regrow size)
             L.meta[qi] = make_uint2(sh_base, ok ? m : 0u);
         }
         nb_lds_barrier();
@@ -558,7 +570,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
         }
         nb_lds_barrier();   // the LDS is reused by the next query
     }
-    if (threadIdx.x == 0 && sh_pos) atomicMax(L.need, sh_pos);   // (no return value awaited)
+    if (threadIdx.x == 0 && sh_need) atomicMax(L.need, sh_need);   // (no return value awaited)
 }
 
 // computeCellSurfaceNormal's tail (:301-340): the normalised sum of the finite neighbours'
@@ -613,7 +625,7 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
     // the lists' largest block uses and overflow word (final: every k_nb_lists ran before this launch)
     // to the caller's pinned landing, one plain store each, then cleared for the next call (no
     // memset launch in front of its k_nb_lists)
-    if (ctl_host && blockIdx.x == 0 && threadIdx.x < 3) {
+    if (ctl_host && blockIdx.x == 0 && threadIdx.x < 5) {
         ctl_host[threadIdx.x] = ctl[threadIdx.x];
         ctl[threadIdx.x] = 0;   // (ctl is written: neither const nor restrict)
     }
@@ -1094,14 +1106,26 @@ namespace pcp {
 // and sums of the cells they leave).  Everything they read is on the device: the indices
 // (exc_norm), the points by input index (nb_pts), the lattice and its count (cells_xyz,
 // cells_n_d), so an overflow can rerun them long after the raw records are gone.
+// a list buffer as the grid's regions (3/4 of its words; PCP_NB_REGION_PCT) and the spill pool
+// behind them.  ctl
+// words: [0] / [1] the area's / cells' largest block use, [2] the overflow, [3] / [4] their pool
+// cursors -- landed in area_host[1 .. 5] and cleared by k_nb_sums<true>
+static NbLists nb_lists_view(const pcp_ctx *ctx, const DevBuf &list, const DevBuf &meta,
+                             uint32_t *need, uint32_t *overflow, uint32_t *cursor, uint32_t grid) {
+    const uint64_t words = std::min<uint64_t>(list.cap / 4, 0xffffffffull);
+    const uint32_t per_block = (uint32_t)(words * (uint64_t)ctx->nb_region_pct / 100 / grid);
+    const uint64_t pool_base = (uint64_t)per_block * grid;
+    return NbLists{list.as<uint32_t>(), meta.as<uint2>(), need, overflow,
+                   per_block, cursor, pool_base, words - pool_base};
+}
+
 static void nb_area_launch(pcp_ctx *ctx, hipStream_t st) {
     const GridView gn = ctx->exc_norm.view();
     const float r2n = (float)(kNormalRadius * kNormalRadius), bscale = (float)kNbBuckets / r2n;
     const uint32_t grid_a = ctx->area_grid_a, npts = ctx->area_npts;
     const uint64_t n = ctx->area_n;
     uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
-    const NbLists La{ctx->nb_list.as<uint32_t>(), ctx->nb_meta.as<uint2>(), ctl, ctl + 2,
-                     (uint32_t)(std::min<uint64_t>(ctx->nb_list.cap / 4, 0xffffffffull) / grid_a)};
+    const NbLists La = nb_lists_view(ctx, ctx->nb_list, ctx->nb_meta, ctl, ctl + 2, ctl + 3, grid_a);
     hipLaunchKernelGGL(k_nb_lists<false>, dim3(grid_a), dim3(kNbT), 0, st, gn, r2n, bscale,
                        (const double *)nullptr, (const uint32_t *)nullptr, La,
                        (const uint32_t *)nullptr);
@@ -1121,8 +1145,7 @@ static void nb_cells_launch(pcp_ctx *ctx, hipStream_t st) {
     const uint32_t *n_d = ctx->cells_n_d.as<uint32_t>();
     const float4 *nrm4 = ctx->nb_pts.as<float4>() + ctx->area_n;
     uint32_t *n_h = ctx->area_host.as<uint32_t>();
-    const NbLists Lc{ctx->nb_list_c.as<uint32_t>(), ctx->nb_meta_c.as<uint2>(), ctl + 1, ctl + 2,
-                     (uint32_t)(std::min<uint64_t>(ctx->nb_list_c.cap / 4, 0xffffffffull) / grid_c)};
+    const NbLists Lc = nb_lists_view(ctx, ctx->nb_list_c, ctx->nb_meta_c, ctl + 1, ctl + 2, ctl + 4, grid_c);
     if (total) {
         hipLaunchKernelGGL(k_cell_sums_exact, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n,
                            (const double *)ctx->cells_xyz.as<double>(), n_d, nrm4,
@@ -1163,10 +1186,12 @@ int area_finish(pcp_ctx *ctx) {
                            "words (32-bit list offsets)",
                            (unsigned long long)std::max(ctx->nb_need, ctx->nb_need_c));
         }
-        PCP_HIP(ctx, ctx->nb_list.ensure(ctx->nb_need * 4 + 64));
-        PCP_HIP(ctx, ctx->nb_list_c.ensure(ctx->nb_need_c * 4 + 64));
+        // twice the measured need: a streamed area keeps changing (the carve), and each regrow
+        // is a free + malloc + a second pass of the normals inside one frame
+        PCP_HIP(ctx, ctx->nb_list.ensure(ctx->nb_need * 8 + 64));
+        PCP_HIP(ctx, ctx->nb_list_c.ensure(ctx->nb_need_c * 8 + 64));
         ctx->normals_regrown++;
-        n_h[1] = n_h[2] = n_h[3] = 0;   // (the control words: cleared by k_nb_sums<true>)
+        n_h[1] = n_h[2] = n_h[3] = n_h[4] = n_h[5] = 0;   // (ctl: cleared by k_nb_sums<true>)
         PCP_HIP(ctx, hipMemsetAsync(ctx->nb_sel.p, 0, sizeof(uint32_t), st));
         nb_area_launch(ctx, st);
         PCP_CHECK_LAUNCH(ctx);
@@ -1179,8 +1204,8 @@ int area_finish(pcp_ctx *ctx) {
                                                 "overflowed after regrowing");
         }
     }
-    ctx->nb_need = std::max<uint64_t>(ctx->nb_need, (uint64_t)n_h[1] * ctx->area_grid_a);
-    ctx->nb_need_c = std::max<uint64_t>(ctx->nb_need_c, (uint64_t)n_h[2] * ctx->area_grid_c);
+    // (nb_need / nb_need_c move only on an overflow: a frame the spill pool absorbed keeps the
+    // buffers, a later setup does not grow them for it)
     ctx->nb_ctl_zero = true;   // k_nb_sums<true> (always launched on this path) cleared them
     ctx->n_cells = n_h[0];
     ctx->area_pending = false;
@@ -1252,7 +1277,7 @@ static int area_setup(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_reso
     defer = defer && exact;   // (the order-free A/B kernels settle before the return)
     PCP_HIP(ctx, ctx->area_host.ensure(64));
     uint32_t *n_h = ctx->area_host.as<uint32_t>();
-    n_h[1] = n_h[2] = n_h[3] = 0;   // the lists' largest block uses + overflow (exact path)
+    n_h[1] = n_h[2] = n_h[3] = n_h[4] = n_h[5] = 0;   // the lists' uses, overflow, pool cursors
     PCP_HIP(ctx, ctx->cells_n_d.ensure(64));
     uint32_t *n_d = ctx->cells_n_d.as<uint32_t>();
     // the lattice of candidate cells (:258-298) on stream st.  Its buffers are sized after the
@@ -1309,8 +1334,8 @@ static int area_setup(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_reso
     ctx->area_npts = npts;
     ctx->area_total = total;
     const uint64_t per_pt = std::min<uint64_t>(npts, 4096);
-    const uint64_t guess_a = std::min<uint64_t>((uint64_t)npts * per_pt, 64ull << 20);
-    const uint64_t guess_c = std::min<uint64_t>(std::max<uint64_t>(total, 1) * per_pt, 64ull << 20);
+    const uint64_t guess_a = std::min<uint64_t>((uint64_t)npts * per_pt, ctx->nb_guess_max);
+    const uint64_t guess_c = std::min<uint64_t>(std::max<uint64_t>(total, 1) * per_pt, ctx->nb_guess_max);
     PCP_HIP(ctx, ctx->nb_list.ensure(std::max<uint64_t>(guess_a, ctx->nb_need) * 4 + 64));
     PCP_HIP(ctx, ctx->nb_list_c.ensure(std::max<uint64_t>(guess_c, ctx->nb_need_c) * 4 + 64));
     PCP_HIP(ctx, ctx->nb_meta.ensure((size_t)npts * sizeof(uint2) + 64));
@@ -1326,7 +1351,7 @@ static int area_setup(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_reso
     hipStream_t st = ctx->stream;
     // the control words are zero: cleared by the previous call's last k_nb_sums<true> (or, on a
     // fresh buffer, by this memset)
-    if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctl, 0, 16, st));
+    if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctl, 0, 32, st));
     // first: the input points by input index for the sums' gathers, the non-finite points' NaN
     // normals (k_area_prep is the raw records' last reader; the exact kernels never write those
     // entries, so a rerun keeps them), and sel's count cleared

@@ -215,19 +215,30 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds) {
 template <int J, int W>
 __device__ __forceinline__ uint32_t round_offsets(const uint64_t (&bal)[J], uint32_t (*wo)[W]) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    static_assert(J * W <= 64, "one wave scans the (round, wave) counts");
+    // one wave scans the J x W counts, R consecutive (round, wave) entries per lane
+    constexpr int E = J * W, R = (E + 63) / 64;
     if (lane == 0)
 #pragma unroll
         for (int j = 0; j < J; ++j) wo[j][wid] = (uint32_t)__popcll(bal[j]);
     __syncthreads();
     __shared__ uint32_t tot;
     if (threadIdx.x < 64) {
-        const int j = threadIdx.x / W, w = threadIdx.x % W;
-        const bool in = threadIdx.x < J * W;
-        const uint32_t v = in ? wo[j][w] : 0u;
-        const uint32_t incl = wave_incl_scan_dpp(v);
-        if (in) wo[j][w] = incl - v;
-        if (threadIdx.x == 63) tot = incl;
+        uint32_t v[R], s = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = lane * R + r;
+            v[r] = e < E ? wo[e / W][e % W] : 0u;
+            s += v[r];
+        }
+        const uint32_t incl = wave_incl_scan_dpp(s);
+        uint32_t ex = incl - s;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = lane * R + r;
+            if (e < E) wo[e / W][e % W] = ex;
+            ex += v[r];
+        }
+        if (lane == 63) tot = incl;
     }
     __syncthreads();
     return tot;

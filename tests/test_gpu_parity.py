@@ -1258,6 +1258,36 @@ def test_excavation_area_normals_long_lists_and_ties(oracle, order_free, monkeyp
             np.testing.assert_array_equal(cn.view(np.uint32), r_cn.view(np.uint32))
 
 
+@pytest.mark.parametrize("region_pct,guess", [("10", None), ("100", "4096"), ("10", "4096"),
+                                              ("75", "4096")])
+def test_excavation_area_list_spill_pool(oracle, region_pct, guess, monkeypatch):
+    """The neighbour lists' capacity paths (k_nb_lists): a list its block's region cannot hold
+    spills to the shared pool behind the regions (PCP_NB_REGION_PCT=10: most lists spill), and a
+    list that fits neither sets the overflow, after which the host regrows both buffers and runs
+    the normals again (PCP_NB_GUESS_WORDS=4096: a first buffer far too small; 100: no pool, the
+    regions alone).  Point and cell normals bit-identical to the oracle on every path, and the
+    second setup of the same area reallocates nothing."""
+    monkeypatch.setenv("PCP_NB_REGION_PCT", region_pct)
+    if guess:
+        monkeypatch.setenv("PCP_NB_GUESS_WORDS", guess)
+    a = _long_list_area()
+    r_n = oracle.area_normals(a, 1.5)
+    r_xyz, r_cn, r_bb, _ = oracle.excavation_grid(a, 0.1, 4, r_n)
+    with _abi.Context(0) as ctx:
+        for rep in range(2):
+            before = _abi.alloc_stats()["device"]
+            bb, n = ctx.set_excavation_area(a, 0.1, 4)
+            grew = _abi.alloc_stats()["device"] - before
+            np.testing.assert_array_equal(bb, r_bb)
+            assert n == r_xyz.shape[0]
+            _normals_equal(ctx.get_area_normals(), r_n)
+            xyz, cn = ctx.get_cells()
+            np.testing.assert_array_equal(xyz, r_xyz)
+            np.testing.assert_array_equal(cn.view(np.uint32), r_cn.view(np.uint32))
+            if rep:
+                assert grew == 0, grew
+
+
 def _long_list_area():
     rng = np.random.default_rng(11)
     g = np.arange(90) * 0.025
