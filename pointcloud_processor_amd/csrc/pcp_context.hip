@@ -476,6 +476,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *sw = std::getenv("PCP_SCORE_WIDE")) ctx->score_wide = std::atoi(sw) != 0;
     if (const char *co = std::getenv("PCP_CELLS_ORDER_FREE")) ctx->cells_all_ordered = std::atoi(co) == 0;
     if (const char *nbk = std::getenv("PCP_NB_BLOCKS")) ctx->nb_blocks = std::atoi(nbk);
+    if (const char *as = std::getenv("PCP_AREA_STREAM")) ctx->area_side = std::atoi(as) != 0;
     if (const char *rp = std::getenv("PCP_NB_REGION_PCT"))
         ctx->nb_region_pct = std::min(100, std::max(1, std::atoi(rp)));
     if (const char *gw = std::getenv("PCP_NB_GUESS_WORDS"))
@@ -508,8 +509,11 @@ void pcp_destroy(pcp_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->area_stream) (void)hipStreamSynchronize(ctx->area_stream);
     prof_resolve(ctx);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->area_fork_ev) (void)hipEventDestroy(ctx->area_fork_ev);
+    if (ctx->area_join_ev) (void)hipEventDestroy(ctx->area_join_ev);
     if (ctx->keys_ev) (void)hipEventDestroy(ctx->keys_ev);
     comm_release(ctx);
     host_copy_release(ctx);
@@ -550,6 +554,8 @@ void pcp_destroy(pcp_ctx *ctx) {
     for (auto &b : ctx->fbuf) b.release();
     if (ctx->fm_exec) (void)hipGraphExecDestroy(ctx->fm_exec);
     if (ctx->fm_graph) (void)hipGraphDestroy(ctx->fm_graph);
+    ctx->lat_flags.release();
+    if (ctx->area_stream) (void)hipStreamDestroy(ctx->area_stream);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -558,6 +564,7 @@ const char *pcp_last_error(const pcp_ctx *ctx) { return ctx ? ctx->err.c_str() :
 
 int pcp_synchronize(pcp_ctx *ctx) {
     if (!ctx) return PCP_E_INVALID;
+    area_join(ctx);
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     prof_resolve(ctx);
     return PCP_OK;

@@ -324,6 +324,23 @@ __device__ __forceinline__ float flann_d2(float qx, float qy, float qz, const fl
     return acc;
 }
 
+// diagnostic build only (make stamps): per (block, query round) phase times of k_nb_lists and
+// per block of k_nb_sums, s_memrealtime (100 MHz)
+#ifdef PCP_STAMPS
+constexpr int kNbStampBlocks = 2048, kNbStampQ = 4, kNbStampPh = 8;
+__device__ unsigned long long g_nb_stamps[2][kNbStampBlocks * kNbStampQ * kNbStampPh];
+#define NB_STAMP(k, q, ph)                                                                    \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < kNbStampBlocks && (q) < kNbStampQ)               \
+            g_nb_stamps[k][(blockIdx.x * kNbStampQ + (q)) * kNbStampPh + (ph)] =              \
+                __builtin_amdgcn_s_memrealtime();                                             \
+    } while (0)
+#else
+#define NB_STAMP(k, q, ph) \
+    do {                   \
+    } while (0)
+#endif
+
 struct NbLists {
     uint32_t *list;                 // entries: input indices of the neighbours, sorted
     uint2 *meta;                    // per query: {base, m}
@@ -386,7 +403,9 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
     if (threadIdx.x == 0) sh_pos = sh_need = 0;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     auto bucket_of = [&](float d) { return min((uint32_t)(d * bscale), kNbBuckets - 1u); };
-    for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+    uint32_t qround = 0;
+    for (uint32_t qi = blockIdx.x; qi < nq; qi += gridDim.x, ++qround) {
+        if (!CELLS) NB_STAMP(0, qround, 0);
         float qx, qy, qz;
         if (CELLS) {
             const uint32_t ci = sel ? sel[1 + qi] : qi;
@@ -402,6 +421,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
         for (int b = threadIdx.x; b < kNbBuckets; b += kNbT) cnt[b] = 0;
         if (threadIdx.x == 0) sh_m = 0;
         nb_lds_barrier();
+        if (!CELLS) NB_STAMP(0, qround, 1);
         uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};
         stencil_ranges(g, qx, qy, qz, lo, hi);   // (false: empty ranges)
         // the one pass over the stencil's four row ranges, kNbU candidates in flight per thread,
@@ -447,6 +467,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
                 }
             }
         nb_lds_barrier();
+        if (!CELLS) NB_STAMP(0, qround, 2);
         // exclusive scan of the buckets: thread t owns buckets [8 t, 8 t + 8)
         constexpr int kPer = kNbBuckets / kNbT;
         uint32_t v[kPer], run = 0;
@@ -495,6 +516,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
             L.meta[qi] = make_uint2(sh_base, ok ? m : 0u);
         }
         nb_lds_barrier();
+        if (!CELLS) NB_STAMP(0, qround, 3);
         const uint32_t base = sh_base;
         if (sh_ok && m) {
             uint32_t *out = L.list + base;
@@ -519,6 +541,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
                         if (i0 + (uint32_t)u * kNbT < m) grp[pos[u]] = (uint16_t)(i0 + (uint32_t)u * kNbT);
                 }
                 nb_lds_barrier();
+                if (!CELLS) NB_STAMP(0, qround, 4);
                 // each key's place = its bucket's start + its rank among the bucket's keys (the
                 // keys are distinct: distinct indices; a bucket holds a distance's exact ties, 2.4
                 // keys on average in C1).  Four grouped positions per thread, in lockstep
@@ -569,6 +592,11 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
             }
         }
         nb_lds_barrier();   // the LDS is reused by the next query
+        if (!CELLS) NB_STAMP(0, qround, 5);
+#ifdef PCP_STAMPS
+        if (!CELLS && threadIdx.x == 0 && blockIdx.x < kNbStampBlocks && qround < kNbStampQ)
+            g_nb_stamps[0][(blockIdx.x * kNbStampQ + qround) * kNbStampPh + 7] = m;
+#endif
     }
     if (threadIdx.x == 0 && sh_need) atomicMax(L.need, sh_need);   // (no return value awaited)
 }
@@ -611,6 +639,10 @@ template <> struct NbCfg<true> {
     static constexpr int NT = 3, QB = 7;
 };
 constexpr int kNbSteps = 64;   // list entries per chunk
+#ifndef PCP_NB_LIST_AHEAD
+#define PCP_NB_LIST_AHEAD 4    // k_nb_sums: chunks of list entries in flight (build knob, A/B)
+#endif
+constexpr int kNbListAhead = PCP_NB_LIST_AHEAD;
 
 
 // one neighbour's gathered record: its point (area moments) or its normal (cells), 16 bytes
@@ -645,7 +677,9 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
     __shared__ T accs[QB][NT];
     const uint32_t nq = CELLS ? (sel ? *sel : *n_dev) : g.n_pts;   // (sel: as k_nb_lists)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint32_t q0 = blockIdx.x * QB; q0 < nq; q0 += gridDim.x * QB) {
+    uint32_t qround = 0;
+    for (uint32_t q0 = blockIdx.x * QB; q0 < nq; q0 += gridDim.x * QB, ++qround) {
+        if (!CELLS) NB_STAMP(1, qround, 0);
         if (threadIdx.x < QB) {
             const uint32_t qi = q0 + threadIdx.x;
             const uint2 mt = qi < nq ? meta[qi] : make_uint2(0u, 0u);
@@ -679,13 +713,18 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
 #pragma unroll
             for (int i = 0; i < PER; ++i) rr[i] = recs[(mk >> i & 1u) ? kk[i] : 0u];
         };
-        uint32_t K1[PER], K2[PER], M1 = 0, M2 = 0;   // list entries of chunks c + 1, c + 2
+        // the list entries of chunks c + 1 .. c + LA in flight (a streamed list misses the
+        // caches: one chunk ahead left each chunk waiting ~1 us for its entries), the records
+        // of chunk c + 1 (the points / normals: cache-resident)
+        constexpr int LA = kNbListAhead;
+        uint32_t KA[LA][PER], MA[LA];
         NbRec R0[PER];                               // records of chunk c
         uint32_t M0 = 0;
         if (wid > 0) {
-            M0 = load_list(0, K1);
-            gather(K1, M0, R0);
-            M1 = load_list(1, K1);
+            M0 = load_list(0, KA[0]);
+            gather(KA[0], M0, R0);
+#pragma unroll
+            for (int d = 0; d < LA; ++d) MA[d] = load_list(1 + d, KA[d]);
         }
         T acc = 0;
         const int cq = lane / NT, ca = lane % NT;   // the consumer lane's (query, summand)
@@ -695,13 +734,16 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
                 const uint32_t mc = M0;
 #pragma unroll
                 for (int i = 0; i < PER; ++i) rc[i] = R0[i];
-                // prefetch: chunk c + 2's list entries, chunk c + 1's records
-                M2 = load_list(c + 2, K2);
-                gather(K1, M1, R0);
-                M0 = M1;
-                M1 = M2;
+                // chunk c + 1's records, then chunk c + 1 + LA's list entries
+                gather(KA[0], MA[0], R0);
+                M0 = MA[0];
 #pragma unroll
-                for (int i = 0; i < PER; ++i) K1[i] = K2[i];
+                for (int d = 0; d + 1 < LA; ++d) {
+                    MA[d] = MA[d + 1];
+#pragma unroll
+                    for (int i = 0; i < PER; ++i) KA[d][i] = KA[d + 1][i];
+                }
+                MA[LA - 1] = load_list(c + 1 + LA, KA[LA - 1]);
                 T (*B)[NT][SP] = buf[c & 1];
 #pragma unroll
                 for (int i = 0; i < PER; ++i) {
@@ -765,6 +807,11 @@ k_nb_sums(GridView g, const uint2 *__restrict__ meta, const uint32_t *__restrict
             }
             nb_lds_barrier();
         }
+        if (!CELLS) NB_STAMP(1, qround, 1);
+#ifdef PCP_STAMPS
+        if (!CELLS && threadIdx.x == 0 && blockIdx.x < kNbStampBlocks && qround < kNbStampQ)
+            g_nb_stamps[1][(blockIdx.x * kNbStampQ + qround) * kNbStampPh + 7] = maxm;
+#endif
         if (wid == 0 && cq < QB) accs[cq][ca] = acc;
         __syncthreads();
         if (threadIdx.x < QB && q0 + threadIdx.x < nq) {
@@ -1169,7 +1216,14 @@ bool area_overflowed(const pcp_ctx *ctx) {
     return ctx->area_host.p && ctx->area_host.as<const uint32_t>()[3] != 0u;
 }
 
+void area_join(pcp_ctx *ctx) {
+    if (!ctx->area_forked) return;
+    (void)hipStreamWaitEvent(ctx->stream, ctx->area_join_ev, 0);
+    ctx->area_forked = false;
+}
+
 int area_finish(pcp_ctx *ctx) {
+    area_join(ctx);
     if (!ctx->area_pending) return PCP_OK;
     hipStream_t st = ctx->stream;
     PCP_HIP(ctx, hipStreamSynchronize(st));
@@ -1280,21 +1334,19 @@ static int area_setup(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_reso
     n_h[1] = n_h[2] = n_h[3] = n_h[4] = n_h[5] = 0;   // the lists' uses, overflow, pool cursors
     PCP_HIP(ctx, ctx->cells_n_d.ensure(64));
     uint32_t *n_d = ctx->cells_n_d.as<uint32_t>();
-    // the lattice of candidate cells (:258-298) on stream st.  Its buffers are sized after the
-    // raw records' last reader was launched: a large area's raw records may sit in ctx->stage,
-    // which the lattice flags reuse (a reallocation frees it only after the device drained)
+    // the lattice of candidate cells (:258-298) on stream st (its per-point flags in lat_flags)
     auto lattice = [&](hipStream_t st) -> int {
-        PCP_HIP(ctx, ctx->stage.ensure(total + 64));
+        PCP_HIP(ctx, ctx->lat_flags.ensure(total + 64));
         PCP_HIP(ctx, ctx->cells_xyz.ensure(total * 3 * sizeof(double) + 16));
         PCP_HIP(ctx, ctx->cells_nrm.ensure(total * 3 * sizeof(float) + 16));
         if (total) {
             hipLaunchKernelGGL(k_lattice_flags,
                                dim3((unsigned)((total + kLatWaves - 1) / kLatWaves)), dim3(kXT), 0,
-                               st, gq, r2q, L, ctx->stage.as<uint8_t>());
+                               st, gq, r2q, L, ctx->lat_flags.as<uint8_t>());
             PCP_CHECK_LAUNCH(ctx);
         }
         hipLaunchKernelGGL(k_lattice_compact, dim3(1), dim3(1024), 0, st,
-                           (const uint8_t *)ctx->stage.as<uint8_t>(), L,
+                           (const uint8_t *)ctx->lat_flags.as<uint8_t>(), L,
                            ctx->cells_xyz.as<double>(), (uint32_t)total, n_d, n_h);
         PCP_CHECK_LAUNCH(ctx);
         return PCP_OK;
@@ -1349,6 +1401,23 @@ static int area_setup(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_reso
     uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
     uint32_t *sel = ctx->nb_sel.as<uint32_t>();
     hipStream_t st = ctx->stream;
+    // deferred: the rest on the side stream, forked here (the indices above are its inputs) and
+    // joined by the scoring / area_finish.  Everything it writes is its own (nb_*, area_nrm,
+    // cells_*, lat_flags, area_host) and nothing on ctx->stream reads those before the join
+    // (not when the raw records sit in ctx->stage: a large area's, DMA'd there, which the next
+    // upload on ctx->stream may overwrite while k_area_prep still reads them)
+    const bool side = defer && ctx->area_side && raw != ctx->stage.as<unsigned char>();
+    if (side) {
+        if (!ctx->area_stream)
+            PCP_HIP(ctx, hipStreamCreateWithFlags(&ctx->area_stream, hipStreamNonBlocking));
+        if (!ctx->area_fork_ev)
+            PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->area_fork_ev, hipEventDisableTiming));
+        if (!ctx->area_join_ev)
+            PCP_HIP(ctx, hipEventCreateWithFlags(&ctx->area_join_ev, hipEventDisableTiming));
+        PCP_HIP(ctx, hipEventRecord(ctx->area_fork_ev, st));
+        PCP_HIP(ctx, hipStreamWaitEvent(ctx->area_stream, ctx->area_fork_ev, 0));
+        st = ctx->area_stream;
+    }
     // the control words are zero: cleared by the previous call's last k_nb_sums<true> (or, on a
     // fresh buffer, by this memset)
     if (ctl_dirty) PCP_HIP(ctx, hipMemsetAsync(ctl, 0, 32, st));
@@ -1364,6 +1433,10 @@ static int area_setup(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_reso
     if (int rcl = lattice(st)) return rcl;
     nb_cells_launch(ctx, st);
     PCP_CHECK_LAUNCH(ctx);
+    if (side) {
+        PCP_HIP(ctx, hipEventRecord(ctx->area_join_ev, st));
+        ctx->area_forked = true;
+    }
     ctx->cells_cap = total;
     ctx->area_pending = true;
     if (defer) {   // the count (<= cells_cap) is settled by the next call that needs it
@@ -1436,5 +1509,18 @@ int pcp_get_area_normals(pcp_ctx *ctx, float *normals, uint64_t cap, uint64_t *n
     PCP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return PCP_OK;
 }
+
+#ifdef PCP_STAMPS
+// diagnostic build only: the stamps of the last k_nb_lists<false> (which 0) / k_nb_sums<false>
+// (which 1) launches: [block][query round][phase], phase 7 = the list length (sums: the longest)
+int pcp_diag_nb_stamps(pcp_ctx *ctx, int which, unsigned long long *out, size_t n) {
+    PCP_HIP(ctx, hipDeviceSynchronize());
+    const size_t per = (size_t)kNbStampBlocks * kNbStampQ * kNbStampPh;
+    n = std::min<size_t>(n, per);
+    PCP_HIP(ctx, hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nb_stamps), n * 8,
+                                     (size_t)(which ? 1 : 0) * per * 8, hipMemcpyDeviceToHost));
+    return PCP_OK;
+}
+#endif
 
 }  // extern "C"

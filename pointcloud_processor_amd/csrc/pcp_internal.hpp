@@ -244,7 +244,15 @@ struct pcp_ctx {
     uint32_t area_npts = 0, area_grid_a = 0, area_grid_c = 0;
     uint64_t area_total = 0;
     pcp::PinnedBuf area_host;        // the setup's landing: [cells, area list use, cell list use,
-                                     // overflow]
+                                     // overflow, pool cursors]
+    // the async setup's normals + lattice on a stream of their own (PCP_AREA_STREAM, default 1):
+    // forked from ctx->stream after the indices, joined by the scoring (score_enqueue) or by
+    // area_finish, so the terrain / zx120 index builds in between overlap the neighbour lists
+    bool area_side = true;
+    bool area_forked = false;        // side work enqueued and not yet joined into ctx->stream
+    hipStream_t area_stream = nullptr;
+    hipEvent_t area_fork_ev = nullptr, area_join_ev = nullptr;
+    pcp::DevBuf lat_flags;           // the lattice's per-point flags (k_lattice_flags)
     // excavation area (pcp_set_excavation_area): indices for the normal radius (1.5 m) and the
     // lattice test radius (1.5 * grid_resolution), and the per-point normals
     pcp::GridIndex exc_norm, exc_near;
@@ -499,6 +507,9 @@ int area_finish(pcp_ctx *ctx);
 // after a stream synchronisation that followed the pending setup: did its lists overflow?  (the
 // count in ctx->area_host is then valid, the cells' normals are not)
 bool area_overflowed(const pcp_ctx *ctx);
+// the async setup's side stream joined into ctx->stream (a stream wait, no host wait); a no-op
+// when nothing is forked
+void area_join(pcp_ctx *ctx);
 
 // the context's RCCL communicator and its buffers (pcp_comm.hip), at pcp_destroy
 void comm_release(pcp_ctx *ctx);

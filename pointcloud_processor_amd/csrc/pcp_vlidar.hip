@@ -1646,6 +1646,7 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
     // stride and the grids' size, the device's count the cells (only pcp_generate_and_score
     // queries it that way: every other caller settled it first)
     const bool pend = ctx->area_pending;
+    area_join(ctx);   // (a setup's side stream: the cells, their normals and count)
     const int C = pend ? (int)ctx->cells_cap : (int)ctx->n_cells, P = (int)n;
     const uint32_t *C_dev = pend ? ctx->cells_n_d.as<const uint32_t>() : nullptr;
     o.C_dev = C_dev;

@@ -1,7 +1,7 @@
 """One steady-state C5 frame from a replay trace (tools/replay_trace.sh) as a sequence: host API
 calls (thread time) and kernels (device time), offsets in us from the frame's first crop launch.
 
-    python tools/c5_sequence.py [TRACE_DIR] [FRAME_INDEX]
+    python tools/c5_sequence.py [TRACE_DIR] [FRAME_INDEX] [CROPS_PER_FRAME]
 """
 import csv
 import sys
@@ -10,8 +10,9 @@ d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/c5tl"
 K = list(csv.DictReader(open(f"{d}/c5_kernel_trace.csv")))
 A = list(csv.DictReader(open(f"{d}/c5_hip_api_trace.csv")))
 starts = sorted(int(r["Start_Timestamp"]) for r in K if "k_crop_tile" in r["Kernel_Name"])
-fr = starts[::2]
-i = int(sys.argv[2]) if len(sys.argv) > 2 else len(fr) // 2
+per = int(sys.argv[3]) if len(sys.argv) > 3 else 1   # crops per frame (2: the filters one by one)
+fr = starts[::per]
+i = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2] else len(fr) // 2
 t0, t1 = fr[i], fr[i + 1]
 # the frame's host side begins before its first kernel: take API calls from the previous
 # frame's last kernel end

@@ -12,8 +12,10 @@ K.sort(key=lambda r: int(r["Start_Timestamp"]))
 A.sort(key=lambda r: int(r["Start_Timestamp"]))
 name = lambda r: r["Kernel_Name"].split("(")[0].replace("void ", "")[:48]
 starts = [int(r["Start_Timestamp"]) for r in K if "k_crop_tile" in r["Kernel_Name"]]
-# two filter calls per frame (robot, zx120): a frame starts at every other crop
-fr = starts[::2]
+# crops per frame: 2 with the filter nodes called one by one, 1 composed (PCP_FRONT_FUSED=1);
+# argv[2] = the replay's frames (+ 2 warm-up) to infer it
+per = round(len(starts) / int(sys.argv[2])) if len(sys.argv) > 2 else 2
+fr = starts[::max(per, 1)]
 fr = fr[len(fr) // 3:]   # steady state
 nf = len(fr) - 1
 kt = collections.Counter()
