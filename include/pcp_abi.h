@@ -256,6 +256,19 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
                  const pcp_rigid *zx120_base, void *terrain_out, uint64_t terrain_cap,
                  uint64_t *n_terrain, void *area_out, uint64_t area_cap, uint64_t *n_area,
                  double pose_out[4]);
+/* The carve node and virtual_lidar's two callbacks for its messages composed in one process
+ * (the C5 chain): pcp_excavate, then pcp_set_excavation_area_async over /excavation_area
+ * (skipped when empty: :168) and pcp_set_terrain over /excavated_terrain, fed from the carve's
+ * records where they land (device-readable pinned memory, no staging copy or upload), the host
+ * copies into terrain_out / area_out made after the setup and the index build are enqueued.
+ * Arguments and results as those three calls'; grid_bbox / cells_cap as
+ * pcp_set_excavation_area_async's (settled the same way).  Waits once (the carve's counts). */
+int pcp_excavate_area_async(pcp_ctx *ctx, const pcp_cloud_view *in,
+                            const pcp_excavation_params *p, const pcp_rigid *zx120_base,
+                            void *terrain_out, uint64_t terrain_cap, uint64_t *n_terrain,
+                            void *area_out, uint64_t area_cap, uint64_t *n_area,
+                            double pose_out[4], double grid_resolution, int32_t vertical_layers,
+                            double grid_bbox[6], uint64_t *cells_cap);
 
 /* ---- calc_drivable_area.cpp (the occupancy-grid node) -------------------------------------- */
 typedef struct pcp_drivable_params {   /* calc_drivable_area.cpp:20-26 */

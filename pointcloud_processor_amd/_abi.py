@@ -132,6 +132,8 @@ _SIGS = [
     ("pcp_get_area_normals", C.c_int, [_P, _P, C.c_uint64, _P]),
     ("pcp_excavate", C.c_int, [_P, _P, _P, _P, _P, C.c_uint64, _P, _P, C.c_uint64, _P, _P]),
     ("pcp_excavate_bounds", C.c_int, [_P, C.c_uint64, _P, _P]),
+    ("pcp_excavate_area_async", C.c_int, [_P, _P, _P, _P, _P, C.c_uint64, _P, _P, C.c_uint64, _P,
+                                          _P, C.c_double, C.c_int32, _P, _P]),
     ("pcp_drivable_area", C.c_int, [_P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double,
                                     _P, _P, C.c_uint64, _P, _P]),
     ("pcp_generate_candidates", C.c_int, [_P, _P, C.POINTER(VlParams), _P, _P, C.c_uint64,
@@ -599,6 +601,28 @@ class Context:
                                           area.shape[0], C.byref(na), _ptr(pose)),
                     "pcp_excavate")
         return terr[:nt.value], area[:na.value], pose
+
+    def excavate_area_async(self, cloud: np.ndarray, zx120_tf, params: ExcavationParams | None = None,
+                            grid_resolution: float = 0.1, vertical_layers: int = 10,
+                            point_step=None, offs=(0, 4, 8)):
+        """pcp_excavate_area_async: excavate(), then set_excavation_area_async() over its area
+        (when not empty) and set_terrain() over its terrain, fed from the carve's landed
+        records.  -> (terrain, area, pose, grid_bbox (6,), cells_cap)."""
+        v = cloud_view(cloud, point_step, offs)
+        p = params or excavation_params()
+        tf = Rigid((C.c_double * 3)(*zx120_tf[0]), (C.c_double * 4)(*zx120_tf[1]))
+        nt, na, cap = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        pose = np.zeros(4, np.float64)
+        bbox = np.zeros(6, np.float64)
+        self._check(self.lib.pcp_excavate_bounds(C.byref(p), v.n, C.byref(nt), C.byref(na)),
+                    "pcp_excavate_bounds")
+        terr = np.empty((max(nt.value, 1), 8), np.float32)
+        area = np.empty((max(na.value, 1), 8), np.float32)
+        self._check(self.lib.pcp_excavate_area_async(
+            self.h, C.byref(v), C.byref(p), C.byref(tf), _ptr(terr), terr.shape[0], C.byref(nt),
+            _ptr(area), area.shape[0], C.byref(na), _ptr(pose), float(grid_resolution),
+            int(vertical_layers), _ptr(bbox), C.byref(cap)), "pcp_excavate_area_async")
+        return terr[:nt.value], area[:na.value], pose, bbox, cap.value
 
     def drivable_area(self, cloud: np.ndarray, cloud_to_map, robot_xy, start_xy,
                       params: DrivableParams | None = None, point_step=None, offs=(0, 4, 8)):

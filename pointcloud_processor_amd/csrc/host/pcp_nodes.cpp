@@ -303,6 +303,58 @@ bool SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg
     return true;
 }
 
+ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
+    ExcavationTerrainGenerator &gen, const PointCloud2 &msg, const Transform *zx120_base) {
+    pcp_cloud_view v;
+    if (!defer_grid_ || multi_ || !gen.p_.enabled || !zx120_base || !cloud_view(msg, v, nullptr)) {
+        ExcavationTerrainGenerator::Output o = gen.matchedCloudCallback(msg, zx120_base);
+        if (o.area_published && !excavationAreaCallback(o.excavation_area) && !err_.empty())
+            return o;
+        terrainCallback(o.excavated_terrain);
+        return o;
+    }
+    ExcavationTerrainGenerator::Output o;
+    gen.err_.clear();
+    err_.clear();
+    pcp_rigid tf;
+    for (int a = 0; a < 3; ++a) tf.t[a] = zx120_base->t[a];
+    for (int a = 0; a < 4; ++a) tf.q[a] = zx120_base->q[a];
+    uint64_t nt = 0, na = 0, ncap = 0;
+    double pose[4], bb[6];
+    if (pcp_excavate_bounds(&gen.p_, v.n, &nt, &na) != PCP_OK) {
+        gen.err_ = "excavated_surface_generator: bad parameters";
+        o.excavated_terrain = msg;
+        terrainCallback(o.excavated_terrain);
+        return o;
+    }
+    uint8_t *terr = landing(gen.terr_, nt * 32 + 32), *area = landing(gen.area_, na * 32 + 32);
+    if (pcp_excavate_area_async(dev_.ctx(), &v, &gen.p_, &tf, terr, nt, &nt, area, na, &na, pose,
+                                p_.grid_resolution, p_.vertical_layers, bb, &ncap) != PCP_OK) {
+        gen.err_ = dev_.error();
+        o.excavated_terrain = msg;
+        return o;
+    }
+    o.excavated_terrain = make_xyzrgb_cloud(terr, nt, "map");
+    o.excavated_terrain.stamp = msg.stamp;
+    o.excavation_area = make_xyzrgb_cloud(area, na, "map");
+    o.excavation_area.stamp = msg.stamp;
+    o.area_published = true;
+    o.center[0] = pose[0];
+    o.center[1] = pose[1];
+    o.center[2] = pose[2];
+    o.yaw = pose[3];
+    // this node as its two callbacks leave it: the terrain message arrived; a non-empty area
+    // rebuilt the (deferred) grid, an empty one kept the previous (:168)
+    terrain_cloud_ = true;
+    if (na) {
+        n_cells_ = ncap;
+        grid_pending_ = ncap != 0;
+        flags_.assign(n_cells_, 0);   // fresh GridCells (:259)
+        std::memcpy(bbox_, bb, sizeof(bbox_));
+    }
+    return o;
+}
+
 size_t SimplifiedDualLidarOptimizer::lastCells() {
     if (grid_pending_) {
         uint64_t n = 0;

@@ -187,6 +187,7 @@ class ExcavationTerrainGenerator {
     const std::string &lastError() const { return err_; }
 
    private:
+    friend class SimplifiedDualLidarOptimizer;   // carveCallbacks: the composed chain
     Device &dev_;
     Params p_;
     // result landings sized by pcp_excavate_bounds (MBs: the generated-point capacities), reused
@@ -273,6 +274,15 @@ class SimplifiedDualLidarOptimizer {
     // runOptimization waits once for both.  Off by default: a ROS shell publishes the grid
     // markers from the area callback, which needs the cells there
     void setDeferredGrid(bool on) { defer_grid_ = on && !multi_; }
+    // composed chain: gen's matchedCloudCallback, then this node's excavationAreaCallback (when
+    // the area is published) and terrainCallback for gen's two messages, in one call
+    // (pcp_excavate_area_async: the carve's records feed the deferred grid setup and the terrain
+    // index where they land, no re-upload).  Same messages, same state as the three calls; with
+    // the grid not deferred (or sharded, or the carve disabled / its TF missing) it makes them.
+    // Errors: gen.lastError() for the carve, lastError() for the two callbacks
+    ExcavationTerrainGenerator::Output carveCallbacks(ExcavationTerrainGenerator &gen,
+                                                      const PointCloud2 &merged,
+                                                      const Transform *zx120_base);
     const std::string &lastError() const { return err_; }
 
    private:

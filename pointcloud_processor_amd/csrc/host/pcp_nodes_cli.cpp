@@ -215,6 +215,9 @@ static int cmd_replay(Device &dev, char **a) {
     ComposedFilterMerge front(dev);
     bool front_fused = true;
     if (const char *ff = std::getenv("PCP_FRONT_FUSED")) front_fused = std::atoi(ff) != 0;
+    // the carve node and virtual_lidar's area + terrain callbacks composed (default)
+    bool carve_fused = true;
+    if (const char *cf = std::getenv("PCP_CARVE_FUSED")) carve_fused = std::atoi(cf) != 0;
     ExcavationTerrainGenerator gen(dev);
     SimplifiedDualLidarOptimizer vl(dev);
     // the nodes composed in one process: the grid setup is enqueued by the area callback and
@@ -284,7 +287,16 @@ static int cmd_replay(Device &dev, char **a) {
             lap(1);
         }
         ExcavationTerrainGenerator::Output e;
-        if (chain) {
+        if (chain && carve_fused) {   // the carve + both callbacks (stage "carve" holds all three)
+            e = vl.carveCallbacks(gen, o.merged, &zx_base);
+            if (!e.area_published) {
+                std::fprintf(stderr, "replay: carve failed: %s\n", gen.lastError().c_str());
+                return 1;
+            }
+            lap(2);
+            lap(3);
+            lap(4);
+        } else if (chain) {
             e = gen.matchedCloudCallback(o.merged, &zx_base);
             if (!e.area_published) {
                 std::fprintf(stderr, "replay: carve failed: %s\n", gen.lastError().c_str());

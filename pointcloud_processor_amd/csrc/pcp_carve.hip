@@ -405,16 +405,19 @@ static float pack_rgb(unsigned r, unsigned g, unsigned b) {
     return f;
 }
 
-}  // namespace pcp
+// the carve (pcp_excavate).  xl non-null (pcp_excavate_area_async): the records land in
+// ctx->exc_land (pinned, device-readable, kept until the next such call) when they fit, and are
+// NOT copied to terrain_out / area_out here -- xl->terr / xl->area point at them and the caller
+// copies them out after enqueueing their consumers
+struct ExcLand {
+    bool landed = false;
+    const unsigned char *terr = nullptr, *area = nullptr;
+};
 
-using namespace pcp;
-
-extern "C" {
-
-int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_params *p,
-                 const pcp_rigid *zx120_base, void *terrain_out, uint64_t terrain_cap,
-                 uint64_t *n_terrain, void *area_out, uint64_t area_cap, uint64_t *n_area,
-                 double pose_out[4]) {
+static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_params *p,
+                         const pcp_rigid *zx120_base, void *terrain_out, uint64_t terrain_cap,
+                         uint64_t *n_terrain, void *area_out, uint64_t area_cap, uint64_t *n_area,
+                         double pose_out[4], ExcLand *xl) {
     if (!ctx) return PCP_E_INVALID;
     if (!p || !zx120_base || !n_terrain || !n_area)
         return set_err(ctx, PCP_E_INVALID, "pcp_excavate: null argument");
@@ -589,7 +592,10 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     const size_t land_b = (n + nsurf + narea) * 32;
     const bool land = ctx->zc_in && land_b <= kPinDirectMax * 8;
     float4 *kept;
-    if (land) {
+    if (land && xl) {
+        PCP_HIP(ctx, ctx->exc_land.ensure(land_b + 256));
+        kept = ctx->exc_land.as<float4>();
+    } else if (land) {
         PCP_HIP(ctx, ctx->tc_host.ensure(land_b + 256));
         kept = ctx->tc_host.as<float4>();
     } else {
@@ -702,7 +708,11 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
     }
     if ((*n_terrain && !terrain_out) || (*n_area && !area_out))
         return set_err(ctx, PCP_E_INVALID, "pcp_excavate: null output");
-    if (land) {   // the records sit in pinned memory already
+    if (land && xl) {   // the caller copies them out
+        xl->landed = true;
+        xl->terr = reinterpret_cast<const unsigned char *>(kept);
+        xl->area = reinterpret_cast<const unsigned char *>(area_d);
+    } else if (land) {   // the records sit in pinned memory already
         if (*n_terrain) host_copy(ctx, terrain_out, kept, *n_terrain * 32);
         if (narea) host_copy(ctx, area_out, area_d, narea * 32);
     } else if (!one_trip) {   // exact-size buffers: the records follow the sizes
@@ -714,6 +724,65 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
         PCP_HIP(ctx, hipStreamSynchronize(st));
     }
     prof_resolve(ctx);
+    return PCP_OK;
+}
+
+}  // namespace pcp
+
+using namespace pcp;
+
+extern "C" {
+
+int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_params *p,
+                 const pcp_rigid *zx120_base, void *terrain_out, uint64_t terrain_cap,
+                 uint64_t *n_terrain, void *area_out, uint64_t area_cap, uint64_t *n_area,
+                 double pose_out[4]) {
+    return excavate_impl(ctx, in, p, zx120_base, terrain_out, terrain_cap, n_terrain, area_out,
+                         area_cap, n_area, pose_out, nullptr);
+}
+
+int pcp_excavate_area_async(pcp_ctx *ctx, const pcp_cloud_view *in,
+                            const pcp_excavation_params *p, const pcp_rigid *zx120_base,
+                            void *terrain_out, uint64_t terrain_cap, uint64_t *n_terrain,
+                            void *area_out, uint64_t area_cap, uint64_t *n_area,
+                            double pose_out[4], double grid_resolution, int32_t vertical_layers,
+                            double grid_bbox[6], uint64_t *n_cells) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!n_cells) return set_err(ctx, PCP_E_INVALID, "pcp_excavate_area_async: null argument");
+    // a setup still in flight may read the landing this carve rewrites
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    if (int rc = area_finish(ctx)) return rc;
+    ExcLand xl;
+    if (int rc = excavate_impl(ctx, in, p, zx120_base, terrain_out, terrain_cap, n_terrain,
+                               area_out, area_cap, n_area, pose_out, &xl))
+        return rc;
+    // the carve's records as the two messages' views (xyz at 0 / 4 / 8 of 32-byte records)
+    auto rec_view = [](const void *d, uint64_t n) {
+        pcp_cloud_view v{};
+        v.data = n ? d : nullptr;
+        v.n = n;
+        v.point_step = 32;
+        v.off_x = 0;
+        v.off_y = 4;
+        v.off_z = 8;
+        return v;
+    };
+    if (!xl.landed) {   // records past the landing's size: the two calls over the copies
+        const pcp_cloud_view va = rec_view(area_out, *n_area), vt = rec_view(terrain_out, *n_terrain);
+        if (int rc = pcp_set_excavation_area_async(ctx, &va, grid_resolution, vertical_layers,
+                                                   grid_bbox, n_cells))
+            return rc;
+        return pcp_set_terrain(ctx, &vt);
+    }
+    // the landed records feed the setup and the terrain index in place (device-readable pinned
+    // memory: no staging copy, no upload); the messages' copies follow the launches
+    const pcp_cloud_view va = rec_view(xl.area, *n_area), vt = rec_view(xl.terr, *n_terrain);
+    if (int rc = area_setup_from(ctx, &va, grid_resolution, vertical_layers, grid_bbox, n_cells,
+                                 true, xl.area))
+        return rc;
+    if (int rc = set_terrain_from(ctx, &vt, xl.terr)) return rc;
+    if (*n_terrain) host_copy(ctx, terrain_out, xl.terr, *n_terrain * 32);
+    if (*n_area) host_copy(ctx, area_out, xl.area, *n_area * 32);
     return PCP_OK;
 }
 

@@ -555,6 +555,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     if (ctx->fm_exec) (void)hipGraphExecDestroy(ctx->fm_exec);
     if (ctx->fm_graph) (void)hipGraphDestroy(ctx->fm_graph);
     ctx->lat_flags.release();
+    ctx->exc_land.release();
     if (ctx->area_stream) (void)hipStreamDestroy(ctx->area_stream);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;

@@ -640,7 +640,7 @@ template <> struct NbCfg<true> {
 };
 constexpr int kNbSteps = 64;   // list entries per chunk
 #ifndef PCP_NB_LIST_AHEAD
-#define PCP_NB_LIST_AHEAD 4    // k_nb_sums: chunks of list entries in flight (build knob, A/B)
+#define PCP_NB_LIST_AHEAD 1    // k_nb_sums: chunks of list entries in flight (build knob, A/B: 1 best)
 #endif
 constexpr int kNbListAhead = PCP_NB_LIST_AHEAD;
 
@@ -1267,10 +1267,11 @@ int area_finish(pcp_ctx *ctx) {
     return PCP_OK;
 }
 
-// pcp_set_excavation_area (defer = false: settled before the return) and its _async form
-static int area_setup(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
-                      int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells,
-                      bool defer) {
+// pcp_set_excavation_area (defer = false: settled before the return) and its _async form;
+// raw_pre: the records already device-readable (pcp_excavate_area_async's landing), else staged
+int area_setup_from(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
+                    int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells, bool defer,
+                    const unsigned char *raw_pre) {
     if (!ctx) return PCP_E_INVALID;
     int rc = check_view(ctx, area, "pcp_set_excavation_area");
     if (rc) return rc;
@@ -1284,7 +1285,7 @@ static int area_setup(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_reso
     ProfScope prof(ctx, PCP_K_EXCAV_SETUP);
     const double r_near = grid_resolution * 1.5;
     // both indices read the same staged bytes (staged once)
-    const unsigned char *raw = nullptr;
+    const unsigned char *raw = raw_pre;
     if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius, false, false, &raw))) return rc;
     rc = build_index(ctx, ctx->exc_near, *area, r_near, false, false, &raw);
     if (rc) return rc;   // (a held slot is drained by the next pin_stage)
@@ -1456,13 +1457,15 @@ extern "C" {
 
 int pcp_set_excavation_area(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
                             int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells) {
-    return area_setup(ctx, area, grid_resolution, vertical_layers, grid_bbox, n_cells, false);
+    return area_setup_from(ctx, area, grid_resolution, vertical_layers, grid_bbox, n_cells, false,
+                           nullptr);
 }
 
 int pcp_set_excavation_area_async(pcp_ctx *ctx, const pcp_cloud_view *area,
                                   double grid_resolution, int32_t vertical_layers,
                                   double grid_bbox[6], uint64_t *cells_cap) {
-    return area_setup(ctx, area, grid_resolution, vertical_layers, grid_bbox, cells_cap, true);
+    return area_setup_from(ctx, area, grid_resolution, vertical_layers, grid_bbox, cells_cap, true,
+                           nullptr);
 }
 
 int pcp_cells_count(pcp_ctx *ctx, uint64_t *n_cells) {

@@ -730,13 +730,7 @@ int terrain_blocks_before_query(pcp_ctx *ctx) {
     return build_blocks(ctx, t);   // the 2x2x2 block copy (also past the fine copy's caps)
 }
 
-}  // namespace pcp
-
-using namespace pcp;
-
-extern "C" {
-
-int pcp_set_terrain(pcp_ctx *ctx, const pcp_cloud_view *terrain) {
+int set_terrain_from(pcp_ctx *ctx, const pcp_cloud_view *terrain, const unsigned char *raw_pre) {
     if (!ctx) return PCP_E_INVALID;
     int rc = check_view(ctx, terrain, "pcp_set_terrain");
     if (rc) return rc;
@@ -744,10 +738,22 @@ int pcp_set_terrain(pcp_ctx *ctx, const pcp_cloud_view *terrain) {
     ctx->terrain_cloud_n = terrain->n;
     if (terrain->n == 0) return PCP_OK;   // terrainCallback: no rebuild on an empty cloud
     // the march probes the z bands; occupancy bits only for the fan's A/B variant 2
-    rc = build_index(ctx, ctx->terrain, *terrain, kRayRadius, true, ctx->fan_batch == 2);
+    const unsigned char *raw = raw_pre;
+    rc = build_index(ctx, ctx->terrain, *terrain, kRayRadius, true, ctx->fan_batch == 2,
+                     raw ? &raw : nullptr);
     ctx->terrain_queries = 0;
     prof_resolve(ctx);
     return rc;
+}
+
+}  // namespace pcp
+
+using namespace pcp;
+
+extern "C" {
+
+int pcp_set_terrain(pcp_ctx *ctx, const pcp_cloud_view *terrain) {
+    return set_terrain_from(ctx, terrain, nullptr);
 }
 
 int pcp_set_aux_cloud(pcp_ctx *ctx, const pcp_cloud_view *aux) {

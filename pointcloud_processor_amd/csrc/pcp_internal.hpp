@@ -253,6 +253,8 @@ struct pcp_ctx {
     hipStream_t area_stream = nullptr;
     hipEvent_t area_fork_ev = nullptr, area_join_ev = nullptr;
     pcp::DevBuf lat_flags;           // the lattice's per-point flags (k_lattice_flags)
+    pcp::PinnedBuf exc_land;         // pcp_excavate_area_async: the carve's records, read in place
+                                     // by the setup + terrain index it enqueues
     // excavation area (pcp_set_excavation_area): indices for the normal radius (1.5 m) and the
     // lattice test radius (1.5 * grid_resolution), and the per-point normals
     pcp::GridIndex exc_norm, exc_near;
@@ -510,6 +512,13 @@ bool area_overflowed(const pcp_ctx *ctx);
 // the async setup's side stream joined into ctx->stream (a stream wait, no host wait); a no-op
 // when nothing is forked
 void area_join(pcp_ctx *ctx);
+// the area setup over records already device-readable (raw_pre: pcp_excavate_area_async's
+// pinned landing; nullptr: staged from area->data as pcp_set_excavation_area does)
+int area_setup_from(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolution,
+                    int32_t vertical_layers, double grid_bbox[6], uint64_t *n_cells, bool defer,
+                    const unsigned char *raw_pre);
+// pcp_set_terrain over records already device-readable (raw_pre), or staged (nullptr)
+int set_terrain_from(pcp_ctx *ctx, const pcp_cloud_view *terrain, const unsigned char *raw_pre);
 
 // the context's RCCL communicator and its buffers (pcp_comm.hip), at pcp_destroy
 void comm_release(pcp_ctx *ctx);

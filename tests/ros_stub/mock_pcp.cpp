@@ -88,6 +88,12 @@ int pcp_set_excavation_area_async(pcp_ctx *c, const pcp_cloud_view *area, double
                                   double bb[6], uint64_t *cap) {
     return pcp_set_excavation_area(c, area, res, l, bb, cap);
 }
+// the composed carve + area + terrain (not used by the shells)
+int pcp_excavate_area_async(pcp_ctx *c, const pcp_cloud_view *, const pcp_excavation_params *,
+                            const pcp_rigid *, void *, uint64_t, uint64_t *, void *, uint64_t,
+                            uint64_t *, double *, double, int32_t, double *, uint64_t *) {
+    return fail(c, "pcp_excavate_area_async: not in the test double");
+}
 int pcp_cells_count(pcp_ctx *c, uint64_t *n) {
     *n = c->cells.size() / 3;
     return PCP_OK;

@@ -1340,6 +1340,54 @@ def test_excavation_area_async_then_tick(oracle, scene, which):
     assert a[5] == b[5] and a[8] == b[8]
 
 
+def test_excavate_area_async_matches_three_calls():
+    """pcp_excavate_area_async (the carve node and virtual_lidar's area + terrain callbacks
+    composed: the carve's landed records feed the grid setup and the terrain index in place)
+    against pcp_excavate + pcp_set_excavation_area + pcp_set_terrain on the same merged cloud:
+    both messages, the pose, the grid bounds, the cells and their normals, and a tick's poses,
+    totals, covered counts, flags and report bit-identical.  Three frames in a row on one
+    context (the landing is reused while the previous setup is pending: the call settles it
+    first), the third with the carve moved (a new generated lattice)."""
+    box = np.array([0.0, 15.0, -10.0, 10.0, -1.5, 10.0])
+    tfs = [((8.0, -3.0, 2.0), (0.0, 0.0, 0.2588190451025208, 0.9659258262890683)),
+           ((0.55, 0.4, 3.5), (0.0, 0.21633, 0.0, 0.97632))]
+    params = _abi.default_vl_params(num_candidates=36)
+    zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])
+    frames = []
+    for f, (seed, base) in enumerate([(101, ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))),
+                                      (131, ((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))),
+                                      (131, ((0.3, -0.2, 0.0), (0.0, 0.0, 0.0998, 0.9950)))]):
+        scans = [synth.lidar_cloud(60_032, sensor_height=2.0, seed=seed),
+                 synth.lidar_cloud(60_032, sensor_height=3.5, seed=seed + 1)]
+        frames.append((scans, base))
+    out = {}
+    for mode in ("calls", "composed"):
+        res = []
+        with _abi.Context(0) as ctx:
+            for scans, base in frames:
+                filt = [ctx.crop_voxel(sc, box, 0.2)[0] for sc in scans]
+                merged = ctx.transform_concat(filt, tfs, [(255, 0, 0), (0, 0, 255)])
+                if mode == "calls":
+                    terr, area, pose = ctx.excavate(merged, base)
+                    bb, n = ctx.set_excavation_area_async(area, 0.1, 10, point_step=32)
+                    ctx.set_terrain(terr, point_step=32)
+                else:
+                    terr, area, pose, bb, n = ctx.excavate_area_async(merged, base)
+                ctx.set_aux_cloud(filt[1])
+                flags = np.zeros(max(n, 1), np.uint8)
+                poses, tot, cov, rep = ctx.generate_and_score(bb, params, zx, flags)
+                nc = ctx.cells_count()
+                xyz, cn = ctx.get_cells()
+                res.append((terr.copy(), area.copy(), pose, bb, nc, poses, tot, cov, flags[:nc].copy(),
+                            rep.as_dict(), xyz, cn))
+        out[mode] = res
+    for a, b in zip(out["calls"], out["composed"]):
+        for i in (0, 1, 2, 3, 5, 6, 7, 8, 10, 11):
+            np.testing.assert_array_equal(np.asarray(a[i]).view(np.uint8), np.asarray(b[i]).view(np.uint8))
+        assert a[4] == b[4] and a[4] > 0
+        assert a[9] == b[9]
+
+
 def _degenerate_areas():
     rng = np.random.default_rng(23)
     out = {}

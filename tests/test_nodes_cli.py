@@ -141,8 +141,9 @@ def test_excavation_area_node(tmp_path, oracle, small_scene):
     assert res["best_idx"] == rep.best_idx
 
 
-@pytest.mark.parametrize("zc,area_async,front", [("1", "1", "1"), ("0", "1", "1"), ("1", "0", "0")])
-def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_async, front):
+@pytest.mark.parametrize("zc,area_async,front,carve", [("1", "1", "1", "1"), ("0", "1", "1", "1"),
+                                                     ("1", "1", "1", "0"), ("1", "0", "0", "0")])
+def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_async, front, carve):
     """C5 with the launch file's whole chain per frame: filter x2 -> merge ->
     excavated_surface_generator (/excavated_terrain, /excavation_area) -> virtual_lidar
     (terrain index, normals + cell grid, pose search).  Frames 0, 1, 2 and the last one are
@@ -155,7 +156,9 @@ def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_as
     default) and DMA'd both ways (0); the grid setup deferred to the tick (PCP_AREA_ASYNC=1, the
     composed chain's default: one wait for both) and settled in the area callback (0); the
     filter and merger nodes composed in one call (PCP_FRONT_FUSED=1, default) and as the three
-    node callbacks (0)."""
+    node callbacks (0); the carve node and virtual_lidar's area + terrain callbacks composed
+    (PCP_CARVE_FUSED=1, default: pcp_excavate_area_async, the carve's landed records feeding the
+    setup and the index in place) and as the three callbacks (0)."""
     np.ascontiguousarray(scene.terrain).tofile(tmp_path / "t.f32")
     np.ascontiguousarray(cells.xyz).tofile(tmp_path / "c.f64")
     np.ascontiguousarray(cells.normals).tofile(tmp_path / "n.f32")
@@ -163,7 +166,7 @@ def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_as
     res = _run("replay", tmp_path / "t.f32", scene.terrain.shape[0], tmp_path / "c.f64",
                tmp_path / "n.f32", cells.xyz.shape[0], _t(cells.grid_bbox), frames, 60032, 1,
                tmp_path, env={"PCP_ZC_IN": zc, "PCP_AREA_ASYNC": area_async,
-                              "PCP_FRONT_FUSED": front})
+                              "PCP_FRONT_FUSED": front, "PCP_CARVE_FUSED": carve})
     assert res["frames"] == frames and res["chain"] == 1
     assert res["cells"] > 0 and res["merged_points"] > 0 and res["best_idx"] >= 0
     assert 0 < res["p50_ms"] <= res["p99_ms"]
