@@ -393,6 +393,83 @@ k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = run;
 }
 
+// one-pass exclusive scan: tiles take tickets in arrival order (a tile waits only for tiles
+// already running), publish their aggregate, then look back over their predecessors' status
+// words 64 at a time (wave 0, one per lane) until an inclusive prefix; a status word is one
+// 64-bit agent-scope store {value, epoch << 2 | flag} (flag 1 aggregate, 2 inclusive), so a
+// reader sees the value with its flag and the previous call's words (older epoch) as absent
+__global__ void __launch_bounds__(kScanThreads)
+k_scan_onepass(const uint32_t *in, uint64_t n, uint32_t *out, uint32_t *out2, int zero2,
+               unsigned long long *state, uint32_t *ticket, uint32_t ticket_base, uint32_t epoch) {
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t sh_tile, sh_prefix;
+    if (threadIdx.x == 0) sh_tile = atomicAdd(ticket, 1u) - ticket_base;
+    __syncthreads();
+    const uint32_t tile = sh_tile;
+    const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems], s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t k = base + i;
+        v[i] = (k < n) ? in[k] : 0u;
+        s += v[i];
+    }
+    uint32_t agg;
+    const uint32_t ex_local = block_excl_scan(s, lds4, &agg);
+    const uint64_t tag = (uint64_t)(epoch << 2);
+    auto publish = [&](uint32_t flag, uint32_t val) {
+        __hip_atomic_store(&state[tile], ((tag | flag) << 32) | val, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (threadIdx.x == 0) publish(tile == 0 ? 2u : 1u, agg);
+    if (tile > 0 && threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        uint32_t prefix = 0;
+        int64_t top = (int64_t)tile - 1;   // the window's first (nearest) predecessor
+        for (;;) {
+            const int64_t j = top - lane;
+            uint64_t w = 0;
+            uint32_t flag = 2;   // (lanes past tile 0: an empty inclusive prefix)
+            if (j >= 0) {
+                for (;;) {
+                    w = __hip_atomic_load(&state[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((uint32_t)(w >> 34) == (epoch & 0x3fffffffu) && ((w >> 32) & 3u) != 0u)
+                        break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                flag = (uint32_t)(w >> 32) & 3u;
+            }
+            const uint32_t val = (uint32_t)w;
+            // the nearest inclusive lane ends the walk: add the lanes up to it
+            const uint64_t inc = __ballot(flag == 2u);
+            const int stop = inc ? __ffsll((unsigned long long)inc) - 1 : 64;
+            uint32_t part = lane <= stop ? val : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            prefix += part;
+            if (inc) break;
+            top -= 64;
+        }
+        if (lane == 0) {
+            publish(2u, prefix + agg);
+            sh_prefix = prefix;
+        }
+    }
+    __syncthreads();
+    uint32_t run = ex_local + (tile > 0 ? sh_prefix : 0u);
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+        const uint64_t k = base + i;
+        if (k < n) {
+            out[k] = run;
+            if (out2) out2[k] = zero2 ? 0u : run;
+        }
+        run += v[i];
+    }
+    // out[n] = the total, by the last tile's last thread (its items past n are zero)
+    if (tile == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = run;
+}
+
 size_t scan_tmp_bytes(uint64_t n) {
     size_t bytes = 0;
     while (n > (uint64_t)kScanTile) {
@@ -410,6 +487,26 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
         return PCP_OK;
     }
     const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+    // one pass only where the look-back is one window (tiles <= 64: tile 0's inclusive prefix
+    // in every tile's first window); longer scans walk windows of aggregates back to tile 0,
+    // which measured slower than the three short launches (terrain grids, ~430 tiles)
+    if (tiles > 1 && tiles <= 64 && ctx->scan_onepass) {
+        const size_t cap0 = ctx->scan_state.cap;
+        PCP_HIP(ctx, ctx->scan_state.ensure(tiles * sizeof(unsigned long long) + 64));
+        if (++ctx->scan_epoch >= (1u << 30) || ctx->scan_state.cap != cap0) {   // wrap / new buffer
+            PCP_HIP(ctx, hipMemsetAsync(ctx->scan_state.p, 0, ctx->scan_state.cap, ctx->stream));
+            ctx->scan_epoch = 1;
+            ctx->scan_ticket = 0;
+        }
+        unsigned long long *state = ctx->scan_state.as<unsigned long long>();
+        uint32_t *ticket = reinterpret_cast<uint32_t *>(ctx->scan_state.as<char>() + ctx->scan_state.cap - 64);
+        hipLaunchKernelGGL(k_scan_onepass, dim3((unsigned)tiles), dim3(kScanThreads), 0, ctx->stream,
+                           in, n, out, out2, zero2 ? 1 : 0, state, ticket, ctx->scan_ticket,
+                           ctx->scan_epoch);
+        PCP_CHECK_LAUNCH(ctx);
+        ctx->scan_ticket += (uint32_t)tiles;
+        return PCP_OK;
+    }
     if (tiles == 1) {
         hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, ctx->stream, in, n,
                            (const uint32_t *)nullptr, out, out2, zero2 ? 1 : 0);
@@ -476,6 +573,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *sw = std::getenv("PCP_SCORE_WIDE")) ctx->score_wide = std::atoi(sw) != 0;
     if (const char *co = std::getenv("PCP_CELLS_ORDER_FREE")) ctx->cells_all_ordered = std::atoi(co) == 0;
     if (const char *nbk = std::getenv("PCP_NB_BLOCKS")) ctx->nb_blocks = std::atoi(nbk);
+    if (const char *sp = std::getenv("PCP_SCAN_ONEPASS")) ctx->scan_onepass = std::atoi(sp) != 0;
     if (const char *as = std::getenv("PCP_AREA_STREAM")) ctx->area_side = std::atoi(as) != 0;
     if (const char *rp = std::getenv("PCP_NB_REGION_PCT"))
         ctx->nb_region_pct = std::min(100, std::max(1, std::atoi(rp)));
@@ -555,6 +653,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     if (ctx->fm_exec) (void)hipGraphExecDestroy(ctx->fm_exec);
     if (ctx->fm_graph) (void)hipGraphDestroy(ctx->fm_graph);
     ctx->lat_flags.release();
+    ctx->scan_state.release();
     ctx->exc_land.release();
     if (ctx->area_stream) (void)hipStreamDestroy(ctx->area_stream);
     (void)hipStreamDestroy(ctx->stream);

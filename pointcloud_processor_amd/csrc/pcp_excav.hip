@@ -1222,11 +1222,12 @@ void area_join(pcp_ctx *ctx) {
     ctx->area_forked = false;
 }
 
-int area_finish(pcp_ctx *ctx) {
+int area_finish(pcp_ctx *ctx, bool stream_synced) {
+    if (ctx->area_forked) stream_synced = false;   // (its join is enqueued below)
     area_join(ctx);
     if (!ctx->area_pending) return PCP_OK;
     hipStream_t st = ctx->stream;
-    PCP_HIP(ctx, hipStreamSynchronize(st));
+    if (!stream_synced) PCP_HIP(ctx, hipStreamSynchronize(st));
     uint32_t *n_h = ctx->area_host.as<uint32_t>();
     if (n_h[3]) {
         // a list buffer too small (first frames, or a denser area): regrow both to their largest

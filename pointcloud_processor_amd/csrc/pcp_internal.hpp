@@ -329,6 +329,11 @@ struct pcp_ctx {
     // host copies of message-sized buffers split over helper threads (pcp_hostcopy.hip,
     // PCP_COPY_THREADS, default 3; 0: plain memcpy)
     int copy_threads = 3;
+    // exclusive_scan_u32's one-pass form (PCP_SCAN_ONEPASS, default 1): the tiles' status words
+    // (value | epoch, flag) and the ticket that orders the tiles; epoch = the call's number
+    bool scan_onepass = true;
+    pcp::DevBuf scan_state;
+    uint32_t scan_epoch = 0, scan_ticket = 0;
     pcp::CopyPool *copy_pool = nullptr;
     pcp::PinnedBuf cv_host;                  // pcp_crop_voxel's fast chain: centroids + result
                                              // sizes stored by the kernels (one round trip)
@@ -505,7 +510,8 @@ void fill_report(const int32_t *st_h, double zx_total, int64_t best_idx, double 
 
 // pcp_set_excavation_area_async's settlement (pcp_excav.hip): waits for the stream, regrows and
 // reruns the neighbour lists on an overflow, sets ctx->n_cells; a no-op with nothing pending
-int area_finish(pcp_ctx *ctx);
+// (stream_synced: the caller has just synchronised ctx->stream after the join)
+int area_finish(pcp_ctx *ctx, bool stream_synced = false);
 // after a stream synchronisation that followed the pending setup: did its lists overflow?  (the
 // count in ctx->area_host is then valid, the cells' normals are not)
 bool area_overflowed(const pcp_ctx *ctx);

@@ -1905,7 +1905,7 @@ int pcp_generate_and_score(pcp_ctx *ctx, const double bb[6], const pcp_vl_params
         // left the cells' normals incomplete -- settle it (regrow, rerun) and tick again from
         // fresh flags; otherwise its count is final (area_finish returns at once)
         const bool over = area_overflowed(ctx);
-        if (int rc = area_finish(ctx)) return rc;
+        if (int rc = area_finish(ctx, true)) return rc;   // (joined by score_enqueue, synced)
         if (over) {
             if (ctx->n_cells) std::memset(cell_flags, 0, ctx->n_cells);
             return pcp_generate_and_score(ctx, bb, p, zx, poses5, cap, n_out, cell_flags,
