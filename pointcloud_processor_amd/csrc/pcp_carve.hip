@@ -75,12 +75,17 @@ __device__ __forceinline__ void dds_add(DDs &a, double x) {
 // candidates of the pit test: points inside some box widened by the largest slope offset
 // (isInsideExcavationArea's offset is slope_offset * (depth + z_rel) / depth <= slope_offset
 // for every z_rel it accepts).  Writes the query (x, y) and the point index.
+// Also presets each keep tile's count (tile_pts points per tile) to its size: k_carve_decide
+// takes the carved points off, so k_keep_emit finds the kept counts without a counting pass.
 __global__ void __launch_bounds__(kCT)
 k_carve_cand(CarveArgs a, double2 *__restrict__ qxy, uint32_t *__restrict__ qidx,
-             uint32_t *__restrict__ count, uint32_t qbase, uint8_t *__restrict__ removed) {
+             uint32_t *__restrict__ count, uint32_t qbase, uint8_t *__restrict__ removed,
+             uint32_t *__restrict__ tcount, uint32_t tile_pts) {
     const uint64_t i = (uint64_t)blockIdx.x * kCT + threadIdx.x;
     bool cand = false;
     float x = 0.f, y = 0.f, z = 0.f;
+    if (i < a.n && i % tile_pts == 0)
+        tcount[i / tile_pts] = (uint32_t)min((uint64_t)tile_pts, a.n - i);
     if (i < a.n) {
         removed[i] = 0;   // (k_carve_decide sets the carved ones)
         load_p(a, i, x, y, z);
@@ -237,7 +242,8 @@ k_nearest(GridView g, const double2 *__restrict__ qxy, const uint32_t *__restric
 // isInsideExcavationArea (:328-348) for each candidate: removed[point] = 1 when inside
 __global__ void __launch_bounds__(kCT)
 k_carve_decide(CarveArgs a, const uint32_t *__restrict__ qidx, const uint32_t *__restrict__ count,
-               const double *__restrict__ h, uint8_t *__restrict__ removed) {
+               const double *__restrict__ h, uint8_t *__restrict__ removed,
+               uint32_t *__restrict__ tcount, uint32_t tile_pts) {
     const uint32_t c = blockIdx.x * kCT + threadIdx.x;
     if (c >= *count) return;
     const uint32_t i = qidx[c];
@@ -257,26 +263,10 @@ k_carve_decide(CarveArgs a, const uint32_t *__restrict__ qidx, const uint32_t *_
             if (fabs(ddx) <= hl && fabs(ddy) <= hw) inside = true;
         }
     }
-    if (inside) removed[i] = 1;
-}
-
-// kept points per 4096-point tile
-__global__ void __launch_bounds__(kCT)
-k_keep_count(uint64_t n, const uint8_t *__restrict__ removed, uint32_t *__restrict__ counts,
-             int items) {
-    const uint64_t base = (uint64_t)blockIdx.x * kCT * items;
-    uint32_t c = 0;
-#pragma unroll 4
-    for (int j = 0; j < items; ++j) {
-        const uint64_t i = base + (uint64_t)j * kCT + threadIdx.x;
-        c += (i < n && !removed[i]) ? 1u : 0u;
+    if (inside) {
+        removed[i] = 1;
+        atomicSub(&tcount[i / tile_pts], 1u);   // (its keep tile's count, preset by k_carve_cand)
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    __shared__ uint32_t w[kCT / 64];
-    if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) counts[blockIdx.x] = w[0] + w[1] + w[2] + w[3];
 }
 
 struct GenPoint {    // a generated point: position, height query, z recipe (reference order)
@@ -291,9 +281,12 @@ struct GenPoint {    // a generated point: position, height query, z recipe (ref
 // queries, in the host's double expressions: record k at out + 2 * (base + k), base = *base_d
 // (the kept count, the generated surface goes after the kept points) or 0
 __global__ void __launch_bounds__(kCT)
-k_gen_emit(const GenPoint *__restrict__ gp, uint32_t ng, const double *__restrict__ h,
-           double depth, const uint32_t *__restrict__ base_d, float4 *__restrict__ out,
-           const uint32_t *__restrict__ ctr, uint32_t *__restrict__ sm_host) {
+k_gen_emit(const GenPoint *__restrict__ gp, uint32_t ns, uint32_t na, const double *__restrict__ h,
+           double depth, const uint32_t *__restrict__ base_d, float4 *__restrict__ out_s,
+           float4 *__restrict__ out_a, const uint32_t *__restrict__ ctr,
+           uint32_t *__restrict__ sm_host) {
+    // the surface records (gp[0 .. ns): after the kept points) and the area's (gp[ns ..)), one
+    // launch
     const uint32_t k = blockIdx.x * kCT + threadIdx.x;
     // the counters and the centre height into the pinned landing (in place of two small DMAs);
     // every kernel that writes them ran before this one
@@ -302,10 +295,12 @@ k_gen_emit(const GenPoint *__restrict__ gp, uint32_t ng, const double *__restric
         const double h0 = h[0];
         __builtin_memcpy(sm_host + 4, &h0, sizeof(double));
     }
-    if (k >= ng) return;
+    if (k >= ns + na) return;
     const GenPoint g = gp[k];
     const double z = g.kind == 0 ? h[g.q] - g.v : (h[g.q] - depth) + g.v;
-    const size_t o = (size_t)(base_d ? *base_d : 0u) + k;
+    const bool surf = k < ns;
+    float4 *out = surf ? out_s : out_a;
+    const size_t o = surf ? (size_t)(base_d ? *base_d : 0u) + k : (size_t)(k - ns);
     out[2 * o] = make_float4((float)g.x, (float)g.y, (float)z, 1.0f);
     out[2 * o + 1] = make_float4(g.rgb, 0.0f, 0.0f, 0.0f);
 }
@@ -625,7 +620,8 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     const float r2 = (float)(p->terrain_search_radius * p->terrain_search_radius);
     const unsigned gn = (unsigned)((n + kCT - 1) / kCT);
     if (n) {
-        hipLaunchKernelGGL(k_carve_cand, dim3(gn), dim3(kCT), 0, st, a, qxy, qidx, ctr, G, removed);
+        hipLaunchKernelGGL(k_carve_cand, dim3(gn), dim3(kCT), 0, st, a, qxy, qidx, ctr, G, removed,
+                           tcount, (uint32_t)kCT * (uint32_t)kitems);
         PCP_CHECK_LAUNCH(ctx);
     }
     const unsigned gq = (unsigned)((nq_max + kCT / 64 - 1) / (kCT / 64));   // a wave per query
@@ -640,10 +636,8 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     PCP_CHECK_LAUNCH(ctx);
     if (n) {
         hipLaunchKernelGGL(k_carve_decide, dim3(gn), dim3(kCT), 0, st, a, (const uint32_t *)qidx,
-                           (const uint32_t *)ctr, (const double *)(h + G), removed);
-        PCP_CHECK_LAUNCH(ctx);
-        hipLaunchKernelGGL(k_keep_count, dim3(nb), dim3(kCT), 0, st, n, (const uint8_t *)removed,
-                           tcount, kitems);
+                           (const uint32_t *)ctr, (const double *)(h + G), removed, tcount,
+                           (uint32_t)kCT * (uint32_t)kitems);
         PCP_CHECK_LAUNCH(ctx);
         hipLaunchKernelGGL(k_keep_emit, dim3(nb), dim3(kCT), 0, st, a, (const uint8_t *)removed,
                            (const uint32_t *)tcount, kept, ctr + 2, kitems);
@@ -655,18 +649,11 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     char *sm = ctx->small_host.as<char>();
     // landed: the first k_gen_emit stores the counters and the centre height too
     uint32_t *sm_k = land ? reinterpret_cast<uint32_t *>(sm) : nullptr;
-    if (nsurf) {
-        hipLaunchKernelGGL(k_gen_emit, dim3((unsigned)((nsurf + kCT - 1) / kCT)), dim3(kCT), 0, st,
-                           (const GenPoint *)gp, (uint32_t)nsurf, (const double *)h, p->depth,
-                           n ? (const uint32_t *)(ctr + 2) : nullptr, kept,
-                           (const uint32_t *)ctr, sm_k);
-        PCP_CHECK_LAUNCH(ctx);
-        sm_k = nullptr;
-    }
-    if (narea) {
-        hipLaunchKernelGGL(k_gen_emit, dim3((unsigned)((narea + kCT - 1) / kCT)), dim3(kCT), 0, st,
-                           (const GenPoint *)(gp + nsurf), (uint32_t)narea, (const double *)h,
-                           p->depth, nullptr, area_d, (const uint32_t *)ctr, sm_k);
+    if (nsurf + narea) {
+        hipLaunchKernelGGL(k_gen_emit, dim3((unsigned)((nsurf + narea + kCT - 1) / kCT)), dim3(kCT),
+                           0, st, (const GenPoint *)gp, (uint32_t)nsurf, (uint32_t)narea,
+                           (const double *)h, p->depth, n ? (const uint32_t *)(ctr + 2) : nullptr,
+                           kept, area_d, (const uint32_t *)ctr, sm_k);
         PCP_CHECK_LAUNCH(ctx);
         sm_k = nullptr;
     }
