@@ -924,20 +924,33 @@ def c1_frame_gpu(ctx, scans, nc_lattice=1):
     (a rosbag message is a host buffer): pointcloud_filter x2 (crop + VoxelGrid 0.2) ->
     pointcloud_merger (transform + colour + concat) -> excavated_surface_generator (carve) ->
     virtual_lidar (normals + cell grid, terrain index, zx120 cloud, runOptimization with ONE
-    candidate pose).  -> (n_candidates, best_idx, totals)."""
+    candidate pose).  -> (n_candidates, best_idx, totals).  The nodes composed as the C5 chain
+    composes them (pcp_filter_merge_nodes: both filters + the merger, one wait;
+    pcp_excavate_area_async: the carve + the area and terrain callbacks, the grid setup left in
+    flight on its side stream while the zx120 index and the candidates are built; the scoring
+    settles it); PCP_C1_CALLS=1: every node callback as its own call (rounds 1-4)."""
     from pointcloud_processor_amd import _abi
 
-    filtered = [ctx.crop_voxel(sc, C1_BOX, C1_LEAF)[0] for sc in scans]
-    merged = ctx.transform_concat(filtered, C1_TFS, [(255, 0, 0), (0, 0, 255)])
-    terr, area, _ = ctx.excavate(merged, C1_ZX_BASE)
-    bbox, nc = ctx.set_excavation_area(area, 0.1, 10)
-    ctx.set_terrain(terr, point_step=32)
-    ctx.set_aux_cloud(filtered[1])
     zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])   # getZX120Position on zx120/base_link
     params = _abi.default_vl_params(num_candidates=nc_lattice)
+    if os.environ.get("PCP_C1_CALLS", "0") == "1":
+        filtered = [ctx.crop_voxel(sc, C1_BOX, C1_LEAF)[0] for sc in scans]
+        merged = ctx.transform_concat(filtered, C1_TFS, [(255, 0, 0), (0, 0, 255)])
+        terr, area, _ = ctx.excavate(merged, C1_ZX_BASE)
+        bbox, nc = ctx.set_excavation_area(area, 0.1, 10)
+        ctx.set_terrain(terr, point_step=32)
+        ctx.set_aux_cloud(filtered[1])
+        cand = ctx.generate_candidates(bbox, params, zx)[:1]   # ONE candidate pose is scored
+        tot, _, rep = ctx.score_poses(cand, zx, params, np.zeros(nc, np.uint8))
+        return cand.shape[0], int(rep.best_idx), tot, cand, nc
+    merged, filtered, _ = ctx.filter_merge_nodes(scans, [C1_BOX, C1_BOX], C1_LEAF, C1_TFS,
+                                                 [(255, 0, 0), (0, 0, 255)])
+    terr, area, _, bbox, cap = ctx.excavate_area_async(merged, C1_ZX_BASE)
+    ctx.set_aux_cloud(filtered[1])
     cand = ctx.generate_candidates(bbox, params, zx)[:1]   # ONE candidate pose is scored
-    tot, _, rep = ctx.score_poses(cand, zx, params, np.zeros(nc, np.uint8))
-    return cand.shape[0], int(rep.best_idx), tot, cand, nc
+    # fresh flags (:259) for the setup's capacity; the scoring settles the count first
+    tot, _, rep = ctx.score_poses(cand, zx, params, np.zeros(max(cap, 1), np.uint8))
+    return cand.shape[0], int(rep.best_idx), tot, cand, ctx.cells_count()
 
 
 def c1_frame_oracle(pyoracle, scans, nc_lattice=1):
