@@ -575,6 +575,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *nbk = std::getenv("PCP_NB_BLOCKS")) ctx->nb_blocks = std::atoi(nbk);
     if (const char *sp = std::getenv("PCP_SCAN_ONEPASS")) ctx->scan_onepass = std::atoi(sp) != 0;
     if (const char *as = std::getenv("PCP_AREA_STREAM")) ctx->area_side = std::atoi(as) != 0;
+    if (const char *ns = std::getenv("PCP_NB_SMALL")) ctx->nb_small = std::atoi(ns) != 0;
     if (const char *rp = std::getenv("PCP_NB_REGION_PCT"))
         ctx->nb_region_pct = std::min(100, std::max(1, std::atoi(rp)));
     if (const char *gw = std::getenv("PCP_NB_GUESS_WORDS"))

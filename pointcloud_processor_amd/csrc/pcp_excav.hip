@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(kXT) k_area_normals(GridView g, float r2, floa
 //  k_cell_sums_exact : the cells' double sums in any order where an exponent bound makes
 //               every order equal; the cells it leaves take k_nb_lists / k_nb_sums in order
 #ifndef PCP_NB_BUCKETS
-#define PCP_NB_BUCKETS 2048   // distance buckets of k_nb_lists (build knob, A/B)
+#define PCP_NB_BUCKETS 1792   // distance buckets of k_nb_lists (build knob, A/B; 7 per thread)
 #endif
 #ifndef PCP_NB_LDS
 #define PCP_NB_LDS 4096       // keys sorted in LDS (build knob, A/B)
@@ -388,13 +388,19 @@ __device__ __forceinline__ void nb_lds_barrier() {
 // to LDS in any order; the keys are then grouped by bucket (indices into the appended array)
 // and each key's rank among its bucket's keys places it in the list.  A query with more than
 // kNbLds neighbours takes a second stencil pass that scatters its keys into global memory.
-template <bool CELLS>
+// SMALL (an area below 2^16 points): the keys' indices as 16 bits, ~40 KB of LDS -- four
+// blocks per CU instead of three
+template <bool CELLS, bool SMALL>
 __global__ void __launch_bounds__(kNbT)
 k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
            const uint32_t *__restrict__ n_dev, NbLists L, const uint32_t *__restrict__ sel) {
+    using IdxT = typename std::conditional<SMALL, uint16_t, uint32_t>::type;
     __shared__ uint32_t cnt[kNbBuckets];
-    __shared__ unsigned long long key[kNbLds];   // appended keys
-    __shared__ uint16_t grp[kNbLds];             // the keys' indices grouped by bucket
+    __shared__ uint32_t kd[kNbLds];   // appended keys: the distance's bits
+    __shared__ IdxT ki[kNbLds];       //   and the input index
+    __shared__ uint16_t grp[kNbLds];  // the keys' positions grouped by bucket
+    // a key as one 64-bit value ordered as FLANN orders neighbours: (distance, index)
+    auto key = [&](uint32_t j) { return ((unsigned long long)kd[j] << 32) | (uint32_t)ki[j]; };
     __shared__ uint32_t wsum[kNbT / 64];
     __shared__ uint32_t sh_base, sh_ok, sh_pos, sh_m, sh_need;
     // CELLS with sel: only the cells sel[1 ..= sel[0]] (those k_cell_sums_exact left to the
@@ -459,9 +465,10 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
                         const uint32_t pos =
                             base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[u] >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
-                        if (in[u] && pos < (uint32_t)kNbLds)
-                            key[pos] = ((unsigned long long)__float_as_uint(dd[u]) << 32) |
-                                       __float_as_uint(p[u].w);
+                        if (in[u] && pos < (uint32_t)kNbLds) {
+                            kd[pos] = __float_as_uint(dd[u]);
+                            ki[pos] = (IdxT)__float_as_uint(p[u].w);
+                        }
                         base += (uint32_t)__popcll(bal[u]);
                     }
                 }
@@ -530,7 +537,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
 #pragma unroll
                     for (int u = 0; u < G4; ++u) {
                         const uint32_t i = min(i0 + (uint32_t)u * kNbT, m - 1);
-                        bk[u] = bucket_of(__uint_as_float((uint32_t)(key[i] >> 32)));
+                        bk[u] = bucket_of(__uint_as_float(kd[i]));
                     }
                     uint32_t pos[G4];
 #pragma unroll
@@ -549,7 +556,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
                     unsigned long long kv[G4];
                     uint32_t s0[G4], len[G4], rank[G4], lmax = 0;
 #pragma unroll
-                    for (int u = 0; u < G4; ++u) kv[u] = key[grp[min(i0 + (uint32_t)u * kNbT, m - 1)]];
+                    for (int u = 0; u < G4; ++u) kv[u] = key(grp[min(i0 + (uint32_t)u * kNbT, m - 1)]);
 #pragma unroll
                     for (int u = 0; u < G4; ++u) {
                         const uint32_t b = bucket_of(__uint_as_float((uint32_t)(kv[u] >> 32)));
@@ -563,7 +570,7 @@ k_nb_lists(GridView g, float r2, float bscale, const double *__restrict__ cells,
                         unsigned long long o[G4];
 #pragma unroll
                         for (int u = 0; u < G4; ++u)
-                            o[u] = key[grp[jj < len[u] ? s0[u] + jj : s0[u]]];
+                            o[u] = key(grp[jj < len[u] ? s0[u] + jj : s0[u]]);
 #pragma unroll
                         for (int u = 0; u < G4; ++u) rank[u] += (jj < len[u]) & (o[u] < kv[u]);
                     }
@@ -1173,9 +1180,14 @@ static void nb_area_launch(pcp_ctx *ctx, hipStream_t st) {
     const uint64_t n = ctx->area_n;
     uint32_t *ctl = ctx->nb_ctl.as<uint32_t>();
     const NbLists La = nb_lists_view(ctx, ctx->nb_list, ctx->nb_meta, ctl, ctl + 2, ctl + 3, grid_a);
-    hipLaunchKernelGGL(k_nb_lists<false>, dim3(grid_a), dim3(kNbT), 0, st, gn, r2n, bscale,
-                       (const double *)nullptr, (const uint32_t *)nullptr, La,
-                       (const uint32_t *)nullptr);
+    if (n <= 65536 && ctx->nb_small)   // (input indices in 16 bits)
+        hipLaunchKernelGGL((k_nb_lists<false, true>), dim3(grid_a), dim3(kNbT), 0, st, gn, r2n,
+                           bscale, (const double *)nullptr, (const uint32_t *)nullptr, La,
+                           (const uint32_t *)nullptr);
+    else
+        hipLaunchKernelGGL((k_nb_lists<false, false>), dim3(grid_a), dim3(kNbT), 0, st, gn, r2n,
+                           bscale, (const double *)nullptr, (const uint32_t *)nullptr, La,
+                           (const uint32_t *)nullptr);
     hipLaunchKernelGGL(k_nb_sums<false>, dim3((npts + NbCfg<false>::QB - 1) / NbCfg<false>::QB),
                        dim3(kNbT), 0, st, gn, (const uint2 *)La.meta, (const uint32_t *)La.list,
                        (const uint32_t *)nullptr, (const float4 *)ctx->nb_pts.as<float4>(),
@@ -1197,9 +1209,14 @@ static void nb_cells_launch(pcp_ctx *ctx, hipStream_t st) {
         hipLaunchKernelGGL(k_cell_sums_exact, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n,
                            (const double *)ctx->cells_xyz.as<double>(), n_d, nrm4,
                            ctx->cells_nrm.as<float>(), sel, ctx->cells_all_ordered ? 1 : 0);
-        hipLaunchKernelGGL(k_nb_lists<true>, dim3(grid_c), dim3(kNbT), 0, st, gn, r2n, bscale,
-                           (const double *)ctx->cells_xyz.as<double>(), n_d, Lc,
-                           (const uint32_t *)sel);
+        if (ctx->area_n <= 65536 && ctx->nb_small)
+            hipLaunchKernelGGL((k_nb_lists<true, true>), dim3(grid_c), dim3(kNbT), 0, st, gn, r2n,
+                               bscale, (const double *)ctx->cells_xyz.as<double>(), n_d, Lc,
+                               (const uint32_t *)sel);
+        else
+            hipLaunchKernelGGL((k_nb_lists<true, false>), dim3(grid_c), dim3(kNbT), 0, st, gn,
+                               r2n, bscale, (const double *)ctx->cells_xyz.as<double>(), n_d, Lc,
+                               (const uint32_t *)sel);
     }
     // launched for an empty selection too: it lands both lists' uses and the overflow word in
     // area_host[1..3], and clears the control words

@@ -267,6 +267,7 @@ struct pcp_ctx {
     bool score_wide = true;          // k_score_cells_wide for few-ray launches (PCP_SCORE_WIDE=0: A/B)
     bool cells_all_ordered = false;  // PCP_CELLS_ORDER_FREE=0: every cell through the lists (A/B)
     int nb_blocks = 0;               // PCP_NB_BLOCKS: k_nb_lists grid (A/B; 0 = kNbBlocks)
+    bool nb_small = true;            // PCP_NB_SMALL=0: 32-bit list keys below 2^16 points too (A/B)
     int nb_region_pct = 75;          // PCP_NB_REGION_PCT: list words in the blocks' regions (rest: spill pool)
     uint64_t nb_guess_max = 64ull << 20;   // PCP_NB_GUESS_WORDS: cap of a first list buffer (words)
     pcp::DevBuf nb_list, nb_meta, nb_ctl, nb_pts;   // nb_pts: input points by index

@@ -1222,8 +1222,8 @@ def test_excavation_area_setup(oracle, scene, mode, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("order_free", ["1", "0"])
-def test_excavation_area_normals_long_lists_and_ties(oracle, order_free, monkeypatch):
+@pytest.mark.parametrize("order_free,small", [("1", "1"), ("0", "1"), ("1", "0")])
+def test_excavation_area_normals_long_lists_and_ties(oracle, order_free, small, monkeypatch):
     """The exact normals where the neighbour lists pass the LDS sort (> 4,096 neighbours within
     1.5 m: sorted in global memory), with exact distance ties (a lattice, duplicated points: the
     reference's order breaks them by index), non-finite points (NaN normals, absent from every
@@ -1231,8 +1231,10 @@ def test_excavation_area_normals_long_lists_and_ties(oracle, order_free, monkeyp
     normals with components ~2^-20 of their largest: the cells near it fail
     k_cell_sums_exact's bound and take the ordered path in the same frame as the others.
     Point and cell normals bit-identical, cells order-free where exact (default) and all
-    ordered (PCP_CELLS_ORDER_FREE=0)."""
+    ordered (PCP_CELLS_ORDER_FREE=0); the lists' LDS keys with 16-bit indices (areas below 2^16
+    points, default) and 32-bit (PCP_NB_SMALL=0, every larger area)."""
     monkeypatch.setenv("PCP_CELLS_ORDER_FREE", order_free)
+    monkeypatch.setenv("PCP_NB_SMALL", small)
     rng = np.random.default_rng(11)
     g = np.arange(90) * 0.025
     X, Y = np.meshgrid(g, g)
