@@ -4,8 +4,9 @@
 #   G: the divergent lane-load ceiling (tools/gather_ceiling.sh -> profiles/r05_gather_ceiling.json)
 #      and the fan's texture-path counters at this tree (tools/pmc_fan.sh + tools/pmc_gather.py
 #      -> profiles/r05_fan_gather_path.json)
-#   T: FETCH/WRITE passes of the fan and the C3 chain (-> profiles/r05_pmc_traffic.json), the C3
-#      chain's eager kernel stats
+#   T: FETCH/WRITE passes of the fan and the C3 chain (parsed afterwards by tools/pmc_traffic.py
+#      -> profiles/r05_pmc_traffic.json), the C3 chain's eager kernel stats
+#   C: the C5 chain under a runtime + kernel trace (tools/c5_timeline.py / c5_sequence.py)
 #   S: rocprofv3 kernel stats of the default bench command
 #   A: every GPU test + smoke, the default bench line
 set -u
@@ -25,16 +26,20 @@ step() {  # name, seconds, command...
 for part in "$@"; do
 case "$part" in
 G)
-  step gather_ceiling 600 bash tools/gather_ceiling.sh
+  # (the ceiling itself, tools/gather_ceiling.sh, is code-independent: re-run it with GC=1)
+  if [ "${GC:-0}" = 1 ]; then step gather_ceiling 600 bash tools/gather_ceiling.sh; fi
   step pmc_fan_path 600 bash tools/pmc_fan.sh "" r05
   step pmc_gather 60 python3 tools/pmc_gather.py gpurun_out/r05_fan_gather_path.json gpurun_out/pmcfr05_1 gpurun_out/pmcfr05_2 gpurun_out/pmcfr05_3 gpurun_out/pmcfr05_4 gpurun_out/pmcfr05_5
   ;;
 T)
+  # (the counter passes only: tools/pmc_traffic.py parses them afterwards in the tree they
+  # came from -- only gpurun_out/ comes back from the box)
   step pmc_fan_traffic 300 bash tools/pmc_fan_traffic.sh r05
-  step pmc_fan_parse 60 python3 tools/pmc_traffic.py fan "k_raycast_fan_xcd<0," gpurun_out/pmctr05_fetch gpurun_out/pmctr05_write per_dispatch r05_pmc_traffic.json profiles/r04_fetch_calibration.json
   step pmc_flt_traffic 300 bash tools/pmc_filter_traffic.sh r05
-  step pmc_flt_parse 60 python3 tools/pmc_traffic.py filter "pcp::" gpurun_out/pmcfltr05_fetch gpurun_out/pmcfltr05_write steps=10 r05_pmc_traffic.json
   step c3_stats 300 env PCP_NO_GRAPHS=1 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --mode filter --steps 20 --warmup 3 --no-pcie --no-cpu-baseline
+  ;;
+C)
+  step c5_trace 300 env FRAMES=30 bash tools/replay_trace.sh
   ;;
 S)
   step rocprof_default 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_default -o run --output-format csv -- python3 bench.py
