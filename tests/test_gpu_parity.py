@@ -1301,14 +1301,19 @@ def _long_list_area():
     return a
 
 
-@pytest.mark.parametrize("which", ["golden", "long_lists"])
-def test_excavation_area_async_then_tick(oracle, scene, which):
+@pytest.mark.parametrize("which,guess", [("golden", None), ("long_lists", None),
+                                         ("long_lists", "4096"), ("golden", "4096")])
+def test_excavation_area_async_then_tick(oracle, scene, which, guess, monkeypatch):
     """pcp_set_excavation_area_async (the composed chain's grid setup: enqueued, not waited for)
     followed by the terrain and the tick (pcp_generate_and_score, which settles it after its own
     synchronisation -- and, on a fresh context whose first neighbour-list guess overflows, regrows
     the lists, reruns them and ticks again): poses, totals, covered counts, flags, the report and
     the cells bit-identical to the synchronous setup's; a second tick from the stale flags too;
-    an async setup settled by pcp_get_cells gives the same cells."""
+    an async setup settled by pcp_get_cells gives the same cells.  PCP_NB_GUESS_WORDS=4096: the
+    first list buffers far too small, so the tick finds the overflow after its wait (the setup
+    ran on its side stream), regrows, reruns the normals and ticks again."""
+    if guess:
+        monkeypatch.setenv("PCP_NB_GUESS_WORDS", guess)
     area = np.load(GOLD / "excavation.npz")["area"] if which == "golden" else _long_list_area()
     params = _abi.default_vl_params(num_candidates=36)
     zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])
