@@ -158,12 +158,21 @@ int pcp_filter_merge(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, const do
  * frame into filtered[i] (host, clouds[i].n PointXYZ 16-B records at most: the node's
  * /filtered_points message) AND all clouds transformed + coloured + concatenated into `out`
  * (host, PointXYZRGB 32-B, cap records: pcp_filter_merge's output), ONE synchronisation.  Host
- * memory in and out (message-sized clouds are read in place from pinned staging).
+ * memory in and out (message-sized clouds are read in place from pinned staging).  `out` and
+ * each filtered[i] may be NULL (not copied: read them with pcp_filter_merge_landed).
  * n_per_cloud / n_cropped (nullable, k entries): centroids and cropped points of each cloud. */
 int pcp_filter_merge_nodes(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds,
                            const double *boxes, float leaf, const pcp_rigid *tf,
                            const uint8_t *rgb, void *out, uint64_t cap, uint64_t *n_out,
                            uint64_t *n_per_cloud, float *const *filtered, uint64_t *n_cropped);
+/* Where the last pcp_filter_merge_nodes call's outputs landed: the context's pinned memory,
+ * host-readable (the same bytes `out` / `filtered[i]` receive; a caller that reads them here may
+ * pass out = NULL, filtered[i] = NULL to that call) -- merged: *n_out PointXYZRGB records,
+ * filtered[i]: n_per_cloud[i] PointXYZ records.  A view over `merged` given to
+ * pcp_excavate_area_async is read in place by the device (no staging copy).  Valid until the
+ * context's next pcp_filter_merge*, pcp_transform_concat or pcp_excavate call; PCP_E_STATE when
+ * there is none, or k differs from that call's. */
+int pcp_filter_merge_landed(pcp_ctx *ctx, int k, const void **merged, const float **filtered);
 
 /* ---- virtual_lidar (SimplifiedDualLidarOptimizer) -------------------------------------- */
 typedef struct pcp_vl_params {      /* virtual_lidar.cpp:66-71 */

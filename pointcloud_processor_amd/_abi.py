@@ -132,6 +132,7 @@ _SIGS = [
     ("pcp_get_area_normals", C.c_int, [_P, _P, C.c_uint64, _P]),
     ("pcp_excavate", C.c_int, [_P, _P, _P, _P, _P, C.c_uint64, _P, _P, C.c_uint64, _P, _P]),
     ("pcp_excavate_bounds", C.c_int, [_P, C.c_uint64, _P, _P]),
+    ("pcp_filter_merge_landed", C.c_int, [_P, C.c_int, _P, _P]),
     ("pcp_excavate_area_async", C.c_int, [_P, _P, _P, _P, _P, C.c_uint64, _P, _P, C.c_uint64, _P,
                                           _P, C.c_double, C.c_int32, _P, _P]),
     ("pcp_drivable_area", C.c_int, [_P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double,

@@ -201,35 +201,39 @@ ComposedFilterMerge::Output ComposedFilterMerge::frame(const PointCloud2 &robot,
             tf[i] = pcp_rigid{{0, 0, 0}, {0, 0, 0, 1}};
         }
     }
-    float *outs[2] = {landing(rf_, 4 * (v[0].n ? v[0].n : 1)), landing(zf_, 4 * (v[1].n ? v[1].n : 1))};
-    const uint64_t cap = v[0].n + v[1].n;
-    uint8_t *mrg = landing(merged_, 32 * (cap ? cap : 1));
+    // the results read where libpcp landed them (pinned): each message is one copy
+    float *none[2] = {nullptr, nullptr};
     uint64_t n = 0, per[2] = {0, 0}, crop[2] = {0, 0};
-    if (pcp_filter_merge_nodes(dev_.ctx(), 2, v, boxes, (float)p_.voxel_leaf_size, tf, rgb, mrg,
-                               cap, &n, per, outs, crop) != PCP_OK) {
+    const void *landed = nullptr;
+    const float *outs[2] = {nullptr, nullptr};
+    if (pcp_filter_merge_nodes(dev_.ctx(), 2, v, boxes, (float)p_.voxel_leaf_size, tf, rgb,
+                               nullptr, 0, &n, per, none, crop) != PCP_OK ||
+        pcp_filter_merge_landed(dev_.ctx(), 2, &landed, outs) != PCP_OK) {
         err_ = dev_.error();
         return o;
     }
+    const uint8_t *mrg = static_cast<const uint8_t *>(landed);
     o.robot_filtered = make_xyz_cloud(outs[0], per[0], robot.frame_id);
     o.robot_filtered.stamp = robot.stamp;
     o.backhoe_filtered = make_xyz_cloud(outs[1], per[1], backhoe.frame_id);
     o.backhoe_filtered.stamp = backhoe.stamp;
     if (!origin_set) return o;   // :309
     // the concatenation of the clouds whose TF was found, robot first (:316-325)
-    uint64_t base = 0, keep_n = 0;
-    std::vector<uint8_t> cat;
+    uint64_t base = 0, keep_off = 0, keep_n = 0;
     const bool both = robot_tf && zx120_tf;
     for (int i = 0; i < 2; ++i) {
-        PointCloud2 part = make_xyzrgb_cloud(mrg + 32 * base, per[i], "map");
-        if (tfs[i]) (i == 0 ? o.merge.robot_colored : o.merge.backhoe_colored) = part;
+        if (tfs[i])
+            (i == 0 ? o.merge.robot_colored : o.merge.backhoe_colored) =
+                make_xyzrgb_cloud(mrg + 32 * base, per[i], "map");
         if (tfs[i] && !both) {
-            cat.assign(mrg + 32 * base, mrg + 32 * (base + per[i]));
+            keep_off = base;
             keep_n = per[i];
         }
         base += per[i];
     }
-    o.merge.merged = both ? make_xyzrgb_cloud(mrg, n, "map")
-                          : make_xyzrgb_cloud(cat.data(), keep_n, "map");
+    if (both) keep_n = n;
+    o.merge.merged = make_xyzrgb_cloud(mrg + 32 * keep_off, keep_n, "map");
+    if (keep_n) o.merged_landed = pcp_cloud_view{mrg + 32 * keep_off, keep_n, 32, 0, 4, 8};
     return o;
 }
 
@@ -304,7 +308,8 @@ bool SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg
 }
 
 ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
-    ExcavationTerrainGenerator &gen, const PointCloud2 &msg, const Transform *zx120_base) {
+    ExcavationTerrainGenerator &gen, const PointCloud2 &msg, const Transform *zx120_base,
+    const pcp_cloud_view *landed) {
     pcp_cloud_view v;
     if (!defer_grid_ || multi_ || !gen.p_.enabled || !zx120_base || !cloud_view(msg, v, nullptr)) {
         ExcavationTerrainGenerator::Output o = gen.matchedCloudCallback(msg, zx120_base);
@@ -327,6 +332,8 @@ ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
         terrainCallback(o.excavated_terrain);
         return o;
     }
+    // (the same bytes as the message, in pinned memory the device reads in place)
+    if (landed && landed->n == v.n && landed->point_step == v.point_step) v = *landed;
     uint8_t *terr = landing(gen.terr_, nt * 32 + 32), *area = landing(gen.area_, na * 32 + 32);
     if (pcp_excavate_area_async(dev_.ctx(), &v, &gen.p_, &tf, terr, nt, &nt, area, na, &na, pose,
                                 p_.grid_resolution, p_.vertical_layers, bb, &ncap) != PCP_OK) {

@@ -150,6 +150,10 @@ class ComposedFilterMerge {
     struct Output {
         PointCloud2 robot_filtered, backhoe_filtered;   // the filter node's two messages
         GnssGicpMatcher::Output merge;                  // the merger node's outputs
+        // merge.merged's bytes where libpcp landed them (pcp_filter_merge_landed; n = 0 when
+        // none): valid until the context's next filter / merge / carve call -- a carve composed
+        // behind this call reads them in place (SimplifiedDualLidarOptimizer::carveCallbacks)
+        pcp_cloud_view merged_landed{};
     };
     Output frame(const PointCloud2 &robot, const PointCloud2 &backhoe, bool origin_set,
                  const Transform *robot_tf, const Transform *zx120_tf);
@@ -158,8 +162,6 @@ class ComposedFilterMerge {
    private:
     Device &dev_;
     SimplifiedScanMatcher::Params p_;
-    std::vector<uint8_t> merged_;
-    std::vector<float> rf_, zf_;
     std::string err_;
 };
 
@@ -280,9 +282,12 @@ class SimplifiedDualLidarOptimizer {
     // index where they land, no re-upload).  Same messages, same state as the three calls; with
     // the grid not deferred (or sharded, or the carve disabled / its TF missing) it makes them.
     // Errors: gen.lastError() for the carve, lastError() for the two callbacks
+    // landed (nullable): merged's bytes in the context's pinned landing
+    // (ComposedFilterMerge::Output::merged_landed), read in place instead of the message
     ExcavationTerrainGenerator::Output carveCallbacks(ExcavationTerrainGenerator &gen,
                                                       const PointCloud2 &merged,
-                                                      const Transform *zx120_base);
+                                                      const Transform *zx120_base,
+                                                      const pcp_cloud_view *landed = nullptr);
     const std::string &lastError() const { return err_; }
 
    private:

@@ -218,6 +218,9 @@ static int cmd_replay(Device &dev, char **a) {
     // the carve node and virtual_lidar's area + terrain callbacks composed (default)
     bool carve_fused = true;
     if (const char *cf = std::getenv("PCP_CARVE_FUSED")) carve_fused = std::atoi(cf) != 0;
+    // the composed carve reads the merger's landed records in place (default) / the message
+    bool carve_landed = true;
+    if (const char *cl = std::getenv("PCP_CARVE_LANDED")) carve_landed = std::atoi(cl) != 0;
     ExcavationTerrainGenerator gen(dev);
     SimplifiedDualLidarOptimizer vl(dev);
     // the nodes composed in one process: the grid setup is enqueued by the area callback and
@@ -266,12 +269,14 @@ static int cmd_replay(Device &dev, char **a) {
         // and merger nodes in one call and one synchronisation (stage "filter" then holds both)
         PointCloud2 rf, zf;
         GnssGicpMatcher::Output o;
+        pcp_cloud_view front_landed{};
         if (front_fused) {
             auto fo = front.frame(rm, zm, true, &robot_tf, &zx_tf);
             if (!front.lastError().empty()) {
                 std::fprintf(stderr, "replay: filter+merge failed: %s\n", front.lastError().c_str());
                 return 1;
             }
+            front_landed = fo.merged_landed;
             rf = std::move(fo.robot_filtered);
             zf = std::move(fo.backhoe_filtered);
             o = std::move(fo.merge);
@@ -288,7 +293,8 @@ static int cmd_replay(Device &dev, char **a) {
         }
         ExcavationTerrainGenerator::Output e;
         if (chain && carve_fused) {   // the carve + both callbacks (stage "carve" holds all three)
-            e = vl.carveCallbacks(gen, o.merged, &zx_base);
+            e = vl.carveCallbacks(gen, o.merged, &zx_base,
+                                  front_fused && carve_landed ? &front_landed : nullptr);
             if (!e.area_published) {
                 std::fprintf(stderr, "replay: carve failed: %s\n", gen.lastError().c_str());
                 return 1;

@@ -540,7 +540,16 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     if (n) {
         const size_t raw_b = n * (size_t)in->point_step;
         PCP_HIP(ctx, ctx->stage.ensure(raw_b));
-        if (int rc0 = upload_async(ctx, ctx->stage.p, in->data, raw_b, st)) return rc0;
+        // composed (xl): a view into the merger's landing (pcp_filter_merge_landed) is pinned,
+        // device-readable memory -- copied by the device, no host staging copy (the non-composed
+        // call may regrow that landing for its own records before the copy ran: staged)
+        const uintptr_t d0 = reinterpret_cast<uintptr_t>(in->data),
+                        l0 = reinterpret_cast<uintptr_t>(ctx->tc_host.p);
+        if (xl && ctx->tc_host.p && d0 >= l0 && d0 + raw_b <= l0 + ctx->tc_host.cap) {
+            if (int rc0 = copy_pinned_async(ctx, ctx->stage.p, in->data, raw_b, st)) return rc0;
+        } else if (int rc0 = upload_async(ctx, ctx->stage.p, in->data, raw_b, st)) {
+            return rc0;
+        }
         raw = ctx->stage.as<unsigned char>();
     }
     if ((rc = build_index(ctx, ctx->carve, *in, p->terrain_search_radius, false, false, &raw)))
@@ -591,6 +600,7 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
         PCP_HIP(ctx, ctx->exc_land.ensure(land_b + 256));
         kept = ctx->exc_land.as<float4>();
     } else if (land) {
+        ctx->fm_land_valid = false;   // (tc_host rewritten)
         PCP_HIP(ctx, ctx->tc_host.ensure(land_b + 256));
         kept = ctx->tc_host.as<float4>();
     } else {

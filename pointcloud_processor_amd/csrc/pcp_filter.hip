@@ -2299,6 +2299,7 @@ int pcp_transform_concat(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds, cons
         std::vector<HostPiece> pc(k);
         for (int i = 0; i < k; ++i)
             pc[i] = HostPiece{soff[i], clouds[i].data, clouds[i].n * (uint64_t)clouds[i].point_step};
+        ctx->fm_land_valid = false;   // (tc_host rewritten)
         PCP_HIP(ctx, ctx->tc_host.ensure(total * 32 + 256));
         float4 *o = ctx->tc_host.as<float4>();
         const void *dv = nullptr;
@@ -2580,6 +2581,7 @@ int pcp_filter_merge_nodes(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds,
             return rc;
     }
     // landing (pinned): [result words | merged records | each cloud's centroids]
+    ctx->fm_land_valid = false;
     const size_t res_b = align256(kResWords * sizeof(uint32_t));
     const size_t mrg_b = align256((upper + 1) * 32);
     std::vector<size_t> koff(k + 1, 0);
@@ -2643,12 +2645,28 @@ int pcp_filter_merge_nodes(pcp_ctx *ctx, int k, const pcp_cloud_view *clouds,
     }
     *n_out = total;
     prof_resolve(ctx);
-    if (total > cap)
+    if (out && total > cap)
         return set_err(ctx, PCP_E_CAPACITY, "pcp_filter_merge_nodes: need %llu, cap %llu",
                        (unsigned long long)total, (unsigned long long)cap);
     if (total && out) host_copy(ctx, out, mrg, total * 32);
     for (int i = 0; i < k; ++i)
         if (clouds[i].n && ri[i].n && filtered[i]) host_copy(ctx, filtered[i], keep(i), (size_t)ri[i].n * 16);
+    ctx->fm_land_merged = mrg;
+    ctx->fm_land_filtered.resize(k);
+    for (int i = 0; i < k; ++i) ctx->fm_land_filtered[i] = reinterpret_cast<const float *>(keep(i));
+    ctx->fm_land_k = k;
+    ctx->fm_land_valid = true;
+    return PCP_OK;
+}
+
+int pcp_filter_merge_landed(pcp_ctx *ctx, int k, const void **merged, const float **filtered) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!ctx->fm_land_valid || k != ctx->fm_land_k)
+        return set_err(ctx, PCP_E_STATE, "pcp_filter_merge_landed: no pcp_filter_merge_nodes "
+                                         "result of %d clouds in place", k);
+    if (merged) *merged = ctx->fm_land_merged;
+    if (filtered)
+        for (int i = 0; i < k; ++i) filtered[i] = ctx->fm_land_filtered[i];
     return PCP_OK;
 }
 

@@ -253,6 +253,12 @@ struct pcp_ctx {
     hipStream_t area_stream = nullptr;
     hipEvent_t area_fork_ev = nullptr, area_join_ev = nullptr;
     pcp::DevBuf lat_flags;           // the lattice's per-point flags (k_lattice_flags)
+    // pcp_filter_merge_nodes' outputs in tc_host (pcp_filter_merge_landed), until tc_host's
+    // next writer
+    bool fm_land_valid = false;
+    int fm_land_k = 0;
+    const void *fm_land_merged = nullptr;
+    std::vector<const float *> fm_land_filtered;
     pcp::PinnedBuf exc_land;         // pcp_excavate_area_async: the carve's records, read in place
                                      // by the setup + terrain index it enqueues
     // excavation area (pcp_set_excavation_area): indices for the normal radius (1.5 m) and the

@@ -88,6 +88,9 @@ int pcp_set_excavation_area_async(pcp_ctx *c, const pcp_cloud_view *area, double
                                   double bb[6], uint64_t *cap) {
     return pcp_set_excavation_area(c, area, res, l, bb, cap);
 }
+int pcp_filter_merge_landed(pcp_ctx *c, int, const void **, const float **) {
+    return fail(c, "pcp_filter_merge_landed: not in the test double");
+}
 // the composed carve + area + terrain (not used by the shells)
 int pcp_excavate_area_async(pcp_ctx *c, const pcp_cloud_view *, const pcp_excavation_params *,
                             const pcp_rigid *, void *, uint64_t, uint64_t *, void *, uint64_t,

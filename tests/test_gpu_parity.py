@@ -381,6 +381,21 @@ def test_filter_merge_nodes(gpu, oracle, case):
            ((0.55, 0.4, 3.5), (0.0, 0.21633, 0.0, 0.97632))]
     rgbs = [(255, 0, 0), (0, 0, 255)]
     merged, filt, crop = gpu.filter_merge_nodes(clouds, [BOX, BOX], leaf, tfs, rgbs)
+    # the same bytes where they landed (pcp_filter_merge_landed: what the C++ composed front
+    # builds its messages from and the composed carve reads in place)
+    mp = ctypes.c_void_p()
+    fp = (ctypes.c_void_p * 2)()
+    assert gpu.lib.pcp_filter_merge_landed(gpu.h, 2, ctypes.byref(mp), fp) == 0
+    if merged.size:
+        got = np.ctypeslib.as_array(ctypes.cast(mp, ctypes.POINTER(ctypes.c_float)),
+                                    (merged.shape[0], 8))
+        np.testing.assert_array_equal(got.view(np.uint32), merged.view(np.uint32))
+    for i, f in enumerate(filt):
+        if f.shape[0]:
+            got = np.ctypeslib.as_array(ctypes.cast(fp[i], ctypes.POINTER(ctypes.c_float)),
+                                        (f.shape[0], 4))
+            np.testing.assert_array_equal(got[:, :3].view(np.uint32), f[:, :3].view(np.uint32))
+    assert gpu.lib.pcp_filter_merge_landed(gpu.h, 3, ctypes.byref(mp), fp) != 0   # (k differs)
     ref_f = []
     for c, f, m in zip(clouds, filt, crop):
         kept = oracle.crop_box(c, BOX)
