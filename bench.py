@@ -1156,6 +1156,8 @@ def run_c5(args, dist, world, rank, local, backend=None, frames=None, check=Fals
            "p50_ms": vals[1], "p99_ms": vals[2], "max_ms_rank0": res.get("max_ms"),
            "p50_ms_worst_rank": vals[1], "p99_ms_worst_rank": vals[2],
            "stage_p50_ms_rank0": res.get("stage_p50_ms"),
+           # the tail's make-up: rank 0's four slowest frames with their stage times
+           "slowest_frames_rank0": res.get("slowest"),
            "reallocs_after_warmup": res.get("reallocs_after_warmup"),
            "candidates_best_idx_last_frame": res.get("best_idx")}
     if check and rank == 0 and res.get("dumped"):
