@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(kCT)
 k_gen_emit(const GenPoint *__restrict__ gp, uint32_t ns, uint32_t na, const double *__restrict__ h,
            double depth, const uint32_t *__restrict__ base_d, float4 *__restrict__ out_s,
            float4 *__restrict__ out_a, const uint32_t *__restrict__ ctr,
-           uint32_t *__restrict__ sm_host) {
+           uint32_t *__restrict__ sm_host, uint32_t *__restrict__ ctr_next) {
     // the surface records (gp[0 .. ns): after the kept points) and the area's (gp[ns ..)), one
     // launch
     const uint32_t k = blockIdx.x * kCT + threadIdx.x;
@@ -295,6 +295,7 @@ k_gen_emit(const GenPoint *__restrict__ gp, uint32_t ns, uint32_t na, const doub
         const double h0 = h[0];
         __builtin_memcpy(sm_host + 4, &h0, sizeof(double));
     }
+    if (ctr_next && k < 4) ctr_next[k] = 0u;   // the next call's counters (the other set)
     if (k >= ns + na) return;
     const GenPoint g = gp[k];
     const double z = g.kind == 0 ? h[g.q] - g.v : (h[g.q] - depth) + g.v;
@@ -590,7 +591,13 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     uint32_t *fb_list = reinterpret_cast<uint32_t *>(base + qb + ib + hb);
     uint8_t *removed = reinterpret_cast<uint8_t *>(base + qb + ib + hb + fb);
     uint32_t *tcount = reinterpret_cast<uint32_t *>(base + qb + ib + hb + fb + rb);
-    uint32_t *ctr = reinterpret_cast<uint32_t *>(base + qb + ib + hb + fb + rb + cb);   // 4 words
+    // the counters: this call's set of two (cleared by the previous call's k_gen_emit, or here)
+    const size_t cap0 = ctx->carve_ctr.cap;
+    PCP_HIP(ctx, ctx->carve_ctr.ensure(64));
+    if (ctx->carve_ctr.cap != cap0) ctx->carve_ctr_clean[0] = ctx->carve_ctr_clean[1] = false;
+    const int cs = ctx->carve_ctr_sel;
+    uint32_t *ctr = ctx->carve_ctr.as<uint32_t>() + 4 * cs;
+    uint32_t *ctr_next = ctx->carve_ctr.as<uint32_t>() + 4 * (1 - cs);
     // the records: straight into pinned memory for message-sized results (the kernels store
     // them there, no D2H copy), else a device buffer copied out
     const size_t land_b = (n + nsurf + narea) * 32;
@@ -626,7 +633,9 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     GenPoint *gp = reinterpret_cast<GenPoint *>(gbase);
     double2 *qxy = reinterpret_cast<double2 *>(gbase + gpb);
     float4 *area_d = land ? kept + 2 * (n + nsurf) : reinterpret_cast<float4 *>(gbase + gpb + qxb);
-    PCP_HIP(ctx, hipMemsetAsync(ctr, 0, 16, st));
+    if (!ctx->carve_ctr_clean[cs]) PCP_HIP(ctx, hipMemsetAsync(ctr, 0, 16, st));
+    ctx->carve_ctr_clean[cs] = false;
+    ctx->carve_ctr_sel = 1 - cs;
     const float r2 = (float)(p->terrain_search_radius * p->terrain_search_radius);
     const unsigned gn = (unsigned)((n + kCT - 1) / kCT);
     if (n) {
@@ -663,8 +672,9 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
         hipLaunchKernelGGL(k_gen_emit, dim3((unsigned)((nsurf + narea + kCT - 1) / kCT)), dim3(kCT),
                            0, st, (const GenPoint *)gp, (uint32_t)nsurf, (uint32_t)narea,
                            (const double *)h, p->depth, n ? (const uint32_t *)(ctr + 2) : nullptr,
-                           kept, area_d, (const uint32_t *)ctr, sm_k);
+                           kept, area_d, (const uint32_t *)ctr, sm_k, ctr_next);
         PCP_CHECK_LAUNCH(ctx);
+        ctx->carve_ctr_clean[1 - cs] = true;
         sm_k = nullptr;
     }
     // the kept count and the centre height land in pinned memory; when the caller's buffers

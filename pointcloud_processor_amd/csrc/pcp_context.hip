@@ -337,7 +337,7 @@ k_scan_tile_sums(const uint32_t *__restrict__ in, uint64_t n, uint32_t *__restri
 // them) receives a second copy of out[0 .. n)
 __global__ void __launch_bounds__(kScanThreads)
 k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
-             uint32_t *__restrict__ out, uint32_t *out2, int zero2) {
+             uint32_t *__restrict__ out, uint32_t *out2, int zero2, uint16_t *__restrict__ preset16) {
     __shared__ uint32_t lds4[4];
     const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
     // a thread's 8 items whole: two 16-byte loads and stores instead of 8 single words at a
@@ -389,6 +389,10 @@ k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
             }
         }
     }
+    if (preset16)
+#pragma unroll
+        for (int i = 0; i < kScanItems; ++i)
+            if (base + i < n) preset16[base + i] = 0x00FFu;
     // out[n] written by the last tile's last thread
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = run;
 }
@@ -400,7 +404,8 @@ k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
 // reader sees the value with its flag and the previous call's words (older epoch) as absent
 __global__ void __launch_bounds__(kScanThreads)
 k_scan_onepass(const uint32_t *in, uint64_t n, uint32_t *out, uint32_t *out2, int zero2,
-               unsigned long long *state, uint32_t *ticket, uint32_t ticket_base, uint32_t epoch) {
+               unsigned long long *state, uint32_t *ticket, uint32_t ticket_base, uint32_t epoch,
+               uint16_t *__restrict__ preset16) {
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t sh_tile, sh_prefix;
     if (threadIdx.x == 0) sh_tile = atomicAdd(ticket, 1u) - ticket_base;
@@ -463,6 +468,7 @@ k_scan_onepass(const uint32_t *in, uint64_t n, uint32_t *out, uint32_t *out2, in
         if (k < n) {
             out[k] = run;
             if (out2) out2[k] = zero2 ? 0u : run;
+            if (preset16) preset16[k] = 0x00FFu;
         }
         run += v[i];
     }
@@ -481,7 +487,7 @@ size_t scan_tmp_bytes(uint64_t n) {
 }
 
 int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp,
-                       uint32_t *out2, bool zero2) {
+                       uint32_t *out2, bool zero2, uint16_t *preset16) {
     if (n == 0) {
         PCP_HIP(ctx, hipMemsetAsync(out, 0, sizeof(uint32_t), ctx->stream));
         return PCP_OK;
@@ -502,14 +508,14 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
         uint32_t *ticket = reinterpret_cast<uint32_t *>(ctx->scan_state.as<char>() + ctx->scan_state.cap - 64);
         hipLaunchKernelGGL(k_scan_onepass, dim3((unsigned)tiles), dim3(kScanThreads), 0, ctx->stream,
                            in, n, out, out2, zero2 ? 1 : 0, state, ticket, ctx->scan_ticket,
-                           ctx->scan_epoch);
+                           ctx->scan_epoch, preset16);
         PCP_CHECK_LAUNCH(ctx);
         ctx->scan_ticket += (uint32_t)tiles;
         return PCP_OK;
     }
     if (tiles == 1) {
         hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(kScanThreads), 0, ctx->stream, in, n,
-                           (const uint32_t *)nullptr, out, out2, zero2 ? 1 : 0);
+                           (const uint32_t *)nullptr, out, out2, zero2 ? 1 : 0, preset16);
         PCP_CHECK_LAUNCH(ctx);
         return PCP_OK;
     }
@@ -522,7 +528,7 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
     int rc = exclusive_scan_u32(ctx, sums, sums_scan, tiles, next);
     if (rc) return rc;
     hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)tiles), dim3(kScanThreads), 0, ctx->stream, in,
-                       n, (const uint32_t *)sums_scan, out, out2, zero2 ? 1 : 0);
+                       n, (const uint32_t *)sums_scan, out, out2, zero2 ? 1 : 0, preset16);
     PCP_CHECK_LAUNCH(ctx);
     return PCP_OK;
 }
@@ -655,6 +661,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     if (ctx->fm_graph) (void)hipGraphDestroy(ctx->fm_graph);
     ctx->lat_flags.release();
     ctx->scan_state.release();
+    ctx->carve_ctr.release();
     ctx->exc_land.release();
     if (ctx->area_stream) (void)hipStreamDestroy(ctx->area_stream);
     (void)hipStreamDestroy(ctx->stream);

@@ -618,11 +618,14 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
                            ctx->scratch[0].as<const float4>(), n, m, cnt, cr);
         PCP_CHECK_LAUNCH(ctx);
     }
-    // 5. prefix -> start; the scan clears the counters behind it
+    // 5. prefix -> start; the scan clears the counters behind it (and, for a mostly empty
+    // z-sorted grid, presets its z bands: no memset launch in front of k_occz_sparse)
     PCP_HIP(ctx, g.start.ensure((ncell + 1) * sizeof(uint32_t)));
     PCP_HIP(ctx, ctx->scratch[4].ensure(scan_tmp_bytes(ncell) + (ncell + 1) * sizeof(uint32_t)));
+    const bool sparse_z = zsort && ncell > kSparseCells * (uint64_t)nfin;
+    if (zsort) PCP_HIP(ctx, g.occz.ensure(ncell * sizeof(uint16_t)));
     int rc = exclusive_scan_u32(ctx, cnt, g.start.as<uint32_t>(), ncell, ctx->scratch[4].p, cnt,
-                                true);
+                                true, sparse_z ? g.occz.as<uint16_t>() : nullptr);
     if (rc) return rc;
     ctx->cell_cnt_dirty = false;
     // 6. every point to its cell's start + its slot
@@ -655,9 +658,7 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     // 8b. z band per stencil corner (the fan march's probe), z-sorted indices only
     g.occz_ok = false;
     if (zsort) {
-        PCP_HIP(ctx, g.occz.ensure(ncell * sizeof(uint16_t)));
-        if (ncell > kSparseCells * (uint64_t)nfin) {   // mostly empty: preset + occupied cells
-            PCP_HIP(ctx, hipMemsetD16Async(g.occz.p, 0x00FFu, ncell, st));
+        if (sparse_z) {   // mostly empty: the scan preset every band, now the occupied cells'
             hipLaunchKernelGGL(k_occz_sparse, dim3((unsigned)((8 * (uint64_t)nfin + kThreads - 1) / kThreads)),
                                dim3(kThreads), 0, st, g.start.as<const uint32_t>(),
                                g.pts.as<const float4>(), m, c, (uint64_t)nfin,

@@ -259,7 +259,12 @@ struct pcp_ctx {
     int fm_land_k = 0;
     const void *fm_land_merged = nullptr;
     std::vector<const float *> fm_land_filtered;
-    pcp::PinnedBuf exc_land;         // pcp_excavate_area_async: the carve's records, read in place
+    pcp::PinnedBuf exc_land;
+    // the carve's four counters, two sets used in turn: each call's k_gen_emit clears the set
+    // the next call uses (no memset launch in front of it)
+    pcp::DevBuf carve_ctr;
+    int carve_ctr_sel = 0;
+    bool carve_ctr_clean[2] = {false, false};         // pcp_excavate_area_async: the carve's records, read in place
                                      // by the setup + terrain index it enqueues
     // excavation area (pcp_set_excavation_area): indices for the normal radius (1.5 m) and the
     // lattice test radius (1.5 * grid_resolution), and the per-point normals
@@ -447,8 +452,9 @@ int terrain_blocks_before_query(pcp_ctx *ctx);
 size_t scan_tmp_bytes(uint64_t n);
 // out2 (optional, may alias in): a second copy of out[0 .. n), e.g. a scatter's cursors; with
 // zero2 it is cleared instead (out2 = in: counters left zero for their next use)
+// preset16 (nullable): n halfwords set to 0x00FF by the same pass (the sparse z bands' preset)
 int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp,
-                       uint32_t *out2 = nullptr, bool zero2 = false);
+                       uint32_t *out2 = nullptr, bool zero2 = false, uint16_t *preset16 = nullptr);
 
 // fan query up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip): device results
 // in flight on return, the caller synchronizes.  n > 0.
