@@ -1410,6 +1410,40 @@ def test_excavate_area_async_matches_three_calls():
         assert a[9] == b[9]
 
 
+def test_excavation_area_async_back_to_back(scene):
+    """Async grid setups in a row with no tick between them (each settles the one before it:
+    its side stream joined, its lists checked), a terrain change and a zx120 cloud between
+    setup and tick, then the tick: cells, normals, poses, totals, flags and report equal to a
+    context that ran only the last setup synchronously."""
+    d = np.load(GOLD / "excavation.npz")
+    areas = [_long_list_area(), d["area"], _long_list_area()[::3].copy()]
+    params = _abi.default_vl_params(num_candidates=25)
+    zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])
+    aux = scene.terrain[::50, :4].copy()
+    out = []
+    for mode in ("sync_last", "async_chain"):
+        with _abi.Context(0) as ctx:
+            ctx.set_terrain(scene.terrain[:1000], point_step=32)
+            if mode == "sync_last":
+                ctx.set_terrain(scene.terrain, point_step=32)
+                bb, n = ctx.set_excavation_area(areas[-1], 0.1, 10, point_step=areas[-1].shape[1] * 4)
+                flags = np.zeros(max(n, 1), np.uint8)
+            else:
+                for a in areas:
+                    bb, cap = ctx.set_excavation_area_async(a, 0.1, 10, point_step=a.shape[1] * 4)
+                ctx.set_terrain(scene.terrain, point_step=32)
+                flags = np.zeros(max(cap, 1), np.uint8)
+            ctx.set_aux_cloud(aux)
+            poses, tot, cov, rep = ctx.generate_and_score(bb, params, zx, flags)
+            n = ctx.cells_count()
+            xyz, cn = ctx.get_cells()
+            out.append((bb, n, poses, tot, cov, flags[:n].copy(), rep.as_dict(), xyz, cn))
+    a, b = out
+    assert a[1] == b[1] and a[1] > 0 and a[6] == b[6]
+    for i in (0, 2, 3, 4, 5, 7, 8):
+        np.testing.assert_array_equal(np.asarray(a[i]).view(np.uint8), np.asarray(b[i]).view(np.uint8))
+
+
 def _degenerate_areas():
     rng = np.random.default_rng(23)
     out = {}
