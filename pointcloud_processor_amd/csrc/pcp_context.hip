@@ -580,6 +580,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *co = std::getenv("PCP_CELLS_ORDER_FREE")) ctx->cells_all_ordered = std::atoi(co) == 0;
     if (const char *nbk = std::getenv("PCP_NB_BLOCKS")) ctx->nb_blocks = std::atoi(nbk);
     if (const char *sp = std::getenv("PCP_SCAN_ONEPASS")) ctx->scan_onepass = std::atoi(sp) != 0;
+    if (const char *ip = std::getenv("PCP_INDEX_PAIR")) ctx->index_pair = std::atoi(ip) != 0;
     if (const char *as = std::getenv("PCP_AREA_STREAM")) ctx->area_side = std::atoi(as) != 0;
     if (const char *ns = std::getenv("PCP_NB_SMALL")) ctx->nb_small = std::atoi(ns) != 0;
     if (const char *rp = std::getenv("PCP_NB_REGION_PCT"))
@@ -644,6 +645,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->carve.release();
     ctx->carve_buf.release();
     ctx->cell_cnt.release();
+    ctx->cell_cnt2.release();
     ctx->carve_gen.release();
     ctx->fan_host.release();
     ctx->res_host.release();

@@ -1024,8 +1024,10 @@ k_lattice_flags(GridView g, float r2, Lattice L, uint8_t *__restrict__ flags) {
 // round covers 4,096 points: a quarter of the dependent rounds of one point per thread
 __global__ void __launch_bounds__(1024)
 k_lattice_compact(const uint8_t *__restrict__ flags, Lattice L, double *__restrict__ cells,
-                  uint32_t cap, uint32_t *__restrict__ n_out, uint32_t *__restrict__ n_host) {
+                  uint32_t cap, uint32_t *__restrict__ n_out, uint32_t *__restrict__ n_host,
+                  uint32_t *__restrict__ sel) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (sel && threadIdx.x == 0) sel[0] = 0;   // (k_cell_sums_exact's count, after this launch)
     __shared__ uint32_t wc[16];
     uint32_t run = 0;
     for (uint32_t base = 0; base < L.total; base += 4096) {
@@ -1304,11 +1306,26 @@ int area_setup_from(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolu
     const double r_near = grid_resolution * 1.5;
     // both indices read the same staged bytes (staged once)
     const unsigned char *raw = raw_pre;
-    if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius, false, false, &raw))) return rc;
-    rc = build_index(ctx, ctx->exc_near, *area, r_near, false, false, &raw);
-    if (rc) return rc;   // (a held slot is drained by the next pin_stage)
     const uint64_t n = area->n;
     PCP_HIP(ctx, ctx->area_nrm.ensure(n * 3 * sizeof(float) + 16));
+    // the exact path: both grids from one pass over the records, which also lays out the points
+    // by input index for the sums and the non-finite points' NaN normals (k_area_prep's work)
+    bool paired = false;
+    if (ctx->normals_exact) {
+        PCP_HIP(ctx, ctx->nb_pts.ensure(2 * n * sizeof(float4) + 64));
+        if ((rc = build_index_pair(ctx, ctx->exc_norm, kNormalRadius, ctx->exc_near, r_near,
+                                   *area, &raw, ctx->nb_pts.as<float4>(),
+                                   ctx->area_nrm.as<float>(), &paired)))
+            return rc;
+    }
+    if (!paired) {
+        if ((rc = build_index(ctx, ctx->exc_norm, *area, kNormalRadius, false, false, &raw)))
+            return rc;
+        rc = build_index(ctx, ctx->exc_near, *area, r_near, false, false, &raw);
+        if (rc) return rc;   // (a held slot is drained by the next pin_stage)
+    } else {
+        pin_release(ctx, ctx->stream);   // (the pair's extraction read the records last)
+    }
     ctx->area_n = n;
     if (ctx->exc_norm.n_pts == 0) {   // no finite point: no lattice bounds, no cells
         PCP_HIP(ctx, hipMemsetAsync(ctx->area_nrm.p, 0xff, n * 3 * sizeof(float), ctx->stream));
@@ -1366,7 +1383,8 @@ int area_setup_from(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolu
         }
         hipLaunchKernelGGL(k_lattice_compact, dim3(1), dim3(1024), 0, st,
                            (const uint8_t *)ctx->lat_flags.as<uint8_t>(), L,
-                           ctx->cells_xyz.as<double>(), (uint32_t)total, n_d, n_h);
+                           ctx->cells_xyz.as<double>(), (uint32_t)total, n_d, n_h,
+                           exact ? ctx->nb_sel.as<uint32_t>() : (uint32_t *)nullptr);
         PCP_CHECK_LAUNCH(ctx);
         return PCP_OK;
     };
@@ -1425,7 +1443,7 @@ int area_setup_from(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolu
     // cells_*, lat_flags, area_host) and nothing on ctx->stream reads those before the join
     // (not when the raw records sit in ctx->stage: a large area's, DMA'd there, which the next
     // upload on ctx->stream may overwrite while k_area_prep still reads them)
-    const bool side = defer && ctx->area_side && raw != ctx->stage.as<unsigned char>();
+    const bool side = defer && ctx->area_side && (paired || raw != ctx->stage.as<unsigned char>());
     if (side) {
         if (!ctx->area_stream)
             PCP_HIP(ctx, hipStreamCreateWithFlags(&ctx->area_stream, hipStreamNonBlocking));
@@ -1443,10 +1461,12 @@ int area_setup_from(pcp_ctx *ctx, const pcp_cloud_view *area, double grid_resolu
     // first: the input points by input index for the sums' gathers, the non-finite points' NaN
     // normals (k_area_prep is the raw records' last reader; the exact kernels never write those
     // entries, so a rerun keeps them), and sel's count cleared
-    hipLaunchKernelGGL(k_area_prep, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0, st, rin,
-                       ctx->nb_pts.as<float4>(), ctx->area_nrm.as<float>(), sel);
-    PCP_CHECK_LAUNCH(ctx);
-    pin_release(ctx, st);
+    if (!paired) {   // (paired: done by the pair's extraction; sel's count by k_lattice_compact)
+        hipLaunchKernelGGL(k_area_prep, dim3((unsigned)((n + kXT - 1) / kXT)), dim3(kXT), 0, st,
+                           rin, ctx->nb_pts.as<float4>(), ctx->area_nrm.as<float>(), sel);
+        PCP_CHECK_LAUNCH(ctx);
+        pin_release(ctx, st);
+    }
     nb_area_launch(ctx, st);
     PCP_CHECK_LAUNCH(ctx);
     if (int rcl = lattice(st)) return rcl;

@@ -480,6 +480,162 @@ static void host_bbox(const pcp_cloud_view &v, float bb[10], uint32_t &nfin) {
     nfin = c;
 }
 
+// the grid over a float bbox (bb[0..2] min, bb[3..5] max; g.r_q set): edge c > 2 (r_q +
+// margin) so a query box spans <= 2 cells per axis, grown while the grid is too large.
+// Returns the cell count
+static uint64_t grid_geometry(GridIndex &g, const float bb[6]) {
+    for (int a = 0; a < 3; ++a) {
+        g.bmin[a] = bb[a];
+        g.bmax[a] = bb[3 + a];
+    }
+    double c = 2.0 * (g.r_q + kCellMargin);
+    uint64_t ncell = 0;
+    for (;;) {
+        int64_t d[3];
+        for (int a = 0; a < 3; ++a)
+            d[a] = (int64_t)std::floor((g.bmax[a] - (g.bmin[a] - c)) / c) + 2;
+        ncell = (uint64_t)d[0] * (uint64_t)d[1] * (uint64_t)d[2];
+        if (ncell <= kMaxCells && d[0] < (1 << 30) && d[1] < (1 << 30) && d[2] < (1 << 30)) {
+            g.nx = (int32_t)d[0];
+            g.ny = (int32_t)d[1];
+            g.nz = (int32_t)d[2];
+            break;
+        }
+        c *= 1.25;
+    }
+    g.c = c;
+    return ncell;
+}
+
+// two order-free indices of one message-sized cloud (the excavation area's normal-radius and
+// lattice-radius grids) from ONE pass over its raw records: extraction, both cells and slots,
+// and the caller's per-point preparation (prep_pts: the points by input index as (x, y, z, 0);
+// prep_nrm: NaN normals of the non-finite points) -- k_extract_count, k_cell_place and
+// k_area_prep of three launches each ... in two
+__global__ void __launch_bounds__(kThreads)
+k_extract_count2(const unsigned char *__restrict__ raw, uint64_t n, uint32_t step, uint32_t ox,
+                 uint32_t oy, uint32_t oz, CellMap ma, CellMap mb, float4 *__restrict__ xyz,
+                 uint32_t *__restrict__ cnt_a, uint2 *__restrict__ cr_a,
+                 uint32_t *__restrict__ cnt_b, uint2 *__restrict__ cr_b,
+                 float4 *__restrict__ prep_pts, float *__restrict__ prep_nrm) {
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;   // (whole waves: the peer masks below see only live lanes)
+    const unsigned char *p = raw + i * step;
+    const float x = ld_f32(p, ox), y = ld_f32(p, oy), z = ld_f32(p, oz);
+    const bool fin = isfinite(x) && isfinite(y) && isfinite(z);
+    xyz[i] = make_float4(x, y, z, __uint_as_float(fin ? (uint32_t)i : 0xFFFFFFFFu));
+    uint2 c;
+    count_ranked(ma, x, y, z, fin, cnt_a, c);
+    cr_a[i] = c;
+    count_ranked(mb, x, y, z, fin, cnt_b, c);
+    cr_b[i] = c;
+    if (prep_pts) {
+        prep_pts[i] = make_float4(x, y, z, 0.0f);
+        if (!fin) prep_nrm[3 * i] = prep_nrm[3 * i + 1] = prep_nrm[3 * i + 2] = NAN;
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_cell_place2(const float4 *__restrict__ xyz, uint64_t n, const uint2 *__restrict__ cr_a,
+              const uint32_t *__restrict__ start_a, float4 *__restrict__ out_a,
+              const uint2 *__restrict__ cr_b, const uint32_t *__restrict__ start_b,
+              float4 *__restrict__ out_b) {
+    const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint2 a = cr_a[i], b = cr_b[i];
+    if (a.x == 0xFFFFFFFFu) return;   // (non-finite: in neither index)
+    const float4 p = xyz[i];
+    out_a[start_a[a.x] + a.y] = p;
+    out_b[start_b[b.x] + b.y] = p;
+}
+
+int build_index_pair(pcp_ctx *ctx, GridIndex &ga, double ra, GridIndex &gb, double rb,
+                     const pcp_cloud_view &v, const unsigned char **raw_io, float4 *prep_pts,
+                     float *prep_nrm, bool *paired) {
+    *paired = false;
+    const uint64_t n = v.n;
+    if (n == 0 || n > kHostBboxMax || !ctx->index_pair) return PCP_OK;   // (the two builds)
+    float bb_h[10];
+    uint32_t nfin = 0;
+    host_bbox(v, bb_h, nfin);
+    if (nfin == 0) return PCP_OK;
+    hipStream_t st = ctx->stream;
+    ProfScope prof(ctx, PCP_K_INDEX_BUILD);
+    for (GridIndex *g : {&ga, &gb}) {
+        g->present = false;
+        g->occz_ok = g->occ2_ok = g->blk_ok = g->blk_fail = g->fine_ok = g->fine_fail = false;
+    }
+    // the raw bytes device-readable (as build_index: given, or read in place from the ring)
+    const uint64_t raw_bytes = n * (uint64_t)v.point_step;
+    const unsigned char *raw = raw_io ? *raw_io : nullptr;
+    bool pinned = false;
+    if (!raw && ctx->zc_in && raw_bytes <= kPinDirectMax) {
+        const HostPiece pc{0, v.data, raw_bytes};
+        const void *dv = nullptr;
+        if (int rc0 = pin_stage(ctx, &pc, 1, raw_bytes, &dv)) return rc0;
+        raw = static_cast<const unsigned char *>(dv);
+        pinned = true;
+    }
+    if (!raw) {
+        PCP_HIP(ctx, ctx->stage.ensure(raw_bytes));
+        if (int rc0 = upload_async(ctx, ctx->stage.p, v.data, raw_bytes, st)) return rc0;
+        raw = ctx->stage.as<unsigned char>();
+    }
+    if (raw_io) *raw_io = raw;
+    ga.r_q = ra;
+    gb.r_q = rb;
+    ga.n_pts = gb.n_pts = nfin;
+    const uint64_t nca = grid_geometry(ga, bb_h), ncb = grid_geometry(gb, bb_h);
+    const GridView va = ga.view(), vb = gb.view();
+    const CellMap ma{va.ox, va.oy, va.oz, va.inv_c, ga.nx, ga.ny, ga.nz};
+    const CellMap mb{vb.ox, vb.oy, vb.oz, vb.inv_c, gb.nx, gb.ny, gb.nz};
+    // both grids' counters: zero between builds (each scan clears its own behind it)
+    const size_t cba = (nca + 1) * sizeof(uint32_t), cbb = (ncb + 1) * sizeof(uint32_t);
+    if (ctx->cell_cnt.cap < cba || ctx->cell_cnt_dirty) {
+        PCP_HIP(ctx, ctx->cell_cnt.ensure(cba));
+        PCP_HIP(ctx, hipMemsetAsync(ctx->cell_cnt.p, 0, ctx->cell_cnt.cap, st));
+        ctx->cell_cnt_dirty = false;
+    }
+    if (ctx->cell_cnt2.cap < cbb || ctx->cell_cnt2_dirty) {
+        PCP_HIP(ctx, ctx->cell_cnt2.ensure(cbb));
+        PCP_HIP(ctx, hipMemsetAsync(ctx->cell_cnt2.p, 0, ctx->cell_cnt2.cap, st));
+        ctx->cell_cnt2_dirty = false;
+    }
+    uint32_t *cnt_a = ctx->cell_cnt.as<uint32_t>(), *cnt_b = ctx->cell_cnt2.as<uint32_t>();
+    PCP_HIP(ctx, ctx->scratch[0].ensure(n * sizeof(float4)));
+    PCP_HIP(ctx, ctx->scratch[2].ensure(2 * n * sizeof(uint2)));
+    uint2 *cr_a = ctx->scratch[2].as<uint2>(), *cr_b = cr_a + n;
+    const unsigned gridn = (unsigned)((n + kThreads - 1) / kThreads);
+    ctx->cell_cnt_dirty = ctx->cell_cnt2_dirty = true;
+    hipLaunchKernelGGL(k_extract_count2, dim3(gridn), dim3(kThreads), 0, st, raw, n, v.point_step,
+                       v.off_x, v.off_y, v.off_z, ma, mb, ctx->scratch[0].as<float4>(), cnt_a,
+                       cr_a, cnt_b, cr_b, prep_pts, prep_nrm);
+    PCP_CHECK_LAUNCH(ctx);
+    if (pinned && !raw_io) pin_release(ctx, st);
+    PCP_HIP(ctx, ga.start.ensure(cba));
+    PCP_HIP(ctx, gb.start.ensure(cbb));
+    const uint64_t ncm = std::max(nca, ncb);
+    PCP_HIP(ctx, ctx->scratch[4].ensure(scan_tmp_bytes(ncm) + (ncm + 1) * sizeof(uint32_t)));
+    if (int rc = exclusive_scan_u32(ctx, cnt_a, ga.start.as<uint32_t>(), nca, ctx->scratch[4].p,
+                                    cnt_a, true))
+        return rc;
+    ctx->cell_cnt_dirty = false;
+    if (int rc = exclusive_scan_u32(ctx, cnt_b, gb.start.as<uint32_t>(), ncb, ctx->scratch[4].p,
+                                    cnt_b, true))
+        return rc;
+    ctx->cell_cnt2_dirty = false;
+    PCP_HIP(ctx, ga.pts.ensure((size_t)nfin * sizeof(float4)));
+    PCP_HIP(ctx, gb.pts.ensure((size_t)nfin * sizeof(float4)));
+    hipLaunchKernelGGL(k_cell_place2, dim3(gridn), dim3(kThreads), 0, st,
+                       ctx->scratch[0].as<const float4>(), n, (const uint2 *)cr_a,
+                       ga.start.as<const uint32_t>(), ga.pts.as<float4>(), (const uint2 *)cr_b,
+                       gb.start.as<const uint32_t>(), gb.pts.as<float4>());
+    PCP_CHECK_LAUNCH(ctx);
+    ga.present = gb.present = true;
+    *paired = true;
+    return PCP_OK;
+}
+
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort,
                 bool occ, const unsigned char **raw_io) {
     const uint64_t n = v.n;
@@ -570,27 +726,9 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         g.present = true;
         return PCP_OK;
     }
-    for (int a = 0; a < 3; ++a) {
-        g.bmin[a] = bb_h[a];
-        g.bmax[a] = bb_h[3 + a];
-    }
-    // 3. grid geometry: edge c > 2 (r_q + margin) so a query box spans <= 2 cells per axis
-    double c = 2.0 * (r_q + kCellMargin);
-    uint64_t ncell = 0;
-    for (;;) {
-        int64_t d[3];
-        for (int a = 0; a < 3; ++a)
-            d[a] = (int64_t)std::floor((g.bmax[a] - (g.bmin[a] - c)) / c) + 2;
-        ncell = (uint64_t)d[0] * (uint64_t)d[1] * (uint64_t)d[2];
-        if (ncell <= kMaxCells && d[0] < (1 << 30) && d[1] < (1 << 30) && d[2] < (1 << 30)) {
-            g.nx = (int32_t)d[0];
-            g.ny = (int32_t)d[1];
-            g.nz = (int32_t)d[2];
-            break;
-        }
-        c *= 1.25;
-    }
-    g.c = c;
+    // 3. grid geometry
+    const uint64_t ncell = grid_geometry(g, bb_h);
+    const double c = g.c;
     const GridView gv = g.view();
     CellMap m{gv.ox, gv.oy, gv.oz, gv.inv_c, g.nx, g.ny, g.nz};
     // 4. each point's cell and slot in it.  The counters are all zero between builds (the scan

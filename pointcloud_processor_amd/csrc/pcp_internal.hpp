@@ -296,6 +296,9 @@ struct pcp_ctx {
     // its count and its scan (the next one clears the buffer first)
     pcp::DevBuf cell_cnt;
     bool cell_cnt_dirty = false;
+    pcp::DevBuf cell_cnt2;           // the second grid's counters of build_index_pair
+    bool cell_cnt2_dirty = false;
+    bool index_pair = true;          // PCP_INDEX_PAIR=0: the area's two grids by two builds (A/B)
     // the generated lattice (surface + area records, their height queries) on the device:
     // [GenPoint surf | GenPoint area | queries (G generated + n input) | area records].  It
     // depends on the parameters and the excavation pose alone; while carve_key matches, the
@@ -437,6 +440,14 @@ struct KernelTimer {
 // after its own last reader.  Larger clouds are DMA'd into ctx->stage.
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
                 bool zsort = true, bool occ = true, const unsigned char **raw_io = nullptr);
+// two order-free indices (no z order, no occupancy bits) of one message-sized cloud from one
+// pass over its raw records, plus the caller's per-point preparation (prep_pts: (x, y, z, 0) by
+// input index; prep_nrm: NaN normals of the non-finite points; both nullable).  *paired false
+// (nothing done): the cloud is empty, has no finite point or is past the host-bbox size -- build
+// them with build_index.  raw_io as build_index's
+int build_index_pair(pcp_ctx *ctx, GridIndex &ga, double ra, GridIndex &gb, double rb,
+                     const pcp_cloud_view &v, const unsigned char **raw_io, float4 *prep_pts,
+                     float *prep_nrm, bool *paired);
 // the block-major copy of a z-sorted index (GridView.bstart / bpts); no-op when built
 int build_blocks(pcp_ctx *ctx, GridIndex &g);
 // the fine-window copy of a z-sorted index (GridView.frec / wpts); no-op when built.  Marks
