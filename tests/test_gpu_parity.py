@@ -1195,18 +1195,22 @@ def _normals_equal(got, ref):
     np.testing.assert_array_equal(got[fin].view(np.uint32), ref[fin].view(np.uint32))
 
 
-@pytest.mark.parametrize("mode", ["exact", "exact_ordered", "fixed"])
+@pytest.mark.parametrize("mode", ["exact", "exact_ordered", "exact_two_builds", "fixed"])
 def test_excavation_area_setup(oracle, scene, mode, monkeypatch):
     """pcp_set_excavation_area against the oracle: grid bounds and the valid cells (positions,
     reference loop order) bit-exact.  Default path (PCP_NORMALS_EXACT=1): point normals and cell
     normals BIT-IDENTICAL -- PCL's float covariance sums in FLANN's (distance, index) order,
     eigen33 with glibc's float libm restated (pcp_libm.h), the cells' double sums where their
     order cannot change them in any order (k_cell_sums_exact), the others in FLANN's order;
-    exact_ordered (PCP_CELLS_ORDER_FREE=0) sends every cell through the ordered lists.  The
+    exact_ordered (PCP_CELLS_ORDER_FREE=0) sends every cell through the ordered lists;
+    exact_two_builds builds the area's two grids separately (PCP_INDEX_PAIR=0).  The
     order-free fixed-point A/B kernels (PCP_NORMALS_EXACT=0): point normals within 2e-3, cells
     within 1e-4.  An empty area keeps the previous cells (virtual_lidar.cpp:168)."""
     exact = "0" if mode == "fixed" else "1"
     monkeypatch.setenv("PCP_NORMALS_EXACT", exact)
+    # exact_two_builds: the area's two grids by two build_index calls + k_area_prep instead of
+    # the paired build (PCP_INDEX_PAIR=0)
+    monkeypatch.setenv("PCP_INDEX_PAIR", "0" if mode == "exact_two_builds" else "1")
     monkeypatch.setenv("PCP_CELLS_ORDER_FREE", "0" if mode == "exact_ordered" else "1")
     d = np.load(GOLD / "excavation.npz")
     ctx = _abi.Context(0)
