@@ -928,7 +928,8 @@ def c1_frame_gpu(ctx, scans, nc_lattice=1):
     composes them (pcp_filter_merge_nodes: both filters + the merger, one wait;
     pcp_excavate_area_async: the carve + the area and terrain callbacks, the grid setup left in
     flight on its side stream while the zx120 index and the candidates are built; the scoring
-    settles it); PCP_C1_CALLS=1: every node callback as its own call (rounds 1-4)."""
+    settles it; the carve's messages copied from its landing after the zx120 index is enqueued);
+    PCP_C1_CALLS=1: every node callback as its own call (rounds 1-4)."""
     from pointcloud_processor_amd import _abi
 
     zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])   # getZX120Position on zx120/base_link
@@ -945,8 +946,13 @@ def c1_frame_gpu(ctx, scans, nc_lattice=1):
         return cand.shape[0], int(rep.best_idx), tot, cand, nc
     merged, filtered, _ = ctx.filter_merge_nodes(scans, [C1_BOX, C1_BOX], C1_LEAF, C1_TFS,
                                                  [(255, 0, 0), (0, 0, 255)])
-    terr, area, _, bbox, cap = ctx.excavate_area_async(merged, C1_ZX_BASE)
+    # the carve's two messages left where they landed until the zx120 index is enqueued, then
+    # copied out (PCP_C1_LANDED=0: copied by the call, as before)
+    landed = os.environ.get("PCP_C1_LANDED", "1") == "1"
+    terr, area, _, bbox, cap = ctx.excavate_area_async(merged, C1_ZX_BASE, landed=landed)
     ctx.set_aux_cloud(filtered[1])
+    if landed:
+        terr, area = terr.copy(), area.copy()   # /excavated_terrain, /excavation_area
     cand = ctx.generate_candidates(bbox, params, zx)[:1]   # ONE candidate pose is scored
     # fresh flags (:259) for the setup's capacity; the scoring settles the count first
     tot, _, rep = ctx.score_poses(cand, zx, params, np.zeros(max(cap, 1), np.uint8))

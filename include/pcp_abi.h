@@ -271,13 +271,21 @@ int pcp_excavate(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excavation_pa
  * records where they land (device-readable pinned memory, no staging copy or upload), the host
  * copies into terrain_out / area_out made after the setup and the index build are enqueued.
  * Arguments and results as those three calls'; grid_bbox / cells_cap as
- * pcp_set_excavation_area_async's (settled the same way).  Waits once (the carve's counts). */
+ * pcp_set_excavation_area_async's (settled the same way).  Waits once (the carve's counts).
+ * terrain_out = area_out = NULL: nothing is copied (the caps are not checked); the records stay
+ * where they landed, read with pcp_excavate_landed -- a composed caller enqueues its next
+ * consumers (the zx120 index) first and builds its messages from there. */
 int pcp_excavate_area_async(pcp_ctx *ctx, const pcp_cloud_view *in,
                             const pcp_excavation_params *p, const pcp_rigid *zx120_base,
                             void *terrain_out, uint64_t terrain_cap, uint64_t *n_terrain,
                             void *area_out, uint64_t area_cap, uint64_t *n_area,
                             double pose_out[4], double grid_resolution, int32_t vertical_layers,
                             double grid_bbox[6], uint64_t *cells_cap);
+/* Where the last pcp_excavate_area_async call made with null outputs left its records: the
+ * context's pinned memory, host-readable -- terrain: *n_terrain, area: *n_area PointXYZRGB
+ * records of that call (the bytes terrain_out / area_out would have received).  Valid until the
+ * context's next pcp_excavate* call; PCP_E_STATE when there is none. */
+int pcp_excavate_landed(pcp_ctx *ctx, const void **terrain, const void **area);
 
 /* ---- calc_drivable_area.cpp (the occupancy-grid node) -------------------------------------- */
 typedef struct pcp_drivable_params {   /* calc_drivable_area.cpp:20-26 */

@@ -135,6 +135,7 @@ _SIGS = [
     ("pcp_filter_merge_landed", C.c_int, [_P, C.c_int, _P, _P]),
     ("pcp_excavate_area_async", C.c_int, [_P, _P, _P, _P, _P, C.c_uint64, _P, _P, C.c_uint64, _P,
                                           _P, C.c_double, C.c_int32, _P, _P]),
+    ("pcp_excavate_landed", C.c_int, [_P, _P, _P]),
     ("pcp_drivable_area", C.c_int, [_P, _P, _P, C.c_double, C.c_double, C.c_double, C.c_double,
                                     _P, _P, C.c_uint64, _P, _P]),
     ("pcp_generate_candidates", C.c_int, [_P, _P, C.POINTER(VlParams), _P, _P, C.c_uint64,
@@ -605,16 +606,34 @@ class Context:
 
     def excavate_area_async(self, cloud: np.ndarray, zx120_tf, params: ExcavationParams | None = None,
                             grid_resolution: float = 0.1, vertical_layers: int = 10,
-                            point_step=None, offs=(0, 4, 8)):
+                            point_step=None, offs=(0, 4, 8), landed: bool = False):
         """pcp_excavate_area_async: excavate(), then set_excavation_area_async() over its area
         (when not empty) and set_terrain() over its terrain, fed from the carve's landed
-        records.  -> (terrain, area, pose, grid_bbox (6,), cells_cap)."""
+        records.  -> (terrain, area, pose, grid_bbox (6,), cells_cap).  landed=True: null
+        outputs, terrain / area are read-only views of the landing (pcp_excavate_landed), valid
+        until the context's next excavate call."""
         v = cloud_view(cloud, point_step, offs)
         p = params or excavation_params()
         tf = Rigid((C.c_double * 3)(*zx120_tf[0]), (C.c_double * 4)(*zx120_tf[1]))
         nt, na, cap = C.c_uint64(), C.c_uint64(), C.c_uint64()
         pose = np.zeros(4, np.float64)
         bbox = np.zeros(6, np.float64)
+        if landed:
+            self._check(self.lib.pcp_excavate_area_async(
+                self.h, C.byref(v), C.byref(p), C.byref(tf), None, 0, C.byref(nt), None, 0,
+                C.byref(na), _ptr(pose), float(grid_resolution), int(vertical_layers), _ptr(bbox),
+                C.byref(cap)), "pcp_excavate_area_async")
+            tp, ap = C.c_void_p(), C.c_void_p()
+            self._check(self.lib.pcp_excavate_landed(self.h, C.byref(tp), C.byref(ap)),
+                        "pcp_excavate_landed")
+
+            def view(ptr, n):
+                if n == 0:
+                    return np.empty((0, 8), np.float32)
+                a = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_float)), shape=(n, 8))
+                a.flags.writeable = False
+                return a
+            return view(tp, nt.value), view(ap, na.value), pose, bbox, cap.value
         self._check(self.lib.pcp_excavate_bounds(C.byref(p), v.n, C.byref(nt), C.byref(na)),
                     "pcp_excavate_bounds")
         terr = np.empty((max(nt.value, 1), 8), np.float32)

@@ -309,13 +309,20 @@ bool SimplifiedDualLidarOptimizer::excavationAreaCallback(const PointCloud2 &msg
 
 ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
     ExcavationTerrainGenerator &gen, const PointCloud2 &msg, const Transform *zx120_base,
-    const pcp_cloud_view *landed) {
+    const pcp_cloud_view *landed, const PointCloud2 *zx120) {
+    // the zx120 callback's own error only when the callbacks before it left none
+    auto zx_callback = [&]() {
+        if (!zx120) return;
+        std::string e0 = err_;
+        zx120PointsCallback(*zx120);
+        if (err_.empty()) err_ = std::move(e0);
+    };
     pcp_cloud_view v;
     if (!defer_grid_ || multi_ || !gen.p_.enabled || !zx120_base || !cloud_view(msg, v, nullptr)) {
         ExcavationTerrainGenerator::Output o = gen.matchedCloudCallback(msg, zx120_base);
-        if (o.area_published && !excavationAreaCallback(o.excavation_area) && !err_.empty())
-            return o;
-        terrainCallback(o.excavated_terrain);
+        if (!(o.area_published && !excavationAreaCallback(o.excavation_area) && !err_.empty()))
+            terrainCallback(o.excavated_terrain);
+        zx_callback();
         return o;
     }
     ExcavationTerrainGenerator::Output o;
@@ -330,17 +337,23 @@ ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
         gen.err_ = "excavated_surface_generator: bad parameters";
         o.excavated_terrain = msg;
         terrainCallback(o.excavated_terrain);
+        zx_callback();
         return o;
     }
     // (the same bytes as the message, in pinned memory the device reads in place)
     if (landed && landed->n == v.n && landed->point_step == v.point_step) v = *landed;
-    uint8_t *terr = landing(gen.terr_, nt * 32 + 32), *area = landing(gen.area_, na * 32 + 32);
-    if (pcp_excavate_area_async(dev_.ctx(), &v, &gen.p_, &tf, terr, nt, &nt, area, na, &na, pose,
-                                p_.grid_resolution, p_.vertical_layers, bb, &ncap) != PCP_OK) {
+    // the records stay where they land (null outputs): the zx120 index is enqueued behind the
+    // carve's consumers first, then the two messages are copied straight from the landing
+    const void *terr = nullptr, *area = nullptr;
+    if (pcp_excavate_area_async(dev_.ctx(), &v, &gen.p_, &tf, nullptr, nt, &nt, nullptr, na, &na,
+                                pose, p_.grid_resolution, p_.vertical_layers, bb, &ncap) != PCP_OK ||
+        pcp_excavate_landed(dev_.ctx(), &terr, &area) != PCP_OK) {
         gen.err_ = dev_.error();
         o.excavated_terrain = msg;
+        zx_callback();
         return o;
     }
+    zx_callback();
     o.excavated_terrain = make_xyzrgb_cloud(terr, nt, "map");
     o.excavated_terrain.stamp = msg.stamp;
     o.excavation_area = make_xyzrgb_cloud(area, na, "map");

@@ -283,11 +283,15 @@ class SimplifiedDualLidarOptimizer {
     // the grid not deferred (or sharded, or the carve disabled / its TF missing) it makes them.
     // Errors: gen.lastError() for the carve, lastError() for the two callbacks
     // landed (nullable): merged's bytes in the context's pinned landing
-    // (ComposedFilterMerge::Output::merged_landed), read in place instead of the message
+    // (ComposedFilterMerge::Output::merged_landed), read in place instead of the message.
+    // zx120 (nullable): this node's zx120PointsCallback for that message as well, made after
+    // the carve's consumers are enqueued and before gen's two messages are built from the
+    // carve's landed records (pcp_excavate_landed): the zx120 index builds while the host copies
     ExcavationTerrainGenerator::Output carveCallbacks(ExcavationTerrainGenerator &gen,
                                                       const PointCloud2 &merged,
                                                       const Transform *zx120_base,
-                                                      const pcp_cloud_view *landed = nullptr);
+                                                      const pcp_cloud_view *landed = nullptr,
+                                                      const PointCloud2 *zx120 = nullptr);
     const std::string &lastError() const { return err_; }
 
    private:

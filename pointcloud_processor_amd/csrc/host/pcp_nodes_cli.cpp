@@ -221,6 +221,10 @@ static int cmd_replay(Device &dev, char **a) {
     // the composed carve reads the merger's landed records in place (default) / the message
     bool carve_landed = true;
     if (const char *cl = std::getenv("PCP_CARVE_LANDED")) carve_landed = std::atoi(cl) != 0;
+    // the zx120 cloud's callback composed into the carve call as well (default): its index is
+    // enqueued before the carve's messages are copied out of the landing
+    bool carve_zx = true;
+    if (const char *cz = std::getenv("PCP_CARVE_ZX")) carve_zx = std::atoi(cz) != 0;
     ExcavationTerrainGenerator gen(dev);
     SimplifiedDualLidarOptimizer vl(dev);
     // the nodes composed in one process: the grid setup is enqueued by the area callback and
@@ -292,9 +296,11 @@ static int cmd_replay(Device &dev, char **a) {
             lap(1);
         }
         ExcavationTerrainGenerator::Output e;
+        const bool zx_in_carve = chain && carve_fused && carve_zx;
         if (chain && carve_fused) {   // the carve + both callbacks (stage "carve" holds all three)
             e = vl.carveCallbacks(gen, o.merged, &zx_base,
-                                  front_fused && carve_landed ? &front_landed : nullptr);
+                                  front_fused && carve_landed ? &front_landed : nullptr,
+                                  zx_in_carve ? &zf : nullptr);
             if (!e.area_published) {
                 std::fprintf(stderr, "replay: carve failed: %s\n", gen.lastError().c_str());
                 return 1;
@@ -314,7 +320,7 @@ static int cmd_replay(Device &dev, char **a) {
             vl.terrainCallback(e.excavated_terrain);
             lap(4);
         }
-        vl.zx120PointsCallback(zf);
+        if (!zx_in_carve) vl.zx120PointsCallback(zf);   // (else made by carveCallbacks)
         lap(5);
         auto r = vl.runOptimization(&zx_base);
         lap(6);

@@ -404,8 +404,10 @@ static float pack_rgb(unsigned r, unsigned g, unsigned b) {
 // the carve (pcp_excavate).  xl non-null (pcp_excavate_area_async): the records land in
 // ctx->exc_land (pinned, device-readable, kept until the next such call) when they fit, and are
 // NOT copied to terrain_out / area_out here -- xl->terr / xl->area point at them and the caller
-// copies them out after enqueueing their consumers
+// copies them out after enqueueing their consumers.  xl->keep (null outputs): the records land
+// there whatever their size and stay (pcp_excavate_landed); no capacity or null-output check
 struct ExcLand {
+    bool keep = false;
     bool landed = false;
     const unsigned char *terr = nullptr, *area = nullptr;
 };
@@ -417,6 +419,7 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     if (!ctx) return PCP_E_INVALID;
     if (!p || !zx120_base || !n_terrain || !n_area)
         return set_err(ctx, PCP_E_INVALID, "pcp_excavate: null argument");
+    ctx->exc_keep_valid = false;   // (exc_land is rewritten below)
     int rc = check_view(ctx, in, "pcp_excavate");
     if (rc) return rc;
     if (!(p->point_density > 0.0) || !(p->depth > 0.0) || !(p->terrain_search_radius > 0.0))
@@ -601,7 +604,7 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     // the records: straight into pinned memory for message-sized results (the kernels store
     // them there, no D2H copy), else a device buffer copied out
     const size_t land_b = (n + nsurf + narea) * 32;
-    const bool land = ctx->zc_in && land_b <= kPinDirectMax * 8;
+    const bool land = (ctx->zc_in && land_b <= kPinDirectMax * 8) || (xl && xl->keep);
     float4 *kept;
     if (land && xl) {
         PCP_HIP(ctx, ctx->exc_land.ensure(land_b + 256));
@@ -707,13 +710,14 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     }
     *n_terrain = nkept + nsurf;
     *n_area = narea;
-    if (*n_terrain > terrain_cap || *n_area > area_cap) {
+    const bool keep = xl && xl->keep;
+    if (!keep && (*n_terrain > terrain_cap || *n_area > area_cap)) {
         prof_resolve(ctx);
         return set_err(ctx, PCP_E_CAPACITY, "pcp_excavate: need %llu / %llu records, cap %llu / %llu",
                        (unsigned long long)*n_terrain, (unsigned long long)*n_area,
                        (unsigned long long)terrain_cap, (unsigned long long)area_cap);
     }
-    if ((*n_terrain && !terrain_out) || (*n_area && !area_out))
+    if (!keep && ((*n_terrain && !terrain_out) || (*n_area && !area_out)))
         return set_err(ctx, PCP_E_INVALID, "pcp_excavate: null output");
     if (land && xl) {   // the caller copies them out
         xl->landed = true;
@@ -760,6 +764,7 @@ int pcp_excavate_area_async(pcp_ctx *ctx, const pcp_cloud_view *in,
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     if (int rc = area_finish(ctx)) return rc;
     ExcLand xl;
+    xl.keep = !terrain_out && !area_out;   // the records stay landed (pcp_excavate_landed)
     if (int rc = excavate_impl(ctx, in, p, zx120_base, terrain_out, terrain_cap, n_terrain,
                                area_out, area_cap, n_area, pose_out, &xl))
         return rc;
@@ -788,8 +793,24 @@ int pcp_excavate_area_async(pcp_ctx *ctx, const pcp_cloud_view *in,
                                  true, xl.area))
         return rc;
     if (int rc = set_terrain_from(ctx, &vt, xl.terr)) return rc;
+    if (xl.keep) {   // read in place by the caller (its own consumers enqueued first)
+        ctx->exc_keep_terr = xl.terr;
+        ctx->exc_keep_area = xl.area;
+        ctx->exc_keep_valid = true;
+        return PCP_OK;
+    }
     if (*n_terrain) host_copy(ctx, terrain_out, xl.terr, *n_terrain * 32);
     if (*n_area) host_copy(ctx, area_out, xl.area, *n_area * 32);
+    return PCP_OK;
+}
+
+int pcp_excavate_landed(pcp_ctx *ctx, const void **terrain, const void **area) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!ctx->exc_keep_valid)
+        return set_err(ctx, PCP_E_STATE, "pcp_excavate_landed: no pcp_excavate_area_async result "
+                                         "left in place");
+    if (terrain) *terrain = ctx->exc_keep_terr;
+    if (area) *area = ctx->exc_keep_area;
     return PCP_OK;
 }
 

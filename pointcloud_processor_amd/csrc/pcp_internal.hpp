@@ -260,6 +260,10 @@ struct pcp_ctx {
     const void *fm_land_merged = nullptr;
     std::vector<const float *> fm_land_filtered;
     pcp::PinnedBuf exc_land;
+    // pcp_excavate_area_async called with null outputs: its records left in exc_land
+    // (pcp_excavate_landed), until the next pcp_excavate* call
+    bool exc_keep_valid = false;
+    const void *exc_keep_terr = nullptr, *exc_keep_area = nullptr;
     // the carve's four counters, two sets used in turn: each call's k_gen_emit clears the set
     // the next call uses (no memset launch in front of it)
     pcp::DevBuf carve_ctr;

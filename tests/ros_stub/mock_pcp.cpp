@@ -97,6 +97,9 @@ int pcp_excavate_area_async(pcp_ctx *c, const pcp_cloud_view *, const pcp_excava
                             uint64_t *, double *, double, int32_t, double *, uint64_t *) {
     return fail(c, "pcp_excavate_area_async: not in the test double");
 }
+int pcp_excavate_landed(pcp_ctx *c, const void **, const void **) {
+    return fail(c, "pcp_excavate_landed: not in the test double");
+}
 int pcp_cells_count(pcp_ctx *c, uint64_t *n) {
     *n = c->cells.size() / 3;
     return PCP_OK;

@@ -1373,7 +1373,9 @@ def test_excavate_area_async_matches_three_calls():
     both messages, the pose, the grid bounds, the cells and their normals, and a tick's poses,
     totals, covered counts, flags and report bit-identical.  Three frames in a row on one
     context (the landing is reused while the previous setup is pending: the call settles it
-    first), the third with the carve moved (a new generated lattice)."""
+    first), the third with the carve moved (a new generated lattice).  "landed": the composed
+    call with null outputs, the messages read in place (pcp_excavate_landed) after the zx120
+    index and the tick -- the same bytes."""
     box = np.array([0.0, 15.0, -10.0, 10.0, -1.5, 10.0])
     tfs = [((8.0, -3.0, 2.0), (0.0, 0.0, 0.2588190451025208, 0.9659258262890683)),
            ((0.55, 0.4, 3.5), (0.0, 0.21633, 0.0, 0.97632))]
@@ -1387,7 +1389,7 @@ def test_excavate_area_async_matches_three_calls():
                  synth.lidar_cloud(60_032, sensor_height=3.5, seed=seed + 1)]
         frames.append((scans, base))
     out = {}
-    for mode in ("calls", "composed"):
+    for mode in ("calls", "composed", "landed"):
         res = []
         with _abi.Context(0) as ctx:
             for scans, base in frames:
@@ -1398,7 +1400,12 @@ def test_excavate_area_async_matches_three_calls():
                     bb, n = ctx.set_excavation_area_async(area, 0.1, 10, point_step=32)
                     ctx.set_terrain(terr, point_step=32)
                 else:
-                    terr, area, pose, bb, n = ctx.excavate_area_async(merged, base)
+                    terr, area, pose, bb, n = ctx.excavate_area_async(merged, base,
+                                                                      landed=mode == "landed")
+                    tp = ctypes.c_void_p()
+                    rc = ctx.lib.pcp_excavate_landed(ctx.h, ctypes.byref(tp), None)
+                    # left in place only by the null-output call
+                    assert (rc == _abi.PCP_OK) == (mode == "landed"), rc
                 ctx.set_aux_cloud(filt[1])
                 flags = np.zeros(max(n, 1), np.uint8)
                 poses, tot, cov, rep = ctx.generate_and_score(bb, params, zx, flags)
@@ -1407,11 +1414,12 @@ def test_excavate_area_async_matches_three_calls():
                 res.append((terr.copy(), area.copy(), pose, bb, nc, poses, tot, cov, flags[:nc].copy(),
                             rep.as_dict(), xyz, cn))
         out[mode] = res
-    for a, b in zip(out["calls"], out["composed"]):
+    for a, b, c in zip(out["calls"], out["composed"], out["landed"]):
         for i in (0, 1, 2, 3, 5, 6, 7, 8, 10, 11):
             np.testing.assert_array_equal(np.asarray(a[i]).view(np.uint8), np.asarray(b[i]).view(np.uint8))
-        assert a[4] == b[4] and a[4] > 0
-        assert a[9] == b[9]
+            np.testing.assert_array_equal(np.asarray(a[i]).view(np.uint8), np.asarray(c[i]).view(np.uint8))
+        assert a[4] == b[4] == c[4] and a[4] > 0
+        assert a[9] == b[9] == c[9]
 
 
 def test_excavation_area_async_back_to_back(scene):

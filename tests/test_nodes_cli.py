@@ -141,9 +141,11 @@ def test_excavation_area_node(tmp_path, oracle, small_scene):
     assert res["best_idx"] == rep.best_idx
 
 
-@pytest.mark.parametrize("zc,area_async,front,carve", [("1", "1", "1", "1"), ("0", "1", "1", "1"),
-                                                     ("1", "1", "1", "0"), ("1", "0", "0", "0")])
-def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_async, front, carve):
+@pytest.mark.parametrize("zc,area_async,front,carve,zx", [
+    ("1", "1", "1", "1", "1"), ("0", "1", "1", "1", "1"), ("1", "1", "1", "0", "1"),
+    ("1", "0", "0", "0", "1"), ("1", "1", "1", "1", "0"), ("1", "0", "1", "1", "1")])
+def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_async, front, carve,
+                                     zx):
     """C5 with the launch file's whole chain per frame: filter x2 -> merge ->
     excavated_surface_generator (/excavated_terrain, /excavation_area) -> virtual_lidar
     (terrain index, normals + cell grid, pose search).  Frames 0, 1, 2 and the last one are
@@ -158,7 +160,10 @@ def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_as
     filter and merger nodes composed in one call (PCP_FRONT_FUSED=1, default) and as the three
     node callbacks (0); the carve node and virtual_lidar's area + terrain callbacks composed
     (PCP_CARVE_FUSED=1, default: pcp_excavate_area_async, the carve's landed records feeding the
-    setup and the index in place) and as the three callbacks (0)."""
+    setup and the index in place) and as the three callbacks (0); with the carve composed, the
+    zx120 cloud's callback made inside that call, the messages copied from the landing after its
+    index is enqueued (PCP_CARVE_ZX=1, default; with the grid not deferred: the node's three
+    callbacks, then the zx120 one) or after the call (0)."""
     np.ascontiguousarray(scene.terrain).tofile(tmp_path / "t.f32")
     np.ascontiguousarray(cells.xyz).tofile(tmp_path / "c.f64")
     np.ascontiguousarray(cells.normals).tofile(tmp_path / "n.f32")
@@ -166,7 +171,8 @@ def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_as
     res = _run("replay", tmp_path / "t.f32", scene.terrain.shape[0], tmp_path / "c.f64",
                tmp_path / "n.f32", cells.xyz.shape[0], _t(cells.grid_bbox), frames, 60032, 1,
                tmp_path, env={"PCP_ZC_IN": zc, "PCP_AREA_ASYNC": area_async,
-                              "PCP_FRONT_FUSED": front, "PCP_CARVE_FUSED": carve})
+                              "PCP_FRONT_FUSED": front, "PCP_CARVE_FUSED": carve,
+                              "PCP_CARVE_ZX": zx})
     assert res["frames"] == frames and res["chain"] == 1
     assert res["cells"] > 0 and res["merged_points"] > 0 and res["best_idx"] >= 0
     assert 0 < res["p50_ms"] <= res["p99_ms"]
