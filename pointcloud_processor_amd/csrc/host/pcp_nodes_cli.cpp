@@ -221,9 +221,10 @@ static int cmd_replay(Device &dev, char **a) {
     // the composed carve reads the merger's landed records in place (default) / the message
     bool carve_landed = true;
     if (const char *cl = std::getenv("PCP_CARVE_LANDED")) carve_landed = std::atoi(cl) != 0;
-    // the zx120 cloud's callback composed into the carve call as well (default): its index is
-    // enqueued before the carve's messages are copied out of the landing
-    bool carve_zx = true;
+    // the zx120 cloud's callback composed into the carve call as well (PCP_CARVE_ZX=1): its
+    // index is enqueued before the carve's messages are copied out of the landing.  Off by
+    // default: no faster (p50 0.644-0.673 vs 0.637-0.648 ms, profiles/r05_c5_host_bbox_zx_ab.log)
+    bool carve_zx = false;
     if (const char *cz = std::getenv("PCP_CARVE_ZX")) carve_zx = std::atoi(cz) != 0;
     ExcavationTerrainGenerator gen(dev);
     SimplifiedDualLidarOptimizer vl(dev);

@@ -162,8 +162,8 @@ def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_as
     (PCP_CARVE_FUSED=1, default: pcp_excavate_area_async, the carve's landed records feeding the
     setup and the index in place) and as the three callbacks (0); with the carve composed, the
     zx120 cloud's callback made inside that call, the messages copied from the landing after its
-    index is enqueued (PCP_CARVE_ZX=1, default; with the grid not deferred: the node's three
-    callbacks, then the zx120 one) or after the call (0)."""
+    index is enqueued (PCP_CARVE_ZX=1; with the grid not deferred: the node's three callbacks,
+    then the zx120 one) or after the call (0, default)."""
     np.ascontiguousarray(scene.terrain).tofile(tmp_path / "t.f32")
     np.ascontiguousarray(cells.xyz).tofile(tmp_path / "c.f64")
     np.ascontiguousarray(cells.normals).tofile(tmp_path / "n.f32")
