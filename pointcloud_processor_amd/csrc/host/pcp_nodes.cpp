@@ -171,7 +171,8 @@ GnssGicpMatcher::Output GnssGicpMatcher::processPointClouds(bool origin_set,
 ComposedFilterMerge::Output ComposedFilterMerge::frame(const PointCloud2 &robot,
                                                        const PointCloud2 &backhoe, bool origin_set,
                                                        const Transform *robot_tf,
-                                                       const Transform *zx120_tf) {
+                                                       const Transform *zx120_tf,
+                                                       bool defer_messages) {
     err_.clear();
     Output o;
     o.robot_filtered = make_xyz_cloud(nullptr, 0, robot.frame_id);
@@ -212,29 +213,57 @@ ComposedFilterMerge::Output ComposedFilterMerge::frame(const PointCloud2 &robot,
         err_ = dev_.error();
         return o;
     }
-    const uint8_t *mrg = static_cast<const uint8_t *>(landed);
-    o.robot_filtered = make_xyz_cloud(outs[0], per[0], robot.frame_id);
-    o.robot_filtered.stamp = robot.stamp;
-    o.backhoe_filtered = make_xyz_cloud(outs[1], per[1], backhoe.frame_id);
-    o.backhoe_filtered.stamp = backhoe.stamp;
-    if (!origin_set) return o;   // :309
-    // the concatenation of the clouds whose TF was found, robot first (:316-325)
-    uint64_t base = 0, keep_off = 0, keep_n = 0;
-    const bool both = robot_tf && zx120_tf;
+    Output::Pending &q = o.pending;
+    q.merged = static_cast<const uint8_t *>(landed);
+    q.origin_set = origin_set;
     for (int i = 0; i < 2; ++i) {
-        if (tfs[i])
-            (i == 0 ? o.merge.robot_colored : o.merge.backhoe_colored) =
-                make_xyzrgb_cloud(mrg + 32 * base, per[i], "map");
-        if (tfs[i] && !both) {
-            keep_off = base;
-            keep_n = per[i];
-        }
-        base += per[i];
+        q.filtered[i] = outs[i];
+        q.per[i] = per[i];
+        q.tf[i] = tfs[i] != nullptr;
     }
-    if (both) keep_n = n;
-    o.merge.merged = make_xyzrgb_cloud(mrg + 32 * keep_off, keep_n, "map");
-    if (keep_n) o.merged_landed = pcp_cloud_view{mrg + 32 * keep_off, keep_n, 32, 0, 4, 8};
+    // the concatenation of the clouds whose TF was found, robot first (:316-325)
+    if (origin_set) {
+        uint64_t base = 0;
+        const bool both = robot_tf && zx120_tf;
+        for (int i = 0; i < 2; ++i) {
+            if (tfs[i] && !both) {
+                q.keep_off = base;
+                q.keep_n = per[i];
+            }
+            base += per[i];
+        }
+        if (both) q.keep_n = n;
+        if (q.keep_n)
+            o.merged_landed = pcp_cloud_view{q.merged + 32 * q.keep_off, q.keep_n, 32, 0, 4, 8};
+    }
+    o.deferred = true;
+    if (defer_messages) {   // the merged message's header (its data follows in messages())
+        o.merge.merged.width = (uint32_t)q.keep_n;
+        o.merge.merged.row_step = 32 * o.merge.merged.width;
+        return o;
+    }
+    messages(o);
     return o;
+}
+
+void ComposedFilterMerge::messages(Output &o) const {
+    if (!o.deferred) return;
+    o.deferred = false;
+    const Output::Pending &q = o.pending;
+    const double rs = o.robot_filtered.stamp, bs = o.backhoe_filtered.stamp;
+    o.robot_filtered = make_xyz_cloud(q.filtered[0], q.per[0], o.robot_filtered.frame_id);
+    o.robot_filtered.stamp = rs;
+    o.backhoe_filtered = make_xyz_cloud(q.filtered[1], q.per[1], o.backhoe_filtered.frame_id);
+    o.backhoe_filtered.stamp = bs;
+    if (!q.origin_set) return;   // :309
+    uint64_t base = 0;
+    for (int i = 0; i < 2; ++i) {
+        if (q.tf[i])
+            (i == 0 ? o.merge.robot_colored : o.merge.backhoe_colored) =
+                make_xyzrgb_cloud(q.merged + 32 * base, q.per[i], "map");
+        base += q.per[i];
+    }
+    o.merge.merged = make_xyzrgb_cloud(q.merged + 32 * q.keep_off, q.keep_n, "map");
 }
 
 // ---- virtual_lidar ---------------------------------------------------------------------------
@@ -317,8 +346,13 @@ ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
         zx120PointsCallback(*zx120);
         if (err_.empty()) err_ = std::move(e0);
     };
-    pcp_cloud_view v;
-    if (!defer_grid_ || multi_ || !gen.p_.enabled || !zx120_base || !cloud_view(msg, v, nullptr)) {
+    // (the same bytes as the message, in pinned memory the device reads in place: then the
+    // message may still be its header, ComposedFilterMerge's deferred messages)
+    pcp_cloud_view v{};
+    const bool in_place = landed && landed->n && landed->n == msg.size() && landed->point_step == 32;
+    if (in_place) v = *landed;
+    if (!defer_grid_ || multi_ || !gen.p_.enabled || !zx120_base ||
+        !(in_place || cloud_view(msg, v, nullptr))) {
         ExcavationTerrainGenerator::Output o = gen.matchedCloudCallback(msg, zx120_base);
         if (!(o.area_published && !excavationAreaCallback(o.excavation_area) && !err_.empty()))
             terrainCallback(o.excavated_terrain);
@@ -340,8 +374,6 @@ ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
         zx_callback();
         return o;
     }
-    // (the same bytes as the message, in pinned memory the device reads in place)
-    if (landed && landed->n == v.n && landed->point_step == v.point_step) v = *landed;
     // the records stay where they land (null outputs): the zx120 index is enqueued behind the
     // carve's consumers first, then the two messages are copied straight from the landing
     const void *terr = nullptr, *area = nullptr;

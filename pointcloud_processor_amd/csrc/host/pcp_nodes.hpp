@@ -154,9 +154,23 @@ class ComposedFilterMerge {
         // none): valid until the context's next filter / merge / carve call -- a carve composed
         // behind this call reads them in place (SimplifiedDualLidarOptimizer::carveCallbacks)
         pcp_cloud_view merged_landed{};
+        // frame(..., defer_messages = true): the messages' data not copied yet -- merge.merged
+        // carries its header (width, fields) only, the rest are empty -- until messages(o)
+        bool deferred = false;
+        struct Pending {
+            const float *filtered[2] = {nullptr, nullptr};
+            const uint8_t *merged = nullptr;
+            uint64_t per[2] = {0, 0}, keep_off = 0, keep_n = 0;
+            bool tf[2] = {false, false}, origin_set = false;
+        } pending;
     };
+    // defer_messages: the launches and the one synchronisation only; the five messages are
+    // copied out of the landing by messages(o) -- e.g. after a composed carve has read the
+    // merged cloud in place (SimplifiedDualLidarOptimizer::carveCallbacks), so the copies run
+    // while the device builds the grid.  Valid until the context's next filter / merge call
     Output frame(const PointCloud2 &robot, const PointCloud2 &backhoe, bool origin_set,
-                 const Transform *robot_tf, const Transform *zx120_tf);
+                 const Transform *robot_tf, const Transform *zx120_tf, bool defer_messages = false);
+    void messages(Output &o) const;
     const std::string &lastError() const { return err_; }
 
    private:
@@ -283,7 +297,9 @@ class SimplifiedDualLidarOptimizer {
     // the grid not deferred (or sharded, or the carve disabled / its TF missing) it makes them.
     // Errors: gen.lastError() for the carve, lastError() for the two callbacks
     // landed (nullable): merged's bytes in the context's pinned landing
-    // (ComposedFilterMerge::Output::merged_landed), read in place instead of the message.
+    // (ComposedFilterMerge::Output::merged_landed), read in place instead of the message --
+    // which may then be its header only (a deferred ComposedFilterMerge frame) as long as the
+    // composed path applies (grid deferred, one device, carve enabled, TF present).
     // zx120 (nullable): this node's zx120PointsCallback for that message as well, made after
     // the carve's consumers are enqueued and before gen's two messages are built from the
     // carve's landed records (pcp_excavate_landed): the zx120 index builds while the host copies

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <malloc.h>
 #include <random>
 #include <sstream>
 #include <string>
@@ -231,10 +232,16 @@ static int cmd_replay(Device &dev, char **a) {
     // the nodes composed in one process: the grid setup is enqueued by the area callback and
     // waited for once by the tick (PCP_AREA_ASYNC=0: settled in the area callback, as a ROS shell
     // that publishes the grid markers there)
-    {
-        const char *ea = std::getenv("PCP_AREA_ASYNC");
-        vl.setDeferredGrid(!ea || std::atoi(ea) != 0);
-    }
+    bool area_async = true;
+    if (const char *ea = std::getenv("PCP_AREA_ASYNC")) area_async = std::atoi(ea) != 0;
+    vl.setDeferredGrid(area_async);
+    // the filter / merger messages copied out of their landing after the composed carve has
+    // read the merged cloud in place (default; only where every composition applies), while the
+    // device builds the grid.  PCP_FRONT_DEFER=0: copied by the front call
+    bool front_defer = true;
+    if (const char *fd = std::getenv("PCP_FRONT_DEFER")) front_defer = std::atoi(fd) != 0;
+    front_defer = front_defer && front_fused && chain && carve_fused && carve_landed && area_async &&
+                  !carve_zx;
     vl.terrainCallback(cloud_from(t, tn, 32, "map"));
     std::vector<double> xyz(cn * 3);
     std::vector<float> nrm(cn * 3);
@@ -275,16 +282,23 @@ static int cmd_replay(Device &dev, char **a) {
         PointCloud2 rf, zf;
         GnssGicpMatcher::Output o;
         pcp_cloud_view front_landed{};
+        ComposedFilterMerge::Output fo;
+        // the front's messages (when deferred: after the carve call)
+        auto take_front = [&]() {
+            front.messages(fo);
+            rf = std::move(fo.robot_filtered);
+            zf = std::move(fo.backhoe_filtered);
+            o = std::move(fo.merge);
+        };
         if (front_fused) {
-            auto fo = front.frame(rm, zm, true, &robot_tf, &zx_tf);
+            fo = front.frame(rm, zm, true, &robot_tf, &zx_tf, front_defer);
             if (!front.lastError().empty()) {
                 std::fprintf(stderr, "replay: filter+merge failed: %s\n", front.lastError().c_str());
                 return 1;
             }
             front_landed = fo.merged_landed;
-            rf = std::move(fo.robot_filtered);
-            zf = std::move(fo.backhoe_filtered);
-            o = std::move(fo.merge);
+            if (front_defer) o.merged = fo.merge.merged;   // (its header: the carve reads the landing)
+            else take_front();
             lap(0);
             lap(1);
         } else {
@@ -306,6 +320,7 @@ static int cmd_replay(Device &dev, char **a) {
                 std::fprintf(stderr, "replay: carve failed: %s\n", gen.lastError().c_str());
                 return 1;
             }
+            if (front_defer) take_front();
             lap(2);
             lap(3);
             lap(4);
@@ -501,6 +516,17 @@ static int cmd_drivable(Device &dev, char **a) {
 }
 
 int main(int argc, char **argv) {
+    // the container keeps the heap it freed: every frame's messages (MBs of PointCloud2 data)
+    // are allocated and freed again, and glibc's defaults would map and unmap them (or trim the
+    // heap top), paying their page faults every frame (C5 p50 -17 us, p99 -30 us,
+    // profiles/r05_c5_malloc_ab.log).  PCP_MALLOC_KEEP=0: glibc's defaults
+    {
+        const char *mk = std::getenv("PCP_MALLOC_KEEP");
+        if (!mk || std::atoi(mk) != 0) {
+            mallopt(M_MMAP_THRESHOLD, 256 << 20);
+            mallopt(M_TRIM_THRESHOLD, 1 << 30);
+        }
+    }
     if (argc < 2) {
         std::fprintf(stderr, "usage: pcp_nodes_cli filter|merge|vlidar|area|drivable|replay ...\n");
         return 2;

@@ -141,11 +141,12 @@ def test_excavation_area_node(tmp_path, oracle, small_scene):
     assert res["best_idx"] == rep.best_idx
 
 
-@pytest.mark.parametrize("zc,area_async,front,carve,zx", [
-    ("1", "1", "1", "1", "1"), ("0", "1", "1", "1", "1"), ("1", "1", "1", "0", "1"),
-    ("1", "0", "0", "0", "1"), ("1", "1", "1", "1", "0"), ("1", "0", "1", "1", "1")])
+@pytest.mark.parametrize("zc,area_async,front,carve,zx,defer", [
+    ("1", "1", "1", "1", "0", "1"), ("0", "1", "1", "1", "0", "1"), ("1", "1", "1", "0", "0", "1"),
+    ("1", "0", "0", "0", "0", "1"), ("1", "1", "1", "1", "1", "1"), ("1", "0", "1", "1", "0", "1"),
+    ("1", "1", "1", "1", "0", "0")])
 def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_async, front, carve,
-                                     zx):
+                                     zx, defer):
     """C5 with the launch file's whole chain per frame: filter x2 -> merge ->
     excavated_surface_generator (/excavated_terrain, /excavation_area) -> virtual_lidar
     (terrain index, normals + cell grid, pose search).  Frames 0, 1, 2 and the last one are
@@ -163,7 +164,9 @@ def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_as
     setup and the index in place) and as the three callbacks (0); with the carve composed, the
     zx120 cloud's callback made inside that call, the messages copied from the landing after its
     index is enqueued (PCP_CARVE_ZX=1; with the grid not deferred: the node's three callbacks,
-    then the zx120 one) or after the call (0, default)."""
+    then the zx120 one) or after the call (0, default); the front's messages copied out of their
+    landing after the composed carve read the merged cloud in place (PCP_FRONT_DEFER=1, default
+    where every composition applies) or by the front call (0)."""
     np.ascontiguousarray(scene.terrain).tofile(tmp_path / "t.f32")
     np.ascontiguousarray(cells.xyz).tofile(tmp_path / "c.f64")
     np.ascontiguousarray(cells.normals).tofile(tmp_path / "n.f32")
@@ -172,7 +175,7 @@ def test_streaming_replay_full_chain(tmp_path, oracle, scene, cells, zc, area_as
                tmp_path / "n.f32", cells.xyz.shape[0], _t(cells.grid_bbox), frames, 60032, 1,
                tmp_path, env={"PCP_ZC_IN": zc, "PCP_AREA_ASYNC": area_async,
                               "PCP_FRONT_FUSED": front, "PCP_CARVE_FUSED": carve,
-                              "PCP_CARVE_ZX": zx})
+                              "PCP_CARVE_ZX": zx, "PCP_FRONT_DEFER": defer})
     assert res["frames"] == frames and res["chain"] == 1
     assert res["cells"] > 0 and res["merged_points"] > 0 and res["best_idx"] >= 0
     assert 0 < res["p50_ms"] <= res["p99_ms"]
