@@ -591,6 +591,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
     if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff);
     if (const char *bg = std::getenv("PCP_BK_GT")) ctx->bk_gt = std::atoi(bg);
+    if (const char *bp = std::getenv("PCP_BK_PTS")) ctx->bk_pts = std::atoi(bp);
     if (const char *zc = std::getenv("PCP_ZC_IN")) ctx->zc_in = std::atoi(zc) != 0;
     if (const char *ck = std::getenv("PCP_COPY_KERNEL")) ctx->copy_kernel = std::atoi(ck) != 0;
     if (const char *tb = std::getenv("PCP_TERRAIN_BLOCKS")) ctx->terrain_blocks = std::atoi(tb);

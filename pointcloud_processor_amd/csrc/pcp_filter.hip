@@ -337,6 +337,7 @@ struct CloudJob {
     // the bucket chain (k_bk_group -> k_bk_sort -> k_bk_emit): groups of gt crop tiles sorted by
     // bucket (PCL idx >> vp.bs) into xyz, one row of bucket starts per group
     int32_t bk;
+    int32_t bkpb;         // bits(input points / PCP_BK_PTS): bs >= bits(nvox) - bkpb (64: unused)
     uint32_t nbkcap;      // buckets the rows and the look-back words are sized for
     uint32_t *brows;      // [ng][nbk + 1] compact position of the group's first item of bucket b
     // pcp_filter_merge_nodes: the cloud's centroids in its own frame beside the merged records
@@ -1200,12 +1201,15 @@ k_bk_group(const JobBatch jobs, uint32_t *__restrict__ res, uint2 *__restrict__ 
         }
     }
     VoxParams p = vox_params_from(tot, mn, mx, J.leaf);
-    // buckets: bs = clamp(bits(nvox) - kBkBits, 0, kBkSubMax), nbk = ceil(nvox / 2^bs)
+    // buckets: bs = clamp(max(bits(nvox) - kBkBits, bits(nvox) - bkpb), 0, kBkSubMax), nbk =
+    // ceil(nvox / 2^bs): ~2^kBkBits buckets, and no more than ~ input points / PCP_BK_PTS (a
+    // sparse cloud -- C5's scans: ~100 points per 2^11 buckets of its box -- fills fewer, fuller
+    // buckets instead of thousands of near-empty blocks)
     bool redo = p.overflow != 0;
     if (tot != 0 && !redo) {
         int bits = 0;
         while (bits < 40 && (1ull << bits) < p.nvox) ++bits;
-        p.bs = (uint32_t)min(max(bits - kBkBits, 0), kBkSubMax);
+        p.bs = (uint32_t)min(max(max(bits - kBkBits, bits - J.bkpb), 0), kBkSubMax);
         const uint64_t nbk = (p.nvox + (1ull << p.bs) - 1) >> p.bs;
         if (nbk > J.nbkcap) redo = true;
         else p.nbk = (uint32_t)nbk;
@@ -1833,8 +1837,16 @@ static bool bucket_geometry(pcp_ctx *ctx, int slot, CloudJob &J, int clouds = 1)
     gt = std::min<uint32_t>(gt, kBkGt);
     const uint32_t ng = (nb + gt - 1) / gt;
     if (ng > (uint32_t)kBkNg) return false;
-    // device: bs = clamp(bits(nvox) - kBkBits, 0, kBkSubMax), nbk = ceil(nvox / 2^bs)
-    const double cap = std::max(std::ldexp(1.0, kBkBits), std::ceil(nv / std::ldexp(1.0, kBkSubMax)));
+    // device: bs = clamp(max(bits(nvox) - kBkBits, bits(nvox) - bkpb), 0, kBkSubMax), nbk =
+    // ceil(nvox / 2^bs) <= 2^min(kBkBits, bkpb), or ceil(nvox / 2^kBkSubMax) where bs is clamped
+    int pb = 64;
+    if (ctx->bk_pts > 0) {
+        const uint64_t tgt = std::max<uint64_t>(J.in.n / (uint64_t)ctx->bk_pts, 1);
+        pb = 0;
+        while ((1ull << pb) < tgt) ++pb;
+    }
+    const double cap = std::max(std::ldexp(1.0, std::min(kBkBits, pb)),
+                                std::ceil(nv / std::ldexp(1.0, kBkSubMax)));
     const uint32_t nbkcap = (uint32_t)std::min<double>(cap, (double)kBkMax);
     CloudBufs &B = ctx->fbuf[slot];
     // rows, and the look-back words of a call's clouds (sized here: enqueue may be capturing)
@@ -1844,6 +1856,7 @@ static bool bucket_geometry(pcp_ctx *ctx, int slot, CloudJob &J, int clouds = 1)
         return false;
     }
     J.bk = 1;
+    J.bkpb = pb;
     J.gt = gt;
     J.ng = ng;
     J.nbkcap = nbkcap;

@@ -370,6 +370,8 @@ struct pcp_ctx {
     pcp::DevBuf bk_stat;                     // the bucket chain's per-bucket words
     int bk_gt = 0;                           // crop tiles per k_bk_group group (PCP_BK_GT; 0: one
                                              // round of blocks)
+    int bk_pts = 512;                        // bucket chain: input points per bucket at least
+                                             // (PCP_BK_PTS; 0: buckets from the voxel count only)
     bool fm_host_out = true;                 // pcp_filter_merge's result sizes stored by its
                                              // kernels into pinned memory (PCP_FM_HOST_OUT)
     int terrain_blocks = 1;                  // block-major terrain copy (PCP_TERRAIN_BLOCKS)
