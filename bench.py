@@ -694,6 +694,13 @@ def run_all(args, dist, world, rank, local, backend):
         out["c4"] = run_c4(args, dist, world, rank, local, backend, ctx=ctx, scene=scene)
     host = _host_cpu()
     cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    if not args.fan_only and rank == 0 and world == 1:
+        # the host-bound chains first, before the CPU baselines below load the host's cores:
+        # configs[4] on this GPU (200 frames of the whole chain through the node cores, the
+        # first and last dumped frames re-run through the oracle chain after the timed frames),
+        # then configs[0] (its one-thread oracle frames after its own timed ones)
+        out["c5"] = run_c5(args, None, 1, 0, local, None, frames=200, check=cpu)
+        out["c1"] = run_c1(args, local, cpu)
     if cpu:
         out["cpu_baseline"] = cpu_baseline_fan(scene.terrain, poses, fan, args.cpu_seconds)
         out["cpu_baseline_mt"] = cpu_baseline_fan(scene.terrain, poses, fan,
@@ -752,11 +759,6 @@ def run_all(args, dist, world, rank, local, backend):
                 kdtree=True)
         out["c3"] = run_filter(args, dist, world, rank, local, backend, embedded=True,
                                cpu=cpu)
-        if rank == 0 and world == 1:
-            out["c1"] = run_c1(args, local, cpu)
-            # configs[4] on this GPU: 200 frames of the whole chain through the node cores,
-            # the first and last dumped frames re-run through the oracle chain
-            out["c5"] = run_c5(args, None, 1, 0, local, None, frames=200, check=cpu)
     ctx.close()
     return out
 
