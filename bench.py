@@ -36,6 +36,12 @@ from pathlib import Path
 
 import numpy as np
 
+# waits poll the completion signals instead of sleeping on an interrupt (the host-bound chains'
+# synchronisations return sooner, profiles/r05_c5_wait_ab.log); set before libpcp's first HIP
+# call, inherited by the ranks and the C5 replay.  PCP_HSA_POLL=0: the runtime's default
+if os.environ.get("PCP_HSA_POLL", "1") != "0":
+    os.environ.setdefault("HSA_ENABLE_INTERRUPT", "0")
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
@@ -930,8 +936,7 @@ def c1_frame_gpu(ctx, scans, nc_lattice=1):
     composes them (pcp_filter_merge_nodes: both filters + the merger, one wait;
     pcp_excavate_area_async: the carve + the area and terrain callbacks, the grid setup left in
     flight on its side stream while the zx120 index and the candidates are built; the scoring
-    settles it; the carve's messages copied from its landing after the zx120 index is enqueued);
-    PCP_C1_CALLS=1: every node callback as its own call (rounds 1-4)."""
+    settles it); PCP_C1_CALLS=1: every node callback as its own call (rounds 1-4)."""
     from pointcloud_processor_amd import _abi
 
     zx = np.array([0.4, 0.5, 3.5, -math.pi / 6, 0.0])   # getZX120Position on zx120/base_link
@@ -948,13 +953,11 @@ def c1_frame_gpu(ctx, scans, nc_lattice=1):
         return cand.shape[0], int(rep.best_idx), tot, cand, nc
     merged, filtered, _ = ctx.filter_merge_nodes(scans, [C1_BOX, C1_BOX], C1_LEAF, C1_TFS,
                                                  [(255, 0, 0), (0, 0, 255)])
-    # the carve's two messages left where they landed until the zx120 index is enqueued, then
-    # copied out (PCP_C1_LANDED=0: copied by the call, as before)
-    landed = os.environ.get("PCP_C1_LANDED", "1") == "1"
-    terr, area, _, bbox, cap = ctx.excavate_area_async(merged, C1_ZX_BASE, landed=landed)
+    # (the carve's messages copied out by the call, split over libpcp's copy threads: reading
+    # them from the landing afterwards, one numpy copy each, measured no faster --
+    # profiles/r05_c1_landed_ab.log, r05_c1_poll_ab.log)
+    terr, area, _, bbox, cap = ctx.excavate_area_async(merged, C1_ZX_BASE)
     ctx.set_aux_cloud(filtered[1])
-    if landed:
-        terr, area = terr.copy(), area.copy()   # /excavated_terrain, /excavation_area
     cand = ctx.generate_candidates(bbox, params, zx)[:1]   # ONE candidate pose is scored
     # fresh flags (:259) for the setup's capacity; the scoring settles the count first
     tot, _, rep = ctx.score_poses(cand, zx, params, np.zeros(max(cap, 1), np.uint8))
