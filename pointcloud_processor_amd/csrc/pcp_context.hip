@@ -335,11 +335,12 @@ k_scan_tile_sums(const uint32_t *__restrict__ in, uint64_t n, uint32_t *__restri
 // scans each tile locally (thread owns kScanItems consecutive items), adds tile offset;
 // out2 (may be null, may be `in` itself: every thread reads its own items before it writes
 // them) receives a second copy of out[0 .. n)
-__global__ void __launch_bounds__(kScanThreads)
-k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
-             uint32_t *__restrict__ out, uint32_t *out2, int zero2, uint16_t *__restrict__ preset16) {
+__device__ __forceinline__ void scan_tile(const uint32_t *in, uint64_t n, uint32_t off,
+                                          uint32_t *__restrict__ out, uint32_t *out2, int zero2,
+                                          uint16_t *__restrict__ preset16, uint32_t tile,
+                                          bool last_tile) {
     __shared__ uint32_t lds4[4];
-    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+    const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
     // a thread's 8 items whole: two 16-byte loads and stores instead of 8 single words at a
     // 32-byte lane stride (4x the cache-line visits per wave) -- when the arrays are 16-byte
     // aligned (item offsets are multiples of 8; the recursion's partial-sum arrays may not be)
@@ -364,7 +365,7 @@ k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) s += v[i];
     uint32_t tot;
-    uint32_t run = block_excl_scan(s, lds4, &tot) + (offs ? offs[blockIdx.x] : 0u);
+    uint32_t run = block_excl_scan(s, lds4, &tot) + off;
     uint32_t o[kScanItems];
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
@@ -394,7 +395,25 @@ k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
         for (int i = 0; i < kScanItems; ++i)
             if (base + i < n) preset16[base + i] = 0x00FFu;
     // out[n] written by the last tile's last thread
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = run;
+    if (last_tile && threadIdx.x == kScanThreads - 1) out[n] = run;
+}
+
+__global__ void __launch_bounds__(kScanThreads)
+k_scan_tiles(const uint32_t *in, uint64_t n, const uint32_t *__restrict__ offs,
+             uint32_t *__restrict__ out, uint32_t *out2, int zero2, uint16_t *__restrict__ preset16) {
+    scan_tile(in, n, offs ? offs[blockIdx.x] : 0u, out, out2, zero2, preset16, blockIdx.x,
+              blockIdx.x == gridDim.x - 1);
+}
+
+// two one-tile scans in one launch (block 0: a, block 1: b; a grid index's pair of builds)
+struct ScanOne {
+    const uint32_t *in;
+    uint64_t n;
+    uint32_t *out, *out2;
+};
+__global__ void __launch_bounds__(kScanThreads) k_scan_pair(ScanOne a, ScanOne b, int zero2) {
+    const ScanOne &q = blockIdx.x ? b : a;
+    scan_tile(q.in, q.n, 0u, q.out, q.out2, zero2, nullptr, 0u, true);
 }
 
 // one-pass exclusive scan: tiles take tickets in arrival order (a tile waits only for tiles
@@ -533,6 +552,22 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
     return PCP_OK;
 }
 
+// exclusive_scan_u32 of two arrays (out2 / zero2 as there, no preset); two one-tile scans
+// (a message-sized cloud's pair of grids) are one launch
+int exclusive_scan_u32_pair(pcp_ctx *ctx, const uint32_t *in_a, uint32_t *out_a, uint64_t n_a,
+                            uint32_t *out2_a, const uint32_t *in_b, uint32_t *out_b, uint64_t n_b,
+                            uint32_t *out2_b, void *tmp, bool zero2) {
+    if (n_a && n_b && n_a <= (uint64_t)kScanTile && n_b <= (uint64_t)kScanTile && ctx->scan_pair) {
+        hipLaunchKernelGGL(k_scan_pair, dim3(2), dim3(kScanThreads), 0, ctx->stream,
+                           ScanOne{in_a, n_a, out_a, out2_a}, ScanOne{in_b, n_b, out_b, out2_b},
+                           zero2 ? 1 : 0);
+        PCP_CHECK_LAUNCH(ctx);
+        return PCP_OK;
+    }
+    if (int rc = exclusive_scan_u32(ctx, in_a, out_a, n_a, tmp, out2_a, zero2)) return rc;
+    return exclusive_scan_u32(ctx, in_b, out_b, n_b, tmp, out2_b, zero2);
+}
+
 }  // namespace pcp
 
 using namespace pcp;
@@ -591,6 +626,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *fo = std::getenv("PCP_FM_HOST_OUT")) ctx->fm_host_out = std::atoi(fo) != 0;
     if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff);
     if (const char *bg = std::getenv("PCP_BK_GT")) ctx->bk_gt = std::atoi(bg);
+    if (const char *sp = std::getenv("PCP_SCAN_PAIR")) ctx->scan_pair = std::atoi(sp) != 0;
     if (const char *bp = std::getenv("PCP_BK_PTS")) ctx->bk_pts = std::atoi(bp);
     if (const char *zc = std::getenv("PCP_ZC_IN")) ctx->zc_in = std::atoi(zc) != 0;
     if (const char *ck = std::getenv("PCP_COPY_KERNEL")) ctx->copy_kernel = std::atoi(ck) != 0;

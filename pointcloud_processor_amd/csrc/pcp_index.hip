@@ -652,14 +652,11 @@ int build_index_pair(pcp_ctx *ctx, GridIndex &ga, double ra, GridIndex &gb, doub
     PCP_HIP(ctx, gb.start.ensure(cbb));
     const uint64_t ncm = std::max(nca, ncb);
     PCP_HIP(ctx, ctx->scratch[4].ensure(scan_tmp_bytes(ncm) + (ncm + 1) * sizeof(uint32_t)));
-    if (int rc = exclusive_scan_u32(ctx, cnt_a, ga.start.as<uint32_t>(), nca, ctx->scratch[4].p,
-                                    cnt_a, true))
+    if (int rc = exclusive_scan_u32_pair(ctx, cnt_a, ga.start.as<uint32_t>(), nca, cnt_a, cnt_b,
+                                         gb.start.as<uint32_t>(), ncb, cnt_b, ctx->scratch[4].p,
+                                         true))
         return rc;
-    ctx->cell_cnt_dirty = false;
-    if (int rc = exclusive_scan_u32(ctx, cnt_b, gb.start.as<uint32_t>(), ncb, ctx->scratch[4].p,
-                                    cnt_b, true))
-        return rc;
-    ctx->cell_cnt2_dirty = false;
+    ctx->cell_cnt_dirty = ctx->cell_cnt2_dirty = false;
     PCP_HIP(ctx, ga.pts.ensure((size_t)nfin * sizeof(float4)));
     PCP_HIP(ctx, gb.pts.ensure((size_t)nfin * sizeof(float4)));
     hipLaunchKernelGGL(k_cell_place2, dim3(gridn), dim3(kThreads), 0, st,

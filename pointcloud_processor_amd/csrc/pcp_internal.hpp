@@ -370,6 +370,8 @@ struct pcp_ctx {
     pcp::DevBuf bk_stat;                     // the bucket chain's per-bucket words
     int bk_gt = 0;                           // crop tiles per k_bk_group group (PCP_BK_GT; 0: one
                                              // round of blocks)
+    bool scan_pair = true;                   // a grid pair's two one-tile scans in one launch
+                                             // (PCP_SCAN_PAIR)
     int bk_pts = 512;                        // bucket chain: input points per bucket at least
                                              // (PCP_BK_PTS; 0: buckets from the voxel count only)
     bool fm_host_out = true;                 // pcp_filter_merge's result sizes stored by its
@@ -472,6 +474,10 @@ size_t scan_tmp_bytes(uint64_t n);
 // preset16 (nullable): n halfwords set to 0x00FF by the same pass (the sparse z bands' preset)
 int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, void *tmp,
                        uint32_t *out2 = nullptr, bool zero2 = false, uint16_t *preset16 = nullptr);
+// two such scans (tmp sized for the larger); two one-tile ones are a single launch
+int exclusive_scan_u32_pair(pcp_ctx *ctx, const uint32_t *in_a, uint32_t *out_a, uint64_t n_a,
+                            uint32_t *out2_a, const uint32_t *in_b, uint32_t *out_b, uint64_t n_b,
+                            uint32_t *out2_b, void *tmp, bool zero2);
 
 // fan query up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip): device results
 // in flight on return, the caller synchronizes.  n > 0.
