@@ -541,22 +541,31 @@ static int excavate_impl(pcp_ctx *ctx, const pcp_cloud_view *in, const pcp_excav
     // (DMA'd, not read in place: three passes below re-read the records, which over the host
     // link cost more than the copy -- k_keep_emit 16 -> 36 us measured)
     const unsigned char *raw = nullptr;
+    unsigned char *raw_copy = nullptr;
     if (n) {
         const size_t raw_b = n * (size_t)in->point_step;
         PCP_HIP(ctx, ctx->stage.ensure(raw_b));
         // composed (xl): a view into the merger's landing (pcp_filter_merge_landed) is pinned,
-        // device-readable memory -- copied by the device, no host staging copy (the non-composed
-        // call may regrow that landing for its own records before the copy ran: staged)
+        // device-readable memory -- copied into ctx->stage by the index's extraction on its way
+        // through (no copy launch, no host staging copy; the non-composed call may regrow that
+        // landing for its own records before the copy ran: staged)
         const uintptr_t d0 = reinterpret_cast<uintptr_t>(in->data),
                         l0 = reinterpret_cast<uintptr_t>(ctx->tc_host.p);
         if (xl && ctx->tc_host.p && d0 >= l0 && d0 + raw_b <= l0 + ctx->tc_host.cap) {
-            if (int rc0 = copy_pinned_async(ctx, ctx->stage.p, in->data, raw_b, st)) return rc0;
-        } else if (int rc0 = upload_async(ctx, ctx->stage.p, in->data, raw_b, st)) {
-            return rc0;
+            raw = static_cast<const unsigned char *>(in->data);
+            raw_copy = ctx->stage.as<unsigned char>();
+            if (!ctx->carve_fuse_copy) {   // (A/B: the copy launch first)
+                if (int rc0 = copy_pinned_async(ctx, raw_copy, raw, raw_b, st)) return rc0;
+                raw = raw_copy;
+                raw_copy = nullptr;
+            }
+        } else {
+            if (int rc0 = upload_async(ctx, ctx->stage.p, in->data, raw_b, st)) return rc0;
+            raw = ctx->stage.as<unsigned char>();
         }
-        raw = ctx->stage.as<unsigned char>();
     }
-    if ((rc = build_index(ctx, ctx->carve, *in, p->terrain_search_radius, false, false, &raw)))
+    if ((rc = build_index(ctx, ctx->carve, *in, p->terrain_search_radius, false, false, &raw,
+                          raw_copy)))
         return rc;
     const GridView g = ctx->carve.view();
     CarveArgs a{};

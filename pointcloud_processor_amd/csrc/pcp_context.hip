@@ -627,6 +627,7 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *ff = std::getenv("PCP_FM_FAST")) ctx->fm_fast = std::atoi(ff);
     if (const char *bg = std::getenv("PCP_BK_GT")) ctx->bk_gt = std::atoi(bg);
     if (const char *sp = std::getenv("PCP_SCAN_PAIR")) ctx->scan_pair = std::atoi(sp) != 0;
+    if (const char *fc = std::getenv("PCP_CARVE_FUSE_COPY")) ctx->carve_fuse_copy = std::atoi(fc) != 0;
     if (const char *bp = std::getenv("PCP_BK_PTS")) ctx->bk_pts = std::atoi(bp);
     if (const char *zc = std::getenv("PCP_ZC_IN")) ctx->zc_in = std::atoi(zc) != 0;
     if (const char *ck = std::getenv("PCP_COPY_KERNEL")) ctx->copy_kernel = std::atoi(ck) != 0;

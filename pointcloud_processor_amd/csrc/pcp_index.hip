@@ -220,10 +220,23 @@ __device__ __forceinline__ void count_ranked(const CellMap &m, float x, float y,
 __global__ void __launch_bounds__(kThreads)
 k_extract_count(const unsigned char *__restrict__ raw, uint64_t n, uint32_t step, uint32_t ox,
                 uint32_t oy, uint32_t oz, CellMap m, float4 *__restrict__ xyz,
-                uint32_t *__restrict__ count, uint2 *__restrict__ cr) {
+                uint32_t *__restrict__ count, uint2 *__restrict__ cr,
+                unsigned char *__restrict__ raw_copy) {
     const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (i >= n) return;   // (whole waves: the peer masks below see only live lanes)
     const unsigned char *p = raw + i * step;
+    if (raw_copy) {   // the record into device memory on the way (step: 16-byte multiple <= 64)
+        uint4 r[4];
+        const uint32_t nq = step >> 4;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (k < nq) r[k] = reinterpret_cast<const uint4 *>(p)[k];
+        unsigned char *d = raw_copy + i * step;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+            if (k < nq) reinterpret_cast<uint4 *>(d)[k] = r[k];
+        p = d;   // (this thread's own stores: x, y, z read back from them)
+    }
     const float x = ld_f32(p, ox), y = ld_f32(p, oy), z = ld_f32(p, oz);
     const bool fin = isfinite(x) && isfinite(y) && isfinite(z);
     xyz[i] = make_float4(x, y, z, __uint_as_float(fin ? (uint32_t)i : 0xFFFFFFFFu));
@@ -670,7 +683,7 @@ int build_index_pair(pcp_ctx *ctx, GridIndex &ga, double ra, GridIndex &gb, doub
 }
 
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q, bool zsort,
-                bool occ, const unsigned char **raw_io) {
+                bool occ, const unsigned char **raw_io, unsigned char *raw_copy) {
     const uint64_t n = v.n;
     hipStream_t st = ctx->stream;
     // the query kernels address points and cells with 32-bit byte offsets (pcp_stencil.hpp)
@@ -705,7 +718,17 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
         if (int rc0 = upload_async(ctx, ctx->stage.p, v.data, raw_bytes, st)) return rc0;
         raw = ctx->stage.as<unsigned char>();
     }
-    if (raw_io) *raw_io = raw;
+    // raw_copy: fused into the extraction (message-sized clouds, 16-byte records), else a
+    // device copy first
+    const bool host_bb = n <= kHostBboxMax;
+    const bool fuse_copy = raw_copy && host_bb && n && (v.point_step & 15u) == 0 &&
+                           v.point_step <= 64 &&
+                           ((reinterpret_cast<uintptr_t>(raw) | reinterpret_cast<uintptr_t>(raw_copy)) & 15u) == 0;
+    if (raw_copy && n && !fuse_copy) {
+        if (int rc0 = copy_pinned_async(ctx, raw_copy, raw, raw_bytes, st)) return rc0;
+        raw = raw_copy;
+    }
+    if (raw_io) *raw_io = raw_copy && n ? raw_copy : raw;
     // the extraction is the index's only reader of the raw bytes
     auto release_raw = [&]() {
         if (pinned && !raw_io) pin_release(ctx, st);
@@ -722,7 +745,6 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     // a message-sized cloud: the grid geometry from the host's copy of the same bytes (the
     // same float min / max over the finite points, order-free) -- no round trip through the
     // stream; the extraction is launched below, fused with the cell count
-    const bool host_bb = n <= kHostBboxMax;
     if (host_bb) {
         host_bbox(v, bb_h, nfin);
     } else {
@@ -741,6 +763,9 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     g.r_q = r_q;
     g.n_pts = nfin;
     if (nfin == 0) {   // a tree over zero valid points: never returns neighbours
+        // (no extraction to carry the copy the caller reads from)
+        if (fuse_copy)
+            if (int rc0 = copy_pinned_async(ctx, raw_copy, raw, raw_bytes, st)) return rc0;
         release_raw();
         g.c = 1.0;
         g.nx = g.ny = g.nz = 1;
@@ -781,7 +806,8 @@ int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
     if (host_bb) {   // one pass over the raw records: extraction, cell, slot
         hipLaunchKernelGGL(k_extract_count, dim3(gridn), dim3(kThreads), 0, st, raw, n,
                            v.point_step, v.off_x, v.off_y, v.off_z, m,
-                           ctx->scratch[0].as<float4>(), cnt, cr);
+                           ctx->scratch[0].as<float4>(), cnt, cr,
+                           fuse_copy ? raw_copy : (unsigned char *)nullptr);
         PCP_CHECK_LAUNCH(ctx);
         release_raw();
     } else {

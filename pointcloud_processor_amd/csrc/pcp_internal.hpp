@@ -370,6 +370,8 @@ struct pcp_ctx {
     pcp::DevBuf bk_stat;                     // the bucket chain's per-bucket words
     int bk_gt = 0;                           // crop tiles per k_bk_group group (PCP_BK_GT; 0: one
                                              // round of blocks)
+    bool carve_fuse_copy = true;             // the composed carve's records copied by its
+                                             // index's extraction (PCP_CARVE_FUSE_COPY)
     bool scan_pair = true;                   // a grid pair's two one-tile scans in one launch
                                              // (PCP_SCAN_PAIR)
     int bk_pts = 512;                        // bucket chain: input points per bucket at least
@@ -445,9 +447,13 @@ struct KernelTimer {
 // previous build's, or a caller's staging); on return *raw_io = where the bytes were read.  A
 // message-sized cloud is read in place from the pinned ring (pin_stage): without raw_io the
 // slot is released behind the extraction; with raw_io the caller releases it (pin_release)
-// after its own last reader.  Larger clouds are DMA'd into ctx->stage.
+// after its own last reader.  Larger clouds are DMA'd into ctx->stage.  raw_copy (nullable,
+// with raw_io: *raw_io then pinned, device-readable memory): the records are also copied there
+// -- by the extraction itself where it can (16-byte multiples) -- and *raw_io = raw_copy on
+// return, so the caller's later kernels read device memory (the composed carve)
 int build_index(pcp_ctx *ctx, GridIndex &g, const pcp_cloud_view &v, double r_q,
-                bool zsort = true, bool occ = true, const unsigned char **raw_io = nullptr);
+                bool zsort = true, bool occ = true, const unsigned char **raw_io = nullptr,
+                unsigned char *raw_copy = nullptr);
 // two order-free indices (no z order, no occupancy bits) of one message-sized cloud from one
 // pass over its raw records, plus the caller's per-point preparation (prep_pts: (x, y, z, 0) by
 // input index; prep_nrm: NaN normals of the non-finite points; both nullable).  *paired false
