@@ -5,7 +5,8 @@
 // (the kernels read it there, pin_stage / upload_*), and each result out of its pinned landing
 // into the caller's array.  One core copies ~25 GB/s, so a 60k-point scan (960 KB) costs ~40 us
 // on the critical path between callbacks.  Copies of at least kSplitMin bytes are split into
-// kParts parts: the calling thread copies the first, helper threads the others.  Helpers spin on
+// kParts parts, claimed by the calling thread and the helper threads alike (a helper that is
+// asleep or preempted leaves its share to the others instead of stalling the copy).  Helpers spin on
 // a job generation for a short while after each job (a streaming chain's next copy is ~100 us
 // away) and then sleep on a condition variable (a 10 Hz node's helpers sleep between frames).
 // PCP_COPY_THREADS=0 turns the helpers off (plain memcpy), N sets their count (default 3).
@@ -26,10 +27,10 @@ namespace {
 constexpr size_t kSplitMin = 256u << 10;
 constexpr int kMaxHelpers = 7;
 constexpr auto kSpin = std::chrono::microseconds(300);
-// every part of a split copy is non-empty, so every helper takes part in every job exactly once
-// (its one decrement of `pending` per job generation is what the caller waits for).  With k
-// parts of per = ceil(n / k) rounded up to 4 KiB < n / k + 4096 bytes, the last part starts at
-// (k - 1) per < n whenever n > k (k - 1) 4096 (2 k 4096 did not imply it)
+// the parts of a job are claimed (one CAS on {job, next part}), the caller included, and each
+// claimed part decrements `pending` once, which the caller waits for.  Every part is non-empty:
+// with k parts of per = ceil(n / k) rounded up to 4 KiB < n / k + 4096 bytes, the last part
+// starts at (k - 1) per < n whenever n > k (k - 1) 4096 (2 k 4096 did not imply it)
 static_assert(kSplitMin > (size_t)(kMaxHelpers + 1) * kMaxHelpers * 4096, "parts must be non-empty");
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
@@ -63,18 +64,39 @@ struct CopyPool {
             part_[i] = Part{static_cast<char *>(dst) + o, static_cast<const char *>(src) + o, e - o};
             if (e > o) used = i + 1;
         }
-        pending_.store(used - 1, std::memory_order_relaxed);
+        used_.store(used, std::memory_order_relaxed);
+        pending_.store(used, std::memory_order_relaxed);
+        const uint64_t g = ++job_;
+        claim_.store(g << 32, std::memory_order_release);   // publishes parts and used_
         {
             std::lock_guard<std::mutex> l(mu_);
-            gen_.fetch_add(1, std::memory_order_release);
+            gen_.store(g, std::memory_order_release);
         }
         cv_.notify_all();
-        std::memcpy(part_[0].d, part_[0].s, part_[0].n);
+        // the parts are claimed, not assigned: the caller takes whatever the helpers have not
+        // started, so a helper that is asleep or preempted (a busy host's timeslice: ms) delays
+        // nothing it has not begun
+        work(g);
         while (pending_.load(std::memory_order_acquire) > 0) cpu_relax();
     }
 
    private:
-    void run(int id) {
+    // copy parts of job g until none is left unclaimed (a claim is one CAS on {job, next part})
+    void work(uint64_t g) {
+        uint64_t c = claim_.load(std::memory_order_acquire);
+        for (;;) {
+            if ((c >> 32) != g || (uint32_t)c >= (uint32_t)used_.load(std::memory_order_relaxed))
+                return;
+            if (!claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel,
+                                              std::memory_order_acquire))
+                continue;
+            const Part p = part_[(uint32_t)c];
+            std::memcpy(p.d, p.s, p.n);
+            pending_.fetch_sub(1, std::memory_order_acq_rel);
+            c = claim_.load(std::memory_order_acquire);
+        }
+    }
+    void run(int) {
         uint64_t seen = 0;
         for (;;) {
             auto t0 = std::chrono::steady_clock::now();
@@ -94,11 +116,7 @@ struct CopyPool {
             }
             if (stop_.load(std::memory_order_acquire)) return;
             seen = g;
-            const Part p = part_[id];
-            if (p.n) {
-                std::memcpy(p.d, p.s, p.n);
-                pending_.fetch_sub(1, std::memory_order_acq_rel);
-            }
+            work(g);   // (a late helper finds the job's parts claimed and goes back to waiting)
         }
     }
     std::vector<std::thread> th_;
@@ -107,6 +125,9 @@ struct CopyPool {
     std::atomic<uint64_t> gen_{0};
     std::atomic<int> pending_{0};
     std::atomic<bool> stop_{false};
+    std::atomic<uint64_t> claim_{0};   // job << 32 | next unclaimed part
+    uint64_t job_ = 0;                 // (the caller's; one copy at a time per pool)
+    std::atomic<int> used_{0};
     Part part_[kMaxHelpers + 1];
 };
 
