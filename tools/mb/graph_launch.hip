@@ -8,6 +8,7 @@
 // Prints one JSON line per mode: us per iteration (host wall, sync included).
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/mb/graph_launch tools/mb/graph_launch.hip
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
