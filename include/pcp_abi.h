@@ -437,6 +437,24 @@ int pcp_raycast_fan_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
                               uint32_t *blocked_all, uint64_t *units, int64_t *best_idx,
                               double *collective_ms);
 
+/* runOptimization's scoring for one rank of N processes (virtual_lidar.cpp:460-519; every
+ * rank calls it with the same p_total, zx120 pose, parameters and cells): this rank's poses5[0 ..
+ * n) -- global poses [lo, lo + n) of p_total -- scored as pcp_score_poses scores them, then ONE
+ * ncclAllReduce(ncclUint64, ncclMax) on the context's stream over [p_total totals (IEEE bits:
+ * totals are >= +0) | p_total covered counts | 3 x n_cells newest-pose flag keys | 1 health
+ * word] (the vector pcp_multi_score_poses reduces), then on every rank: the stale GridCell flags
+ * resolved from the newest pose overall (:480-519, cell_flags in/out as pcp_score_poses), the
+ * strict-'>' argmax over all totals (:471-474) and the colour statistics into *rep.
+ * total_all / covered_all (host, p_total entries, nullable): every pose's total and covered
+ * count.  collective_ms (nullable): the all-reduce between two events on the stream.
+ * A rank whose work before the collective fails still runs it with a poisoned health word: it
+ * returns its own error, every other rank PCP_E_STATE (nobody is left blocked in RCCL).
+ * Results are identical to pcp_score_poses over all p_total poses on one context. */
+int pcp_score_poses_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                              const double zx120_pose5[5], const pcp_vl_params *p, uint64_t lo,
+                              uint64_t p_total, uint8_t *cell_flags, double *total_all,
+                              int32_t *covered_all, pcp_vl_report *rep, double *collective_ms);
+
 /* ---- one process, n GPUs: the pose search sharded over devices ------ */
 /* pcp_multi_create(n_dev, devices, &m): one context per device (devices NULL: 0 .. n_dev-1)
  * and ONE RCCL communicator over them (ncclCommInitAll).  Poses are partitioned contiguously

@@ -159,6 +159,9 @@ _SIGS = [
     ("pcp_raycast_fan_allreduce", C.c_int, [_P, _P, C.c_uint64, C.POINTER(FanParams), C.c_uint64,
                                             C.c_uint64, _P, _P, C.POINTER(C.c_int64),
                                             C.POINTER(C.c_double)]),
+    ("pcp_score_poses_allreduce", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams),
+                                            C.c_uint64, C.c_uint64, _P, _P, _P,
+                                            C.POINTER(VlReport), C.POINTER(C.c_double)]),
     ("pcp_stream_create", C.c_int, [_P, C.POINTER(_P)]),
     ("pcp_stream_destroy", C.c_int, [_P, _P]),
     ("pcp_step_table", C.c_int, [C.c_double, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
@@ -820,6 +823,31 @@ class Context:
             _ptr(blocked_all), _ptr(units), C.byref(best), C.byref(ms) if timed else None),
             "pcp_raycast_fan_allreduce")
         return best.value, (ms.value if timed else None)
+
+    def score_poses_allreduce(self, poses5: np.ndarray, zx120_pose5: np.ndarray,
+                              params: VlParams, lo: int, p_total: int, cell_flags: np.ndarray,
+                              tot_all: np.ndarray | None, cov_all: np.ndarray | None,
+                              rep: "VlReport", timed: bool = False):
+        """pcp_score_poses_allreduce: runOptimization's scoring of this rank's poses [lo, lo + P)
+        of p_total, ONE ncclAllReduce(MAX) over libpcp's own communicator (comm_init_rank), the
+        stale flags, argmax (rep.best_idx, global) and colour statistics on every rank.
+        tot_all float64 / cov_all int32 ([>= p_total], or None) receive every pose's total and
+        covered count; cell_flags updated in place.  -> collective ms (timed) or None."""
+        P = poses5.shape[0]
+        if (poses5.dtype != np.float64 or not poses5.flags.c_contiguous or poses5.ndim != 2
+                or zx120_pose5.dtype != np.float64 or not zx120_pose5.flags.c_contiguous
+                or cell_flags.dtype != np.uint8 or not cell_flags.flags.c_contiguous
+                or (tot_all is not None and (tot_all.dtype != np.float64
+                                             or tot_all.shape[0] < p_total))
+                or (cov_all is not None and (cov_all.dtype != np.int32
+                                             or cov_all.shape[0] < p_total))):
+            raise ValueError("score_poses_allreduce: bad array types or sizes")
+        ms = C.c_double()
+        self._check(self.lib.pcp_score_poses_allreduce(
+            self.h, poses5.ctypes.data if P else None, P, zx120_pose5.ctypes.data,
+            C.byref(params), lo, p_total, cell_flags.ctypes.data, _ptr(tot_all), _ptr(cov_all),
+            C.byref(rep), C.byref(ms) if timed else None), "pcp_score_poses_allreduce")
+        return ms.value if timed else None
 
     def raycast_fan(self, poses5: np.ndarray, fan: FanParams, want_first_hit=False):
         poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)

@@ -12,8 +12,10 @@
 
 #include <dlfcn.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <string>
 
 #include "pcp_internal.hpp"
 
@@ -44,13 +46,38 @@ void comm_release(pcp_ctx *ctx) {
 
 static_assert(sizeof(ncclUniqueId) == PCP_COMM_ID_BYTES, "ncclUniqueId size");
 
+// Every rank reaches the collective, whatever happened before it.  RCCL has no timeout: a rank
+// that returned early would leave the others blocked inside ncclAllReduce (ncclCommAbort frees
+// only the calling rank's resources; the peers would wait until the launcher kills them).  So
+// the reduced vector carries one HEALTH word at its end: a healthy rank writes the reduction's
+// identity there (MIN: ~0, MAX: 0), a rank whose work before the collective failed fills its
+// whole vector with the absorbing value (MIN: 0, MAX: ~0) and still runs the collective.
+// Afterwards every rank sees the failure in that word and returns PCP_E_STATE; the failing
+// rank returns its own error.  Only when even the poison cannot be enqueued (no vector, a
+// dead stream) does the rank abort its communicator, and the launcher's kill-on-failure is
+// then what releases the others.
+static void comm_drop(pcp_ctx *ctx) {
+    (void)ncclCommAbort(static_cast<ncclComm_t>(ctx->comm));
+    ctx->comm = nullptr;
+    ctx->comm_nranks = 0;
+    ctx->comm_rank = 0;
+}
+
+// the failed rank's vector: count words of the absorbing value, on the context's stream
+static bool comm_poison(pcp_ctx *ctx, size_t count, bool is_max) {
+    if (hipSetDevice(ctx->device) != hipSuccess) return false;
+    if (ctx->comm_keys.ensure(count * 8 + 64) != hipSuccess) return false;
+    return hipMemsetAsync(ctx->comm_keys.p, is_max ? 0xff : 0x00, count * 8, ctx->stream) ==
+           hipSuccess;
+}
+
 // the shard's fans and its keys on the context's stream, up to (not including) the collective
 static int fan_allreduce_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n,
                                  const pcp_fan_params *fan, uint64_t lo, uint32_t P,
                                  double *collective_ms, const unsigned long long **units_out) {
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    PCP_HIP(ctx, ctx->comm_keys.ensure((size_t)P * 8 + 64));
+    PCP_HIP(ctx, ctx->comm_keys.ensure((size_t)(P + 1) * 8 + 64));
     const uint32_t *blocked_d = nullptr;
     if (n) {
         FanEnq o;   // device results (no host landing): the keys kernel reads them
@@ -59,7 +86,8 @@ static int fan_allreduce_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n,
         *units_out = o.units_d;
     }
     unsigned long long *keys = ctx->comm_keys.as<unsigned long long>();
-    launch_fan_keys(st, blocked_d, (uint32_t)lo, (uint32_t)n, P, keys);   // ~0 elsewhere
+    // ~0 in the other ranks' slots and in the health word (slot P: no pose of any shard)
+    launch_fan_keys(st, blocked_d, (uint32_t)lo, (uint32_t)n, P + 1, keys);
     PCP_CHECK_LAUNCH(ctx);
     if (collective_ms)
         for (hipEvent_t &e : ctx->comm_ev)
@@ -128,37 +156,48 @@ int pcp_raycast_fan_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
                                          "(pcp_comm_init_rank)");
     if (!fan || (n && !poses5))
         return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan_allreduce: null argument");
-    if (lo + n > p_total || p_total > 65535u * 64u)
-        return set_err(ctx, PCP_E_INVALID,
-                       "pcp_raycast_fan_allreduce: shard [%llu, %llu) of %llu poses",
-                       (unsigned long long)lo, (unsigned long long)(lo + n),
+    // (every rank sees the same p_total: a bad one fails on every rank and none reduces)
+    if (p_total > 65535u * 64u)
+        return set_err(ctx, PCP_E_INVALID, "pcp_raycast_fan_allreduce: %llu poses",
                        (unsigned long long)p_total);
-    if (p_total == 0) return PCP_OK;   // every rank sees the same p_total: no rank reduces
+    if (p_total == 0) return PCP_OK;
     const uint32_t P = (uint32_t)p_total;
     const unsigned long long *units_d = nullptr;
-    // everything before the collective: a failure here would leave the other ranks blocked in
-    // ncclAllReduce with no timeout, so it aborts the communicator (their collective then fails
-    // instead of hanging) and marks this context's communicator gone
-    if (int rc = fan_allreduce_enqueue(ctx, poses5, n, fan, lo, P, collective_ms, &units_d)) {
-        (void)ncclCommAbort(static_cast<ncclComm_t>(ctx->comm));
-        ctx->comm = nullptr;
-        ctx->comm_nranks = 0;
-        ctx->comm_rank = 0;
-        return rc;
+    // everything before the collective; a failure poisons this rank's vector (health word 0)
+    int rc = PCP_OK;
+    if (lo + n > p_total)
+        rc = set_err(ctx, PCP_E_INVALID,
+                     "pcp_raycast_fan_allreduce: shard [%llu, %llu) of %llu poses",
+                     (unsigned long long)lo, (unsigned long long)(lo + n),
+                     (unsigned long long)p_total);
+    else
+        rc = fan_allreduce_enqueue(ctx, poses5, n, fan, lo, P, collective_ms, &units_d);
+    if (rc) {
+        const std::string why = ctx->err;
+        if (!comm_poison(ctx, (size_t)P + 1, false)) {
+            comm_drop(ctx);
+            return set_err(ctx, rc, "%s", why.c_str());
+        }
+        collective_ms = nullptr;
+        units = nullptr;
     }
     hipStream_t st = ctx->stream;
     unsigned long long *keys = ctx->comm_keys.as<unsigned long long>();
-    PCP_NCCL(ctx, ncclAllReduce(keys, keys, P, ncclUint64, ncclMin,
+    PCP_NCCL(ctx, ncclAllReduce(keys, keys, (size_t)P + 1, ncclUint64, ncclMin,
                                 static_cast<ncclComm_t>(ctx->comm), st));   // the one collective
     if (collective_ms) PCP_HIP(ctx, hipEventRecord(ctx->comm_ev[1], st));
-    // the reduced vector and this shard's units into one pinned block
-    PCP_HIP(ctx, ctx->comm_host.ensure((size_t)(P + n) * 8 + 64));
+    // the reduced vector (+ health word) and this shard's units into one pinned block
+    PCP_HIP(ctx, ctx->comm_host.ensure((size_t)(P + 1 + n) * 8 + 64));
     unsigned long long *kh = ctx->comm_host.as<unsigned long long>();
-    PCP_HIP(ctx, hipMemcpyAsync(kh, keys, (size_t)P * 8, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipMemcpyAsync(kh, keys, (size_t)(P + 1) * 8, hipMemcpyDeviceToHost, st));
     if (n && units)
-        PCP_HIP(ctx, hipMemcpyAsync(kh + P, units_d, n * 8, hipMemcpyDeviceToHost, st));
+        PCP_HIP(ctx, hipMemcpyAsync(kh + P + 1, units_d, n * 8, hipMemcpyDeviceToHost, st));
     PCP_HIP(ctx, hipStreamSynchronize(st));
     prof_resolve(ctx);
+    if (rc) return rc;   // (ctx->err: this rank's own failure, set before the poison)
+    if (kh[P] != ~0ull)
+        return set_err(ctx, PCP_E_STATE, "pcp_raycast_fan_allreduce: a peer rank failed before "
+                                         "the collective (health word poisoned)");
     if (collective_ms) {
         float ms = 0.0f;
         PCP_HIP(ctx, hipEventElapsedTime(&ms, ctx->comm_ev[0], ctx->comm_ev[1]));
@@ -170,12 +209,129 @@ int pcp_raycast_fan_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
         kmin = kh[i] < kmin ? kh[i] : kmin;
     }
     if (units)
-        for (uint64_t i = 0; i < n; ++i) units[i] = kh[P + i];
+        for (uint64_t i = 0; i < n; ++i) units[i] = kh[P + 1 + i];
     for (uint32_t i = 0; i < P; ++i)   // a slot no rank wrote: the ranks' shards disagree
         if (kh[i] == ~0ull)
             return set_err(ctx, PCP_E_STATE, "pcp_raycast_fan_allreduce: pose %u has no rank "
                                              "(shards do not cover [0, p_total))", i);
     if (best_idx) *best_idx = (int64_t)(kmin & 0xffffffffull);
+    return PCP_OK;
+}
+
+// runOptimization's scoring for N processes (virtual_lidar.cpp:460-519): this rank's shard
+// scored as pcp_multi_score_poses scores a rank's (k_score_cells + k_row_sum, then the keys:
+// k_score_keys), ONE ncclAllReduce(ncclUint64, ncclMax) over [P totals | P covered | 3 x C
+// newest-pose flag keys | health], then every rank resolves the stale flags from the reduced
+// keys (k_flags_from_keys) and runs the strict-'>' argmax on the host
+int pcp_score_poses_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
+                              const pcp_vl_params *p, uint64_t lo, uint64_t p_total,
+                              uint8_t *cell_flags, double *total_all, int32_t *covered_all,
+                              pcp_vl_report *rep, double *collective_ms) {
+    if (!ctx) return PCP_E_INVALID;
+    if (!ctx->comm)
+        return set_err(ctx, PCP_E_STATE, "pcp_score_poses_allreduce: no communicator "
+                                         "(pcp_comm_init_rank)");
+    if (!zx || !p || !rep)   // (every rank passes the same kind of arguments)
+        return set_err(ctx, PCP_E_INVALID, "pcp_score_poses_allreduce: null argument");
+    if (p_total > 65535u * 64u)
+        return set_err(ctx, PCP_E_INVALID, "pcp_score_poses_allreduce: %llu poses",
+                       (unsigned long long)p_total);
+    int rc = area_finish(ctx);   // (the cells' count sizes the vector: every rank holds the same)
+    const uint64_t C = ctx->n_cells;
+    const uint32_t P = (uint32_t)p_total;
+    const size_t count = 2 * (size_t)P + 3 * (size_t)C + 1, hw = count - 1;
+    ScoreEnq o;
+    hipStream_t st = ctx->stream;
+    if (!rc) {
+        if ((n && !poses5) || (C && !cell_flags))
+            rc = set_err(ctx, PCP_E_INVALID, "pcp_score_poses_allreduce: null argument");
+        else if (lo + n > p_total || n > 65535)
+            rc = set_err(ctx, PCP_E_INVALID,
+                         "pcp_score_poses_allreduce: shard [%llu, %llu) of %llu poses",
+                         (unsigned long long)lo, (unsigned long long)(lo + n),
+                         (unsigned long long)p_total);
+    }
+    auto enqueue = [&]() -> int {
+        PCP_HIP(ctx, hipSetDevice(ctx->device));
+        PCP_HIP(ctx, ctx->comm_keys.ensure(count * 8 + 64));
+        if (int e = score_enqueue(ctx, poses5, n, zx, p, o)) return e;
+        unsigned long long *v = ctx->comm_keys.as<unsigned long long>();
+        launch_score_keys(st, o, (int)lo, (int)P, v);
+        PCP_CHECK_LAUNCH(ctx);
+        PCP_HIP(ctx, hipMemsetAsync(v + hw, 0, 8, st));   // health: MAX's identity
+        if (collective_ms) {
+            for (hipEvent_t &e : ctx->comm_ev)
+                if (!e) PCP_HIP(ctx, hipEventCreate(&e));
+            PCP_HIP(ctx, hipEventRecord(ctx->comm_ev[0], st));
+        }
+        return PCP_OK;
+    };
+    if (!rc) rc = enqueue();
+    if (rc) {
+        const std::string why = ctx->err;
+        if (!comm_poison(ctx, count, true)) {
+            comm_drop(ctx);
+            return set_err(ctx, rc, "%s", why.c_str());
+        }
+        collective_ms = nullptr;
+    }
+    unsigned long long *v = ctx->comm_keys.as<unsigned long long>();
+    PCP_NCCL(ctx, ncclAllReduce(v, v, count, ncclUint64, ncclMax,
+                                static_cast<ncclComm_t>(ctx->comm), st));   // the one collective
+    if (collective_ms) PCP_HIP(ctx, hipEventRecord(ctx->comm_ev[1], st));
+    // pinned: [2P keys | zx120 total | health | C flags | 64 stats]
+    const size_t v_bytes = 2 * (size_t)P * 8, fl_off = (v_bytes + 16 + 15) & ~(size_t)15;
+    const size_t st_off = (fl_off + C + 15) & ~(size_t)15;
+    PCP_HIP(ctx, ctx->comm_host.ensure(st_off + 64 * sizeof(int32_t) + 64));
+    char *pin = ctx->comm_host.as<char>();
+    if (rc) {   // the failed rank only completes its collective
+        PCP_HIP(ctx, hipStreamSynchronize(st));
+        return set_err(ctx, rc, "%s", ctx->err.c_str());
+    }
+    if (C) {
+        std::memcpy(pin + fl_off, cell_flags, C);
+        PCP_HIP(ctx, hipMemcpyAsync(o.flags_d, pin + fl_off, C, hipMemcpyHostToDevice, st));
+    }
+    PCP_HIP(ctx, hipMemsetAsync(o.stats, 0, 64 * sizeof(int32_t), st));
+    launch_flags_from_keys(st, v, o.zbits, (int)C, (int)P, o.flags_d, o.stats);
+    PCP_CHECK_LAUNCH(ctx);
+    if (P) PCP_HIP(ctx, hipMemcpyAsync(pin, v, v_bytes, hipMemcpyDeviceToHost, st));
+    // the zx120 total (row n of this rank's totals: every rank evaluates it) and the health word
+    PCP_HIP(ctx, hipMemcpyAsync(pin + v_bytes, o.tot_d + n, sizeof(double), hipMemcpyDeviceToHost,
+                                st));
+    PCP_HIP(ctx, hipMemcpyAsync(pin + v_bytes + 8, v + hw, 8, hipMemcpyDeviceToHost, st));
+    if (C) PCP_HIP(ctx, hipMemcpyAsync(pin + fl_off, o.flags_d, C, hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipMemcpyAsync(pin + st_off, o.stats, 64 * sizeof(int32_t),
+                                hipMemcpyDeviceToHost, st));
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    prof_resolve(ctx);
+    unsigned long long health;
+    std::memcpy(&health, pin + v_bytes + 8, 8);
+    if (health != 0)
+        return set_err(ctx, PCP_E_STATE, "pcp_score_poses_allreduce: a peer rank failed before "
+                                         "the collective (health word poisoned)");
+    if (collective_ms) {
+        float ms = 0.0f;
+        PCP_HIP(ctx, hipEventElapsedTime(&ms, ctx->comm_ev[0], ctx->comm_ev[1]));
+        *collective_ms = ms;
+    }
+    if (C) std::memcpy(cell_flags, pin + fl_off, C);
+    const unsigned long long *vh = reinterpret_cast<const unsigned long long *>(pin);
+    double zx_total;
+    std::memcpy(&zx_total, pin + v_bytes, sizeof(double));
+    double best = -INFINITY;
+    int64_t best_idx = -1;
+    for (uint32_t k = 0; k < P; ++k) {   // runOptimization :471-474, the first maximum wins
+        double t;
+        std::memcpy(&t, &vh[k], sizeof(double));
+        if (total_all) total_all[k] = t;
+        if (covered_all) covered_all[k] = (int32_t)vh[P + k];
+        if (t > best) {
+            best = t;
+            best_idx = k;
+        }
+    }
+    fill_report(reinterpret_cast<const int32_t *>(pin + st_off), zx_total, best_idx, best, rep);
     return PCP_OK;
 }
 

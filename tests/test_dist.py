@@ -31,6 +31,18 @@ def _free_port():
     return p
 
 
+def _pose_bits(pyoracle, Ts, A, s, poses, vp):
+    """[n, C] result bits of each pose alone on zeroed GridCells (the kernel's mbits rows)"""
+    from pointcloud_processor_amd import dist as pd
+
+    rows = []
+    for q in range(poses.shape[0]):
+        f = np.zeros(s["cells"].shape[0], np.uint8)
+        pyoracle.score_poses(Ts, A, s["cells"], s["normals"], poses[q:q + 1], s["zx"], vp, f)
+        rows.append(pd.pose_bits(f))
+    return np.array(rows, np.uint8).reshape(poses.shape[0], s["cells"].shape[0])
+
+
 def _worker(rank, world, port, out_q):
     import torch.distributed as dist
 
@@ -58,11 +70,16 @@ def _worker(rank, world, port, out_q):
         cand = s["candidates"]
         lo2, hi2 = pd.shard(cand.shape[0], world, rank)
         flags = np.zeros(s["cells"].shape[0], np.uint8)
-        tot, _, _ = pyoracle.score_poses(Ts, A, s["cells"], s["normals"], cand[lo2:hi2], s["zx"],
-                                         pyoracle.vl_params(max_distance=float(s["max_distance"])),
-                                         flags)
+        vp = pyoracle.vl_params(max_distance=float(s["max_distance"]))
+        tot, cov, _ = pyoracle.score_poses(Ts, A, s["cells"], s["normals"], cand[lo2:hi2], s["zx"],
+                                           vp, flags)
         vec, bidx, bscore = pd.reduce_scores(tot, lo2, hi2, cand.shape[0], dist, "cpu")
-        out_q.put((rank, keys, best, vec, bidx, bscore))
+        # the GPU path's one reference-mode collective (pcp_score_poses_allreduce), restated:
+        # this shard's key vector, all-reduced by MAX (int64 view: every key is below 2^63)
+        bits = _pose_bits(pyoracle, Ts, A, s, cand[lo2:hi2], vp)
+        v = pd.score_keys(tot, cov, bits, lo2, cand.shape[0])
+        red = pd._reduce(v.view(np.int64), "max", dist, "cpu").view(np.uint64)
+        out_q.put((rank, keys, best, vec, bidx, bscore, red))
     finally:
         dist.destroy_process_group()
 
@@ -111,12 +128,31 @@ def test_two_rank_gloo_matches_single_process():
                                    float(d["el_max"]), float(d["max_distance"]),
                                    want_first_hit=False)
     s = np.load(GOLD / "score.npz")
-    for rank, keys, best, vec, bidx, bscore in res:
+    from pointcloud_processor_amd import dist as pd
+
+    Ts, A = pyoracle.Cloud(s["terrain"]), pyoracle.Cloud(s["aux"])
+    vp = pyoracle.vl_params(max_distance=float(s["max_distance"]))
+    cand = s["candidates"]
+    P, C = cand.shape[0], s["cells"].shape[0]
+    f_all = np.zeros(C, np.uint8)
+    tot1, cov1, _ = pyoracle.score_poses(Ts, A, s["cells"], s["normals"], cand, s["zx"], vp, f_all)
+    v1 = pd.score_keys(tot1, cov1, _pose_bits(pyoracle, Ts, A, s, cand, vp), 0, P)
+    fz = np.zeros(C, np.uint8)   # evaluateZX120Only alone: the zx120 bits
+    pyoracle.score_poses(Ts, A, s["cells"], s["normals"], cand[:0], s["zx"], vp, fz)
+    for rank, keys, best, vec, bidx, bscore, red in res:
         np.testing.assert_array_equal(keys, b.astype(np.int64))
         assert best == int(np.argmin(b))
         np.testing.assert_array_equal(vec, s["total"])     # golden: one process, all poses
         assert bidx == int(s["report"][0])
         assert bscore == float(s["best_score"])
+        # the reference-mode key vector: the shards' MAX is the one-process vector, and it
+        # resolves to the reference's stale flags from a fresh GridCell state
+        np.testing.assert_array_equal(red, v1)
+        np.testing.assert_array_equal(red[:P].view(np.float64), s["total"])
+        np.testing.assert_array_equal(red[P:2 * P].astype(np.int32), s["covered"])
+        np.testing.assert_array_equal(pd.flags_from_keys(red, fz & 7, np.zeros(C, np.uint8), P),
+                                      f_all)
+        np.testing.assert_array_equal(f_all, s["flags"])
 
 
 @pytest.mark.parametrize("n", [2, 3])

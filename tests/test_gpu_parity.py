@@ -1848,6 +1848,65 @@ def test_fan_allreduce_own_communicator(gpu, loaded, scene):
         assert best == -1
 
 
+def test_score_allreduce_own_communicator(oracle, loaded, scene, cells, aux):
+    """runOptimization's scoring for N processes in ONE RCCL collective
+    (pcp_score_poses_allreduce: [P totals | P covered | 3 x C newest-pose flag keys | health],
+    ncclAllReduce(MAX) on the context's stream).  At N = 1 it is bit-identical to
+    pcp_score_poses on the same context: every total's bits, the covered counts, the stale flags
+    of two ticks (the second from the first's flags, poses reversed), the report; the oracle
+    agrees on the flags and the best index.  A rank whose arguments fail before the collective
+    still runs it with a poisoned health word: it reports its own error, and the communicator
+    stays usable (the next query is exact again)."""
+    T, A = loaded
+    params = _abi.default_vl_params()
+    zx = np.ascontiguousarray(scene.zx120_pose5, np.float64)
+    with _abi.Context(0) as ctx:
+        ctx.set_terrain(scene.terrain, point_step=32)
+        ctx.set_aux_cloud(aux, point_step=32)
+        ctx.set_cells(cells.xyz, cells.normals)
+        poses = ctx.generate_candidates(cells.grid_bbox, params, scene.zx120_pose5)
+        P, C = poses.shape[0], cells.xyz.shape[0]
+        rep = _abi.VlReport()
+        fl = np.zeros(C, np.uint8)
+        with pytest.raises(_abi.PcpError):          # no communicator yet
+            ctx.score_poses_allreduce(poses, zx, params, 0, P, fl, None, None, rep)
+        ctx.comm_init_rank(1, _abi.comm_unique_id(), 0)
+        f1, f2, fr = np.zeros(C, np.uint8), np.zeros(C, np.uint8), np.zeros(C, np.uint8)
+        for tick, pz in enumerate((poses, poses[::-1].copy())):
+            t1, c1, r1 = ctx.score_poses(pz, zx, params, f1)
+            t2, c2 = np.zeros(P, np.float64), np.zeros(P, np.int32)
+            rep2 = _abi.VlReport()
+            ms = ctx.score_poses_allreduce(pz, zx, params, 0, P, f2, t2, c2, rep2, timed=True)
+            assert ms is not None and ms >= 0.0
+            np.testing.assert_array_equal(t2.view(np.uint64), t1.view(np.uint64))
+            np.testing.assert_array_equal(c2, c1)
+            np.testing.assert_array_equal(f2, f1)
+            assert rep2.as_dict() == r1.as_dict(), tick
+            _, _, rr = oracle.score_poses(T, A, cells.xyz, cells.normals, pz, scene.zx120_pose5,
+                                          oracle.vl_params(), fr)
+            np.testing.assert_array_equal(f2, fr)
+            assert rep2.best_idx == rr.best_idx
+        # a bad shard fails on this rank only; the collective still ran (health word poisoned)
+        with pytest.raises(_abi.PcpError):
+            ctx.score_poses_allreduce(poses, zx, params, 5, P, f2.copy(), None, None, rep)
+        assert ctx.comm_info() == (1, 0)
+        f3 = np.zeros(C, np.uint8)
+        t3 = np.zeros(P, np.float64)
+        ctx.score_poses_allreduce(poses, zx, params, 0, P, f3, t3, None, rep)
+        t4, _, r4 = ctx.score_poses(poses, zx, params, np.zeros(C, np.uint8))
+        np.testing.assert_array_equal(t3.view(np.uint64), t4.view(np.uint64))
+        assert rep.best_idx == r4.best_idx
+        # the fan's collective carries the same health word: a bad shard, then an exact query
+        fan = _abi.fan_params(n_az=128, n_el=32)
+        with pytest.raises(_abi.PcpError):
+            ctx.raycast_fan_allreduce(poses, fan, 3, P)
+        bl = np.zeros(P, np.uint32)
+        best, _ = ctx.raycast_fan_allreduce(poses, fan, 0, P, bl)
+        b_ref, _, _, best_ref = ctx.raycast_fan(poses, fan)
+        np.testing.assert_array_equal(bl, b_ref[:P])
+        assert best == best_ref
+
+
 def test_fan_keys_wait_stream_then_fan(gpu, loaded, scene, oracle):
     """a keys query handed to a libpcp wait_stream returns before its pose upload
     has read the pinned staging; the next fan query on the context (other poses) must not
