@@ -334,6 +334,25 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
                     const pcp_vl_params *p, uint8_t *cell_flags, double *total_score,
                     int32_t *covered, pcp_vl_report *rep);
 
+/* Diagnostics of the reference's own ray march (the roofline of k_score_cells, bench.py
+ * reference_mode; never used for results).  pcp_score_poses_stats: the query's visibility rays
+ * (the same rows, cells and march as pcp_score_poses) counted by a twin of the kernel --
+ * stats[0] z-band probes (2-byte records), stats[1] candidates' walk starts (4 bytes),
+ * stats[2] point records tested (12 bytes), stats[3] directory loads (0 with the fine-window
+ * copy).  pcp_score_poses_burst: the query's production k_score_cells launch `reps` times
+ * back-to-back between two stream events; *ms_per_launch = the interval / reps.  Neither
+ * touches the caller's GridCell flags. */
+/* evaluateCellScore's value for every (pose, cell) of the query (k_score_cells' rows, before
+ * evaluatePosition's std::max): score_mobile [n][n_cells], score_zx120 [n_cells] (host).  The
+ * per-cell parity bar (tests); the caller's GridCell flags are not touched. */
+int pcp_score_matrix(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx120_pose5[5],
+                     const pcp_vl_params *p, double *score_mobile, double *score_zx120);
+int pcp_score_poses_stats(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                          const double zx120_pose5[5], const pcp_vl_params *p, uint64_t stats[4]);
+int pcp_score_poses_burst(pcp_ctx *ctx, const double *poses5, uint64_t n,
+                          const double zx120_pose5[5], const pcp_vl_params *p, int reps,
+                          double *ms_per_launch);
+
 /* runOptimization's device part in one call (:455-519): pcp_generate_candidates then
  * pcp_score_poses on those candidates, identical results, one synchronisation -- the scoring
  * reads the candidates and their count where the generation left them on the device (the
@@ -492,6 +511,11 @@ int pcp_multi_score_poses(pcp_multi *m, const double *poses5, uint64_t n,
 /* The march's sample distances: s_0 = 0.5, s_{k+1} = s_k + 0.3 (repeated double addition,
  * :765-796) while s_k < end.  Returns the count in *n (writes min(cap, n) values). */
 int pcp_step_table(double end, double *steps, uint64_t cap, uint64_t *n);
+
+/* Test infrastructure: the library's device exclusive scan (the index builds' prefix sums)
+ * over a host array; out: n + 1 entries (out[n] = the total).  Scans of 2-64 tiles of 2,048
+ * run as one look-back pass (PCP_SCAN_ONEPASS, default 1), others as three launches. */
+int pcp_debug_exclusive_scan(pcp_ctx *ctx, const uint32_t *in, uint64_t n, uint32_t *out);
 
 /* diagnostics of the terrain index (cell edge, dims, points) */
 typedef struct pcp_index_info {

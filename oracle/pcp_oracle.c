@@ -546,6 +546,28 @@ void orc_score_poses(const orc_cloud *terrain, const orc_cloud *aux, int64_t aux
     }
 }
 
+/* evaluateCellScore's value for every (pose, cell) and for the zx120 pose (test
+ * infrastructure: the per-cell parity bar): sm[k * C + i] = the pose's score_mobile of cell i,
+ * sz[i] = score_zx120 (evaluatePosition :634-645 before the std::max).  Flags are scratch. */
+void orc_score_matrix(const orc_cloud *terrain, const orc_cloud *aux, int64_t aux_n,
+                      const double *cxyz, const float *cn, int64_t C,
+                      const double *poses5, int64_t P, const double zx120[5],
+                      const orc_vl_params *p, double *sm, double *sz)
+{
+    vl_env E = {terrain, aux, aux_n, p->max_distance};
+    uint8_t *fl = (uint8_t *)calloc((size_t)(C > 0 ? C : 1), 1);
+    for (int64_t i = 0; i < C; ++i) sz[i] = eval_cell(&E, zx120, cxyz + 3 * i, cn + 3 * i, &fl[i], 1);
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(g_threads) schedule(dynamic, 1)
+#endif
+    for (int64_t k = 0; k < P; ++k) {
+        uint8_t f = 0;
+        for (int64_t i = 0; i < C; ++i)
+            sm[k * C + i] = eval_cell(&E, poses5 + 5 * k, cxyz + 3 * i, cn + 3 * i, &f, 0);
+    }
+    free(fl);
+}
+
 /* The candidate loop's per-pose totals alone (evaluatePosition :627-654 for every pose),
  * OpenMP over poses -- the CPU baseline's multi-threaded variant.  The flags a pose writes
  * never feed a score, so each thread keeps its own scratch flags; totals and covered counts

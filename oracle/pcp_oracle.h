@@ -144,6 +144,13 @@ void orc_score_totals(const orc_cloud *terrain, const orc_cloud *aux, int64_t au
                       const double *poses5, int64_t n_poses, const double zx120[5],
                       const orc_vl_params *p, double *total_score, int32_t *covered);
 
+/* evaluateCellScore per (pose, cell) and for the zx120 pose (the per-cell parity bar):
+ * sm [n_poses][n_cells] = score_mobile, sz [n_cells] = score_zx120 */
+void orc_score_matrix(const orc_cloud *terrain, const orc_cloud *aux, int64_t aux_n,
+                      const double *cells_xyz, const float *cells_nrm, int64_t n_cells,
+                      const double *poses5, int64_t n_poses, const double zx120[5],
+                      const orc_vl_params *p, double *sm, double *sz);
+
 /* Dense azimuth x elevation fan (BASELINE configs[1]): per pose, ray
  * (az_i, el_j) with local dir (cos el cos a_i, cos el sin a_i, sin el), a_i = 2*pi*i/n_az,
  * el_j = el_min + (el_max-el_min)*(j+0.5)/n_el, rotated by the pose yaw; marched with

@@ -55,6 +55,8 @@ _SIGS = [
                                C.POINTER(VlParams), _P, _P, _P, C.POINTER(VlReport)]),
     ("orc_score_totals", None, [_P, _P, C.c_int64, _P, _P, C.c_int64, _P, C.c_int64, _P,
                                 C.POINTER(VlParams), _P, _P]),
+    ("orc_score_matrix", None, [_P, _P, C.c_int64, _P, _P, C.c_int64, _P, C.c_int64, _P,
+                                C.POINTER(VlParams), _P, _P]),
     ("orc_raycast_fan", None, [_P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                C.c_double, _P, _P, _P]),
     ("orc_cloud_use_kdtree", None, [_P, _P]),
@@ -292,6 +294,23 @@ def score_poses(terrain: Cloud | None, aux: Cloud | None, cells_xyz, cells_nrm, 
                           aux.n if aux else 0, _p(cx), _p(cn), cx.shape[0], _p(poses), P, _p(zx),
                           C.byref(params), _p(cell_flags), _p(tot), _p(cov), C.byref(rep))
     return tot[:P].copy(), cov[:P].copy(), rep
+
+
+def score_matrix(terrain: Cloud | None, aux: Cloud | None, cells_xyz, cells_nrm, poses5,
+                 zx120_pose5, params):
+    """evaluateCellScore per (pose, cell) -> (score_mobile [P, C], score_zx120 [C]) (OpenMP
+    over poses; the per-cell parity bar)."""
+    cx = np.ascontiguousarray(cells_xyz, np.float64).reshape(-1, 3)
+    cn = np.ascontiguousarray(cells_nrm, np.float32).reshape(-1, 3)
+    poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+    zx = np.ascontiguousarray(zx120_pose5, np.float64)
+    P, nc = poses.shape[0], cx.shape[0]
+    sm = np.zeros((max(P, 1), max(nc, 1)), np.float64)
+    sz = np.zeros(max(nc, 1), np.float64)
+    lib().orc_score_matrix(terrain.h if terrain else None, aux.h if aux else None,
+                           aux.n if aux else 0, _p(cx), _p(cn), nc, _p(poses), P, _p(zx),
+                           C.byref(params), _p(sm), _p(sz))
+    return sm[:P, :nc].copy(), sz[:nc].copy()
 
 
 def score_totals(terrain: Cloud | None, aux: Cloud | None, cells_xyz, cells_nrm, poses5,

@@ -162,6 +162,11 @@ _SIGS = [
     ("pcp_score_poses_allreduce", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams),
                                             C.c_uint64, C.c_uint64, _P, _P, _P,
                                             C.POINTER(VlReport), C.POINTER(C.c_double)]),
+    ("pcp_score_poses_stats", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams), _P]),
+    ("pcp_score_matrix", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams), _P, _P]),
+    ("pcp_debug_exclusive_scan", C.c_int, [_P, _P, C.c_uint64, _P]),
+    ("pcp_score_poses_burst", C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(VlParams), C.c_int,
+                                        C.POINTER(C.c_double)]),
     ("pcp_stream_create", C.c_int, [_P, C.POINTER(_P)]),
     ("pcp_stream_destroy", C.c_int, [_P, _P]),
     ("pcp_step_table", C.c_int, [C.c_double, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
@@ -609,12 +614,15 @@ class Context:
 
     def excavate_area_async(self, cloud: np.ndarray, zx120_tf, params: ExcavationParams | None = None,
                             grid_resolution: float = 0.1, vertical_layers: int = 10,
-                            point_step=None, offs=(0, 4, 8), landed: bool = False):
+                            point_step=None, offs=(0, 4, 8), landed: bool = False,
+                            zero_copy: bool = False):
         """pcp_excavate_area_async: excavate(), then set_excavation_area_async() over its area
         (when not empty) and set_terrain() over its terrain, fed from the carve's landed
         records.  -> (terrain, area, pose, grid_bbox (6,), cells_cap).  landed=True: null
-        outputs, terrain / area are read-only views of the landing (pcp_excavate_landed), valid
-        until the context's next excavate call."""
+        outputs, terrain / area read from the landing (pcp_excavate_landed) and returned as
+        copies; zero_copy=True (explicit opt-in) returns read-only views of the landing instead,
+        valid only until the context's next excavate call or close() (the landing may be
+        reallocated or freed then: a view held past that reads freed memory)."""
         v = cloud_view(cloud, point_step, offs)
         p = params or excavation_params()
         tf = Rigid((C.c_double * 3)(*zx120_tf[0]), (C.c_double * 4)(*zx120_tf[1]))
@@ -634,6 +642,8 @@ class Context:
                 if n == 0:
                     return np.empty((0, 8), np.float32)
                 a = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_float)), shape=(n, 8))
+                if not zero_copy:
+                    return a.copy()
                 a.flags.writeable = False
                 return a
             return view(tp, nt.value), view(ap, na.value), pose, bbox, cap.value
@@ -823,6 +833,50 @@ class Context:
             _ptr(blocked_all), _ptr(units), C.byref(best), C.byref(ms) if timed else None),
             "pcp_raycast_fan_allreduce")
         return best.value, (ms.value if timed else None)
+
+    def debug_exclusive_scan(self, a: np.ndarray) -> np.ndarray:
+        """pcp_debug_exclusive_scan: the device exclusive scan of uint32 `a` -> (n + 1,)."""
+        a = np.ascontiguousarray(a, np.uint32)
+        out = np.zeros(a.size + 1, np.uint32)
+        self._check(self.lib.pcp_debug_exclusive_scan(self.h, _ptr(a), a.size, _ptr(out)),
+                    "pcp_debug_exclusive_scan")
+        return out
+
+    def score_matrix(self, poses5, zx120_pose5, params: VlParams):
+        """pcp_score_matrix -> (score_mobile [P, C], score_zx120 [C]): evaluateCellScore per
+        (pose, cell) as k_score_cells computes it (the per-cell parity bar)."""
+        poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+        zx = np.ascontiguousarray(zx120_pose5, np.float64)
+        C_ = self.cells_count()
+        P = poses.shape[0]
+        sm = np.zeros((max(P, 1), max(C_, 1)), np.float64)
+        sz = np.zeros(max(C_, 1), np.float64)
+        self._check(self.lib.pcp_score_matrix(self.h, _ptr(poses), P, _ptr(zx), C.byref(params),
+                                              _ptr(sm), _ptr(sz)), "pcp_score_matrix")
+        return sm[:P, :C_].copy(), sz[:C_].copy()
+
+    def score_poses_stats(self, poses5, zx120_pose5, params: VlParams) -> dict:
+        """pcp_score_poses_stats: the gather lane-loads of the query's visibility rays
+        (diagnostic twin of k_score_cells; the caller's flags are not touched)."""
+        poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+        zx = np.ascontiguousarray(zx120_pose5, np.float64)
+        st = np.zeros(4, np.uint64)
+        self._check(self.lib.pcp_score_poses_stats(self.h, _ptr(poses), poses.shape[0], _ptr(zx),
+                                                   C.byref(params), _ptr(st)),
+                    "pcp_score_poses_stats")
+        return {"probes": int(st[0]), "walk_starts": int(st[1]), "point_tests": int(st[2]),
+                "directory_loads": int(st[3])}
+
+    def score_poses_burst(self, poses5, zx120_pose5, params: VlParams, reps: int = 20) -> float:
+        """pcp_score_poses_burst: the query's production k_score_cells launch `reps` times
+        back-to-back between two events -> ms per launch."""
+        poses = np.ascontiguousarray(poses5, np.float64).reshape(-1, 5)
+        zx = np.ascontiguousarray(zx120_pose5, np.float64)
+        ms = C.c_double()
+        self._check(self.lib.pcp_score_poses_burst(self.h, _ptr(poses), poses.shape[0], _ptr(zx),
+                                                   C.byref(params), reps, C.byref(ms)),
+                    "pcp_score_poses_burst")
+        return ms.value
 
     def score_poses_allreduce(self, poses5: np.ndarray, zx120_pose5: np.ndarray,
                               params: VlParams, lo: int, p_total: int, cell_flags: np.ndarray,

@@ -18,6 +18,9 @@ WORKLOAD_SOURCES = {
     "fan": ["pcp_vlidar.hip", "pcp_fine.hip", "pcp_index.hip", "pcp_stencil.hpp",
             "pcp_grid.hpp"] + _COMMON,
     "filter": ["pcp_filter.hip", "pcp_rigid.hpp"] + _COMMON,
+    # reference mode (k_score_cells: the same march over the same terrain copy)
+    "cells": ["pcp_vlidar.hip", "pcp_fine.hip", "pcp_index.hip", "pcp_stencil.hpp",
+              "pcp_grid.hpp"] + _COMMON,
 }
 
 

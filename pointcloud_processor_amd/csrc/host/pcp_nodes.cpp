@@ -351,9 +351,18 @@ ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
     pcp_cloud_view v{};
     const bool in_place = landed && landed->n && landed->n == msg.size() && landed->point_step == 32;
     if (in_place) v = *landed;
+    // the message the reference's callbacks see: a deferred message (header only) rebuilt from
+    // its landing when a path below republishes it or hands it to the per-node callbacks
+    PointCloud2 full;
+    auto whole = [&]() -> const PointCloud2 & {
+        if (!(in_place && msg.data.empty())) return msg;
+        full = make_xyzrgb_cloud(landed->data, landed->n, msg.frame_id);
+        full.stamp = msg.stamp;
+        return full;
+    };
     if (!defer_grid_ || multi_ || !gen.p_.enabled || !zx120_base ||
         !(in_place || cloud_view(msg, v, nullptr))) {
-        ExcavationTerrainGenerator::Output o = gen.matchedCloudCallback(msg, zx120_base);
+        ExcavationTerrainGenerator::Output o = gen.matchedCloudCallback(whole(), zx120_base);
         if (!(o.area_published && !excavationAreaCallback(o.excavation_area) && !err_.empty()))
             terrainCallback(o.excavated_terrain);
         zx_callback();
@@ -369,7 +378,7 @@ ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
     double pose[4], bb[6];
     if (pcp_excavate_bounds(&gen.p_, v.n, &nt, &na) != PCP_OK) {
         gen.err_ = "excavated_surface_generator: bad parameters";
-        o.excavated_terrain = msg;
+        o.excavated_terrain = whole();
         terrainCallback(o.excavated_terrain);
         zx_callback();
         return o;
@@ -381,7 +390,7 @@ ExcavationTerrainGenerator::Output SimplifiedDualLidarOptimizer::carveCallbacks(
                                 pose, p_.grid_resolution, p_.vertical_layers, bb, &ncap) != PCP_OK ||
         pcp_excavate_landed(dev_.ctx(), &terr, &area) != PCP_OK) {
         gen.err_ = dev_.error();
-        o.excavated_terrain = msg;
+        o.excavated_terrain = whole();
         zx_callback();
         return o;
     }

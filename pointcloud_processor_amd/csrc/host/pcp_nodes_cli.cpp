@@ -242,6 +242,12 @@ static int cmd_replay(Device &dev, char **a) {
     if (const char *fd = std::getenv("PCP_FRONT_DEFER")) front_defer = std::atoi(fd) != 0;
     front_defer = front_defer && front_fused && chain && carve_fused && carve_landed && area_async &&
                   !carve_zx;
+    // PCP_REPLAY_NO_TF=k: frame k's map -> zx120/base_link lookup fails (the carve's fallback:
+    // the merged cloud republished as the terrain, no area); the line reports that frame's
+    // terrain message (a deferred merged message must not go out as its header)
+    long no_tf_frame = -1;
+    if (const char *nt = std::getenv("PCP_REPLAY_NO_TF")) no_tf_frame = std::atol(nt);
+    size_t no_tf_points = 0, no_tf_bytes = 0, no_tf_merged = 0;
     vl.terrainCallback(cloud_from(t, tn, 32, "map"));
     std::vector<double> xyz(cn * 3);
     std::vector<float> nrm(cn * 3);
@@ -312,11 +318,16 @@ static int cmd_replay(Device &dev, char **a) {
         }
         ExcavationTerrainGenerator::Output e;
         const bool zx_in_carve = chain && carve_fused && carve_zx;
+        const bool no_tf = (long)f == no_tf_frame;
         if (chain && carve_fused) {   // the carve + both callbacks (stage "carve" holds all three)
-            e = vl.carveCallbacks(gen, o.merged, &zx_base,
+            e = vl.carveCallbacks(gen, o.merged, no_tf ? nullptr : &zx_base,
                                   front_fused && carve_landed ? &front_landed : nullptr,
                                   zx_in_carve ? &zf : nullptr);
-            if (!e.area_published) {
+            if (no_tf) {
+                no_tf_points = e.excavated_terrain.size();
+                no_tf_bytes = e.excavated_terrain.data.size();
+                no_tf_merged = front_landed.n;
+            } else if (!e.area_published) {
                 std::fprintf(stderr, "replay: carve failed: %s\n", gen.lastError().c_str());
                 return 1;
             }
@@ -431,10 +442,13 @@ static int cmd_replay(Device &dev, char **a) {
     std::printf("{\"frames\": %zu, \"points_per_scan\": %zu, \"chain\": %d, \"p50_ms\": %.4f, "
                 "\"p99_ms\": %.4f, \"max_ms\": %.4f, \"merged_points\": %zu, \"cells\": %zu, "
                 "\"best_idx\": %zu, \"reallocs_after_warmup\": %llu, \"dumped\": [%s], "
-                "\"stage_p50_ms\": {%s}, \"slowest\": [%s], \"lat_ms\": [%s]}\n",
+                "\"stage_p50_ms\": {%s}, \"slowest\": [%s], \"lat_ms\": [%s], "
+                "\"no_tf\": {\"frame\": %ld, \"terrain_points\": %zu, \"terrain_bytes\": %zu, "
+                "\"merged_points\": %zu}}\n",
                 lat.size(), npts, chain ? 1 : 0, q(0.5), q(0.99), lat.back(), merged_n, cells_n,
                 best, (unsigned long long)realloc_after_warmup, dumped.c_str(), stage_s.c_str(),
-                slow_s.c_str(), lat_s.c_str());
+                slow_s.c_str(), lat_s.c_str(), no_tf_frame, no_tf_points, no_tf_bytes,
+                no_tf_merged);
     return 0;
 }
 

@@ -552,6 +552,38 @@ int exclusive_scan_u32(pcp_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
     return PCP_OK;
 }
 
+}  // namespace pcp
+
+// the library's device exclusive scan on a host array (diagnostic entry point: the one-pass
+// look-back form against the three-launch form, tests/test_gpu_parity.py::test_exclusive_scan_*)
+extern "C" int pcp_debug_exclusive_scan(pcp_ctx *ctx, const uint32_t *in, uint64_t n,
+                                        uint32_t *out) {
+    using namespace pcp;
+    if (!ctx || (n && !in) || !out) return PCP_E_INVALID;
+    PCP_HIP(ctx, hipSetDevice(ctx->device));
+    DevBuf din, dout, dtmp;
+    PCP_HIP(ctx, din.ensure((n + 1) * sizeof(uint32_t)));
+    PCP_HIP(ctx, dout.ensure((n + 1) * sizeof(uint32_t)));
+    PCP_HIP(ctx, dtmp.ensure(scan_tmp_bytes(n) + 256));
+    int rc = PCP_OK;
+    hipError_t e = n ? hipMemcpyAsync(din.p, in, n * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                      ctx->stream)
+                     : hipSuccess;
+    if (e == hipSuccess)
+        rc = exclusive_scan_u32(ctx, din.as<const uint32_t>(), dout.as<uint32_t>(), n, dtmp.p);
+    if (e == hipSuccess && rc == PCP_OK)
+        e = hipMemcpyAsync(out, dout.p, (n + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    din.release();
+    dout.release();
+    dtmp.release();
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_fail(ctx, e, "pcp_debug_exclusive_scan", __FILE__, __LINE__);
+    return PCP_OK;
+}
+
+namespace pcp {
 // exclusive_scan_u32 of two arrays (out2 / zero2 as there, no preset); two one-tile scans
 // (a message-sized cloud's pair of grids) are one launch
 int exclusive_scan_u32_pair(pcp_ctx *ctx, const uint32_t *in_a, uint32_t *out_a, uint64_t n_a,
@@ -692,7 +724,8 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->area_host.release();
     DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->cells_n_d, &ctx->stage, &ctx->fan_tab,
                       &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,
-                      &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->f_in,
+                      &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->cr_cnt,
+                      &ctx->cr_list,   &ctx->f_in,
                       &ctx->f_misc,    &ctx->bk_stat};
     for (DevBuf *b : bufs) b->release();
     for (auto &b : ctx->scratch) b.release();

@@ -9,9 +9,11 @@
  * with cos m and sin m in double-double (Cody-Waite reduction by pi / 2 in three parts, Taylor
  * series to t^31 for |t| <= pi / 4), so the sign is decided unless t lies within ~2^-100 of a
  * midpoint.  Zeros, infinities, NaNs and |r| < 2^-900 return r unchanged.
- * (The same construction for the scoring's acos and sin, virtual_lidar.cpp:700-705, lives in
- * tests/libm/crmath_extra.h: checked on the CPU, not used by a kernel, because glibc misrounds
- * those near ties more often than ocml disagrees with it -- DESIGN.md §8.)
+ * The scoring's acos and sin (evaluateCellScore, virtual_lidar.cpp:689-700) the same way
+ * (round 6): pcp_cr_acos_fix(d, r) from ocml's acos, pcp_cr_sin(a) from the double-double sin.
+ * Measured per cell (tests/test_gpu_parity.py::test_parity_bar_per_cell, 91-candidate tick):
+ * ocml's acos / sin made 9 % of the positive cell scores differ from glibc's (up to 8 ulps where
+ * pi / 2 - theta is small, 2:1 downward); glibc rounds these correctly but for rare near ties.
  * Compile with -ffp-contract=off: the error-free transformations need every operation rounded
  * on its own (fma() is called explicitly where one is meant).
  */
@@ -179,6 +181,137 @@ PCP_CR double pcp_cr_atan2_fix(double y, double x, double r) {
         if (side == 1 && v > 0.0) return hi;
     }
     return r;
+}
+
+/* acos(d) for 0 < d < 1 from a faithful first result r: acos is decreasing, so the true angle
+ * lies below the midpoint m = r + h (h = half the gap to a neighbour) exactly when d > cos m,
+ * with cos m = C - h S - h^2 / 2 C from ONE double-double sin / cos at r (the h^3 terms are
+ * ~2^-160).  Other d (0, 1, outside, NaN) and r = 0 return r unchanged. */
+PCP_CR double pcp_cr_acos_fix(double d, double r) {
+    if (!(d > 0.0 && d < 1.0) || !isfinite(r) || r == 0.0) return r;
+    const double lo = nextafter(r, -INFINITY), hi = nextafter(r, INFINITY);
+    pcp_dd S, C;
+    pcp_dd_sincos(pcp_dd_make(r, 0.0), &S, &C);
+    for (int side = 0; side < 2; ++side) {
+        const double h = 0.5 * ((side ? hi : lo) - r);
+        pcp_dd cm = pcp_dd_add(C, pcp_dd_neg(pcp_dd_mul_d(S, h)));
+        cm = pcp_dd_add(cm, pcp_dd_make(-0.5 * h * h * C.hi, 0.0));
+        const pcp_dd e = pcp_dd_add(pcp_dd_make(d, 0.0), pcp_dd_neg(cm));   /* d - cos m */
+        const double v = e.hi != 0.0 ? e.hi : e.lo;
+        if (side == 0 && v > 0.0) return lo;
+        if (side == 1 && v < 0.0) return hi;
+    }
+    return r;
+}
+
+/* sin(a) for 2^-500 <= |a| <= 4: the double-double value rounded once (its normalised high
+ * part) -- correct unless sin(a) lies within ~2^-100 relative of a midpoint; other a: sin(a) */
+PCP_CR double pcp_cr_sin(double a) {
+    if (!isfinite(a) || fabs(a) > 4.0 || fabs(a) < 0x1p-500) return sin(a);
+    pcp_dd s, c;
+    pcp_dd_sincos(pcp_dd_make(a, 0.0), &s, &c);
+    return s.hi + s.lo;
+}
+
+/* ---- the scoring's sin(pi / 2 - acos(d)) at speed (round 6) -------------------------------
+ * A two-phase (Ziv) evaluation.  Phase 1: sin / cos from the table of k pi / 512
+ * (pcp_crmath_tab.h, tools/gen/crmath_table.py) and short polynomials in |t| <= pi / 1024, good
+ * to ~2^-70 absolute; each rounding decision is taken only when the value lies more than
+ * PCP_CR_FAST_MARGIN from the decision's boundary, else phase 2 (pcp_cr_acos_fix +
+ * pcp_cr_sin above, ~2^-100) decides.  tests/test_crmath.py checks phase 1's decisions against
+ * phase 2 and the result against glibc's sin(M_PI / 2 - acos(d)). */
+#include "pcp_crmath_tab.h"
+
+/* phase 1's decision margins: absolute for d - cos m (values <= 1), relative for a rounding */
+#define PCP_CR_FAST_MARGIN 0x1p-74
+#define PCP_CR_FAST_MARGIN_REL 0x1p-66
+
+/* sin / cos of 0 <= x <= 1.61 as double-doubles, |error| below ~2^-84 (absolute; relative for
+ * sin of x < pi / 1024): the table's k pi / 512, t = x - k pi / 512 in double-double,
+ * sin t = t + t^3 (-1/6 + t^2/120 - t^4/5040), cos t = 1 - u / 2 + u^2 / 24 - u^3 / 720 with
+ * u = t^2 in double-double (the terms past those are below 2^-90 for |t| <= pi / 1024) */
+PCP_CR void pcp_fast_sincos(double x, pcp_dd *s_out, pcp_dd *c_out) {
+    int k = (int)nearbyint(x * (512.0 / 3.141592653589793));
+    k = k < 0 ? 0 : (k > PCP_CR_TAB_N - 1 ? PCP_CR_TAB_N - 1 : k);
+    const double kd = (double)k;
+    /* t = x - k (Q1 + Q2 + Q3): k Q1, k Q2 exact; x - k Q1 exact (Sterbenz) */
+    const double t1 = x - kd * PCP_CR_Q1;
+    const pcp_dd t2 = pcp_two_sum(t1, -(kd * PCP_CR_Q2));
+    const pcp_dd t = pcp_fast_two_sum(t2.hi, t2.lo - kd * PCP_CR_Q3);
+    const pcp_dd u2 = pcp_two_prod(t.hi, t.hi);
+    const pcp_dd u = pcp_fast_two_sum(u2.hi, u2.lo + 2.0 * t.hi * t.lo);   /* t^2 */
+    const double ud = u.hi;
+    /* sin t = t + st, st = t^3 (-1/6 + ...) (|st| < 2^-27 |t|: double suffices) */
+    const double st = t.hi * ud * (-1.0 / 6.0 + ud * (1.0 / 120.0 + ud * (-1.0 / 5040.0)));
+    /* cos t = 1 + ct, ct = -u / 2 (double-double) + u^2 (1/24 - u / 720) */
+    const pcp_dd ct = pcp_dd_add(pcp_dd_make(-0.5 * u.hi, -0.5 * u.lo),
+                                 pcp_dd_make(ud * ud * (1.0 / 24.0 + ud * (-1.0 / 720.0)), 0.0));
+    const pcp_dd sint = pcp_dd_add(t, pcp_dd_make(st, 0.0));
+    const pcp_dd Sk = pcp_dd_make(kPcpSinCos512[k][0], kPcpSinCos512[k][1]);
+    const pcp_dd Ck = pcp_dd_make(kPcpSinCos512[k][2], kPcpSinCos512[k][3]);
+    /* sin x = Sk + Sk ct + Ck sin t, cos x = Ck + Ck ct - Sk sin t */
+    *s_out = pcp_dd_add(pcp_dd_add(Sk, pcp_dd_mul(Sk, ct)), pcp_dd_mul(Ck, sint));
+    *c_out = pcp_dd_add(pcp_dd_add(Ck, pcp_dd_mul(Ck, ct)), pcp_dd_neg(pcp_dd_mul(Sk, sint)));
+}
+
+/* the double nearest v = hi + lo (lo normalised below hi's ulp), if v lies more than
+ * margin * |v| from a rounding boundary: *ok = 1; else *ok = 0 */
+PCP_CR double pcp_round_dd_checked(pcp_dd v, double margin, int *ok) {
+    const double R = v.hi + v.lo;
+    const double res = (v.hi - R) + v.lo;   /* v - R */
+    const double half = 0.5 * (res > 0.0 ? nextafter(R, INFINITY) - R : R - nextafter(R, -INFINITY));
+    *ok = fabs(fabs(res) - fabs(half)) > margin * fabs(R);
+    return R;
+}
+
+/* evaluateCellScore's sin(M_PI / 2 - theta), theta = acos(d), as glibc evaluates it (both
+ * functions rounded correctly), from a faithful first result r of acos(d).  phase_out
+ * (nullable): 1 when phase 1 decided, 2 when phase 2 did */
+PCP_CR double pcp_score_sin_part(double d, double r, int *phase_out) {
+    const double P1 = 1.5707963267948966, P2 = 6.123233995736766e-17,
+                 P3 = -1.4973849048591698e-33;   /* pi / 2 = P1 + P2 + P3; M_PI / 2 == P1 */
+    if (phase_out) *phase_out = 2;
+    if (!(d > 0x1p-20 && d < 1.0) || !isfinite(r) || !(r > 0.0 && r < 1.6))
+        return pcp_cr_sin(P1 - pcp_cr_acos_fix(d, r));
+    pcp_dd S, C;
+    pcp_fast_sincos(r, &S, &C);
+    const double lo = nextafter(r, -INFINITY), hi = nextafter(r, INFINITY);
+    double th = r;
+    for (int side = 0; side < 2; ++side) {
+        /* d - cos(r + h), cos(r + h) = C - h S - h^2 / 2 C (h half the gap to a neighbour) */
+        const double h = 0.5 * ((side ? hi : lo) - r);
+        pcp_dd cm = pcp_dd_add(C, pcp_dd_neg(pcp_dd_mul_d(S, h)));
+        cm = pcp_dd_add(cm, pcp_dd_make(-0.5 * h * h * C.hi, 0.0));
+        const pcp_dd e = pcp_dd_add(pcp_dd_make(d, 0.0), pcp_dd_neg(cm));
+        if (fabs(e.hi) <= PCP_CR_FAST_MARGIN) return pcp_cr_sin(P1 - pcp_cr_acos_fix(d, r));
+        if (side == 0 && e.hi > 0.0) { th = lo; break; }
+        if (side == 1 && e.hi < 0.0) { th = hi; break; }
+    }
+    pcp_dd St = S, Ct = C;
+    if (th != r) {   /* sin / cos at th = r + w: the w^3 terms are below 2^-150 */
+        const double w = th - r;
+        St = pcp_dd_add(pcp_dd_add(S, pcp_dd_mul_d(C, w)), pcp_dd_make(-0.5 * w * w * S.hi, 0.0));
+        Ct = pcp_dd_add(pcp_dd_add(C, pcp_dd_neg(pcp_dd_mul_d(S, w))),
+                        pcp_dd_make(-0.5 * w * w * C.hi, 0.0));
+    }
+    const double a = P1 - th;   /* the reference's argument, rounded */
+    if (a == 0.0) return 0.0;
+    pcp_dd v;
+    if (a < 0.25) {   /* small: sin(a) itself (no cancellation) */
+        pcp_dd ca;
+        pcp_fast_sincos(a, &v, &ca);
+    } else {
+        /* a = (pi / 2 - th) - eta, eta = (P1 - th - a) + P2 + P3: sin(a) = cos(th + eta)
+         * = Ct - St eta - Ct eta^2 / 2 (|eta| < 2^-52: the eta^2 term is below 2^-106) */
+        const pcp_dd ea = pcp_two_sum(P1, -th);
+        const pcp_dd eta = pcp_dd_add(pcp_dd_make(ea.lo, 0.0), pcp_dd_make(P2, P3));
+        v = pcp_dd_add(Ct, pcp_dd_neg(pcp_dd_mul(St, eta)));
+    }
+    int ok = 0;
+    const double R = pcp_round_dd_checked(v, PCP_CR_FAST_MARGIN_REL, &ok);
+    if (!ok) return pcp_cr_sin(a);
+    if (phase_out) *phase_out = 1;
+    return R;
 }
 
 #endif /* PCP_CRMATH_H */

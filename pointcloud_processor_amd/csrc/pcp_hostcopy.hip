@@ -32,6 +32,7 @@ constexpr auto kSpin = std::chrono::microseconds(300);
 // with k parts of per = ceil(n / k) rounded up to 4 KiB < n / k + 4096 bytes, the last part
 // starts at (k - 1) per < n whenever n > k (k - 1) 4096 (2 k 4096 did not imply it)
 static_assert(kSplitMin > (size_t)(kMaxHelpers + 1) * kMaxHelpers * 4096, "parts must be non-empty");
+static_assert(kMaxHelpers + 1 < 0xffff, "part count and index fit the claim word's 16-bit fields");
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
 }  // namespace
@@ -64,10 +65,11 @@ struct CopyPool {
             part_[i] = Part{static_cast<char *>(dst) + o, static_cast<const char *>(src) + o, e - o};
             if (e > o) used = i + 1;
         }
-        used_.store(used, std::memory_order_relaxed);
         pending_.store(used, std::memory_order_relaxed);
         const uint64_t g = ++job_;
-        claim_.store(g << 32, std::memory_order_release);   // publishes parts and used_
+        // publishes the parts; the job's part count travels in the same word as its id, so a
+        // late helper can never pair job g's id with another job's count
+        claim_.store((g << 32) | ((uint64_t)used << 16), std::memory_order_release);
         {
             std::lock_guard<std::mutex> l(mu_);
             gen_.store(g, std::memory_order_release);
@@ -81,16 +83,17 @@ struct CopyPool {
     }
 
    private:
-    // copy parts of job g until none is left unclaimed (a claim is one CAS on {job, next part})
+    // copy parts of job g until none is left unclaimed (a claim is one CAS on {job, parts, next
+    // part}: job << 32 | used << 16 | next)
     void work(uint64_t g) {
         uint64_t c = claim_.load(std::memory_order_acquire);
         for (;;) {
-            if ((c >> 32) != g || (uint32_t)c >= (uint32_t)used_.load(std::memory_order_relaxed))
-                return;
+            const uint32_t next = (uint32_t)c & 0xffffu, used = ((uint32_t)c >> 16) & 0xffffu;
+            if ((c >> 32) != g || next >= used) return;
             if (!claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel,
                                               std::memory_order_acquire))
                 continue;
-            const Part p = part_[(uint32_t)c];
+            const Part p = part_[next];
             std::memcpy(p.d, p.s, p.n);
             pending_.fetch_sub(1, std::memory_order_acq_rel);
             c = claim_.load(std::memory_order_acquire);
@@ -125,9 +128,8 @@ struct CopyPool {
     std::atomic<uint64_t> gen_{0};
     std::atomic<int> pending_{0};
     std::atomic<bool> stop_{false};
-    std::atomic<uint64_t> claim_{0};   // job << 32 | next unclaimed part
+    std::atomic<uint64_t> claim_{0};   // job << 32 | parts << 16 | next unclaimed part
     uint64_t job_ = 0;                 // (the caller's; one copy at a time per pool)
-    std::atomic<int> used_{0};
     Part part_[kMaxHelpers + 1];
 };
 

@@ -454,14 +454,46 @@ struct VisEnv {
     float rexit_ray;       // exit_dist(r2_ray)
 };
 
+// evaluateCellScore's score of a visible cell (:689-700): the cosine d = |dot| clamped to
+// [0, 1] gives sin(pi / 2 - acos(d)) (score_sin_part), then + 1 / L and the clamp at 0
+// (score_finish).  glibc's acos and sin, which the reference calls, round correctly but for
+// rare near ties: ocml's first results, then the midpoint tests / one rounding of pcp_crmath.h
+// (ocml alone left 9 % of the cell scores off by 1-8 ulps, test_parity_bar_per_cell)
+__device__ __forceinline__ double score_sin_part(double ad) {
+#ifdef PCP_SCORE_OCML   // A/B build only (tools/r6_cr_ab.sh): ocml's acos / sin as they come
+    return sin(kPi / 2 - acos(ad));
+#else
+    return pcp_score_sin_part(ad, acos(ad), nullptr);   // (two phases, pcp_crmath.h)
+#endif
+}
+#ifndef PCP_SCORE_CR_PASS
+#define PCP_SCORE_CR_PASS 1   // visible cells scored by k_score_cr (0: inline in k_score_cells)
+#endif
+__device__ __forceinline__ double score_finish(double sin_part, double L, int cell) {
+    const double score = 1.0 * sin_part + 1.0 * (1.0 / L);
+#if PCP_SCORE_ULP   // parity-bar check builds only: the score of every PCP_SCORE_ULP-th cell
+                    // one ulp up (make perturb: every cell; make perturb8: every 8th)
+    if (cell % PCP_SCORE_ULP == 0) return fmax(0.0, nextafter(score, INFINITY));
+#else
+    (void)cell;
+#endif
+    return fmax(0.0, score);
+}
+
 // result bits: 1 = in_range, 2 = in_fov (valid if in_range), 4 = visible (valid if both)
 // G > 1: the G lanes of an aligned lane group evaluate the same (pose, cell), each marching the
 // samples koff (mod G) (march's koff / kstr); every lane returns the same result
-template <int G = 1>
+// STATS (pcp_score_poses_stats): the march's probes / walk starts / point tests into cnt[0..2]
+// DEFER: a visible cell returns -1 with its cosine and distance in *ad_out / *L_out, for the
+// caller to score (k_score_cells gathers its block's visible cells into one queue, so the
+// correctly rounded acos / sin run in as few waves as there are visible cells / 64)
+template <int G = 1, bool STATS = false, bool DEFER = false>
 __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double py, double pz,
                                             double pitch, double cx, double cy, double cz,
                                             float nx, float ny, float nz, bool is_zx120,
-                                            uint32_t &bits, const double *steps) {
+                                            uint32_t &bits, const double *steps,
+                                            uint32_t *cnt = nullptr, int cell = 0,
+                                            double *ad_out = nullptr, double *L_out = nullptr) {
     const double dx = cx - px, dy = cy - py, dz = cz - pz;
     const double L = sqrt(dx * dx + dy * dy + dz * dz);
     bits = 0;
@@ -497,9 +529,9 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
                                                       steps, E.K, end, 1e30f, 1e15f) < 0;
 #else
         const int lane = threadIdx.x & 63;
-        const bool clear = march<false, true, PCP_CELL_PROBES, 2>(
+        const bool clear = march<STATS, true, PCP_CELL_PROBES, 2>(
                                E.terrain, px, py, pz, ndx, ndy, ndz, steps, E.K, end, E.r2_ray,
-                               E.rexit_ray, nullptr, G > 1 ? lane % G : 0, G) < 0;
+                               E.rexit_ray, cnt, G > 1 ? lane % G : 0, G) < 0;
         if (G > 1) {   // the group's lanes all reach here (same inputs, same branches)
             const uint64_t blocked = __ballot(!clear);
             visible = ((blocked >> (lane & ~(G - 1))) & ((1ull << G) - 1)) == 0;
@@ -511,13 +543,13 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
     if (!visible) return 0.0;
     bits |= 4u;
     const double dot = ndx * (double)nx + ndy * (double)ny + ndz * (double)nz;
-    const double theta = acos(fmax(0.0, fmin(1.0, fabs(dot))));
-    const double score = 1.0 * sin(kPi / 2 - theta) + 1.0 * (1.0 / L);
-#if PCP_SCORE_ULP   // parity-bar check build only (make perturb): every cell score one ulp up
-    return fmax(0.0, nextafter(score, INFINITY));
-#else
-    return fmax(0.0, score);
-#endif
+    const double ad = fmax(0.0, fmin(1.0, fabs(dot)));
+    if (DEFER) {
+        *ad_out = ad;
+        *L_out = L;
+        return -1.0;
+    }
+    return score_finish(score_sin_part(ad), L, cell);
 }
 
 // one thread per (cell c, row r): rows r < P are the candidate poses (evaluatePosition's
@@ -537,7 +569,7 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
               double *__restrict__ sm_out, uint8_t *__restrict__ mbits,
               double *__restrict__ score_z, uint8_t *__restrict__ zbits,
               int32_t *__restrict__ stats, const uint32_t *__restrict__ P_dev,
-              const uint32_t *__restrict__ C_dev) {
+              const uint32_t *__restrict__ C_dev, CrList cr) {
     const int c = blockIdx.x * kT + threadIdx.x;
     // the colour-statistics slots k_cell_flags accumulates into (it runs after this kernel)
     if (stats && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) stats[threadIdx.x] = 0;
@@ -556,15 +588,86 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
     if (P_dev && !zrow && p >= (int)*P_dev) return;
     const double *Q = zrow ? zx5 : poses5 + 5 * (size_t)p;
     uint32_t bits;
-    const double s = eval_cell(E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1],
-                               cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], zrow, bits,
-                               steps);
+    double ad = 0.0, L = 0.0;
+    double s = eval_cell<1, false, PCP_SCORE_CR_PASS != 0>(
+        E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1], cxyz[3 * c + 2], cn[3 * c],
+        cn[3 * c + 1], cn[3 * c + 2], zrow, bits, steps, nullptr, c, &ad, &L);
+    // a visible cell's score is k_score_cr's: the wave's visible lanes take consecutive slots of
+    // the block's list (one atomic per wave); the score stays as written below until then
+    const bool vis = s < 0.0;
+    const uint64_t bal = __ballot(vis);
+    if (bal) {
+        const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)bal) - 1;
+        const uint32_t blk = blockIdx.y * gridDim.x + blockIdx.x;
+        uint32_t base = 0;
+        if (lane == first) base = atomicAdd(&cr.cnt[blk], (uint32_t)__popcll(bal));
+        base = (uint32_t)__shfl(base, first, 64);
+        if (vis) {
+            const size_t e = (size_t)blk * kT + base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+            cr.cell[e] = (uint32_t)c;
+            cr.ad[e] = ad;
+            cr.L[e] = L;
+            s = 0.0;
+        }
+    }
     if (zrow) {
         score_z[c] = s;
         zbits[c] = (uint8_t)bits;
     } else {
         sm_out[(size_t)p * C + c] = s;
         mbits[(size_t)p * C + c] = (uint8_t)bits;
+    }
+}
+
+// The visible cells' scores (evaluateCellScore :689-700 with the correctly rounded acos / sin):
+// one wave per k_score_cells block, its list entries packed into whole lanes, so the
+// double-double work runs once per 64 visible cells instead of once per wave holding one
+__global__ void __launch_bounds__(64)
+k_score_cr(CrList cr, int C, int P, double *__restrict__ sm_out, double *__restrict__ score_z) {
+    const uint32_t blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t n = cr.cnt[blk];
+    const int p = blockIdx.y;
+    for (uint32_t j = threadIdx.x; j < n; j += 64) {
+        const size_t e = (size_t)blk * kT + j;
+        const int c = (int)cr.cell[e];
+        const double s = score_finish(score_sin_part(cr.ad[e]), cr.L[e], c);
+        if (p == P) score_z[c] = s;
+        else sm_out[(size_t)p * C + c] = s;
+    }
+    if (threadIdx.x == 0 && n) cr.cnt[blk] = 0u;   // zero for the next query's k_score_cells
+}
+
+// Diagnostic twin of k_score_cells (pcp_score_poses_stats; never timed): the same rows and the
+// same march, counting per launch the gather lane-loads its visibility rays issue -- z-band
+// probes (2-byte thresholds), candidates' walk starts (4 bytes), point records (12 bytes) --
+// into stats[0..2] (u64, one atomic per wave and counter).  No scores are written.
+template <bool SL>
+__global__ void __launch_bounds__(kT)
+k_score_cells_stats(VisEnv E, const double *__restrict__ cxyz, const float *__restrict__ cn,
+                    int C, const double *__restrict__ poses5, int P,
+                    const double *__restrict__ zx5, unsigned long long *__restrict__ stats) {
+    const int c = blockIdx.x * kT + threadIdx.x;
+    __shared__ double s_steps[SL ? kStepLds : 1];
+    if (SL) {
+        for (int q = threadIdx.x; q < E.K; q += kT) s_steps[q] = E.steps[q];
+        __syncthreads();
+    }
+    const double *steps = SL ? s_steps : E.steps;
+    uint32_t cnt[4] = {0u, 0u, 0u, 0u};
+    if (c < C) {
+        const int p = blockIdx.y;
+        const double *Q = p == P ? zx5 : poses5 + 5 * (size_t)p;
+        uint32_t bits;
+        (void)eval_cell<1, true>(E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1],
+                                 cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], p == P,
+                                 bits, steps, cnt, c);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        unsigned long long v = cnt[i];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&stats[i], v);
     }
 }
 
@@ -597,7 +700,7 @@ k_score_cells_wide(VisEnv E, const double *__restrict__ cxyz, const float *__res
     uint32_t bits;
     const double s = eval_cell<G>(E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1],
                                   cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], zrow,
-                                  bits, steps);
+                                  bits, steps, nullptr, c);
     if ((threadIdx.x & (G - 1)) != 0) return;
     if (zrow) {
         score_z[c] = s;
@@ -1633,6 +1736,57 @@ static int ensure_steps(pcp_ctx *ctx, double end, int *K) {
 }  // extern "C"
 
 namespace pcp {
+// the production k_score_cells launch of a query (one lane per ray, or kWideG lanes per ray for
+// the few-ray queries of C1 / C5); score_enqueue and pcp_score_poses_burst
+static void launch_score_cells(hipStream_t st, pcp_ctx *ctx, const VisEnv &E, int C, int P,
+                               const double *poses_k, const double *zx_k, const ScoreEnq &o,
+                               double *score_z, const uint32_t *P_dev, const uint32_t *C_dev) {
+    const unsigned cb = (unsigned)((C + kT - 1) / kT);
+    const dim3 g(cb, (unsigned)(P + 1));
+    const bool wide = (uint64_t)(P + 1) * (uint64_t)C <= (uint64_t)kWideMaxRays && ctx->score_wide;
+    const dim3 gw((unsigned)(((uint64_t)C * kWideG + kT - 1) / kT), (unsigned)(P + 1));
+    const double *cx = ctx->cells_xyz.as<const double>();
+    const float *cn = ctx->cells_nrm.as<const float>();
+    if (wide && E.K <= kStepLds)
+        hipLaunchKernelGGL((k_score_cells_wide<true, kWideG>), gw, dim3(kT), 0, st, E, cx, cn, C,
+                           poses_k, P, zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev,
+                           C_dev);
+    else if (wide)
+        hipLaunchKernelGGL((k_score_cells_wide<false, kWideG>), gw, dim3(kT), 0, st, E, cx, cn, C,
+                           poses_k, P, zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev,
+                           C_dev);
+    else {
+        if (E.K <= kStepLds)
+            hipLaunchKernelGGL(k_score_cells<true>, g, dim3(kT), 0, st, E, cx, cn, C, poses_k, P,
+                               zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev,
+                               o.cr);
+        else
+            hipLaunchKernelGGL(k_score_cells<false>, g, dim3(kT), 0, st, E, cx, cn, C, poses_k, P,
+                               zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev,
+                               o.cr);
+        if (PCP_SCORE_CR_PASS)
+            hipLaunchKernelGGL(k_score_cr, g, dim3(64), 0, st, o.cr, C, P, o.comb, score_z);
+    }
+}
+
+// the list k_score_cells / k_score_cr share: one slot per ray of the grid, per-block counts
+// zeroed when (re)allocated (afterwards k_score_cr leaves them zero)
+static int cr_ensure(pcp_ctx *ctx, int C, int P, CrList &cr) {
+    const size_t nblk = (size_t)((C + kT - 1) / kT) * (size_t)(P + 1);
+    const size_t cap0 = ctx->cr_cnt.cap;
+    PCP_HIP(ctx, ctx->cr_cnt.ensure(nblk * sizeof(uint32_t) + 64));
+    if (ctx->cr_cnt.cap != cap0)
+        PCP_HIP(ctx, hipMemsetAsync(ctx->cr_cnt.p, 0, ctx->cr_cnt.cap, ctx->stream));
+    const size_t ne = nblk * kT;
+    PCP_HIP(ctx, ctx->cr_list.ensure(ne * (sizeof(uint32_t) + 2 * sizeof(double)) + 256));
+    char *b = ctx->cr_list.as<char>();
+    cr.cnt = ctx->cr_cnt.as<uint32_t>();
+    cr.ad = reinterpret_cast<double *>(b);
+    cr.L = cr.ad + ne;
+    cr.cell = reinterpret_cast<uint32_t *>(cr.L + ne);
+    return PCP_OK;
+}
+
 // runOptimization's scoring up to the per-pose sums, enqueued on ctx->stream: poses + the
 // zx120 pose uploaded through the pinned block, k_score_cells (rows 0..P-1 = poses, row P =
 // zx120), k_row_sum.  On return the device holds comb/mbits [P][C], zbits [C], tot_d/cov_d
@@ -1708,34 +1862,13 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
     const double *poses_k = reinterpret_cast<const double *>(pose_blk);
     const double *zx_k = poses_k + 5 * (size_t)P;
     if (poses_dev) poses_k = poses_dev;   // (the zx120 pose stays in the block)
-    const unsigned cb = (unsigned)((C + kT - 1) / kT);
+    o.poses_k = poses_k;
+    o.zx_k = zx_k;
+    if (C && (rc = cr_ensure(ctx, C, P, o.cr))) return rc;
     if (C) {
         {
             ProfScope ps(ctx, PCP_K_SCORE_CELLS);
-            const dim3 g(cb, (unsigned)(P + 1));
-            const bool wide = (uint64_t)(P + 1) * (uint64_t)C <= (uint64_t)kWideMaxRays &&
-                              ctx->score_wide;
-            const dim3 gw((unsigned)(((uint64_t)C * kWideG + kT - 1) / kT), (unsigned)(P + 1));
-            if (wide && E.K <= kStepLds)
-                hipLaunchKernelGGL((k_score_cells_wide<true, kWideG>), gw, dim3(kT), 0, st, E,
-                                   ctx->cells_xyz.as<const double>(),
-                                   ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
-                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
-            else if (wide)
-                hipLaunchKernelGGL((k_score_cells_wide<false, kWideG>), gw, dim3(kT), 0, st, E,
-                                   ctx->cells_xyz.as<const double>(),
-                                   ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
-                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
-            else if (E.K <= kStepLds)
-                hipLaunchKernelGGL(k_score_cells<true>, g, dim3(kT), 0, st, E,
-                                   ctx->cells_xyz.as<const double>(),
-                                   ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
-                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
-            else
-                hipLaunchKernelGGL(k_score_cells<false>, g, dim3(kT), 0, st, E,
-                                   ctx->cells_xyz.as<const double>(),
-                                   ctx->cells_nrm.as<const float>(), C, poses_k, P, zx_k,
-                                   o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
+            launch_score_cells(st, ctx, E, C, P, poses_k, zx_k, o, score_z, P_dev, C_dev);
             PCP_CHECK_LAUNCH(ctx);
         }
         o.score_z = score_z;
@@ -1831,6 +1964,104 @@ int pcp_score_poses(pcp_ctx *ctx, const double *poses5, uint64_t n, const double
     }
     fill_report(st_h, tot_h[P], best_idx, best, rep);
     return PCP_OK;
+}
+
+// the roofline's inputs for the reference's own ray march (k_score_cells): the query's
+// production launch set up by score_enqueue, then either its lane-loads counted by the STATS
+// twin or the production launch `reps` times back-to-back between two events
+static int score_diag(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
+                      const pcp_vl_params *p, uint64_t *stats, int reps, double *ms) {
+    if (!ctx) return PCP_E_INVALID;
+    if (int rc = area_finish(ctx)) return rc;
+    if (!zx || !p || (n && !poses5))
+        return set_err(ctx, PCP_E_INVALID, "pcp_score_poses_stats/burst: null argument");
+    if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_score_poses_stats/burst: too many poses");
+    ScoreEnq o;
+    if (int rc = score_enqueue(ctx, poses5, n, zx, p, o)) return rc;
+    hipStream_t st = ctx->stream;
+    const int C = o.C, P = o.P;
+    int K = 0;
+    if (int rc = ensure_steps(ctx, p->max_distance - kVisRadius, &K)) return rc;
+    const VisEnv E = make_env(ctx, p, ctx->steps_d.as<const double>(), K);
+    if (stats) {
+        PCP_HIP(ctx, ctx->stats_d.ensure(4 * sizeof(unsigned long long) + 64));
+        unsigned long long *sd = ctx->stats_d.as<unsigned long long>();
+        PCP_HIP(ctx, hipMemsetAsync(sd, 0, 4 * sizeof(unsigned long long), st));
+        if (C) {
+            const dim3 g((unsigned)((C + kT - 1) / kT), (unsigned)(P + 1));
+            if (E.K <= kStepLds)
+                hipLaunchKernelGGL(k_score_cells_stats<true>, g, dim3(kT), 0, st, E,
+                                   ctx->cells_xyz.as<const double>(),
+                                   ctx->cells_nrm.as<const float>(), C, o.poses_k, P, o.zx_k, sd);
+            else
+                hipLaunchKernelGGL(k_score_cells_stats<false>, g, dim3(kT), 0, st, E,
+                                   ctx->cells_xyz.as<const double>(),
+                                   ctx->cells_nrm.as<const float>(), C, o.poses_k, P, o.zx_k, sd);
+            PCP_CHECK_LAUNCH(ctx);
+        }
+        unsigned long long h[4] = {0, 0, 0, 0};
+        PCP_HIP(ctx, hipMemcpyAsync(h, sd, sizeof(h), hipMemcpyDeviceToHost, st));
+        PCP_HIP(ctx, hipStreamSynchronize(st));
+        for (int i = 0; i < 4; ++i) stats[i] = h[i];
+    }
+    if (ms) {
+        *ms = 0.0;
+        hipEvent_t a = nullptr, b = nullptr;
+        PCP_HIP(ctx, hipEventCreate(&a));
+        PCP_HIP(ctx, hipEventCreate(&b));
+        hipError_t e = hipEventRecord(a, st);
+        for (int r = 0; r < reps && e == hipSuccess && C; ++r) {
+            launch_score_cells(st, ctx, E, C, P, o.poses_k, o.zx_k, o, o.score_z, nullptr, nullptr);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventRecord(b, st);
+        if (e == hipSuccess) e = hipEventSynchronize(b);
+        float t = 0.0f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&t, a, b);
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+        if (e != hipSuccess) return hip_fail(ctx, e, "pcp_score_poses_burst", __FILE__, __LINE__);
+        *ms = (double)t / reps;
+    }
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    prof_resolve(ctx);
+    return PCP_OK;
+}
+
+int pcp_score_matrix(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
+                     const pcp_vl_params *p, double *score_mobile, double *score_zx120) {
+    if (!ctx) return PCP_E_INVALID;
+    if (int rc = area_finish(ctx)) return rc;
+    if (!zx || !p || (n && !poses5) || (ctx->n_cells && (!score_zx120 || (n && !score_mobile))))
+        return set_err(ctx, PCP_E_INVALID, "pcp_score_matrix: null argument");
+    if (n > 65535) return set_err(ctx, PCP_E_INVALID, "pcp_score_matrix: too many poses");
+    ScoreEnq o;
+    if (int rc = score_enqueue(ctx, poses5, n, zx, p, o)) return rc;
+    hipStream_t st = ctx->stream;
+    const size_t C = (size_t)o.C, P = (size_t)o.P;
+    if (C) {
+        if (P)
+            PCP_HIP(ctx, hipMemcpyAsync(score_mobile, o.comb, P * C * sizeof(double),
+                                        hipMemcpyDeviceToHost, st));
+        PCP_HIP(ctx, hipMemcpyAsync(score_zx120, o.score_z, C * sizeof(double),
+                                    hipMemcpyDeviceToHost, st));
+    }
+    PCP_HIP(ctx, hipStreamSynchronize(st));
+    prof_resolve(ctx);
+    return PCP_OK;
+}
+
+int pcp_score_poses_stats(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
+                          const pcp_vl_params *p, uint64_t stats[4]) {
+    if (!ctx || !stats) return PCP_E_INVALID;
+    stats[0] = stats[1] = stats[2] = stats[3] = 0;
+    return score_diag(ctx, poses5, n, zx, p, stats, 0, nullptr);
+}
+
+int pcp_score_poses_burst(pcp_ctx *ctx, const double *poses5, uint64_t n, const double zx[5],
+                          const pcp_vl_params *p, int reps, double *ms_per_launch) {
+    if (!ctx || !ms_per_launch || reps <= 0) return PCP_E_INVALID;
+    return score_diag(ctx, poses5, n, zx, p, nullptr, reps, ms_per_launch);
 }
 
 int pcp_generate_and_score(pcp_ctx *ctx, const double bb[6], const pcp_vl_params *p,

@@ -10,7 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "crmath_extra.h"
+#include "pcp_crmath.h"
 
 static uint64_t s = 0x9E3779B97F4A7C15ull;
 static uint64_t rnd(void) {
@@ -75,5 +75,24 @@ int main(int argc, char **argv) {
     }
     printf("acos %ld %ld 0\n", n, bad_acos);
     printf("sin %ld %ld 0\n", n, bad_sin);
+    /* the scoring's composite (pcp_score_sin_part, round 6): against glibc's
+     * sin(M_PI / 2 - acos(d)), and phase 1's decisions against phase 2's (the exact path) */
+    long bad_spa = 0, disagree = 0, slow = 0;
+    for (long i = 0; i < n; ++i) {
+        const int kind = (int)(i % 4);
+        const double d = kind == 0 ? uni(0x1p-20, 0.01) : kind == 3 ? uni(0.99, 1.0) : uni(0.0, 1.0);
+        if (!(d > 0.0 && d < 1.0)) continue;
+        const double ga = acos(d);
+        const double g = sin(M_PI / 2 - ga);
+        const int pick = (int)(rnd() % 3);
+        const double r0 = pick == 0 ? nextafter(ga, -INFINITY) : pick == 2 ? nextafter(ga, INFINITY) : ga;
+        int ph = 0;
+        const double got = pcp_score_sin_part(d, r0, &ph);
+        const double exact = pcp_cr_sin(1.5707963267948966 - pcp_cr_acos_fix(d, r0));
+        if (memcmp(&got, &g, 8) != 0) ++bad_spa;
+        if (memcmp(&got, &exact, 8) != 0) ++disagree;
+        if (ph != 1) ++slow;
+    }
+    printf("spa %ld %ld %ld %ld\n", n, bad_spa, disagree, slow);
     return 0;
 }

@@ -6,10 +6,15 @@ import math
 
 import numpy as np
 
-TOTAL_MAX_ULPS = 4          # per total: twice the census's largest gap
-# totals not bit-identical: the census's 3-5 % on the 91-1,418-candidate ticks, up to 5 of 32
-# (16 %) on the small area test's tick -- a one-ulp error of every cell score moves nearly all
-TOTAL_DIFFER_FRAC = 0.25
+TOTAL_MAX_ULPS = 2          # per total
+# totals not bit-identical: round 6 scores with correctly rounded acos / sin (pcp_crmath.h), as
+# glibc rounds them but for rare near ties -- 0 of 91 totals differ on the 91-candidate tick and
+# on the C5 frames (with ocml's acos / sin it was 2-20 %).  At most 5 % (at least 2) may differ;
+# the bar fails a one-ulp error of every cell score (make perturb: 61 of 91) and of every 8th
+# cell's (make perturb8: 10 of 91) -- test_parity_bar_catches_one_ulp.  The per-cell bar below
+# sees the same drifts cell by cell.
+TOTAL_DIFFER_FRAC = 0.05
+TOTAL_DIFFER_FLOOR = 2
 
 
 def ulps(a, b) -> np.ndarray:
@@ -28,7 +33,7 @@ def totals_report(got, ref) -> dict:
     d = ulps(got, ref) if got.size else np.zeros(0)
     return {"n": int(got.size), "max_ulps": float(d.max()) if d.size else 0.0,
             "differ": int((d != 0).sum()),
-            "allowed_differ": max(2, math.ceil(TOTAL_DIFFER_FRAC * got.size))}
+            "allowed_differ": max(TOTAL_DIFFER_FLOOR, math.ceil(TOTAL_DIFFER_FRAC * got.size))}
 
 
 def totals_match(got, ref) -> bool:
@@ -49,3 +54,16 @@ def assert_angles(got, ref):
     d = ulps(got, ref)
     assert d.max(initial=0) <= 1 and int((d != 0).sum()) <= ANGLE_DIFFER_MAX, \
         (int((d != 0).sum()), d.max(initial=0))
+
+
+# per-cell bar (evaluateCellScore values, test_parity_bar_per_cell / the C5 frames): glibc's
+# near-tie misroundings leave 0.16-0.17 % of the positive cell scores off by 1-4 ulps (round 6,
+# both ways, 2:1 downward); at most 1 % may differ, by at most 8 ulps each.  make perturb8 moves
+# 12.5 % of the cells, make perturb all of them.
+CELL_MAX_ULPS = 8
+CELL_DIFFER_FRAC = 0.01
+
+
+def cell_bar(census: dict) -> bool:
+    return (census["max_ulps"] <= CELL_MAX_ULPS
+            and census["differ"] <= max(5, CELL_DIFFER_FRAC * census["positive"]))

@@ -51,5 +51,13 @@ def test_bench_parity_helpers():
     t = np.linspace(1.0, 2.0, 40)
     assert bench._totals_bar(t, t)["ok"] and parity.totals_match(t, t)
     t2 = t.copy()
-    t2[:12] = np.nextafter(t2[:12], 3.0)   # 12 of 40 differ: past max(2, 25 %)
+    t2[:12] = np.nextafter(t2[:12], 3.0)   # 12 of 40 differ: past max(2, 5 %)
     assert not bench._totals_bar(t2, t)["ok"] and not parity.totals_match(t2, t)
+    t3 = t.copy()
+    t3[:2] = np.nextafter(t3[:2], 3.0)     # 2 of 40: at the bar
+    assert bench._totals_bar(t3, t)["ok"] and parity.totals_match(t3, t)
+    t3[2] = np.nextafter(t3[2], 3.0)       # 3 of 40 (7.5 %): past it
+    assert not bench._totals_bar(t3, t)["ok"] and not parity.totals_match(t3, t)
+    t4 = t.copy()
+    t4[0] = np.nextafter(np.nextafter(np.nextafter(t4[0], 3.0), 3.0), 3.0)   # one total 3 ulps
+    assert not bench._totals_bar(t4, t)["ok"] and not parity.totals_match(t4, t)

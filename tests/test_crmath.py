@@ -38,3 +38,8 @@ def test_cr_atan2_acos_sin_match_glibc_but_near_ties(checker):
     for fn in ("acos", "sin"):
         n, bad, _ = lines[fn]
         assert n == 4_000_000 and bad < 3e-3 * n, r.stdout
+    # the scoring's composite sin(M_PI / 2 - acos(d)) (pcp_score_sin_part, round 6): glibc's value
+    # but for its near ties; the fast phase never decides against the exact path (20 M
+    # arguments: 0 of 20,000,000), and hands fewer than 1e-3 of the arguments to it
+    n, bad, disagree, slow = lines["spa"]
+    assert n == 4_000_000 and bad < 3e-3 * n and disagree == 0 and slow < 1e-3 * n, r.stdout

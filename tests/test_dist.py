@@ -176,6 +176,15 @@ def test_bench_self_launch(n):
     # configs[3]: 4096 poses strong-scaled over the N ranks (not 256 per GPU)
     assert out["c4"]["poses_total"] == 4096 and out["c4"]["scaling"] == "strong"
     assert sum(out["c4"]["poses_per_rank"]) == 4096 and len(out["c4"]["poses_per_rank"]) == n
+    # a SCALE line's c4 checks itself: per-rank kernel times and their
+    # spread, the collective's time, the ranks RCCL saw (none in the gloo rehearsal), the runtime
+    c4 = out["c4"]
+    for k in ("kernel_ms_per_rank", "kernel_ms_max", "kernel_ms_min", "collective_ms",
+              "rccl_nranks", "runtime"):
+        assert k in c4, k
+    assert len(c4["kernel_ms_per_rank"]) == n
+    assert c4["rccl_nranks"] == 0 and c4["collective_ms"] is None
+    assert c4["runtime"] is None or "hip_runtime_version" in c4["runtime"]
 
 
 def test_bench_rejects_mismatched_world():

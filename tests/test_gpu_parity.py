@@ -912,14 +912,16 @@ def test_terrain_replaced_after_block_copy(oracle, small_scene, scene):
 
 
 def _rel_close(a, b):
-    """The totals' parity bar (tests/parity.py): every value within 4 ulps of the oracle's and
-    at most max(2, 25 %) of them not bit-identical -- the census's 3-5 %, <= 2 ulps (was a
+    """The totals' parity bar (tests/parity.py): every value within 2 ulps of the oracle's and
+    at most max(5, 10 %) of them not bit-identical -- the census's 3-5 %, <= 2 ulps (was a
     1e-12 relative tolerance, ~2,600x looser than the kernels' results)."""
     return parity.totals_match(a, b)
 
 
 PERTURB_LIB = Path(__file__).resolve().parents[1] / "pointcloud_processor_amd" / "_lib" / \
     "perturb" / "libpcp.so"
+PERTURB8_LIB = Path(__file__).resolve().parents[1] / "pointcloud_processor_amd" / "_lib" / \
+    "perturb8" / "libpcp.so"
 
 
 def test_parity_bar_catches_one_ulp(oracle, loaded, scene, cells, aux):
@@ -928,11 +930,13 @@ def test_parity_bar_catches_one_ulp(oracle, loaded, scene, cells, aux):
     else the production objects) fails it on the 91-candidate tick, the production build passes
     it on the same inputs, and the flags / covered counts / best index stay equal (only the
     totals' bits can show such an error)."""
-    assert PERTURB_LIB.exists(), "build first (__graft_entry__.build(): make perturb)"
+    assert PERTURB_LIB.exists() and PERTURB8_LIB.exists(), \
+        "build first (__graft_entry__.build(): make perturb perturb8)"
     T, A = loaded
     params = _abi.default_vl_params()
     res = {}
-    for tag, path in (("prod", None), ("perturbed", str(PERTURB_LIB))):
+    for tag, path in (("prod", None), ("perturbed", str(PERTURB_LIB)),
+                      ("perturbed8", str(PERTURB8_LIB))):
         with _abi.Context(0, lib_path=path) as ctx:
             ctx.set_terrain(scene.terrain, point_step=32)
             ctx.set_aux_cloud(aux, point_step=32)
@@ -945,13 +949,15 @@ def test_parity_bar_catches_one_ulp(oracle, loaded, scene, cells, aux):
     r_tot, r_cov, r_rep = oracle.score_poses(T, A, cells.xyz, cells.normals, poses,
                                              scene.zx120_pose5, oracle.vl_params(),
                                              np.zeros(cells.xyz.shape[0], np.uint8))
-    prod, bad = parity.totals_report(res["prod"][1], r_tot), \
-        parity.totals_report(res["perturbed"][1], r_tot)
-    print("parity bar: production", prod, "one-ulp perturbed", bad)
+    prod = parity.totals_report(res["prod"][1], r_tot)
+    print("parity bar: production", prod)
     assert parity.totals_match(res["prod"][1], r_tot), prod
-    assert not parity.totals_match(res["perturbed"][1], r_tot), bad
-    np.testing.assert_array_equal(res["perturbed"][2], r_cov)
-    assert res["perturbed"][3] == r_rep.best_idx == res["prod"][3]
+    for tag in ("perturbed", "perturbed8"):   # every cell / every 8th cell one ulp up
+        bad = parity.totals_report(res[tag][1], r_tot)
+        print("parity bar:", tag, bad)
+        assert not parity.totals_match(res[tag][1], r_tot), (tag, bad)
+        np.testing.assert_array_equal(res[tag][2], r_cov)
+        assert res[tag][3] == r_rep.best_idx == res["prod"][3]
 
 
 def test_score_poses_matches_reference_loop(gpu, oracle, loaded, scene, cells):
@@ -1905,6 +1911,99 @@ def test_score_allreduce_own_communicator(oracle, loaded, scene, cells, aux):
         b_ref, _, _, best_ref = ctx.raycast_fan(poses, fan)
         np.testing.assert_array_equal(bl, b_ref[:P])
         assert best == best_ref
+
+
+@pytest.mark.parametrize("onepass", ["1", "0"])
+def test_exclusive_scan_tile_boundaries(onepass, monkeypatch):
+    """the index builds' device scan on its own.  Back-to-back scans sized to 1, 2,
+    63, 64 (the one-pass look-back's largest) and 65 (three launches) tiles of 2,048, growing
+    and shrinking (the look-back state regrows, the epoch and ticket advance), each equal to
+    numpy's, with PCP_SCAN_ONEPASS=1 (default) and 0."""
+    monkeypatch.setenv("PCP_SCAN_ONEPASS", onepass)
+    rng = np.random.default_rng(11)
+    with _abi.Context(0) as ctx:
+        for tiles in (1, 2, 63, 64, 65, 2, 64, 3, 200, 64, 1):
+            for n in (tiles * 2048, tiles * 2048 - 5):
+                if n <= 0:
+                    continue
+                a = rng.integers(0, 1000, n, dtype=np.uint32)
+                ref = np.zeros(n + 1, np.uint64)
+                ref[1:] = np.cumsum(a, dtype=np.uint64)
+                got = ctx.debug_exclusive_scan(a)
+                np.testing.assert_array_equal(got, ref.astype(np.uint32)), (tiles, n)
+
+
+def _cell_census(got_sm, got_sz, ref_sm, ref_sz):
+    """Per-cell comparison of evaluateCellScore values: cells whose score differs, by how many
+    ulps, and the signed balance of the differences (a systematic drift leans one way)."""
+    g = np.concatenate([got_sm.ravel(), got_sz])
+    r = np.concatenate([ref_sm.ravel(), ref_sz])
+    d = parity.ulps(g, r)
+    pos = r > 0
+    up = int(((g > r) & (d > 0)).sum())
+    return {"cells": int(g.size), "positive": int(pos.sum()), "differ": int((d > 0).sum()),
+            "up": up, "down": int((d > 0).sum()) - up, "max_ulps": float(d.max(initial=0)),
+            "zero_mismatch": int(((g > 0) != pos).sum())}
+
+
+def test_parity_bar_per_cell(oracle, loaded, scene, cells, aux):
+    """VERDICT r5 item 5, at the cells: evaluateCellScore per (pose, cell) on the device
+    (pcp_score_matrix) against the oracle's (orc_score_matrix) on the 91-candidate tick.  The
+    production build rounds acos / sin correctly (pcp_crmath.h), as glibc does but for its rare
+    near ties: 0.16 % of the positive cell scores differ, by 1-4 ulps (ocml's own functions
+    left 9 %, up to 8 ulps); the `make perturb` (every cell) and `make perturb8` (every 8th cell)
+    builds fail the per-cell bar (tests/parity.py: cell_bar)."""
+    T, A = loaded
+    params = _abi.default_vl_params()
+    zx = np.ascontiguousarray(scene.zx120_pose5, np.float64)
+    res = {}
+    for tag, path in (("prod", None), ("perturbed", str(PERTURB_LIB)),
+                      ("perturbed8", str(PERTURB8_LIB))):
+        with _abi.Context(0, lib_path=path) as ctx:
+            ctx.set_terrain(scene.terrain, point_step=32)
+            ctx.set_aux_cloud(aux, point_step=32)
+            ctx.set_cells(cells.xyz, cells.normals)
+            poses = ctx.generate_candidates(cells.grid_bbox, params, scene.zx120_pose5)
+            res[tag] = (poses, ctx.score_matrix(poses, zx, params))
+    poses = res["prod"][0]
+    r_sm, r_sz = oracle.score_matrix(T, A, cells.xyz, cells.normals, poses, scene.zx120_pose5,
+                                     oracle.vl_params())
+    for tag in res:
+        np.testing.assert_array_equal(res[tag][0], poses)
+        cen = _cell_census(*res[tag][1], r_sm, r_sz)
+        print("cell census", tag, cen, parity.cell_bar(cen))
+        assert cen["zero_mismatch"] == 0
+        assert parity.cell_bar(cen) == (tag == "prod"), (tag, cen)
+
+
+def test_score_stats_and_burst(loaded, scene, cells, aux):
+    """The reference-mode roofline's inputs: pcp_score_poses_stats counts
+    the visibility rays' gather lane-loads with a twin of k_score_cells -- deterministic, every
+    walk start follows a probe, the fine-window copy needs no directory loads -- and
+    pcp_score_poses_burst times the production launch; neither touches the caller's flags nor
+    changes the next query's results."""
+    params = _abi.default_vl_params()
+    zx = np.ascontiguousarray(scene.zx120_pose5, np.float64)
+    with _abi.Context(0) as ctx:
+        ctx.set_terrain(scene.terrain, point_step=32)
+        ctx.set_aux_cloud(aux, point_step=32)
+        ctx.set_cells(cells.xyz, cells.normals)
+        poses = ctx.generate_candidates(cells.grid_bbox, params, scene.zx120_pose5)
+        C = cells.xyz.shape[0]
+        t0, c0, r0 = ctx.score_poses(poses, zx, params, np.zeros(C, np.uint8))
+        st = ctx.score_poses_stats(poses, zx, params)
+        assert st == ctx.score_poses_stats(poses, zx, params)
+        assert st["probes"] >= st["walk_starts"] > 0 and st["point_tests"] > 0
+        assert st["directory_loads"] == 0
+        # more poses, more rays: the counts grow
+        st2 = ctx.score_poses_stats(np.concatenate([poses, poses]), zx, params)
+        assert st2["probes"] > st["probes"]
+        ms = ctx.score_poses_burst(poses, zx, params, reps=5)
+        assert ms > 0.0
+        t1, c1, r1 = ctx.score_poses(poses, zx, params, np.zeros(C, np.uint8))
+        np.testing.assert_array_equal(t1.view(np.uint64), t0.view(np.uint64))
+        np.testing.assert_array_equal(c1, c0)
+        assert r1.as_dict() == r0.as_dict()
 
 
 def test_fan_keys_wait_stream_then_fan(gpu, loaded, scene, oracle):

@@ -68,6 +68,28 @@ def test_golden_score(oracle):
 
 
 # ------------------------------------------------------------------------------ independent checks
+def test_score_matrix_sums_to_golden_totals(oracle):
+    """orc_score_matrix (the per-cell parity bar's reference values): evaluatePosition's ordered
+    sum of max(score_zx120, score_mobile) over the positive cells (:634-645), taken over the
+    matrix in cell order, is bit-identical to the golden totals, and the positive counts are the
+    covered counts."""
+    s = np.load(GOLD / "score.npz")
+    T, A = oracle.Cloud(s["terrain"]), oracle.Cloud(s["aux"])
+    vp = oracle.vl_params(max_distance=float(s["max_distance"]))
+    sm, sz = oracle.score_matrix(T, A, s["cells"], s["normals"], s["candidates"], s["zx"], vp)
+    comb = np.maximum(sm, sz[None, :])
+    tot = np.array([_seq_sum(row[row > 0]) for row in comb])
+    np.testing.assert_array_equal(tot, s["total"])
+    np.testing.assert_array_equal((comb > 0).sum(axis=1), s["covered"])
+
+
+def _seq_sum(v):
+    acc = 0.0
+    for x in v:
+        acc += float(x)
+    return acc
+
+
 def test_crop_vs_numpy(oracle):
     rng = np.random.default_rng(0)
     a = rng.uniform(-5, 20, (20000, 4)).astype(F32)

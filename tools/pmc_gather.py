@@ -2,7 +2,8 @@
 fractions and L1 tag lookups per launch from tools/pmc_fan.sh's rocprofv3 --pmc passes ->
 profiles/r05_fan_gather_path.json.  bench.py prints them as roofline.gather_path and marks them
 stale (gather_path_stale) when the tree's fan sources differ from the stamp.
-usage: python tools/pmc_gather.py OUT.json gpurun_out/pmcf_*"""
+usage: python tools/pmc_gather.py OUT.json [fan|cells] gpurun_out/pmcf_*
+(cells: reference mode's k_score_cells from tools/pmc_cells.sh's passes, stamped "cells")"""
 import csv
 import glob
 import json
@@ -14,10 +15,16 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 from pointcloud_processor_amd._stamps import workload_stamp  # noqa: E402
 
-KERNEL = "k_raycast_fan_xcd<0,"   # the production launch (MODE 0), not the stats variant
+KERNELS = {"fan": "k_raycast_fan_xcd<0,",   # the production launch (MODE 0), not the stats one
+           "cells": "k_score_cells<"}          # not k_score_cells_stats / _wide
+args = sys.argv[2:]
+WL = "fan"
+if args and args[0] in KERNELS:
+    WL, args = args[0], args[1:]
+KERNEL = KERNELS[WL]
 vals = defaultdict(list)
 kname = None
-for d in sys.argv[2:]:
+for d in args:
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             if KERNEL in row.get("Kernel_Name", ""):
@@ -28,7 +35,7 @@ n_cu, n_xcd = 256, 8
 cyc = mean["GRBM_GUI_ACTIVE"] / n_xcd   # GRBM_GUI_ACTIVE sums the XCDs' busy cycles
 out = {
     "kernel": kname,
-    "source_stamp": workload_stamp("fan"),
+    "source_stamp": workload_stamp(WL),
     "td_busy_frac": mean["TD_TD_BUSY_sum"] / n_cu / cyc,
     "ta_busy_frac": mean["TA_TA_BUSY_sum"] / n_cu / cyc,
     "ta_addr_stalled_by_tc_frac": mean.get("TA_ADDR_STALLED_BY_TC_CYCLES_sum", 0.0) / n_cu / cyc,
@@ -39,9 +46,12 @@ out = {
     "busy_cycles_per_xcd": cyc,
     "counters_mean_per_dispatch": mean,
     "dispatches_per_counter": {k: len(v) for k, v in vals.items()},
-    "note": "per launch; rocprofv3 --pmc passes of `bench.py --mode fan` (tools/pmc_fan.sh), busy "
+    "note": f"per launch; rocprofv3 --pmc passes of `bench.py --mode {WL}` (tools/pmc_{WL}.sh), busy "
             "fractions = *_BUSY_sum / 256 CUs / (GRBM_GUI_ACTIVE / 8 XCDs)",
 }
+if mean.get("SQ_WAVE_CYCLES"):
+    out["wave_wait_any_frac"] = mean.get("SQ_WAIT_ANY", 0.0) / mean["SQ_WAVE_CYCLES"]
+    out["wave_valu_active_frac"] = mean.get("SQ_ACTIVE_INST_VALU", 0.0) / mean["SQ_WAVE_CYCLES"]
 if out["vmem_read_instructions"] and out["l1_tag_lookups"]:
     out["tags_per_vmem_instruction"] = out["l1_tag_lookups"] / out["vmem_read_instructions"]
 Path(sys.argv[1]).write_text(json.dumps(out, indent=1) + "\n")
