@@ -724,8 +724,7 @@ void pcp_destroy(pcp_ctx *ctx) {
     ctx->area_host.release();
     DevBuf *bufs[] = {&ctx->cells_xyz, &ctx->cells_nrm, &ctx->cells_n_d, &ctx->stage, &ctx->fan_tab,
                       &ctx->poses_d,   &ctx->steps_d,   &ctx->out_a, &ctx->out_b,
-                      &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->cr_cnt,
-                      &ctx->cr_list,   &ctx->f_in,
+                      &ctx->out_c,     &ctx->out_d,     &ctx->stats_d, &ctx->f_in,
                       &ctx->f_misc,    &ctx->bk_stat};
     for (DevBuf *b : bufs) b->release();
     for (auto &b : ctx->scratch) b.release();

@@ -21,11 +21,14 @@
 #define PCP_CRMATH_H
 
 #include <math.h>
+#include <string.h>
 
 #if defined(__HIPCC__)
 #define PCP_CR static __host__ __device__ __forceinline__
+#define PCP_CR_COLD static __host__ __device__ __attribute__((noinline))
 #else
 #define PCP_CR static inline
+#define PCP_CR_COLD static __attribute__((noinline))
 #endif
 
 typedef struct {
@@ -254,62 +257,86 @@ PCP_CR void pcp_fast_sincos(double x, pcp_dd *s_out, pcp_dd *c_out) {
     *c_out = pcp_dd_add(pcp_dd_add(Ck, pcp_dd_mul(Ck, ct)), pcp_dd_neg(pcp_dd_mul(Sk, sint)));
 }
 
-/* the double nearest v = hi + lo (lo normalised below hi's ulp), if v lies more than
- * margin * |v| from a rounding boundary: *ok = 1; else *ok = 0 */
+/* neighbours of a positive finite double (bit steps; no call into libm) */
+PCP_CR double pcp_next_up(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __longlong_as_double(__double_as_longlong(x) + 1);
+#else
+    long long b;
+    memcpy(&b, &x, 8);
+    ++b;
+    memcpy(&x, &b, 8);
+    return x;
+#endif
+}
+PCP_CR double pcp_next_down(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __longlong_as_double(__double_as_longlong(x) - 1);
+#else
+    long long b;
+    memcpy(&b, &x, 8);
+    --b;
+    memcpy(&x, &b, 8);
+    return x;
+#endif
+}
+
+/* the double nearest v = hi + lo (v > 0, lo normalised below hi's ulp), if v lies more than
+ * margin * v from a rounding boundary: *ok = 1; else *ok = 0 */
 PCP_CR double pcp_round_dd_checked(pcp_dd v, double margin, int *ok) {
     const double R = v.hi + v.lo;
     const double res = (v.hi - R) + v.lo;   /* v - R */
-    const double half = 0.5 * (res > 0.0 ? nextafter(R, INFINITY) - R : R - nextafter(R, -INFINITY));
-    *ok = fabs(fabs(res) - fabs(half)) > margin * fabs(R);
+    const double half = 0.5 * (res > 0.0 ? pcp_next_up(R) - R : R - pcp_next_down(R));
+    *ok = fabs(fabs(res) - half) > margin * R;
     return R;
+}
+
+/* phase 2 (rare: one call, kept out of line so that its registers do not weigh on the fast
+ * path's occupancy) */
+PCP_CR_COLD double pcp_score_sin_part_exact(double d, double r) {
+    return pcp_cr_sin(1.5707963267948966 - pcp_cr_acos_fix(d, r));
 }
 
 /* evaluateCellScore's sin(M_PI / 2 - theta), theta = acos(d), as glibc evaluates it (both
  * functions rounded correctly), from a faithful first result r of acos(d).  phase_out
- * (nullable): 1 when phase 1 decided, 2 when phase 2 did */
+ * (nullable): 1 when phase 1 decided, 2 when phase 2 did.  Straight-line: every lane of a
+ * wave runs the same instructions but for the rare phase 2. */
 PCP_CR double pcp_score_sin_part(double d, double r, int *phase_out) {
-    const double P1 = 1.5707963267948966, P2 = 6.123233995736766e-17,
-                 P3 = -1.4973849048591698e-33;   /* pi / 2 = P1 + P2 + P3; M_PI / 2 == P1 */
+    const double P1 = 1.5707963267948966, P2 = 6.123233995736766e-17;   /* pi / 2 = P1 + P2 + ~1e-33 */
     if (phase_out) *phase_out = 2;
-    if (!(d > 0x1p-20 && d < 1.0) || !isfinite(r) || !(r > 0.0 && r < 1.6))
-        return pcp_cr_sin(P1 - pcp_cr_acos_fix(d, r));
+    if (!(d > 0x1p-20 && d < 1.0) || !(r > 0.0 && r < 1.6)) return pcp_score_sin_part_exact(d, r);
     pcp_dd S, C;
     pcp_fast_sincos(r, &S, &C);
-    const double lo = nextafter(r, -INFINITY), hi = nextafter(r, INFINITY);
-    double th = r;
-    for (int side = 0; side < 2; ++side) {
-        /* d - cos(r + h), cos(r + h) = C - h S - h^2 / 2 C (h half the gap to a neighbour) */
-        const double h = 0.5 * ((side ? hi : lo) - r);
-        pcp_dd cm = pcp_dd_add(C, pcp_dd_neg(pcp_dd_mul_d(S, h)));
-        cm = pcp_dd_add(cm, pcp_dd_make(-0.5 * h * h * C.hi, 0.0));
-        const pcp_dd e = pcp_dd_add(pcp_dd_make(d, 0.0), pcp_dd_neg(cm));
-        if (fabs(e.hi) <= PCP_CR_FAST_MARGIN) return pcp_cr_sin(P1 - pcp_cr_acos_fix(d, r));
-        if (side == 0 && e.hi > 0.0) { th = lo; break; }
-        if (side == 1 && e.hi < 0.0) { th = hi; break; }
-    }
-    pcp_dd St = S, Ct = C;
-    if (th != r) {   /* sin / cos at th = r + w: the w^3 terms are below 2^-150 */
-        const double w = th - r;
-        St = pcp_dd_add(pcp_dd_add(S, pcp_dd_mul_d(C, w)), pcp_dd_make(-0.5 * w * w * S.hi, 0.0));
-        Ct = pcp_dd_add(pcp_dd_add(C, pcp_dd_neg(pcp_dd_mul_d(S, w))),
-                        pcp_dd_make(-0.5 * w * w * C.hi, 0.0));
-    }
-    const double a = P1 - th;   /* the reference's argument, rounded */
-    if (a == 0.0) return 0.0;
+    /* d - cos(r + h) at both midpoints, cos(r + h) = C - S h - C h^2 / 2: d - C.hi is exact
+     * (Sterbenz: d ~ cos r), and the terms in h (|h| < 2^-53) are exact to ~2^-106 in double */
+    const double lo = pcp_next_down(r), hi = pcp_next_up(r);
+    const double hl = 0.5 * (lo - r), hh = 0.5 * (hi - r);
+    const double dCh = d - C.hi;
+    const double el = dCh + (S.hi * hl + (0.5 * hl * hl * C.hi - C.lo));
+    const double eh = dCh + (S.hi * hh + (0.5 * hh * hh * C.hi - C.lo));
+    if (fabs(el) <= PCP_CR_FAST_MARGIN || fabs(eh) <= PCP_CR_FAST_MARGIN)
+        return pcp_score_sin_part_exact(d, r);
+    /* acos decreases: d above cos(lower midpoint) -> lo; below cos(upper midpoint) -> hi */
+    const double th = el > 0.0 ? lo : (eh < 0.0 ? hi : r);
+    /* a = P1 - th rounded: P1 - th = a + e exactly, pi / 2 = P1 + P2 + P3, so
+     * a = pi / 2 - (th + e + P2 + P3) and sin(a) = cos(r + delta), delta = (th - r) + e + P2
+     * (|delta| < 2^-51; P3 and S.lo delta are below 2^-104): cos(r + delta) = C - S delta -
+     * C delta^2 / 2.  C's absolute error (~2^-84) is relative to sin(a) ~ a: below a = 2^-8,
+     * sin(a) = a + a^3 (-1/6 + a^2/120 - a^4/5040) directly (a exact; the correction's error
+     * is below 2^-71 of a, the a^9 term below 2^-90) */
+    const pcp_dd ea = pcp_two_sum(P1, -th);
+    const double a = ea.hi;
     pcp_dd v;
-    if (a < 0.25) {   /* small: sin(a) itself (no cancellation) */
-        pcp_dd ca;
-        pcp_fast_sincos(a, &v, &ca);
+    if (a < 0x1p-8) {
+        const double u = a * a;
+        v = pcp_fast_two_sum(a, a * u * (-1.0 / 6.0 + u * (1.0 / 120.0 + u * (-1.0 / 5040.0))));
     } else {
-        /* a = (pi / 2 - th) - eta, eta = (P1 - th - a) + P2 + P3: sin(a) = cos(th + eta)
-         * = Ct - St eta - Ct eta^2 / 2 (|eta| < 2^-52: the eta^2 term is below 2^-106) */
-        const pcp_dd ea = pcp_two_sum(P1, -th);
-        const pcp_dd eta = pcp_dd_add(pcp_dd_make(ea.lo, 0.0), pcp_dd_make(P2, P3));
-        v = pcp_dd_add(Ct, pcp_dd_neg(pcp_dd_mul(St, eta)));
+        const double delta = (th - r) + (ea.lo + P2);
+        v = pcp_fast_two_sum(C.hi, C.lo - (S.hi * delta + 0.5 * C.hi * delta * delta));
     }
     int ok = 0;
     const double R = pcp_round_dd_checked(v, PCP_CR_FAST_MARGIN_REL, &ok);
-    if (!ok) return pcp_cr_sin(a);
+    if (!ok) return pcp_score_sin_part_exact(d, r);
     if (phase_out) *phase_out = 1;
     return R;
 }

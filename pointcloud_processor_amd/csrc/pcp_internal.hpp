@@ -315,10 +315,6 @@ struct pcp_ctx {
     // scratch
     pcp::DevBuf stage, scratch[8];
     pcp::DevBuf fan_tab, poses_d, steps_d, out_a, out_b, out_c, out_d, stats_d;
-    // k_score_cells' visible cells, compacted per block, for k_score_cr (the correctly rounded
-    // acos / sin): per-block counts (zero between queries: k_score_cr resets what it read) and
-    // the entries {cell, cosine, distance} at block * 256 + slot
-    pcp::DevBuf cr_cnt, cr_list;
     pcp::PinnedBuf fan_host;                 // pinned staging of poses in / counts out
     pcp::PinnedBuf res_host;                 // pinned landing of the filter chain's sizes
     pcp::PinnedBuf fm_res_host;              // pcp_filter_merge's result sizes, stored by its
@@ -507,16 +503,8 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
                 bool want_fh, bool stats, bool stamps, FanEnq &o, int burst = 0,
                 double *burst_ms = nullptr, bool host_out = false);
 
-// the visible cells k_score_cells leaves to k_score_cr (the correctly rounded acos / sin):
-// block b's at [b * 256, b * 256 + cnt[b]) (pcp_vlidar.hip)
-struct CrList {
-    uint32_t *cnt = nullptr;    // per block; k_score_cr resets what it reads
-    uint32_t *cell = nullptr;
-    double *ad = nullptr, *L = nullptr;   // clamped |cos| of the view angle, distance
-};
 // runOptimization's scoring up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip)
 struct ScoreEnq {
-    CrList cr;
     int P = 0, C = 0;
     double *comb = nullptr;        // [P][C] mobile scores
     double *score_z = nullptr;     // [C] zx120 scores

@@ -466,9 +466,7 @@ __device__ __forceinline__ double score_sin_part(double ad) {
     return pcp_score_sin_part(ad, acos(ad), nullptr);   // (two phases, pcp_crmath.h)
 #endif
 }
-#ifndef PCP_SCORE_CR_PASS
-#define PCP_SCORE_CR_PASS 1   // visible cells scored by k_score_cr (0: inline in k_score_cells)
-#endif
+
 __device__ __forceinline__ double score_finish(double sin_part, double L, int cell) {
     const double score = 1.0 * sin_part + 1.0 * (1.0 / L);
 #if PCP_SCORE_ULP   // parity-bar check builds only: the score of every PCP_SCORE_ULP-th cell
@@ -484,16 +482,12 @@ __device__ __forceinline__ double score_finish(double sin_part, double L, int ce
 // G > 1: the G lanes of an aligned lane group evaluate the same (pose, cell), each marching the
 // samples koff (mod G) (march's koff / kstr); every lane returns the same result
 // STATS (pcp_score_poses_stats): the march's probes / walk starts / point tests into cnt[0..2]
-// DEFER: a visible cell returns -1 with its cosine and distance in *ad_out / *L_out, for the
-// caller to score (k_score_cells gathers its block's visible cells into one queue, so the
-// correctly rounded acos / sin run in as few waves as there are visible cells / 64)
-template <int G = 1, bool STATS = false, bool DEFER = false>
+template <int G = 1, bool STATS = false>
 __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double py, double pz,
                                             double pitch, double cx, double cy, double cz,
                                             float nx, float ny, float nz, bool is_zx120,
                                             uint32_t &bits, const double *steps,
-                                            uint32_t *cnt = nullptr, int cell = 0,
-                                            double *ad_out = nullptr, double *L_out = nullptr) {
+                                            uint32_t *cnt = nullptr, int cell = 0) {
     const double dx = cx - px, dy = cy - py, dz = cz - pz;
     const double L = sqrt(dx * dx + dy * dy + dz * dz);
     bits = 0;
@@ -544,11 +538,6 @@ __device__ __forceinline__ double eval_cell(const VisEnv &E, double px, double p
     bits |= 4u;
     const double dot = ndx * (double)nx + ndy * (double)ny + ndz * (double)nz;
     const double ad = fmax(0.0, fmin(1.0, fabs(dot)));
-    if (DEFER) {
-        *ad_out = ad;
-        *L_out = L;
-        return -1.0;
-    }
     return score_finish(score_sin_part(ad), L, cell);
 }
 
@@ -569,7 +558,7 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
               double *__restrict__ sm_out, uint8_t *__restrict__ mbits,
               double *__restrict__ score_z, uint8_t *__restrict__ zbits,
               int32_t *__restrict__ stats, const uint32_t *__restrict__ P_dev,
-              const uint32_t *__restrict__ C_dev, CrList cr) {
+              const uint32_t *__restrict__ C_dev) {
     const int c = blockIdx.x * kT + threadIdx.x;
     // the colour-statistics slots k_cell_flags accumulates into (it runs after this kernel)
     if (stats && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) stats[threadIdx.x] = 0;
@@ -588,28 +577,9 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
     if (P_dev && !zrow && p >= (int)*P_dev) return;
     const double *Q = zrow ? zx5 : poses5 + 5 * (size_t)p;
     uint32_t bits;
-    double ad = 0.0, L = 0.0;
-    double s = eval_cell<1, false, PCP_SCORE_CR_PASS != 0>(
-        E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1], cxyz[3 * c + 2], cn[3 * c],
-        cn[3 * c + 1], cn[3 * c + 2], zrow, bits, steps, nullptr, c, &ad, &L);
-    // a visible cell's score is k_score_cr's: the wave's visible lanes take consecutive slots of
-    // the block's list (one atomic per wave); the score stays as written below until then
-    const bool vis = s < 0.0;
-    const uint64_t bal = __ballot(vis);
-    if (bal) {
-        const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)bal) - 1;
-        const uint32_t blk = blockIdx.y * gridDim.x + blockIdx.x;
-        uint32_t base = 0;
-        if (lane == first) base = atomicAdd(&cr.cnt[blk], (uint32_t)__popcll(bal));
-        base = (uint32_t)__shfl(base, first, 64);
-        if (vis) {
-            const size_t e = (size_t)blk * kT + base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-            cr.cell[e] = (uint32_t)c;
-            cr.ad[e] = ad;
-            cr.L[e] = L;
-            s = 0.0;
-        }
-    }
+    const double s = eval_cell(E, Q[0], Q[1], Q[2], Q[3], cxyz[3 * c], cxyz[3 * c + 1],
+                               cxyz[3 * c + 2], cn[3 * c], cn[3 * c + 1], cn[3 * c + 2], zrow, bits,
+                               steps, nullptr, c);
     if (zrow) {
         score_z[c] = s;
         zbits[c] = (uint8_t)bits;
@@ -617,24 +587,6 @@ k_score_cells(VisEnv E, const double *__restrict__ cxyz, const float *__restrict
         sm_out[(size_t)p * C + c] = s;
         mbits[(size_t)p * C + c] = (uint8_t)bits;
     }
-}
-
-// The visible cells' scores (evaluateCellScore :689-700 with the correctly rounded acos / sin):
-// one wave per k_score_cells block, its list entries packed into whole lanes, so the
-// double-double work runs once per 64 visible cells instead of once per wave holding one
-__global__ void __launch_bounds__(64)
-k_score_cr(CrList cr, int C, int P, double *__restrict__ sm_out, double *__restrict__ score_z) {
-    const uint32_t blk = blockIdx.y * gridDim.x + blockIdx.x;
-    const uint32_t n = cr.cnt[blk];
-    const int p = blockIdx.y;
-    for (uint32_t j = threadIdx.x; j < n; j += 64) {
-        const size_t e = (size_t)blk * kT + j;
-        const int c = (int)cr.cell[e];
-        const double s = score_finish(score_sin_part(cr.ad[e]), cr.L[e], c);
-        if (p == P) score_z[c] = s;
-        else sm_out[(size_t)p * C + c] = s;
-    }
-    if (threadIdx.x == 0 && n) cr.cnt[blk] = 0u;   // zero for the next query's k_score_cells
 }
 
 // Diagnostic twin of k_score_cells (pcp_score_poses_stats; never timed): the same rows and the
@@ -1755,36 +1707,12 @@ static void launch_score_cells(hipStream_t st, pcp_ctx *ctx, const VisEnv &E, in
         hipLaunchKernelGGL((k_score_cells_wide<false, kWideG>), gw, dim3(kT), 0, st, E, cx, cn, C,
                            poses_k, P, zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev,
                            C_dev);
-    else {
-        if (E.K <= kStepLds)
-            hipLaunchKernelGGL(k_score_cells<true>, g, dim3(kT), 0, st, E, cx, cn, C, poses_k, P,
-                               zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev,
-                               o.cr);
-        else
-            hipLaunchKernelGGL(k_score_cells<false>, g, dim3(kT), 0, st, E, cx, cn, C, poses_k, P,
-                               zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev,
-                               o.cr);
-        if (PCP_SCORE_CR_PASS)
-            hipLaunchKernelGGL(k_score_cr, g, dim3(64), 0, st, o.cr, C, P, o.comb, score_z);
-    }
-}
-
-// the list k_score_cells / k_score_cr share: one slot per ray of the grid, per-block counts
-// zeroed when (re)allocated (afterwards k_score_cr leaves them zero)
-static int cr_ensure(pcp_ctx *ctx, int C, int P, CrList &cr) {
-    const size_t nblk = (size_t)((C + kT - 1) / kT) * (size_t)(P + 1);
-    const size_t cap0 = ctx->cr_cnt.cap;
-    PCP_HIP(ctx, ctx->cr_cnt.ensure(nblk * sizeof(uint32_t) + 64));
-    if (ctx->cr_cnt.cap != cap0)
-        PCP_HIP(ctx, hipMemsetAsync(ctx->cr_cnt.p, 0, ctx->cr_cnt.cap, ctx->stream));
-    const size_t ne = nblk * kT;
-    PCP_HIP(ctx, ctx->cr_list.ensure(ne * (sizeof(uint32_t) + 2 * sizeof(double)) + 256));
-    char *b = ctx->cr_list.as<char>();
-    cr.cnt = ctx->cr_cnt.as<uint32_t>();
-    cr.ad = reinterpret_cast<double *>(b);
-    cr.L = cr.ad + ne;
-    cr.cell = reinterpret_cast<uint32_t *>(cr.L + ne);
-    return PCP_OK;
+    else if (E.K <= kStepLds)
+        hipLaunchKernelGGL(k_score_cells<true>, g, dim3(kT), 0, st, E, cx, cn, C, poses_k, P, zx_k,
+                           o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
+    else
+        hipLaunchKernelGGL(k_score_cells<false>, g, dim3(kT), 0, st, E, cx, cn, C, poses_k, P,
+                           zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
 }
 
 // runOptimization's scoring up to the per-pose sums, enqueued on ctx->stream: poses + the
@@ -1864,7 +1792,6 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
     if (poses_dev) poses_k = poses_dev;   // (the zx120 pose stays in the block)
     o.poses_k = poses_k;
     o.zx_k = zx_k;
-    if (C && (rc = cr_ensure(ctx, C, P, o.cr))) return rc;
     if (C) {
         {
             ProfScope ps(ctx, PCP_K_SCORE_CELLS);
