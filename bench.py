@@ -158,8 +158,8 @@ def _grid_bbox(area, res=0.1):
                      p[:, 1].max() + res, p[:, 2].min() - res, p[:, 2].max() + res])
 
 
-TRAFFIC_FILES = ("r05_pmc_traffic.json", "r04_pmc_traffic.json", "r03_pmc_traffic.json",
-                 "pmc_traffic.json")
+TRAFFIC_FILES = ("r06_pmc_traffic.json", "r05_pmc_traffic.json", "r04_pmc_traffic.json",
+                 "r03_pmc_traffic.json", "pmc_traffic.json")
 
 
 def _traffic_from_profiles(workload_key: str):
@@ -408,16 +408,18 @@ def _profiled(ctx, step, reps, names):
     return out
 
 
-GATHER_PATH_FILES = ("r05_fan_gather_path.json",)
+GATHER_PATH_FILES = {"fan": ("r06_fan_gather_path.json", "r05_fan_gather_path.json"),
+                     "cells": ("r06_cells_gather_path.json",)}
 
 
-def _gather_path():
-    """The fan kernel's texture-path counters (tools/pmc_fan.sh + tools/pmc_gather.py): TA / TD
-    busy, L1 tag lookups per instruction -- stamped with the fan's sources like the traffic
-    file, and marked stale (gather_path_stale) when this tree's fan sources differ."""
+def _gather_path(workload="fan"):
+    """A gather kernel's texture-path counters (tools/pmc_fan.sh or tools/pmc_cells.sh +
+    tools/pmc_gather.py): TA / TD busy, L1 tag lookups per instruction, wave wait / VALU
+    shares -- stamped with the kernel's sources like the traffic file, and marked stale
+    (gather_path_stale) when this tree's sources differ."""
     from pointcloud_processor_amd._stamps import workload_stamp
 
-    for name in GATHER_PATH_FILES:
+    for name in GATHER_PATH_FILES[workload]:
         f = ROOT / "profiles" / name
         try:
             d = json.loads(f.read_text())
@@ -425,7 +427,7 @@ def _gather_path():
             continue
         d = {k: v for k, v in d.items() if k != "counters_mean_per_dispatch"}
         d["source"] = f"profiles/{name}"
-        d["gather_path_stale"] = d.get("source_stamp") != workload_stamp("fan")
+        d["gather_path_stale"] = d.get("source_stamp") != workload_stamp(workload)
         return d
     return None
 
@@ -596,6 +598,10 @@ def _cells_roofline(ctx, cposes, zx5, params, n_cells, kern):
         "model": "frac = (probes + walk starts + point records + directory loads per launch, "
                  "pcp_score_poses_stats) / avg_kernel_ms / mix-weighted gather ceiling; "
                  "hbm_frac = PMC traffic per launch / avg_kernel_ms / 8 TB/s",
+        "gather_path": _gather_path("cells"),
+        "limiter": "latency: ~950 k short rays (8.3 lane-loads each) in ~2.4 rounds of waves at 6 "
+                   "waves per SIMD -- texture data path 67 % busy, waves waiting 55 % of their "
+                   "life (gather_path); the furthest of the hot kernels below its ceiling",
     }
 
 
