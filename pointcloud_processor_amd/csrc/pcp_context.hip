@@ -644,6 +644,8 @@ int pcp_create(int device, pcp_ctx **out) {
     if (const char *ho = std::getenv("PCP_FAN_HOST_OUT")) ctx->fan_host_out = std::atoi(ho) != 0;
     if (const char *ne = std::getenv("PCP_NORMALS_EXACT")) ctx->normals_exact = std::atoi(ne) != 0;
     if (const char *sw = std::getenv("PCP_SCORE_WIDE")) ctx->score_wide = std::atoi(sw) != 0;
+    if (const char *wr = std::getenv("PCP_SCORE_WIDE_RAYS")) ctx->score_wide_rays = std::atoll(wr);
+    if (const char *wg = std::getenv("PCP_SCORE_WIDE_G")) ctx->score_wide_g = std::atoi(wg);
     if (const char *co = std::getenv("PCP_CELLS_ORDER_FREE")) ctx->cells_all_ordered = std::atoi(co) == 0;
     if (const char *nbk = std::getenv("PCP_NB_BLOCKS")) ctx->nb_blocks = std::atoi(nbk);
     if (const char *sp = std::getenv("PCP_SCAN_ONEPASS")) ctx->scan_onepass = std::atoi(sp) != 0;

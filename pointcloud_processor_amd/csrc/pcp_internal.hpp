@@ -280,6 +280,8 @@ struct pcp_ctx {
     // {base, count}, cursors + overflow word; list entries the last call needed
     bool normals_exact = true;       // PCP_NORMALS_EXACT=0: round 3's order-free normals (A/B)
     bool score_wide = true;          // k_score_cells_wide for few-ray launches (PCP_SCORE_WIDE=0: A/B)
+    int64_t score_wide_rays = -1;    // PCP_SCORE_WIDE_RAYS: rays up to which it runs (A/B; -1: default)
+    int score_wide_g = 0;            // PCP_SCORE_WIDE_G: its lanes per ray, 2 / 4 / 8 / 16 (A/B; 0: default)
     bool cells_all_ordered = false;  // PCP_CELLS_ORDER_FREE=0: every cell through the lists (A/B)
     int nb_blocks = 0;               // PCP_NB_BLOCKS: k_nb_lists grid (A/B; 0 = kNbBlocks)
     bool nb_small = true;            // PCP_NB_SMALL=0: 32-bit list keys below 2^16 points too (A/B)

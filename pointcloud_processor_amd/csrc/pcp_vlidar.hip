@@ -1695,24 +1695,31 @@ static void launch_score_cells(hipStream_t st, pcp_ctx *ctx, const VisEnv &E, in
                                double *score_z, const uint32_t *P_dev, const uint32_t *C_dev) {
     const unsigned cb = (unsigned)((C + kT - 1) / kT);
     const dim3 g(cb, (unsigned)(P + 1));
-    const bool wide = (uint64_t)(P + 1) * (uint64_t)C <= (uint64_t)kWideMaxRays && ctx->score_wide;
-    const dim3 gw((unsigned)(((uint64_t)C * kWideG + kT - 1) / kT), (unsigned)(P + 1));
+    const uint64_t wide_rays = ctx->score_wide_rays >= 0 ? (uint64_t)ctx->score_wide_rays
+                                                         : (uint64_t)kWideMaxRays;
+    const bool wide = (uint64_t)(P + 1) * (uint64_t)C <= wide_rays && ctx->score_wide;
+    const int G = ctx->score_wide_g ? ctx->score_wide_g : kWideG;
+    const dim3 gw((unsigned)(((uint64_t)C * G + kT - 1) / kT), (unsigned)(P + 1));
     const double *cx = ctx->cells_xyz.as<const double>();
     const float *cn = ctx->cells_nrm.as<const float>();
-    if (wide && E.K <= kStepLds)
-        hipLaunchKernelGGL((k_score_cells_wide<true, kWideG>), gw, dim3(kT), 0, st, E, cx, cn, C,
-                           poses_k, P, zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev,
-                           C_dev);
-    else if (wide)
-        hipLaunchKernelGGL((k_score_cells_wide<false, kWideG>), gw, dim3(kT), 0, st, E, cx, cn, C,
-                           poses_k, P, zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev,
-                           C_dev);
-    else if (E.K <= kStepLds)
+#define PCP_WIDE_LAUNCH(SL, GG)                                                                  \
+    hipLaunchKernelGGL((k_score_cells_wide<SL, GG>), gw, dim3(kT), 0, st, E, cx, cn, C, poses_k, \
+                       P, zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev)
+    if (wide && E.K <= kStepLds) {
+        if (G == 2) PCP_WIDE_LAUNCH(true, 2);
+        else if (G == 4) PCP_WIDE_LAUNCH(true, 4);
+        else if (G == 8) PCP_WIDE_LAUNCH(true, 8);
+        else PCP_WIDE_LAUNCH(true, kWideG);
+    } else if (wide) {
+        PCP_WIDE_LAUNCH(false, kWideG);   // (a step table past LDS: the default width only)
+    } else if (E.K <= kStepLds) {
         hipLaunchKernelGGL(k_score_cells<true>, g, dim3(kT), 0, st, E, cx, cn, C, poses_k, P, zx_k,
                            o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
-    else
+    } else {
         hipLaunchKernelGGL(k_score_cells<false>, g, dim3(kT), 0, st, E, cx, cn, C, poses_k, P,
                            zx_k, o.comb, o.mbits, score_z, o.zbits, o.stats, P_dev, C_dev);
+    }
+#undef PCP_WIDE_LAUNCH
 }
 
 // runOptimization's scoring up to the per-pose sums, enqueued on ctx->stream: poses + the
