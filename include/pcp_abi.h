@@ -468,6 +468,7 @@ int pcp_raycast_fan_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
  * count.  collective_ms (nullable): the all-reduce between two events on the stream.
  * A rank whose work before the collective fails still runs it with a poisoned health word: it
  * returns its own error, every other rank PCP_E_STATE (nobody is left blocked in RCCL).
+ * PCP_E_STATE too when a pose of [0, p_total) was scored by no rank (cell_flags untouched).
  * Results are identical to pcp_score_poses over all p_total poses on one context. */
 int pcp_score_poses_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
                               const double zx120_pose5[5], const pcp_vl_params *p, uint64_t lo,

@@ -310,13 +310,17 @@ int pcp_score_poses_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n, co
     if (health != 0)
         return set_err(ctx, PCP_E_STATE, "pcp_score_poses_allreduce: a peer rank failed before "
                                          "the collective (health word poisoned)");
+    const unsigned long long *vh = reinterpret_cast<const unsigned long long *>(pin);
+    for (uint32_t k = 0; k < P; ++k)   // (cell_flags untouched: the query did not complete)
+        if (!(vh[P + k] & kScoreWritten))
+            return set_err(ctx, PCP_E_STATE, "pcp_score_poses_allreduce: pose %u of %u was "
+                                             "scored by no rank", k, P);
     if (collective_ms) {
         float ms = 0.0f;
         PCP_HIP(ctx, hipEventElapsedTime(&ms, ctx->comm_ev[0], ctx->comm_ev[1]));
         *collective_ms = ms;
     }
     if (C) std::memcpy(cell_flags, pin + fl_off, C);
-    const unsigned long long *vh = reinterpret_cast<const unsigned long long *>(pin);
     double zx_total;
     std::memcpy(&zx_total, pin + v_bytes, sizeof(double));
     double best = -INFINITY;

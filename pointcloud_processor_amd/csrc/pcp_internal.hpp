@@ -545,6 +545,8 @@ int score_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const double z
 // int64 MIN as torch.distributed reduces it)
 void launch_fan_keys(hipStream_t st, const uint32_t *blocked_d, uint32_t lo, uint32_t cnt,
                      uint32_t P, unsigned long long *keys, unsigned long long identity = ~0ull);
+// the covered key's mark of a pose some rank scored (k_score_keys; the low 32 bits: the count)
+constexpr unsigned long long kScoreWritten = 1ull << 32;
 void launch_score_keys(hipStream_t st, const ScoreEnq &o, int lo, int P, unsigned long long *v);
 void launch_flags_from_keys(hipStream_t st, const unsigned long long *v, const uint8_t *zbits,
                             int C, int P, uint8_t *flags, int32_t *stats);

@@ -409,7 +409,7 @@ int pcp_multi_score_poses(pcp_multi *m, const double *poses5, uint64_t n,
         double t;
         std::memcpy(&t, &vh[k], sizeof(double));
         if (total_score) total_score[k] = t;
-        if (covered) covered[k] = (int32_t)vh[P + k];
+        if (covered) covered[k] = (int32_t)vh[P + k];   // (the low 32 bits: kScoreWritten dropped)
         if (t > best) {
             best = t;
             best_idx = k;

@@ -1045,7 +1045,9 @@ k_fan_keys(const uint32_t *__restrict__ blocked, uint32_t lo, uint32_t cnt, uint
 
 // reference mode: v = [P totals | P covered | C range | C fov | C vis], all-reduce(MAX).
 // Totals are >= +0.0 (sums of positive scores from +0.0), so their IEEE bits order like the
-// values; 0 = +0.0 marks other ranks' poses.  Per cell, the newest pose of this rank that
+// values; 0 = +0.0 marks other ranks' poses.  A covered key carries kScoreWritten beside the
+// count, so a pose no rank scored reduces to 0 and is reported, not read as a zero total (as the
+// fan's UINT64_MAX key).  Per cell, the newest pose of this rank that
 // reached each stale-flag assignment (:662-687) as ((global index + 1) << 1) | bit, 0 = none:
 // the maximum over the ranks is the newest pose overall, which is what k_cell_flags resolves.
 __global__ void __launch_bounds__(kT)
@@ -1056,7 +1058,7 @@ k_score_keys(const double *__restrict__ tot, const int32_t *__restrict__ cov,
     if (i < P) {
         const bool mine = i >= lo && i - lo < Pl;
         v[i] = mine ? (unsigned long long)__double_as_longlong(tot[i - lo]) : 0ull;
-        v[P + i] = mine ? (unsigned long long)(uint32_t)cov[i - lo] : 0ull;
+        v[P + i] = mine ? (kScoreWritten | (unsigned long long)(uint32_t)cov[i - lo]) : 0ull;
     }
     if (i < C) {
         unsigned long long kr = 0, kf = 0, kv = 0;

@@ -86,11 +86,15 @@ def pose_bits(flags_after: np.ndarray) -> np.ndarray:
             | (((f & F_VIS_M) != 0) << 2)).astype(np.uint8)
 
 
+SCORE_WRITTEN = np.uint64(1 << 32)   # kScoreWritten: a covered key of a pose some rank scored
+
+
 def score_keys(tot_local: np.ndarray, cov_local: np.ndarray, bits_local: np.ndarray, lo: int,
                total: int) -> np.ndarray:
     """k_score_keys restated: this rank's vector [P total bits | P covered | C range keys | C fov
     keys | C visible keys] for ALL-REDUCE(MAX).  Totals are >= +0.0, so their IEEE bits order
-    like the values and 0 (= +0.0) marks other ranks' poses.  Per cell and stale-flag assignment,
+    like the values and 0 (= +0.0) marks other ranks' poses; a covered key is SCORE_WRITTEN | the
+    count, so a pose no rank scored reduces to 0 (pcp_score_poses_allreduce reports it).  Per cell and stale-flag assignment,
     the newest pose of this shard that made it: ((global index + 1) << 1) | bit, 0 = none.
     bits_local: [n, C] pose_bits rows of the shard's poses in order."""
     tot = np.asarray(tot_local, np.float64)
@@ -99,7 +103,8 @@ def score_keys(tot_local: np.ndarray, cov_local: np.ndarray, bits_local: np.ndar
     C = bits.shape[1]
     v = np.zeros(2 * total + 3 * C, np.uint64)
     v[lo:lo + n] = tot.view(np.uint64)
-    v[total + lo:total + lo + n] = np.asarray(cov_local, np.int64).astype(np.uint32)
+    v[total + lo:total + lo + n] = (np.asarray(cov_local, np.int64).astype(np.uint32)
+                                    .astype(np.uint64) | SCORE_WRITTEN)
     if n and C:
         g1 = (lo + np.arange(n, dtype=np.uint64) + 1) << np.uint64(1)   # (global + 1) << 1
 

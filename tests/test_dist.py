@@ -149,7 +149,8 @@ def test_two_rank_gloo_matches_single_process():
         # resolves to the reference's stale flags from a fresh GridCell state
         np.testing.assert_array_equal(red, v1)
         np.testing.assert_array_equal(red[:P].view(np.float64), s["total"])
-        np.testing.assert_array_equal(red[P:2 * P].astype(np.int32), s["covered"])
+        np.testing.assert_array_equal(red[P:2 * P] & np.uint64(0xFFFFFFFF), s["covered"])
+        assert np.all(red[P:2 * P] & pd.SCORE_WRITTEN)      # every pose scored by some rank
         np.testing.assert_array_equal(pd.flags_from_keys(red, fz & 7, np.zeros(C, np.uint8), P),
                                       f_all)
         np.testing.assert_array_equal(f_all, s["flags"])

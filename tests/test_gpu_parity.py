@@ -1862,7 +1862,7 @@ def test_score_allreduce_own_communicator(oracle, loaded, scene, cells, aux):
     of two ticks (the second from the first's flags, poses reversed), the report; the oracle
     agrees on the flags and the best index.  A rank whose arguments fail before the collective
     still runs it with a poisoned health word: it reports its own error, and the communicator
-    stays usable (the next query is exact again)."""
+    stays usable (the next query is exact again); poses that no rank scored are reported."""
     T, A = loaded
     params = _abi.default_vl_params()
     zx = np.ascontiguousarray(scene.zx120_pose5, np.float64)
@@ -1902,6 +1902,14 @@ def test_score_allreduce_own_communicator(oracle, loaded, scene, cells, aux):
         t4, _, r4 = ctx.score_poses(poses, zx, params, np.zeros(C, np.uint8))
         np.testing.assert_array_equal(t3.view(np.uint64), t4.view(np.uint64))
         assert rep.best_idx == r4.best_idx
+        # poses no rank scored (here: [0, 3) of a one-rank communicator) are an error, as the
+        # fan's unwritten keys are -- not zero totals; the caller's flags stay as they were
+        f5 = np.full(C, 0x5A, np.uint8)
+        with pytest.raises(_abi.PcpError, match="scored by no rank"):
+            ctx.score_poses_allreduce(poses[3:], zx, params, 3, P, f5, None, None, rep)
+        assert (f5 == 0x5A).all()
+        ctx.score_poses_allreduce(poses, zx, params, 0, P, f3 * 0, t3, None, rep)
+        np.testing.assert_array_equal(t3.view(np.uint64), t4.view(np.uint64))
         # the fan's collective carries the same health word: a bad shard, then an exact query
         fan = _abi.fan_params(n_az=128, n_el=32)
         with pytest.raises(_abi.PcpError):
