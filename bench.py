@@ -115,8 +115,17 @@ def _dist_init(n_gpus: int):
         ndev = 0
     backend = None
     group = None
-    if world > 1:
+    # PCP_DIST_FORCE=1: the distributed path at one rank too (the host group, libpcp's RCCL
+    # communicator, the one-collective queries, c4) -- a hardware check of the SCALE path's code
+    # on a one-GPU box (profiles/r06_bench_rccl_n1.json)
+    if world > 1 or os.environ.get("PCP_DIST_FORCE") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
         backend = os.environ.get("PCP_DIST_BACKEND", "rccl" if ndev >= world else "gloo")
         backend = "rccl" if backend == "nccl" else backend
         if ndev:
@@ -807,7 +816,7 @@ def run_all(args, dist, world, rank, local, backend):
     if dist is not None and backend == "gloo":
         out["rehearsal"] = (f"{world} ranks on {_abi.device_count()} GPU(s): collective "
                             "over gloo, ranks share devices")
-    if world > 1:   # configs[3]: the 4096-pose search strong-scaled over these ranks
+    if dist is not None:   # configs[3]: the 4096-pose search strong-scaled over these ranks
         out["c4"] = run_c4(args, dist, world, rank, local, backend, ctx=ctx, scene=scene)
     host = _host_cpu()
     cpu = rank == 0 and world == 1 and not args.no_cpu_baseline

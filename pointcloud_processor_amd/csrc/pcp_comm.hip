@@ -77,18 +77,22 @@ static int fan_allreduce_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n,
                                  double *collective_ms, const unsigned long long **units_out) {
     PCP_HIP(ctx, hipSetDevice(ctx->device));
     hipStream_t st = ctx->stream;
-    PCP_HIP(ctx, ctx->comm_keys.ensure((size_t)(P + 1) * 8 + 64));
-    const uint32_t *blocked_d = nullptr;
-    if (n) {
-        FanEnq o;   // device results (no host landing): the keys kernel reads them
-        if (int rc = fan_enqueue(ctx, poses5, n, fan, false, false, false, o)) return rc;
-        blocked_d = o.blocked_d;
-        *units_out = o.units_d;
-    }
+    // [P + 1 keys (the reduced span) | this shard's n unit counts]: one landing copy afterwards
+    PCP_HIP(ctx, ctx->comm_keys.ensure((size_t)(P + 1 + n) * 8 + 64));
     unsigned long long *keys = ctx->comm_keys.as<unsigned long long>();
-    // ~0 in the other ranks' slots and in the health word (slot P: no pose of any shard)
-    launch_fan_keys(st, blocked_d, (uint32_t)lo, (uint32_t)n, P + 1, keys);
-    PCP_CHECK_LAUNCH(ctx);
+    if (n) {
+        // k_fan_reduce writes the vector itself: the shard's keys, ~0 in the other ranks' slots
+        // and in the health word (slot P: no pose of any shard), the units behind it
+        FanEnq o;
+        o.keys = keys;
+        o.keys_lo = (uint32_t)lo;
+        o.keys_P = P;
+        if (int rc = fan_enqueue(ctx, poses5, n, fan, false, false, false, o)) return rc;
+        *units_out = o.units_d;
+    } else {   // no poses here: the identity everywhere
+        launch_fan_keys(st, nullptr, (uint32_t)lo, 0u, P + 1, keys);
+        PCP_CHECK_LAUNCH(ctx);
+    }
     if (collective_ms)
         for (hipEvent_t &e : ctx->comm_ev)
             if (!e) PCP_HIP(ctx, hipEventCreate(&e));
@@ -162,7 +166,8 @@ int pcp_raycast_fan_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
                        (unsigned long long)p_total);
     if (p_total == 0) return PCP_OK;
     const uint32_t P = (uint32_t)p_total;
-    const unsigned long long *units_d = nullptr;
+    const unsigned long long *units_d = nullptr;   // (the shard's units: k_fan_reduce also puts
+                                                   // them behind the health word, landed below)
     // everything before the collective; a failure poisons this rank's vector (health word 0)
     int rc = PCP_OK;
     if (lo + n > p_total)
@@ -186,12 +191,12 @@ int pcp_raycast_fan_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n,
     PCP_NCCL(ctx, ncclAllReduce(keys, keys, (size_t)P + 1, ncclUint64, ncclMin,
                                 static_cast<ncclComm_t>(ctx->comm), st));   // the one collective
     if (collective_ms) PCP_HIP(ctx, hipEventRecord(ctx->comm_ev[1], st));
-    // the reduced vector (+ health word) and this shard's units into one pinned block
+    // the reduced vector (+ health word) and this shard's units (behind it in the same device
+    // vector) into one pinned block by ONE copy kernel
     PCP_HIP(ctx, ctx->comm_host.ensure((size_t)(P + 1 + n) * 8 + 64));
     unsigned long long *kh = ctx->comm_host.as<unsigned long long>();
-    PCP_HIP(ctx, hipMemcpyAsync(kh, keys, (size_t)(P + 1) * 8, hipMemcpyDeviceToHost, st));
-    if (n && units)
-        PCP_HIP(ctx, hipMemcpyAsync(kh + P + 1, units_d, n * 8, hipMemcpyDeviceToHost, st));
+    if (int rcc = copy_to_pinned_async(ctx, kh, keys, (size_t)(P + 1 + (n && units ? n : 0)) * 8, st))
+        return rcc;
     PCP_HIP(ctx, hipStreamSynchronize(st));
     prof_resolve(ctx);
     if (rc) return rc;   // (ctx->err: this rank's own failure, set before the poison)
@@ -254,7 +259,8 @@ int pcp_score_poses_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n, co
     auto enqueue = [&]() -> int {
         PCP_HIP(ctx, hipSetDevice(ctx->device));
         PCP_HIP(ctx, ctx->comm_keys.ensure(count * 8 + 64));
-        if (int e = score_enqueue(ctx, poses5, n, zx, p, o)) return e;
+        // (the caller's flags ride in the query's one upload: k_flags_from_keys updates them)
+        if (int e = score_enqueue(ctx, poses5, n, zx, p, o, C ? cell_flags : nullptr)) return e;
         unsigned long long *v = ctx->comm_keys.as<unsigned long long>();
         launch_score_keys(st, o, (int)lo, (int)P, v);
         PCP_CHECK_LAUNCH(ctx);
@@ -288,21 +294,14 @@ int pcp_score_poses_allreduce(pcp_ctx *ctx, const double *poses5, uint64_t n, co
         PCP_HIP(ctx, hipStreamSynchronize(st));
         return set_err(ctx, rc, "%s", ctx->err.c_str());
     }
-    if (C) {
-        std::memcpy(pin + fl_off, cell_flags, C);
-        PCP_HIP(ctx, hipMemcpyAsync(o.flags_d, pin + fl_off, C, hipMemcpyHostToDevice, st));
-    }
-    PCP_HIP(ctx, hipMemsetAsync(o.stats, 0, 64 * sizeof(int32_t), st));
+    // the statistics were zeroed by k_score_cells (C > 0; else k_score_enqueue's memset), the
+    // caller's flags uploaded with the poses: resolve, then ONE landing kernel for everything
+    // the host reads -- the zx120 total is row n of this rank's totals (every rank evaluates it)
     launch_flags_from_keys(st, v, o.zbits, (int)C, (int)P, o.flags_d, o.stats);
     PCP_CHECK_LAUNCH(ctx);
-    if (P) PCP_HIP(ctx, hipMemcpyAsync(pin, v, v_bytes, hipMemcpyDeviceToHost, st));
-    // the zx120 total (row n of this rank's totals: every rank evaluates it) and the health word
-    PCP_HIP(ctx, hipMemcpyAsync(pin + v_bytes, o.tot_d + n, sizeof(double), hipMemcpyDeviceToHost,
-                                st));
-    PCP_HIP(ctx, hipMemcpyAsync(pin + v_bytes + 8, v + hw, 8, hipMemcpyDeviceToHost, st));
-    if (C) PCP_HIP(ctx, hipMemcpyAsync(pin + fl_off, o.flags_d, C, hipMemcpyDeviceToHost, st));
-    PCP_HIP(ctx, hipMemcpyAsync(pin + st_off, o.stats, 64 * sizeof(int32_t),
-                                hipMemcpyDeviceToHost, st));
+    launch_score_land(st, v, (int)P, hw, o.tot_d + n, o.flags_d, (int)C, o.stats, pin, fl_off,
+                      st_off);
+    PCP_CHECK_LAUNCH(ctx);
     PCP_HIP(ctx, hipStreamSynchronize(st));
     prof_resolve(ctx);
     unsigned long long health;

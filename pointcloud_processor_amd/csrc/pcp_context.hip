@@ -106,6 +106,22 @@ int copy_pinned_async(pcp_ctx *ctx, void *dst_d, const void *src_pinned, size_t 
     return PCP_OK;
 }
 
+int copy_to_pinned_async(pcp_ctx *ctx, void *dst_pinned, const void *src_d, size_t bytes,
+                         hipStream_t st) {
+    if (!bytes) return PCP_OK;
+    if (!ctx->copy_kernel || (((uintptr_t)dst_pinned | (uintptr_t)src_d) & 15u)) {
+        PCP_HIP(ctx, hipMemcpyAsync(dst_pinned, src_d, bytes, hipMemcpyDeviceToHost, st));
+        return PCP_OK;
+    }
+    const uint64_t n16 = (bytes + 15) / 16;
+    const unsigned g = (unsigned)std::min<uint64_t>((n16 + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_copy_pinned, dim3(g), dim3(256), 0, st,
+                       static_cast<const unsigned char *>(src_d),
+                       static_cast<unsigned char *>(dst_pinned), (uint64_t)bytes);
+    PCP_CHECK_LAUNCH(ctx);
+    return PCP_OK;
+}
+
 // slot s must hold `bytes`: when it has to grow, every slot of the ring grows with it (their
 // earlier transfers drained first), so a stream of same-sized messages pays the pinned
 // allocations once, on its first message, not on each slot's first turn

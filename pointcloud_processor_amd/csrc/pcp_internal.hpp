@@ -490,6 +490,12 @@ int exclusive_scan_u32_pair(pcp_ctx *ctx, const uint32_t *in_a, uint32_t *out_a,
 // fan query up to the per-pose sums, enqueued on ctx->stream (pcp_vlidar.hip): device results
 // in flight on return, the caller synchronizes.  n > 0.
 struct FanEnq {
+    // input (pcp_raycast_fan_allreduce): k_fan_reduce also writes the one-collective vector --
+    // keys[keys_lo + p] = (blocked << 32) | (keys_lo + p), ~0 in the other slots [0, keys_P]
+    // (the health word at keys_P included), the units behind it at keys[keys_P + 1 + p]
+    unsigned long long *keys = nullptr;
+    uint32_t keys_lo = 0, keys_P = 0;
+    // outputs
     uint32_t *blocked_d = nullptr;
     unsigned long long *units_d = nullptr;
     int16_t *fh_d = nullptr;
@@ -552,6 +558,14 @@ void launch_flags_from_keys(hipStream_t st, const unsigned long long *v, const u
                             int C, int P, uint8_t *flags, int32_t *stats);
 void launch_keys_combine(hipStream_t st, unsigned long long *a, const unsigned long long *b,
                          size_t n, bool is_max);
+// pcp_score_poses_allreduce's landing: reduced keys, zx120 total, health, flags, stats -> pinned
+void launch_score_land(hipStream_t st, const unsigned long long *v, int P, size_t hw,
+                       const double *zx_total, const uint8_t *flags, int C, const int32_t *stats,
+                       void *pin, size_t fl_off, size_t st_off);
+// a device buffer into pinned host memory by a copy kernel (k_copy_pinned; a DMA when the copy
+// kernel is off or the pointers are not 16-byte aligned)
+int copy_to_pinned_async(pcp_ctx *ctx, void *dst_pinned, const void *src_d, size_t bytes,
+                         hipStream_t st);
 // the colour-statistics slots (k_cell_flags order) -> pcp_vl_report
 void fill_report(const int32_t *st_h, double zx_total, int64_t best_idx, double best,
                  pcp_vl_report *rep);

@@ -1149,6 +1149,31 @@ void launch_flags_from_keys(hipStream_t st, const unsigned long long *v, const u
         hipLaunchKernelGGL(k_flags_from_keys, dim3((unsigned)((C + kT - 1) / kT)), dim3(kT), 0, st,
                            v, zbits, C, P, flags, stats);
 }
+// the one-collective scoring's results into the caller's pinned block in one launch (instead of
+// five D2H copies): [2P reduced keys | the zx120 total | the health word | C flags | 64 stats]
+__global__ void __launch_bounds__(kT)
+k_score_land(const unsigned long long *__restrict__ v, int P, size_t hw,
+             const double *__restrict__ zx_total, const uint8_t *__restrict__ flags, int C,
+             const int32_t *__restrict__ stats, unsigned char *__restrict__ pin, size_t fl_off,
+             size_t st_off) {
+    const size_t t = (size_t)blockIdx.x * kT + threadIdx.x, nt = (size_t)gridDim.x * kT;
+    unsigned long long *ph = reinterpret_cast<unsigned long long *>(pin);
+    for (size_t i = t; i < 2 * (size_t)P; i += nt) ph[i] = v[i];
+    if (t == 0) {
+        ph[2 * (size_t)P] = (unsigned long long)__double_as_longlong(*zx_total);
+        ph[2 * (size_t)P + 1] = v[hw];
+    }
+    for (size_t i = t; i < (size_t)C; i += nt) pin[fl_off + i] = flags[i];
+    if (t < 64) reinterpret_cast<int32_t *>(pin + st_off)[t] = stats[t];
+}
+void launch_score_land(hipStream_t st, const unsigned long long *v, int P, size_t hw,
+                       const double *zx_total, const uint8_t *flags, int C, const int32_t *stats,
+                       void *pin, size_t fl_off, size_t st_off) {
+    const size_t work = std::max<size_t>(std::max<size_t>(2 * (size_t)P, (size_t)C), 64);
+    const unsigned g = (unsigned)std::min<size_t>((work + kT - 1) / kT, 64);
+    hipLaunchKernelGGL(k_score_land, dim3(g), dim3(kT), 0, st, v, P, hw, zx_total, flags, C,
+                       stats, static_cast<unsigned char *>(pin), fl_off, st_off);
+}
 void launch_keys_combine(hipStream_t st, unsigned long long *a, const unsigned long long *b,
                          size_t n, bool is_max) {
     if (n)
@@ -1476,8 +1501,12 @@ k_sum_u64(const unsigned long long *__restrict__ in, size_t n, unsigned long lon
 // exact and deterministic)
 __global__ void __launch_bounds__(kT)
 k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves,
-             uint32_t *__restrict__ blocked, unsigned long long *__restrict__ units) {
+             uint32_t *__restrict__ blocked, unsigned long long *__restrict__ units,
+             unsigned long long *__restrict__ keys, uint32_t lo, uint32_t Pall) {
     const uint32_t p = blockIdx.x;
+    if (keys)   // (FanEnq.keys) the other ranks' slots and the health word: the MIN identity
+        for (uint32_t i = p * kT + threadIdx.x; i <= Pall; i += gridDim.x * kT)
+            if (i < lo || i - lo >= gridDim.x) keys[i] = ~0ull;
     const uint2 *row = part + (size_t)p * waves;   // the pose's partials, contiguous
     uint32_t b = 0;
     unsigned long long u = 0;
@@ -1499,8 +1528,14 @@ k_fan_reduce(const uint2 *__restrict__ part, uint32_t waves,
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        blocked[p] = sb[0] + sb[1] + sb[2] + sb[3];
-        units[p] = su[0] + su[1] + su[2] + su[3];
+        const uint32_t bs = sb[0] + sb[1] + sb[2] + sb[3];
+        const unsigned long long us = su[0] + su[1] + su[2] + su[3];
+        blocked[p] = bs;
+        units[p] = us;
+        if (keys) {
+            keys[lo + p] = ((unsigned long long)bs << 32) | (unsigned long long)(lo + p);
+            keys[(size_t)Pall + 1 + p] = us;
+        }
         // the outputs may be pinned host memory (fan_host_out): the caller reads them after
         // hipStreamSynchronize, whose completion signal carries the kernel's system-scope
         // release.  A __threadfence_system() per block here measured 11.7 vs 5.8 us per launch
@@ -2331,7 +2366,7 @@ int fan_enqueue(pcp_ctx *ctx, const double *poses5, uint64_t n, const pcp_fan_pa
 #undef PCP_FAN_LAUNCH_T
     hipLaunchKernelGGL(k_fan_reduce, dim3(P), dim3(kT), 0, st,
                        (const uint2 *)a.wave_part, waves, blocked_d,
-                       units_d);
+                       units_d, o.keys, o.keys_lo, o.keys_P);
     PCP_CHECK_LAUNCH(ctx);
     o.blocked_d = host_out ? nullptr : blocked_d;
     o.units_d = host_out ? nullptr : units_d;
