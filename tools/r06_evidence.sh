@@ -8,6 +8,8 @@
 #   S: rocprofv3 kernel stats of the default bench command
 #   A: every GPU test + smoke, the default bench line
 #   N: the N = 2 rehearsal (two ranks on the one GPU over gloo), reference mode
+#   R: the default line through the distributed path at one rank (PCP_DIST_FORCE=1: host group,
+#      libpcp's RCCL communicator, the one-collective queries, c4)
 # parse afterwards (in this tree: only gpurun_out/ comes back):
 #   python3 tools/pmc_gather.py profiles/r06_fan_gather_path.json fan gpurun_out/pmcfr06_[1-5]
 #   python3 tools/pmc_gather.py profiles/r06_cells_gather_path.json cells gpurun_out/pmccr06_[1-5]
@@ -52,6 +54,9 @@ A)
   ;;
 N)
   step bench_n2 600 python bench.py --gpus 2 --mode cells --steps 5 --warmup 2 --no-cpu-baseline
+  ;;
+R)
+  step bench_rccl_n1 600 env WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 PCP_DIST_FORCE=1 python bench.py --gpus 1
   ;;
 esac
 done
