@@ -767,10 +767,11 @@ def run_all(args, dist, world, rank, local, backend):
                                                 timed=True)[1])
         collective = {"op": "ncclAllReduce(ncclUint64, ncclMin)", "backend": "rccl (libpcp)",
                       "bytes": 8 * P_total, "collective_ms": float(np.median(ms)),
-                      "path": "device keys in libpcp's vector, libpcp's own RCCL communicator on "
-                              "its stream (pcp_raycast_fan_allreduce), reduced vector D2H once; "
-                              "torch.distributed (gloo, in a helper process: hostgroup.py) only "
-                              "for the id hand-off and barriers"}
+                      "path": "device keys in libpcp's vector (written by k_fan_reduce), libpcp's "
+                              "own RCCL communicator on its stream (pcp_raycast_fan_allreduce), "
+                              "the reduced vector and the shard's units landed by one copy "
+                              "kernel; torch.distributed (gloo, in a helper process: "
+                              "hostgroup.py) only for the id hand-off and barriers"}
         nr, rr = ctx.comm_info()
         collective["rccl_nranks"] = nr   # the ranks RCCL's communicator saw (pcp_comm_info)
         collective["runtime"] = _runtime()

@@ -196,3 +196,31 @@ def test_bench_rejects_mismatched_world():
                         "--mode", "launch-check"], capture_output=True, text=True, env=env,
                        timeout=300)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_rccl_one_rank_gpu():
+    """The SCALE path's own code on the GPU at one rank (PCP_DIST_FORCE=1): the host group,
+    libpcp's RCCL communicator (pcp_comm_init_rank over the id the group hands out) and the
+    one-collective fan query every step; the line names RCCL with one rank, and the reduced
+    vector's argmin is the plain query's best pose (the same seeded workload, no collective)."""
+    import json
+    import subprocess
+
+    def run(extra):
+        env = {k: v for k, v in os.environ.items() if k != "MASTER_PORT"}
+        env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", **extra)
+        r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--mode",
+                            "fan", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"],
+                           capture_output=True, text=True, env=env, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+    dist_line = run({"PCP_DIST_FORCE": "1"})
+    col = dist_line["collective"]
+    assert col["backend"].startswith("rccl") and col["rccl_nranks"] == 1
+    assert col["collective_ms"] is None or col["collective_ms"] >= 0.0
+    assert dist_line["runtime"]["torch_in_process"] is False
+    plain = run({})
+    assert plain["collective"] is None
+    assert dist_line["best_pose"] == plain["best_pose"]
